@@ -1,0 +1,879 @@
+// dab_kernels.hip — gfx950 kernels of the BA hot path.
+//
+// Every kernel is wave64-native and works on point-major SoA data:
+//   obs_idx  int4 (point, ext0, ext1, intr)    16 B / observation, one dwordx4 load
+//   obs_xy   double2                           16 B / observation
+//   r        double2                           16 B / observation (written)
+//   J        [plane][N] doubles, plane = 2*col + row, col in X(3) w0(3) t0(3) w1(3) t1(3)
+//            18 planes (single extrinsic) or 30 (arc∘ring): 144 / 240 B per observation.
+// Per-extrinsic rotation data is precomputed once per parameter state (launch_cam_tables)
+// so the per-observation kernels carry no transcendental: the Jacobian of
+// R(w)X with respect to w is -R [X]x J_r(w) (right Jacobian of SO(3)); in Ceres'
+// first-order branch (|w|^2 <= DBL_EPSILON, rotation.h) R = I + [w]x and the
+// derivative is -[X]x, which the table encodes as Rd = I, Jd = I.
+// All reductions are deterministic: fixed-shape wave butterflies + fixed-order block and
+// chunk sums, so results are bitwise reproducible run to run.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+
+#include "dab_kernels.h"
+
+namespace dab {
+
+int grid_for(int n, int block, int cap) {
+  int g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return g;
+}
+
+// ------------------------------------------------------------------------------------
+// reductions
+// ------------------------------------------------------------------------------------
+template <int K>
+__device__ __forceinline__ void block_reduce_store(double (&acc)[K], double* __restrict__ out) {
+  __shared__ double sh[kRedBlock / 64][K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    double v = acc[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    acc[i] = v;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) sh[w][i] = acc[i];
+  }
+  __syncthreads();
+  if (threadIdx.x < K) {
+    double v = sh[0][threadIdx.x];
+#pragma unroll
+    for (int q = 1; q < kRedBlock / 64; ++q) v += sh[q][threadIdx.x];
+    out[threadIdx.x] = v;
+  }
+}
+
+__global__ void k_seg_final(int nseg, int K, const int* __restrict__ seg_chunk,
+                            const double* __restrict__ partial, double* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nseg * K) return;
+  const int seg = t / K, k = t - seg * K;
+  double v = 0.0;
+  for (int c = seg_chunk[seg]; c < seg_chunk[seg + 1]; ++c) v += partial[(size_t)c * K + k];
+  out[t] = v;
+}
+
+__global__ void k_final_sum(int grid, int K, const double* __restrict__ partial,
+                            double* __restrict__ out, unsigned max_mask) {
+  const int k = threadIdx.x;
+  if (k >= K) return;
+  const bool is_max = (max_mask >> k) & 1u;
+  double v = 0.0;
+  for (int c = 0; c < grid; ++c) {
+    const double x = partial[(size_t)c * K + k];
+    v = is_max ? fmax(v, x) : v + x;
+  }
+  out[k] = v;
+}
+
+__global__ void k_cam_norms(int E, const int* __restrict__ ext_col, const double* __restrict__ ext,
+                            const double* __restrict__ ext_c, const double* __restrict__ ug,
+                            double* __restrict__ out) {
+  // single block of 256 threads, fixed-order combine
+  __shared__ double sh[256][5];
+  double a[5] = {0, 0, 0, 0, 0};
+  for (int t = threadIdx.x; t < 6 * E; t += blockDim.x) {
+    const int e = t / 6, k = t - 6 * (t / 6);
+    const int c = ext_col[e];
+    if (c < 0) continue;
+    const double x = ext[t], xc = ext_c ? ext_c[t] : x;
+    const double dd = x - xc;
+    a[0] += dd * dd;
+    a[1] += xc * xc;
+    const double gg = ug ? x - (x + (-ug[27 * (size_t)c + 21 + k])) : 0.0;
+    a[2] = fmax(a[2], fabs(gg));
+    a[3] += gg * gg;
+    a[4] += x * x;
+  }
+#pragma unroll
+  for (int i = 0; i < 5; ++i) sh[threadIdx.x][i] = a[i];
+  __syncthreads();
+  if (threadIdx.x < 5) {
+    const int i = threadIdx.x;
+    double v = 0.0;
+    for (int q = 0; q < 256; ++q) v = (i == 2) ? fmax(v, sh[q][i]) : v + sh[q][i];
+    out[i] = v;
+  }
+}
+
+void launch_cam_norms(hipStream_t s, int E, const int* ext_col, const double* ext, const double* ext_c,
+                      const double* ug, double* out) {
+  k_cam_norms<<<1, 256, 0, s>>>(E, ext_col, ext, ext_c, ug, out);
+}
+
+void launch_seg_final(hipStream_t s, int nseg, int K, const int* seg_chunk, const double* partial,
+                      double* out) {
+  if (nseg <= 0) return;
+  const int n = nseg * K;
+  k_seg_final<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(nseg, K, seg_chunk, partial, out);
+}
+void launch_final_sum(hipStream_t s, int grid, int K, const double* partial, double* out,
+                      unsigned max_mask) {
+  k_final_sum<<<1, 64, 0, s>>>(grid, K, partial, out, max_mask);
+}
+
+__global__ __launch_bounds__(256) void k_r_sumsq(int N, const double2* __restrict__ r,
+                                                 double* __restrict__ partial) {
+  double acc[2] = {0.0, 0.0};
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < N; s += gridDim.x * blockDim.x) {
+    const double2 v = r[s];
+    acc[0] += v.x * v.x + v.y * v.y;
+    acc[1] += (isfinite(v.x) && isfinite(v.y)) ? 0.0 : 1.0;
+  }
+  block_reduce_store<2>(acc, partial + 2 * (size_t)blockIdx.x);
+}
+
+void launch_r_sumsq(hipStream_t s, int N, const double* r, double* partial, int grid) {
+  k_r_sumsq<<<grid, 256, 0, s>>>(N, reinterpret_cast<const double2*>(r), partial);
+}
+
+// ------------------------------------------------------------------------------------
+// per-extrinsic tables (R, t, Rd, Jd)
+// ------------------------------------------------------------------------------------
+__global__ void k_cam_tables(int E, const double* __restrict__ ext, double* __restrict__ tab) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const double w0 = ext[6 * e], w1 = ext[6 * e + 1], w2 = ext[6 * e + 2];
+  double* T = tab + (size_t)kCamTab * e;
+  double R[9], Rd[9], Jd[9];
+  const double th2 = w0 * w0 + w1 * w1 + w2 * w2;
+  if (th2 > DBL_EPSILON) {
+    const double th = sqrt(th2);
+    double sn, cs;
+    sincos(th, &sn, &cs);
+    const double x = w0 / th, y = w1 / th, z = w2 / th, omc = 1.0 - cs;
+    // ceres::AngleAxisToRotationMatrix, row-major
+    R[0] = cs + x * x * omc;      R[1] = x * y * omc - z * sn;  R[2] = y * sn + x * z * omc;
+    R[3] = z * sn + x * y * omc;  R[4] = cs + y * y * omc;      R[5] = -x * sn + y * z * omc;
+    R[6] = -y * sn + x * z * omc; R[7] = x * sn + y * z * omc;  R[8] = cs + z * z * omc;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Rd[i] = R[i];
+    // right Jacobian J_r = I - a [w]x + b [w]x^2, a = (1-cos)/th^2, b = (th-sin)/th^3
+    double a, b;
+    if (th < 0.1) {
+      const double t2 = th2;
+      a = 0.5 + t2 * (-1.0 / 24 + t2 * (1.0 / 720 + t2 * (-1.0 / 40320 + t2 * (1.0 / 3628800))));
+      b = 1.0 / 6 + t2 * (-1.0 / 120 + t2 * (1.0 / 5040 + t2 * (-1.0 / 362880 + t2 * (1.0 / 39916800))));
+    } else {
+      const double sh = sin(0.5 * th);
+      a = 2.0 * sh * sh / th2;
+      b = (th - sn) / (th2 * th);
+    }
+    Jd[0] = 1.0 + b * (w0 * w0 - th2); Jd[1] = a * w2 + b * w0 * w1;        Jd[2] = -a * w1 + b * w0 * w2;
+    Jd[3] = -a * w2 + b * w1 * w0;     Jd[4] = 1.0 + b * (w1 * w1 - th2); Jd[5] = a * w0 + b * w1 * w2;
+    Jd[6] = a * w1 + b * w2 * w0;      Jd[7] = -a * w0 + b * w2 * w1;     Jd[8] = 1.0 + b * (w2 * w2 - th2);
+  } else {
+    R[0] = 1.0; R[1] = -w2; R[2] = w1;
+    R[3] = w2;  R[4] = 1.0; R[5] = -w0;
+    R[6] = -w1; R[7] = w0;  R[8] = 1.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Rd[i] = (i % 4 == 0) ? 1.0 : 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Jd[i] = (i % 4 == 0) ? 1.0 : 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) T[i] = R[i];
+  T[9] = ext[6 * e + 3];
+  T[10] = ext[6 * e + 4];
+  T[11] = ext[6 * e + 5];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) T[12 + i] = Rd[i];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) T[21 + i] = Jd[i];
+  T[30] = 0.0;
+  T[31] = 0.0;
+}
+
+void launch_cam_tables(hipStream_t s, int E, const double* ext, double* camtab) {
+  if (E <= 0) return;
+  k_cam_tables<<<grid_for(E, 64, 1 << 20), 64, 0, s>>>(E, ext, camtab);
+}
+
+// ------------------------------------------------------------------------------------
+// residual + Jacobian (rows a1-a4)
+// ------------------------------------------------------------------------------------
+struct Proj {
+  double ru, rv;
+  double A0[3], A1[3];  // d(ru,rv)/dP
+};
+
+__device__ __forceinline__ void project(const double P[3], const double* __restrict__ K, double ox,
+                                        double oy, Proj& o, bool want_jac) {
+  const double cx = K[0], cy = K[1], fx = K[2], fy = K[3], k0 = K[4], k1 = K[5];
+  const double xp = P[0] / P[2];
+  const double yp = P[1] / P[2];
+  const double r2 = xp * xp + yp * yp;
+  // |k| = 0, 1, 2 are all this expression with unused coefficients zeroed (exact)
+  const double d = 1.0 + r2 * (k0 + k1 * r2);
+  o.ru = fx * d * xp + cx - ox;
+  o.rv = fy * d * yp + cy - oy;
+  if (!want_jac) return;
+  const double dd = k0 + 2.0 * k1 * r2;
+  const double du_dx = fx * (d + 2.0 * xp * xp * dd), du_dy = fx * (2.0 * xp * yp * dd);
+  const double dv_dx = fy * (2.0 * xp * yp * dd), dv_dy = fy * (d + 2.0 * yp * yp * dd);
+  const double iz = 1.0 / P[2];
+  o.A0[0] = du_dx * iz;
+  o.A0[1] = du_dy * iz;
+  o.A0[2] = -(du_dx * xp + du_dy * yp) * iz;
+  o.A1[0] = dv_dx * iz;
+  o.A1[1] = dv_dy * iz;
+  o.A1[2] = -(dv_dx * xp + dv_dy * yp) * iz;
+}
+
+__device__ __forceinline__ void rowmat(const double a[3], const double* __restrict__ M, double o[3]) {
+  o[0] = a[0] * M[0] + a[1] * M[3] + a[2] * M[6];
+  o[1] = a[0] * M[1] + a[1] * M[4] + a[2] * M[7];
+  o[2] = a[0] * M[2] + a[1] * M[5] + a[2] * M[8];
+}
+__device__ __forceinline__ void matvec_add(const double* __restrict__ M, const double x[3],
+                                           const double* __restrict__ t, double o[3]) {
+  o[0] = M[0] * x[0] + M[1] * x[1] + M[2] * x[2] + t[0];
+  o[1] = M[3] * x[0] + M[4] * x[1] + M[5] * x[2] + t[1];
+  o[2] = M[6] * x[0] + M[7] * x[1] + M[8] * x[2] + t[2];
+}
+// o = -((a x X)^T Jd)
+__device__ __forceinline__ void dwrot(const double a[3], const double X[3], const double* __restrict__ Jd,
+                                      double o[3]) {
+  const double c0 = a[1] * X[2] - a[2] * X[1];
+  const double c1 = a[2] * X[0] - a[0] * X[2];
+  const double c2 = a[0] * X[1] - a[1] * X[0];
+  o[0] = -(c0 * Jd[0] + c1 * Jd[3] + c2 * Jd[6]);
+  o[1] = -(c0 * Jd[1] + c1 * Jd[4] + c2 * Jd[7]);
+  o[2] = -(c0 * Jd[2] + c1 * Jd[5] + c2 * Jd[8]);
+}
+
+__device__ __forceinline__ void load_tab(const double* __restrict__ camtab, int e, double (&T)[30]) {
+  const double2* p = reinterpret_cast<const double2*>(camtab + (size_t)kCamTab * e);
+#pragma unroll
+  for (int i = 0; i < 15; ++i) {
+    const double2 v = p[i];
+    T[2 * i] = v.x;
+    T[2 * i + 1] = v.y;
+  }
+}
+__device__ __forceinline__ void load_rt(const double* __restrict__ camtab, int e, double (&T)[12]) {
+  const double2* p = reinterpret_cast<const double2*>(camtab + (size_t)kCamTab * e);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const double2 v = p[i];
+    T[2 * i] = v.x;
+    T[2 * i + 1] = v.y;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_jacobian(DevView v, const double* __restrict__ points,
+                                                  const double* __restrict__ camtab,
+                                                  double2* __restrict__ r, double* __restrict__ J) {
+  const int N = v.N;
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < N; s += gridDim.x * blockDim.x) {
+    const int4 id = v.obs_idx[s];
+    const double2 xy = v.obs_xy[s];
+    const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
+    const double* K = v.intr + (size_t)kIntr * id.w;
+    double T0[30];
+    load_tab(camtab, id.y, T0);
+    Proj pr;
+    double jx0[3], jx1[3], jw0a[3], jw0b[3], jw1a[3], jw1b[3], jt1a[3], jt1b[3];
+    if (id.z >= 0) {
+      double T1[30];
+      load_tab(camtab, id.z, T1);
+      double P2[3], P[3];
+      matvec_add(T1, X, T1 + 9, P2);
+      matvec_add(T0, P2, T0 + 9, P);
+      project(P, K, xy.x, xy.y, pr, true);
+      double B0a[3], B0b[3];
+      rowmat(pr.A0, T0, B0a);  // A R0
+      rowmat(pr.A1, T0, B0b);
+      rowmat(B0a, T1, jx0);    // A R0 R1
+      rowmat(B0b, T1, jx1);
+      double Ca[3], Cb[3];
+      rowmat(B0a, T1 + 12, Ca);  // A R0 Rd1
+      rowmat(B0b, T1 + 12, Cb);
+      dwrot(Ca, X, T1 + 21, jw1a);
+      dwrot(Cb, X, T1 + 21, jw1b);
+      double Da[3], Db[3];
+      rowmat(pr.A0, T0 + 12, Da);  // A Rd0
+      rowmat(pr.A1, T0 + 12, Db);
+      dwrot(Da, P2, T0 + 21, jw0a);
+      dwrot(Db, P2, T0 + 21, jw0b);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) { jt1a[i] = B0a[i]; jt1b[i] = B0b[i]; }
+    } else {
+      double P[3];
+      matvec_add(T0, X, T0 + 9, P);
+      project(P, K, xy.x, xy.y, pr, true);
+      rowmat(pr.A0, T0, jx0);
+      rowmat(pr.A1, T0, jx1);
+      double Da[3], Db[3];
+      rowmat(pr.A0, T0 + 12, Da);
+      rowmat(pr.A1, T0 + 12, Db);
+      dwrot(Da, X, T0 + 21, jw0a);
+      dwrot(Db, X, T0 + 21, jw0b);
+    }
+    r[s] = make_double2(pr.ru, pr.rv);
+    double* Jp = J + s;
+    const size_t Ns = (size_t)N;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      Jp[(2 * c) * Ns] = jx0[c];
+      Jp[(2 * c + 1) * Ns] = jx1[c];
+      Jp[(2 * (3 + c)) * Ns] = jw0a[c];
+      Jp[(2 * (3 + c) + 1) * Ns] = jw0b[c];
+      Jp[(2 * (6 + c)) * Ns] = pr.A0[c];
+      Jp[(2 * (6 + c) + 1) * Ns] = pr.A1[c];
+    }
+    if (id.z >= 0) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        Jp[(2 * (9 + c)) * Ns] = jw1a[c];
+        Jp[(2 * (9 + c) + 1) * Ns] = jw1b[c];
+        Jp[(2 * (12 + c)) * Ns] = jt1a[c];
+        Jp[(2 * (12 + c) + 1) * Ns] = jt1b[c];
+      }
+    }
+  }
+}
+
+void launch_jacobian(hipStream_t s, const DevView& v, const double* points, const double* camtab,
+                     double* r, double* J) {
+  if (v.N <= 0) return;
+  k_jacobian<<<grid_for(v.N, 256, 1 << 20), 256, 0, s>>>(v, points, camtab,
+                                                        reinterpret_cast<double2*>(r), J);
+}
+
+// residual at a parameter state: partial[block] = {sum r^2, nonfinite count}
+__device__ __forceinline__ void residual_at(const DevView& v, const double* __restrict__ points,
+                                            const double* __restrict__ camtab, int s, double& ru,
+                                            double& rv) {
+  const int4 id = v.obs_idx[s];
+  const double2 xy = v.obs_xy[s];
+  const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
+  const double* K = v.intr + (size_t)kIntr * id.w;
+  double T0[12];
+  load_rt(camtab, id.y, T0);
+  double P[3];
+  if (id.z >= 0) {
+    double T1[12], P2[3];
+    load_rt(camtab, id.z, T1);
+    matvec_add(T1, X, T1 + 9, P2);
+    matvec_add(T0, P2, T0 + 9, P);
+  } else {
+    matvec_add(T0, X, T0 + 9, P);
+  }
+  Proj pr;
+  project(P, K, xy.x, xy.y, pr, false);
+  ru = pr.ru;
+  rv = pr.rv;
+}
+
+__global__ __launch_bounds__(256) void k_residual(DevView v, const double* __restrict__ points,
+                                                  const double* __restrict__ camtab,
+                                                  double2* __restrict__ rout,
+                                                  double* __restrict__ partial) {
+  double acc[2] = {0.0, 0.0};
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < v.N; s += gridDim.x * blockDim.x) {
+    double ru, rv;
+    residual_at(v, points, camtab, s, ru, rv);
+    if (rout) rout[s] = make_double2(ru, rv);
+    acc[0] += ru * ru + rv * rv;
+    acc[1] += (isfinite(ru) && isfinite(rv)) ? 0.0 : 1.0;
+  }
+  block_reduce_store<2>(acc, partial + 2 * (size_t)blockIdx.x);
+}
+
+void launch_residual(hipStream_t s, const DevView& v, const double* points, const double* camtab,
+                     double* r_out, double* partial, int grid) {
+  k_residual<<<grid, 256, 0, s>>>(v, points, camtab, reinterpret_cast<double2*>(r_out), partial);
+}
+
+// ------------------------------------------------------------------------------------
+// J^T J / J^T r block assembly (row a7, normal-equation side)
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_point_vg(DevView v, const double2* __restrict__ r,
+                                                  const double* __restrict__ J, double* __restrict__ V,
+                                                  double* __restrict__ g) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= v.NP) return;
+  const size_t Ns = (size_t)v.N, NPs = (size_t)v.NP;
+  double a00 = 0, a01 = 0, a02 = 0, a11 = 0, a12 = 0, a22 = 0, g0 = 0, g1 = 0, g2 = 0;
+  for (int s = v.pt_obs_ptr[p]; s < v.pt_obs_ptr[p + 1]; ++s) {
+    const double2 rr = r[s];
+    const double x0 = J[0 * Ns + s], y0 = J[1 * Ns + s];
+    const double x1 = J[2 * Ns + s], y1 = J[3 * Ns + s];
+    const double x2 = J[4 * Ns + s], y2 = J[5 * Ns + s];
+    a00 += x0 * x0 + y0 * y0;
+    a01 += x0 * x1 + y0 * y1;
+    a02 += x0 * x2 + y0 * y2;
+    a11 += x1 * x1 + y1 * y1;
+    a12 += x1 * x2 + y1 * y2;
+    a22 += x2 * x2 + y2 * y2;
+    g0 += x0 * rr.x + y0 * rr.y;
+    g1 += x1 * rr.x + y1 * rr.y;
+    g2 += x2 * rr.x + y2 * rr.y;
+  }
+  V[0 * NPs + p] = a00; V[1 * NPs + p] = a01; V[2 * NPs + p] = a02;
+  V[3 * NPs + p] = a11; V[4 * NPs + p] = a12; V[5 * NPs + p] = a22;
+  g[0 * NPs + p] = g0; g[1 * NPs + p] = g1; g[2 * NPs + p] = g2;
+}
+
+void launch_point_vg(hipStream_t s, const DevView& v, const double* r, const double* J, double* V,
+                     double* g) {
+  if (v.NP <= 0) return;
+  k_point_vg<<<grid_for(v.NP, 256, 1 << 20), 256, 0, s>>>(v, reinterpret_cast<const double2*>(r), J, V, g);
+}
+
+__global__ __launch_bounds__(256) void k_cam_ug_partial(DevView v, const int* __restrict__ chunk_beg,
+                                                        const int* __restrict__ cam_ent,
+                                                        const double2* __restrict__ r,
+                                                        const double* __restrict__ J,
+                                                        double* __restrict__ partial) {
+  const int c = blockIdx.x;
+  const int b = chunk_beg[c], e = chunk_beg[c + 1];
+  const size_t Ns = (size_t)v.N;
+  double acc[27];
+#pragma unroll
+  for (int i = 0; i < 27; ++i) acc[i] = 0.0;
+  for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
+    const int os = v.ent_os[cam_ent[i]];
+    const int s = os >> 1, slot = os & 1;
+    const double2 rr = r[s];
+    double ja[6], jb[6];
+    const int col0 = 3 + 6 * slot;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      ja[a] = J[(size_t)(2 * (col0 + a)) * Ns + s];
+      jb[a] = J[(size_t)(2 * (col0 + a) + 1) * Ns + s];
+    }
+    int q = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int bb = a; bb < 6; ++bb) acc[q++] += ja[a] * ja[bb] + jb[a] * jb[bb];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[21 + a] += ja[a] * rr.x + jb[a] * rr.y;
+  }
+  block_reduce_store<27>(acc, partial + 27 * (size_t)c);
+}
+
+void launch_cam_ug_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
+                           const int* cam_ent, const double* r, const double* J, double* partial) {
+  if (nchunk <= 0) return;
+  k_cam_ug_partial<<<nchunk, 256, 0, s>>>(v, chunk_beg, cam_ent, reinterpret_cast<const double2*>(r), J,
+                                          partial);
+}
+
+__global__ __launch_bounds__(256) void k_cross_partial(DevView v, const int* __restrict__ chunk_beg,
+                                                       const int* __restrict__ xobs,
+                                                       const double* __restrict__ J,
+                                                       double* __restrict__ partial) {
+  const int c = blockIdx.x;
+  const int b = chunk_beg[c], e = chunk_beg[c + 1];
+  const size_t Ns = (size_t)v.N;
+  double acc[36];
+#pragma unroll
+  for (int i = 0; i < 36; ++i) acc[i] = 0.0;
+  for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
+    const int s = xobs[i];
+    double a0[6], a1[6], b0[6], b1[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      a0[a] = J[(size_t)(2 * (3 + a)) * Ns + s];
+      a1[a] = J[(size_t)(2 * (3 + a) + 1) * Ns + s];
+      b0[a] = J[(size_t)(2 * (9 + a)) * Ns + s];
+      b1[a] = J[(size_t)(2 * (9 + a) + 1) * Ns + s];
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) acc[6 * a + bb] += a0[a] * b0[bb] + a1[a] * b1[bb];
+  }
+  block_reduce_store<36>(acc, partial + 36 * (size_t)c);
+}
+
+void launch_cross_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
+                          const int* xobs, const double* J, double* partial) {
+  if (nchunk <= 0) return;
+  k_cross_partial<<<nchunk, 256, 0, s>>>(v, chunk_beg, xobs, J, partial);
+}
+
+// ------------------------------------------------------------------------------------
+// LM step: point elimination (Schur complement) and back-substitution
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_point_factor(DevView v, const double* __restrict__ V,
+                                                      const double* __restrict__ g,
+                                                      const double* __restrict__ sp, StepScalars sc,
+                                                      double* __restrict__ L, double* __restrict__ q,
+                                                      int* __restrict__ fail) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= v.NP) return;
+  const size_t NPs = (size_t)v.NP;
+  const double s0 = sp[p], s1 = sp[NPs + p], s2 = sp[2 * NPs + p];
+  double v00 = s0 * V[p] * s0, v01 = s0 * V[NPs + p] * s1, v02 = s0 * V[2 * NPs + p] * s2;
+  double v11 = s1 * V[3 * NPs + p] * s1, v12 = s1 * V[4 * NPs + p] * s2, v22 = s2 * V[5 * NPs + p] * s2;
+  auto lmd = [&](double d) {
+    d = fmin(fmax(d, sc.min_diag), sc.max_diag);
+    const double D = sqrt(d / sc.radius);
+    return D * D;
+  };
+  v00 += lmd(v00);
+  v11 += lmd(v11);
+  v22 += lmd(v22);
+  bool ok = v00 > 0.0;
+  const double l00 = sqrt(v00);
+  const double l10 = v01 / l00, l20 = v02 / l00;
+  const double d1 = v11 - l10 * l10;
+  ok = ok && d1 > 0.0;
+  const double l11 = sqrt(d1);
+  const double l21 = (v12 - l20 * l10) / l11;
+  const double d2 = v22 - l20 * l20 - l21 * l21;
+  ok = ok && d2 > 0.0;
+  const double l22 = sqrt(d2);
+  const double gs0 = s0 * g[p], gs1 = s1 * g[NPs + p], gs2 = s2 * g[2 * NPs + p];
+  const double q0 = gs0 / l00;
+  const double q1 = (gs1 - l10 * q0) / l11;
+  const double q2 = (gs2 - l20 * q0 - l21 * q1) / l22;
+  ok = ok && isfinite(q0) && isfinite(q1) && isfinite(q2);
+  if (!ok) atomicOr(fail, 1);
+  L[p] = l00; L[NPs + p] = l10; L[2 * NPs + p] = l20;
+  L[3 * NPs + p] = l11; L[4 * NPs + p] = l21; L[5 * NPs + p] = l22;
+  q[p] = q0; q[NPs + p] = q1; q[2 * NPs + p] = q2;
+}
+
+void launch_point_factor(hipStream_t s, const DevView& v, const double* V, const double* g,
+                         const double* scale_p, StepScalars sc, double* L, double* q, int* fail) {
+  if (v.NP <= 0) return;
+  k_point_factor<<<grid_for(v.NP, 256, 1 << 20), 256, 0, s>>>(v, V, g, scale_p, sc, L, q, fail);
+}
+
+__global__ __launch_bounds__(256) void k_entry_y(DevView v, const double* __restrict__ J,
+                                                 const double* __restrict__ sp,
+                                                 const double* __restrict__ scc,
+                                                 const double* __restrict__ L, double* __restrict__ Y) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= v.NE) return;
+  const int os = v.ent_os[e], s = os >> 1, slot = os & 1;
+  const int p = v.ent_pt[e], c = v.ent_cam[e];
+  const size_t Ns = (size_t)v.N, NPs = (size_t)v.NP, NEs = (size_t)v.NE;
+  const double spv[3] = {sp[p], sp[NPs + p], sp[2 * NPs + p]};
+  const double l00 = L[p], l10 = L[NPs + p], l20 = L[2 * NPs + p];
+  const double l11 = L[3 * NPs + p], l21 = L[4 * NPs + p], l22 = L[5 * NPs + p];
+  double jp0[3], jp1[3];
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    jp0[b] = J[(size_t)(2 * b) * Ns + s];
+    jp1[b] = J[(size_t)(2 * b + 1) * Ns + s];
+  }
+  const int col0 = 3 + 6 * slot;
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    const double ja = J[(size_t)(2 * (col0 + a)) * Ns + s];
+    const double jb = J[(size_t)(2 * (col0 + a) + 1) * Ns + s];
+    const double sa = scc[6 * c + a];
+    const double w0 = sa * (ja * jp0[0] + jb * jp1[0]) * spv[0];
+    const double w1 = sa * (ja * jp0[1] + jb * jp1[1]) * spv[1];
+    const double w2 = sa * (ja * jp0[2] + jb * jp1[2]) * spv[2];
+    const double y0 = w0 / l00;
+    const double y1 = (w1 - l10 * y0) / l11;
+    const double y2 = (w2 - l20 * y0 - l21 * y1) / l22;
+    Y[(size_t)(3 * a) * NEs + e] = y0;
+    Y[(size_t)(3 * a + 1) * NEs + e] = y1;
+    Y[(size_t)(3 * a + 2) * NEs + e] = y2;
+  }
+}
+
+void launch_entry_y(hipStream_t s, const DevView& v, const double* J, const double* scale_p,
+                    const double* scale_c, const double* L, double* Y) {
+  if (v.NE <= 0) return;
+  k_entry_y<<<grid_for(v.NE, 256, 1 << 20), 256, 0, s>>>(v, J, scale_p, scale_c, L, Y);
+}
+
+// one wave per S block; lane (a,b) < 36 accumulates -sum Y_row[a,:] . Y_col[b,:]
+__global__ __launch_bounds__(256) void k_s_blocks(int NE, int nblk, const int* __restrict__ blk_pair_beg,
+                                                  const int2* __restrict__ pairs,
+                                                  const double* __restrict__ Y,
+                                                  double* __restrict__ packed) {
+  const int blk = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (blk >= nblk || lane >= 36) return;
+  const int a = lane / 6, b = lane - 6 * (lane / 6);
+  const size_t NEs = (size_t)NE;
+  double acc = 0.0;
+  for (int i = blk_pair_beg[blk]; i < blk_pair_beg[blk + 1]; ++i) {
+    const int2 pr = pairs[i];
+    acc += Y[(size_t)(3 * a) * NEs + pr.x] * Y[(size_t)(3 * b) * NEs + pr.y] +
+           Y[(size_t)(3 * a + 1) * NEs + pr.x] * Y[(size_t)(3 * b + 1) * NEs + pr.y] +
+           Y[(size_t)(3 * a + 2) * NEs + pr.x] * Y[(size_t)(3 * b + 2) * NEs + pr.y];
+  }
+  packed[36 * (size_t)blk + lane] = -acc;
+}
+
+void launch_s_blocks(hipStream_t s, const DevView& v, int nblk, const int* blk_pair_beg,
+                     const int2* pairs, const double* Y, double* packed) {
+  if (nblk <= 0) return;
+  k_s_blocks<<<(nblk + 3) / 4, 256, 0, s>>>(v.NE, nblk, blk_pair_beg, pairs, Y, packed);
+}
+
+__global__ __launch_bounds__(256) void k_cam_rhs_partial(DevView v, const int* __restrict__ chunk_beg,
+                                                         const int* __restrict__ cam_ent,
+                                                         const double* __restrict__ Y,
+                                                         const double* __restrict__ q,
+                                                         double* __restrict__ partial) {
+  const int c = blockIdx.x;
+  const int b = chunk_beg[c], e = chunk_beg[c + 1];
+  const size_t NEs = (size_t)v.NE, NPs = (size_t)v.NP;
+  double acc[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
+    const int en = cam_ent[i];
+    const int p = v.ent_pt[en];
+    const double q0 = q[p], q1 = q[NPs + p], q2 = q[2 * NPs + p];
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+      acc[a] -= Y[(size_t)(3 * a) * NEs + en] * q0 + Y[(size_t)(3 * a + 1) * NEs + en] * q1 +
+                Y[(size_t)(3 * a + 2) * NEs + en] * q2;
+  }
+  block_reduce_store<6>(acc, partial + 6 * (size_t)c);
+}
+
+void launch_cam_rhs_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
+                            const int* cam_ent, const double* Y, const double* q, double* partial) {
+  if (nchunk <= 0) return;
+  k_cam_rhs_partial<<<nchunk, 256, 0, s>>>(v, chunk_beg, cam_ent, Y, q, partial);
+}
+
+// --- dense reduced camera system ------------------------------------------------------
+__global__ void k_s_scatter(int nblk, const int2* __restrict__ blk_cam, const double* __restrict__ packed,
+                            double* __restrict__ S, int lds) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nblk * 36) return;
+  const int blk = t / 36, ab = t - 36 * blk, a = ab / 6, b = ab - 6 * (ab / 6);
+  const int2 rc = blk_cam[blk];  // (row cam, col cam), row >= col
+  S[(size_t)(6 * rc.x + a) * lds + 6 * rc.y + b] = packed[t];
+}
+__global__ void k_s_diag(int NC, const double* __restrict__ ug, const double* __restrict__ scc,
+                         StepScalars sc, const double* __restrict__ ybc,
+                         double* __restrict__ S, int lds) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= NC * 36) return;
+  const int c = t / 36, ab = t - 36 * c, a = ab / 6, b = ab - 6 * (ab / 6);
+  if (b > a) return;  // lower triangle of the diagonal block
+  // upper-packed index of (b,a), b <= a
+  const int q = b * 6 - (b * (b - 1)) / 2 + (a - b);
+  const double sa = scc[6 * c + a], sb = scc[6 * c + b];
+  double u = sa * ug[27 * (size_t)c + q] * sb;
+  if (a == b) {
+    double d = fmin(fmax(u, sc.min_diag), sc.max_diag);
+    const double D = sqrt(d / sc.radius);
+    u += D * D;
+  }
+  const size_t n = (size_t)6 * NC;
+  S[(size_t)(6 * c + a) * lds + 6 * c + b] += u;
+  if (b == 0) {  // rhs row: b_c = s_c g_c - sum Y q
+    S[n * lds + 6 * c + a] = sa * ug[27 * (size_t)c + 21 + a] + ybc[6 * c + a];
+  }
+}
+__global__ void k_s_cross(int ncross, const int2* __restrict__ cross_cam, const double* __restrict__ X,
+                          const double* __restrict__ scc, double* __restrict__ S, int lds) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ncross * 36) return;
+  const int k = t / 36, ab = t - 36 * k, a = ab / 6, b = ab - 6 * (ab / 6);
+  const int2 cc = cross_cam[k];  // (c0 = arc, c1 = ring): X = Jc0^T Jc1
+  const double v = scc[6 * cc.x + a] * X[36 * (size_t)k + ab] * scc[6 * cc.y + b];
+  if (cc.x > cc.y) S[(size_t)(6 * cc.x + a) * lds + 6 * cc.y + b] += v;
+  else S[(size_t)(6 * cc.y + b) * lds + 6 * cc.x + a] += v;
+}
+
+void launch_s_unpack(hipStream_t s, int NC, int nblk, const int2* blk_cam, const double* packed,
+                     const double* ug, int ncross, const int2* cross_cam, const double* Ucross,
+                     const double* scale_c, StepScalars sc, const double* ybc, double* S, int lds) {
+  const size_t n = (size_t)6 * NC;
+  (void)hipMemsetAsync(S, 0, sizeof(double) * (n + 1) * lds, s);
+  if (nblk > 0) k_s_scatter<<<grid_for(nblk * 36, 256, 1 << 20), 256, 0, s>>>(nblk, blk_cam, packed, S, lds);
+  if (NC > 0) k_s_diag<<<grid_for(NC * 36, 256, 1 << 20), 256, 0, s>>>(NC, ug, scale_c, sc, ybc, S, lds);
+  if (ncross > 0)
+    k_s_cross<<<grid_for(ncross * 36, 256, 1 << 20), 256, 0, s>>>(ncross, cross_cam, Ucross, scale_c, S, lds);
+}
+
+__global__ __launch_bounds__(256) void k_backsub(DevView v, const double* __restrict__ L,
+                                                 const double* __restrict__ q,
+                                                 const double* __restrict__ Y,
+                                                 const double* __restrict__ yc,
+                                                 const double* __restrict__ sp,
+                                                 double* __restrict__ dp) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= v.NP) return;
+  const size_t NPs = (size_t)v.NP, NEs = (size_t)v.NE;
+  double r0 = q[p], r1 = q[NPs + p], r2 = q[2 * NPs + p];
+  if (yc) {
+    for (int e = v.pt_ent_ptr[p]; e < v.pt_ent_ptr[p + 1]; ++e) {
+      const int c = v.ent_cam[e];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        const double y = yc[6 * c + a];
+        r0 -= Y[(size_t)(3 * a) * NEs + e] * y;
+        r1 -= Y[(size_t)(3 * a + 1) * NEs + e] * y;
+        r2 -= Y[(size_t)(3 * a + 2) * NEs + e] * y;
+      }
+    }
+  }
+  const double l00 = L[p], l10 = L[NPs + p], l20 = L[2 * NPs + p];
+  const double l11 = L[3 * NPs + p], l21 = L[4 * NPs + p], l22 = L[5 * NPs + p];
+  const double y2 = r2 / l22;
+  const double y1 = (r1 - l21 * y2) / l11;
+  const double y0 = (r0 - l10 * y1 - l20 * y2) / l00;
+  // step = -y (Ceres solves J y = r then negates), delta = step * scale
+  dp[p] = -y0 * sp[p];
+  dp[NPs + p] = -y1 * sp[NPs + p];
+  dp[2 * NPs + p] = -y2 * sp[2 * NPs + p];
+}
+
+void launch_backsub(hipStream_t s, const DevView& v, const double* L, const double* q, const double* Y,
+                    const double* yc, const double* scale_p, double* delta_p) {
+  if (v.NP <= 0) return;
+  k_backsub<<<grid_for(v.NP, 256, 1 << 20), 256, 0, s>>>(v, L, q, Y, yc, scale_p, delta_p);
+}
+
+__global__ __launch_bounds__(256) void k_axpy_points(int NP, const double* __restrict__ x,
+                                                     const double* __restrict__ d,
+                                                     double* __restrict__ xc, double* __restrict__ partial) {
+  double acc[2] = {0.0, 0.0};
+  const size_t NPs = (size_t)NP;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 3 * NP; i += gridDim.x * blockDim.x) {
+    const int p = i / 3, k = i - 3 * (i / 3);
+    const double xv = x[i];
+    const double c = xv + d[k * NPs + p];
+    xc[i] = c;
+    const double dd = xv - c;
+    acc[0] += dd * dd;
+    acc[1] += c * c;
+  }
+  block_reduce_store<2>(acc, partial + 2 * (size_t)blockIdx.x);
+}
+
+void launch_axpy_points(hipStream_t s, int NP, const double* x, const double* d, double* xc,
+                        double* partial, int grid) {
+  k_axpy_points<<<grid, 256, 0, s>>>(NP, x, d, xc, partial);
+}
+
+__global__ void k_cam_candidate(int E, const int* __restrict__ ext_col, const double* __restrict__ ext,
+                                const double* __restrict__ yc, const double* __restrict__ scc,
+                                double* __restrict__ ext_c, double* __restrict__ dc) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 6 * E) return;
+  const int e = t / 6, k = t - 6 * (t / 6);
+  const int c = ext_col[e];
+  if (c >= 0 && yc) {
+    const double d = -yc[6 * c + k] * scc[6 * c + k];
+    ext_c[t] = ext[t] + d;
+    dc[6 * c + k] = d;
+  } else {
+    ext_c[t] = ext[t];
+  }
+}
+
+void launch_cam_candidate(hipStream_t s, int E, const int* ext_col, const double* ext, const double* yc,
+                          const double* scale_c, double* ext_c, double* delta_c) {
+  if (E <= 0) return;
+  k_cam_candidate<<<grid_for(6 * E, 256, 1 << 20), 256, 0, s>>>(E, ext_col, ext, yc, scale_c, ext_c, delta_c);
+}
+
+__global__ __launch_bounds__(256) void k_candidate(DevView v, const double* __restrict__ J,
+                                                   const double2* __restrict__ r,
+                                                   const double* __restrict__ dp,
+                                                   const double* __restrict__ dc,
+                                                   const double* __restrict__ points_c,
+                                                   const double* __restrict__ camtab_c,
+                                                   double* __restrict__ partial) {
+  double acc[3] = {0.0, 0.0, 0.0};
+  const size_t Ns = (size_t)v.N, NPs = (size_t)v.NP;
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < v.N; s += gridDim.x * blockDim.x) {
+    const int4 id = v.obs_idx[s];
+    double m0 = 0.0, m1 = 0.0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const double d = dp[c * NPs + id.x];
+      m0 += J[(size_t)(2 * c) * Ns + s] * d;
+      m1 += J[(size_t)(2 * c + 1) * Ns + s] * d;
+    }
+    const int c0 = v.ext_col[id.y];
+    if (c0 >= 0) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const double d = dc[6 * c0 + k];
+        m0 += J[(size_t)(2 * (3 + k)) * Ns + s] * d;
+        m1 += J[(size_t)(2 * (3 + k) + 1) * Ns + s] * d;
+      }
+    }
+    if (id.z >= 0) {
+      const int c1 = v.ext_col[id.z];
+      if (c1 >= 0) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          const double d = dc[6 * c1 + k];
+          m0 += J[(size_t)(2 * (9 + k)) * Ns + s] * d;
+          m1 += J[(size_t)(2 * (9 + k) + 1) * Ns + s] * d;
+        }
+      }
+    }
+    const double2 rr = r[s];
+    acc[0] += -(m0 * (rr.x + m0 / 2.0) + m1 * (rr.y + m1 / 2.0));
+    double ru, rv;
+    residual_at(v, points_c, camtab_c, s, ru, rv);
+    acc[1] += ru * ru + rv * rv;
+    acc[2] += (isfinite(ru) && isfinite(rv)) ? 0.0 : 1.0;
+  }
+  block_reduce_store<3>(acc, partial + 3 * (size_t)blockIdx.x);
+}
+
+void launch_candidate(hipStream_t s, const DevView& v, const double* J, const double* r,
+                      const double* delta_p, const double* delta_c, const double* points_c,
+                      const double* camtab_c, double* partial, int grid) {
+  k_candidate<<<grid, 256, 0, s>>>(v, J, reinterpret_cast<const double2*>(r), delta_p, delta_c, points_c,
+                                   camtab_c, partial);
+}
+
+__global__ __launch_bounds__(256) void k_grad_points(int NP, const double* __restrict__ x,
+                                                     const double* __restrict__ g,
+                                                     double* __restrict__ partial) {
+  double acc[3] = {0.0, 0.0, 0.0};
+  const size_t NPs = (size_t)NP;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 3 * NP; i += gridDim.x * blockDim.x) {
+    const int p = i / 3, k = i - 3 * (i / 3);
+    const double xv = x[i];
+    const double d = xv - (xv + (-g[k * NPs + p]));
+    acc[0] = fmax(acc[0], fabs(d));
+    acc[1] += d * d;
+    acc[2] += xv * xv;
+  }
+  // max needs its own reduction
+  __shared__ double shm[kRedBlock / 64];
+  double m = acc[0];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off, 64));
+  if ((threadIdx.x & 63) == 0) shm[threadIdx.x >> 6] = m;
+  acc[0] = 0.0;
+  block_reduce_store<3>(acc, partial + 3 * (size_t)blockIdx.x);
+  if (threadIdx.x == 0) {
+    double mm = shm[0];
+    for (int q = 1; q < kRedBlock / 64; ++q) mm = fmax(mm, shm[q]);
+    partial[3 * (size_t)blockIdx.x] = mm;
+  }
+}
+
+void launch_grad_points(hipStream_t s, int NP, const double* x, const double* g, double* partial,
+                        int grid) {
+  k_grad_points<<<grid, 256, 0, s>>>(NP, x, g, partial);
+}
+
+}  // namespace dab

@@ -1,0 +1,1071 @@
+// dab_solver.hip — C ABI + device-resident trust-region LM driver.
+//
+// Replaces ceres::Solve(options{DENSE_SCHUR}, &problem, &summary) as called by
+// solve() at src/sfm.cc:31-75. The minimizer mirrors Ceres' TrustRegionMinimizer +
+// LevenbergMarquardtStrategy: Jacobi scaling computed at iteration 0,
+// LM diagonal clamp [1e-6, 1e32] / radius, step quality = actual/model decrease,
+// radius /= max(1/3, 1-(2q-1)^3) on accept, /= decrease_factor (doubling) on reject,
+// parameter / function / gradient tolerance tests in Ceres' order, five consecutive
+// invalid steps => FAILURE, final_cost = min over iteration costs. The step solves
+// (Js^T Js + D^2) y = Js^T r exactly: points are eliminated per point (3x3 Cholesky)
+// and the reduced camera system is factored densely (dab_chol.hip) — DENSE_SCHUR.
+//
+// Multi-GPU: one process per GPU, observations sharded by point; the camera-side
+// normal-equation pieces (U, g_c, the reduced system S and its rhs) and the scalar
+// reductions are all-reduced with RCCL over xGMI; every rank then factors the same S
+// and back-substitutes its own points.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "dab_internal.h"
+#include "dab_kernels.h"
+
+using namespace dab;
+
+#define HIP_OK(expr)                                                                           \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      return set_error(DAB_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));      \
+  } while (0)
+#define NCCL_OK(expr)                                                                          \
+  do {                                                                                         \
+    ncclResult_t e_ = (expr);                                                                  \
+    if (e_ != ncclSuccess)                                                                     \
+      return set_error(DAB_E_COMM, std::string(#expr) + ": " + ncclGetErrorString(e_));       \
+  } while (0)
+#define CHECK_RC(expr)       \
+  do {                       \
+    int rc_ = (expr);        \
+    if (rc_ != 0) return rc_; \
+  } while (0)
+
+namespace {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// scalar slots of the per-handle scalar buffer
+enum Slot {
+  S_COST = 0,      // sum r^2 at x
+  S_COST_BAD,      // non-finite residuals at x
+  S_GMAX_P,        // max |x-(x-g)| over points
+  S_GNORM_P,       // sum (x-(x-g))^2 over points
+  S_XNORM_P,       // sum x^2 over points
+  S_MODEL,         // model cost change
+  S_CAND,          // sum r^2 at candidate
+  S_CAND_BAD,      // non-finite residuals at candidate
+  S_STEP_P,        // sum (x - xc)^2 over points
+  S_XCNORM_P,      // sum xc^2 over points
+  S_CAM0,          // 5 camera slots (launch_cam_norms)
+  S_END = S_CAM0 + 5,
+  S_NSLOTS = 16
+};
+
+struct Dev {
+  std::vector<void*> allocs;
+  ~Dev() { release(); }
+  void release() {
+    for (void* p : allocs) (void)hipFree(p);
+    allocs.clear();
+  }
+  template <class T>
+  int alloc(T** out, size_t n) {
+    void* p = nullptr;
+    if (n == 0) n = 1;
+    if (hipMalloc(&p, n * sizeof(T)) != hipSuccess)
+      return set_error(DAB_E_NOMEM, "hipMalloc of " + std::to_string(n * sizeof(T)) + " bytes failed");
+    allocs.push_back(p);
+    *out = static_cast<T*>(p);
+    return 0;
+  }
+};
+
+template <class T>
+int upload(T** dptr, Dev& dev, const std::vector<T>& h, hipStream_t s) {
+  CHECK_RC(dev.alloc(dptr, h.size()));
+  if (!h.empty()) HIP_OK(hipMemcpyAsync(*dptr, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s));
+  return 0;
+}
+
+}  // namespace
+
+struct dab_handle {
+  int device = 0;
+  int rank = 0, world = 1;
+  hipStream_t stream = nullptr;
+  ncclComm_t comm = nullptr;
+  CholCtx* chol = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  // bench bookkeeping
+  double bench_jac_ms = 0, bench_asm_ms = 0;
+  int bench_count = 0;
+
+  // ---- host-side problem structure ----
+  bool have_problem = false;
+  dab_problem prob{};               // caller's arrays (pointers valid until next set_problem)
+  int N = 0, NP = 0, E = 0, NI = 0, NC = 0, NE = 0, nplanes = 18;
+  bool any_compose = false;
+  std::vector<int> perm;            // sorted obs -> caller's obs index
+  std::vector<int> pt_of;           // local point -> caller's point id
+  std::vector<int> ext_col;         // ext -> free camera column
+  int nchunk = 0, nxchunk = 0, ncross = 0, nblk = 0;
+  long long npairs = 0;
+  int lds = 0;                      // leading dim of dense S
+
+  // ---- device buffers ----
+  Dev dev;
+  DevView view{};
+  int4* d_obs_idx = nullptr;
+  double2* d_obs_xy = nullptr;
+  int *d_pt_obs_ptr = nullptr, *d_pt_ent_ptr = nullptr, *d_ent_os = nullptr, *d_ent_cam = nullptr,
+      *d_ent_pt = nullptr, *d_ext_col = nullptr;
+  int *d_cam_ent = nullptr, *d_chunk_beg = nullptr, *d_seg_chunk = nullptr;
+  int *d_xobs = nullptr, *d_xchunk_beg = nullptr, *d_xseg_chunk = nullptr;
+  int2* d_cross_cam = nullptr;
+  int2 *d_pairs = nullptr, *d_blk_cam = nullptr;
+  int* d_blk_pair_beg = nullptr;
+  double* d_intr = nullptr;
+  double *d_points = nullptr, *d_points_c = nullptr, *d_ext = nullptr, *d_ext_c = nullptr;
+  double *d_camtab = nullptr, *d_camtab_c = nullptr;
+  double *d_r = nullptr, *d_J = nullptr;
+  double *d_V = nullptr, *d_g = nullptr, *d_scale_p = nullptr, *d_scale_c = nullptr;
+  double *d_L = nullptr, *d_q = nullptr, *d_Y = nullptr;
+  double* d_camred = nullptr;  // [Ucc NC*21 | gc NC*6 | Ux ncross*36] (all-reduced)
+  double* d_partial = nullptr; // chunk partials (max of chunk counts * 36)
+  double* d_spack = nullptr;   // [packed nblk*36 | ybc NC*6] (all-reduced)
+  double* d_S = nullptr;
+  double *d_yc = nullptr, *d_dp = nullptr, *d_dc = nullptr;
+  double* d_gpart = nullptr;   // grid partials
+  double* d_scal = nullptr;    // S_NSLOTS
+  int* d_flags = nullptr;      // [0] point factor fail, [1] chol fail
+  double* h_scal = nullptr;    // pinned
+  int* h_flags = nullptr;      // pinned
+  int red_grid = 1;
+
+  ~dab_handle() {
+    dev.release();
+    if (h_scal) (void)hipHostFree(h_scal);
+    if (h_flags) (void)hipHostFree(h_flags);
+    if (chol) chol_destroy(chol);
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (ev2) (void)hipEventDestroy(ev2);
+    if (comm) ncclCommDestroy(comm);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  double* ug() { return d_camred; }  // [NC][27]: U upper-packed (21) | g_c (6)
+  double* Ux() { return d_camred + (size_t)27 * NC; }
+  size_t camred_count() const { return (size_t)27 * NC + (size_t)36 * ncross; }
+  double* packed() { return d_spack; }
+  double* ybc() { return d_spack + (size_t)36 * nblk; }
+  size_t spack_count() const { return (size_t)36 * nblk + (size_t)6 * NC; }
+
+  int allreduce(double* buf, size_t n, ncclRedOp_t op) {
+    if (world <= 1 || n == 0) return 0;
+    NCCL_OK(ncclAllReduce(buf, buf, n, ncclDouble, op, comm, stream));
+    return 0;
+  }
+};
+
+// ------------------------------------------------------------------------------------
+// lifecycle
+// ------------------------------------------------------------------------------------
+static int create_common(int device, dab_handle** out) {
+  if (!out) return set_error(DAB_E_INVALID, "null handle pointer");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return set_error(DAB_E_DEVICE, "no HIP device available");
+  if (device < 0 || device >= ndev) return set_error(DAB_E_INVALID, "device ordinal out of range");
+  HIP_OK(hipSetDevice(device));
+  dab_handle* h = new dab_handle();
+  h->device = device;
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return set_error(DAB_E_DEVICE, "hipStreamCreate failed");
+  }
+  h->chol = chol_create();
+  if (!h->chol) {
+    delete h;
+    return set_error(DAB_E_DEVICE, "rocblas handle creation failed");
+  }
+  if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
+      hipEventCreate(&h->ev2) != hipSuccess) {
+    delete h;
+    return set_error(DAB_E_DEVICE, "hipEventCreate failed");
+  }
+  if (hipHostMalloc(reinterpret_cast<void**>(&h->h_scal), sizeof(double) * S_NSLOTS) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&h->h_flags), sizeof(int) * 4) != hipSuccess) {
+    delete h;
+    return set_error(DAB_E_NOMEM, "hipHostMalloc failed");
+  }
+  *out = h;
+  return 0;
+}
+
+extern "C" int dab_create(int device, dab_handle** out) {
+  clear_error();
+  return create_common(device, out);
+}
+
+extern "C" int dab_comm_unique_id(uint8_t out_id[128]) {
+  clear_error();
+  if (!out_id) return set_error(DAB_E_INVALID, "null id buffer");
+  ncclUniqueId id;
+  NCCL_OK(ncclGetUniqueId(&id));
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  std::memcpy(out_id, &id, 128);
+  return 0;
+}
+
+extern "C" int dab_create_dist(int device, int rank, int world_size, const uint8_t unique_id[128],
+                               dab_handle** out) {
+  clear_error();
+  if (world_size < 1 || rank < 0 || rank >= world_size) return set_error(DAB_E_INVALID, "bad rank/world");
+  if (world_size > 1 && !unique_id) return set_error(DAB_E_INVALID, "null unique id");
+  CHECK_RC(create_common(device, out));
+  dab_handle* h = *out;
+  h->rank = rank;
+  h->world = world_size;
+  if (world_size > 1) {
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, 128);
+    ncclResult_t r = ncclCommInitRank(&h->comm, world_size, id, rank);
+    if (r != ncclSuccess) {
+      std::string msg = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+      delete h;
+      *out = nullptr;
+      return set_error(DAB_E_COMM, msg);
+    }
+  }
+  return 0;
+}
+
+extern "C" int dab_destroy(dab_handle* h) {
+  clear_error();
+  if (!h) return 0;
+  (void)hipSetDevice(h->device);
+  (void)hipStreamSynchronize(h->stream);
+  delete h;
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------
+// problem setup: orderings and reduction tables (built once)
+// ------------------------------------------------------------------------------------
+static int validate(const dab_problem* p) {
+  if (!p) return set_error(DAB_E_INVALID, "null problem");
+  if (p->num_obs < 0 || p->num_points < 0 || p->num_ext < 0 || p->num_intr < 0)
+    return set_error(DAB_E_INVALID, "negative size");
+  if (p->num_obs > 0 && (!p->obs_xy || !p->obs_point || !p->obs_ext0 || !p->obs_ext1 || !p->obs_intr))
+    return set_error(DAB_E_INVALID, "null observation array");
+  if ((p->num_points > 0 && !p->points) || (p->num_ext > 0 && !p->ext) ||
+      (p->num_intr > 0 && (!p->intr || !p->intr_nf || !p->intr_nk)))
+    return set_error(DAB_E_INVALID, "null parameter array");
+  for (int i = 0; i < p->num_intr; ++i) {
+    if (p->intr_nf[i] < 1 || p->intr_nf[i] > 2) return set_error(DAB_E_INVALID, "intr_nf must be 1 or 2");
+    if (p->intr_nk[i] < 0 || p->intr_nk[i] > 2) return set_error(DAB_E_INVALID, "intr_nk must be 0, 1 or 2");
+  }
+  for (int o = 0; o < p->num_obs; ++o) {
+    const int pt = p->obs_point[o], e0 = p->obs_ext0[o], e1 = p->obs_ext1[o], ii = p->obs_intr[o];
+    if (pt < 0 || pt >= p->num_points || e0 < 0 || e0 >= p->num_ext || e1 < -1 || e1 >= p->num_ext ||
+        ii < 0 || ii >= p->num_intr)
+      return set_error(DAB_E_INVALID, "observation " + std::to_string(o) + " has an out-of-range index");
+  }
+  return 0;
+}
+
+extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
+  clear_error();
+  if (!h) return set_error(DAB_E_INVALID, "null handle");
+  CHECK_RC(validate(p));
+  HIP_OK(hipSetDevice(h->device));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  h->dev.release();
+  h->have_problem = false;
+  h->prob = *p;
+  const int N = p->num_obs;
+  h->N = N;
+  h->E = p->num_ext;
+  h->NI = p->num_intr;
+  hipStream_t s = h->stream;
+
+  // referenced points (local compact ids, in id order) and extrinsics
+  std::vector<int> pt_local(p->num_points, -1);
+  std::vector<char> pref(p->num_points, 0);
+  std::vector<double> eref(std::max(1, p->num_ext), 0.0);
+  h->any_compose = false;
+  for (int o = 0; o < N; ++o) {
+    pref[p->obs_point[o]] = 1;
+    eref[p->obs_ext0[o]] = 1.0;
+    if (p->obs_ext1[o] >= 0) {
+      eref[p->obs_ext1[o]] = 1.0;
+      h->any_compose = true;
+    }
+  }
+  h->pt_of.clear();
+  for (int i = 0; i < p->num_points; ++i)
+    if (pref[i]) {
+      pt_local[i] = (int)h->pt_of.size();
+      h->pt_of.push_back(i);
+    }
+  h->NP = (int)h->pt_of.size();
+  // the free camera set must agree on every rank
+  if (h->world > 1) {
+    double* d_tmp = nullptr;
+    CHECK_RC(h->dev.alloc(&d_tmp, eref.size() + 1));
+    eref.push_back(h->any_compose ? 1.0 : 0.0);
+    HIP_OK(hipMemcpyAsync(d_tmp, eref.data(), eref.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    CHECK_RC(h->allreduce(d_tmp, eref.size(), ncclMax));
+    HIP_OK(hipMemcpyAsync(eref.data(), d_tmp, eref.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    h->any_compose = eref.back() != 0.0;
+    eref.pop_back();
+  }
+  h->ext_col.assign(p->num_ext, -1);
+  h->NC = 0;
+  for (int e = 0; e < p->num_ext; ++e) {
+    const bool is_const = p->freeze_camera || (p->ext_const && p->ext_const[e]);
+    if (eref[e] != 0.0 && !is_const) h->ext_col[e] = h->NC++;
+  }
+  const int NP = h->NP, NC = h->NC;
+  h->nplanes = h->any_compose ? 30 : 18;
+
+  // point-major observation order (stable)
+  std::vector<int> cnt(NP + 1, 0);
+  for (int o = 0; o < N; ++o) cnt[pt_local[p->obs_point[o]] + 1]++;
+  for (int i = 0; i < NP; ++i) cnt[i + 1] += cnt[i];
+  std::vector<int> pt_obs_ptr = cnt;
+  h->perm.assign(N, 0);
+  {
+    std::vector<int> fill(cnt.begin(), cnt.end() - 1);
+    for (int o = 0; o < N; ++o) h->perm[fill[pt_local[p->obs_point[o]]]++] = o;
+  }
+  std::vector<int4> obs_idx(N);
+  std::vector<double2> obs_xy(N);
+  for (int s2 = 0; s2 < N; ++s2) {
+    const int o = h->perm[s2];
+    obs_idx[s2] = make_int4(pt_local[p->obs_point[o]], p->obs_ext0[o], p->obs_ext1[o], p->obs_intr[o]);
+    obs_xy[s2] = make_double2(p->obs_xy[2 * (size_t)o], p->obs_xy[2 * (size_t)o + 1]);
+  }
+  // entries (observation slots on free cameras), point-major
+  std::vector<int> ent_os, ent_cam, ent_pt, pt_ent_ptr(NP + 1, 0);
+  ent_os.reserve((size_t)N * (h->any_compose ? 2 : 1));
+  for (int pt = 0; pt < NP; ++pt) {
+    pt_ent_ptr[pt] = (int)ent_os.size();
+    for (int s2 = pt_obs_ptr[pt]; s2 < pt_obs_ptr[pt + 1]; ++s2) {
+      for (int slot = 0; slot < 2; ++slot) {
+        const int e = slot ? obs_idx[s2].z : obs_idx[s2].y;
+        if (e < 0 || h->ext_col[e] < 0) continue;
+        ent_os.push_back(2 * s2 + slot);
+        ent_cam.push_back(h->ext_col[e]);
+        ent_pt.push_back(pt);
+      }
+    }
+  }
+  pt_ent_ptr[NP] = (int)ent_os.size();
+  h->NE = (int)ent_os.size();
+  const int NE = h->NE;
+
+  // camera-major entry lists, chunked (deterministic two-level reductions)
+  std::vector<int> cam_ent(NE), cam_cnt(NC + 1, 0);
+  for (int e = 0; e < NE; ++e) cam_cnt[ent_cam[e] + 1]++;
+  for (int c = 0; c < NC; ++c) cam_cnt[c + 1] += cam_cnt[c];
+  {
+    std::vector<int> fill(cam_cnt.begin(), cam_cnt.end() - 1);
+    for (int e = 0; e < NE; ++e) cam_ent[fill[ent_cam[e]]++] = e;
+  }
+  std::vector<int> chunk_beg, seg_chunk(NC + 1, 0);
+  for (int c = 0; c < NC; ++c) {
+    seg_chunk[c] = (int)chunk_beg.size();
+    for (int b = cam_cnt[c]; b < cam_cnt[c + 1]; b += kChunk) chunk_beg.push_back(b);
+  }
+  seg_chunk[NC] = (int)chunk_beg.size();
+  h->nchunk = (int)chunk_beg.size();
+  chunk_beg.push_back(NE);
+
+  // arc∘ring cross blocks: composed observations whose two cameras are both free.
+  // The pair table is the union over ranks so the all-reduced layout matches.
+  std::vector<long long> xkeys;
+  for (int s2 = 0; s2 < N; ++s2) {
+    const int e0 = obs_idx[s2].y, e1 = obs_idx[s2].z;
+    if (e1 < 0) continue;
+    const int c0 = h->ext_col[e0], c1 = e1 >= 0 ? h->ext_col[e1] : -1;
+    if (c0 < 0 || c1 < 0) continue;
+    xkeys.push_back(((long long)c0 * NC + c1) * (long long)N + s2);
+  }
+  std::sort(xkeys.begin(), xkeys.end());
+  std::vector<long long> pairkeys;  // unique (c0*NC+c1)
+  for (long long k : xkeys) {
+    const long long pk = k / N;
+    if (pairkeys.empty() || pairkeys.back() != pk) pairkeys.push_back(pk);
+  }
+  if (h->world > 1 && h->any_compose && NC > 0) {
+    // union of pair keys via an NC x NC bitmap all-reduce(max)
+    std::vector<double> bm((size_t)NC * NC, 0.0);
+    for (long long pk : pairkeys) bm[(size_t)pk] = 1.0;
+    double* d_bm = nullptr;
+    CHECK_RC(h->dev.alloc(&d_bm, bm.size()));
+    HIP_OK(hipMemcpyAsync(d_bm, bm.data(), bm.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    CHECK_RC(h->allreduce(d_bm, bm.size(), ncclMax));
+    HIP_OK(hipMemcpyAsync(bm.data(), d_bm, bm.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    pairkeys.clear();
+    for (size_t i = 0; i < bm.size(); ++i)
+      if (bm[i] != 0.0) pairkeys.push_back((long long)i);
+  }
+  h->ncross = (int)pairkeys.size();
+  std::vector<int2> cross_cam(h->ncross);
+  for (int k = 0; k < h->ncross; ++k) cross_cam[k] = make_int2((int)(pairkeys[k] / NC), (int)(pairkeys[k] % NC));
+  std::vector<int> xobs(xkeys.size()), xchunk_beg, xseg_chunk(h->ncross + 1, 0);
+  {
+    size_t i = 0;
+    for (int k = 0; k < h->ncross; ++k) {
+      xseg_chunk[k] = (int)xchunk_beg.size();
+      const size_t b = i;
+      while (i < xkeys.size() && xkeys[i] / N == pairkeys[k]) {
+        xobs[i] = (int)(xkeys[i] % N);
+        ++i;
+      }
+      for (size_t q = b; q < i; q += kChunk) xchunk_beg.push_back((int)q);
+    }
+    xseg_chunk[h->ncross] = (int)xchunk_beg.size();
+    h->nxchunk = (int)xchunk_beg.size();
+    xchunk_beg.push_back((int)xkeys.size());
+  }
+
+  // reduced-camera-system blocks: ordered entry pairs (e, f) of one point with
+  // cam(e) >= cam(f); block (cam(e), cam(f)) of the lower triangle of S.
+  std::vector<long long> blkkeys;
+  std::vector<int2> pairs;
+  std::vector<int> blk_pair_beg;
+  if (NC > 0) {
+    struct PK { long long key; int e, f; };
+    std::vector<PK> tmp;
+    long long total = 0;
+    for (int pt = 0; pt < NP; ++pt) {
+      const long long m = pt_ent_ptr[pt + 1] - pt_ent_ptr[pt];
+      total += m * (m + 1) / 2 + m;  // upper bound
+    }
+    tmp.reserve((size_t)total);
+    for (int pt = 0; pt < NP; ++pt)
+      for (int e = pt_ent_ptr[pt]; e < pt_ent_ptr[pt + 1]; ++e)
+        for (int f = pt_ent_ptr[pt]; f < pt_ent_ptr[pt + 1]; ++f) {
+          const int ce = ent_cam[e], cf = ent_cam[f];
+          if (ce < cf) continue;
+          tmp.push_back({(long long)ce * NC + cf, e, f});
+        }
+    std::sort(tmp.begin(), tmp.end(), [](const PK& a, const PK& b) {
+      if (a.key != b.key) return a.key < b.key;
+      if (a.e != b.e) return a.e < b.e;
+      return a.f < b.f;
+    });
+    pairs.resize(tmp.size());
+    std::vector<long long> local_keys;
+    for (size_t i = 0; i < tmp.size(); ++i) {
+      pairs[i] = make_int2(tmp[i].e, tmp[i].f);
+      if (local_keys.empty() || local_keys.back() != tmp[i].key) local_keys.push_back(tmp[i].key);
+    }
+    // diagonal blocks always exist; union across ranks
+    std::vector<long long> keys = local_keys;
+    for (int c = 0; c < NC; ++c) keys.push_back((long long)c * NC + c);
+    if (h->world > 1) {
+      std::vector<double> bm((size_t)NC * NC, 0.0);
+      for (long long k : keys) bm[(size_t)k] = 1.0;
+      double* d_bm = nullptr;
+      CHECK_RC(h->dev.alloc(&d_bm, bm.size()));
+      HIP_OK(hipMemcpyAsync(d_bm, bm.data(), bm.size() * sizeof(double), hipMemcpyHostToDevice, s));
+      CHECK_RC(h->allreduce(d_bm, bm.size(), ncclMax));
+      HIP_OK(hipMemcpyAsync(bm.data(), d_bm, bm.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+      HIP_OK(hipStreamSynchronize(s));
+      keys.clear();
+      for (size_t i = 0; i < bm.size(); ++i)
+        if (bm[i] != 0.0) keys.push_back((long long)i);
+    } else {
+      std::sort(keys.begin(), keys.end());
+      keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    }
+    blkkeys = keys;
+    blk_pair_beg.assign(blkkeys.size() + 1, 0);
+    size_t i = 0;
+    for (size_t b = 0; b < blkkeys.size(); ++b) {
+      blk_pair_beg[b] = (int)i;
+      while (i < tmp.size() && tmp[i].key == blkkeys[b]) ++i;
+    }
+    blk_pair_beg[blkkeys.size()] = (int)i;
+  } else {
+    blk_pair_beg.assign(1, 0);
+  }
+  h->nblk = (int)blkkeys.size();
+  h->npairs = (long long)pairs.size();
+  std::vector<int2> blk_cam(h->nblk);
+  for (int b = 0; b < h->nblk; ++b) blk_cam[b] = make_int2((int)(blkkeys[b] / NC), (int)(blkkeys[b] % NC));
+
+  // intrinsics: (cx, cy, fx, fy', k0, k1) with unused distortion terms zeroed
+  std::vector<double> intr((size_t)kIntr * std::max(1, h->NI), 0.0);
+  for (int i = 0; i < h->NI; ++i) {
+    const double* K = p->intr + 6 * (size_t)i;
+    double* o = &intr[(size_t)kIntr * i];
+    o[0] = K[0];
+    o[1] = K[1];
+    o[2] = K[2];
+    o[3] = p->intr_nf[i] == 2 ? K[3] : K[2];
+    o[4] = p->intr_nk[i] >= 1 ? K[4] : 0.0;
+    o[5] = p->intr_nk[i] >= 2 ? K[5] : 0.0;
+  }
+  std::vector<double> points((size_t)3 * NP);
+  for (int i = 0; i < NP; ++i)
+    for (int k = 0; k < 3; ++k) points[3 * (size_t)i + k] = p->points[3 * (size_t)h->pt_of[i] + k];
+  std::vector<double> ext(p->ext, p->ext + 6 * (size_t)h->E);
+
+  // ---- upload ----
+  Dev& d = h->dev;
+  CHECK_RC(upload(&h->d_obs_idx, d, obs_idx, s));
+  CHECK_RC(upload(&h->d_obs_xy, d, obs_xy, s));
+  CHECK_RC(upload(&h->d_pt_obs_ptr, d, pt_obs_ptr, s));
+  CHECK_RC(upload(&h->d_pt_ent_ptr, d, pt_ent_ptr, s));
+  CHECK_RC(upload(&h->d_ent_os, d, ent_os, s));
+  CHECK_RC(upload(&h->d_ent_cam, d, ent_cam, s));
+  CHECK_RC(upload(&h->d_ent_pt, d, ent_pt, s));
+  CHECK_RC(upload(&h->d_ext_col, d, h->ext_col, s));
+  CHECK_RC(upload(&h->d_cam_ent, d, cam_ent, s));
+  CHECK_RC(upload(&h->d_chunk_beg, d, chunk_beg, s));
+  CHECK_RC(upload(&h->d_seg_chunk, d, seg_chunk, s));
+  CHECK_RC(upload(&h->d_xobs, d, xobs, s));
+  CHECK_RC(upload(&h->d_xchunk_beg, d, xchunk_beg, s));
+  CHECK_RC(upload(&h->d_xseg_chunk, d, xseg_chunk, s));
+  CHECK_RC(upload(&h->d_cross_cam, d, cross_cam, s));
+  CHECK_RC(upload(&h->d_pairs, d, pairs, s));
+  CHECK_RC(upload(&h->d_blk_cam, d, blk_cam, s));
+  CHECK_RC(upload(&h->d_blk_pair_beg, d, blk_pair_beg, s));
+  CHECK_RC(upload(&h->d_intr, d, intr, s));
+  CHECK_RC(upload(&h->d_points, d, points, s));
+  CHECK_RC(upload(&h->d_ext, d, ext, s));
+  CHECK_RC(d.alloc(&h->d_points_c, (size_t)3 * NP));
+  CHECK_RC(d.alloc(&h->d_ext_c, (size_t)6 * h->E));
+  CHECK_RC(d.alloc(&h->d_camtab, (size_t)kCamTab * h->E));
+  CHECK_RC(d.alloc(&h->d_camtab_c, (size_t)kCamTab * h->E));
+  CHECK_RC(d.alloc(&h->d_r, (size_t)2 * N));
+  CHECK_RC(d.alloc(&h->d_J, (size_t)h->nplanes * N));
+  CHECK_RC(d.alloc(&h->d_V, (size_t)6 * NP));
+  CHECK_RC(d.alloc(&h->d_g, (size_t)3 * NP));
+  CHECK_RC(d.alloc(&h->d_scale_p, (size_t)3 * NP));
+  CHECK_RC(d.alloc(&h->d_scale_c, (size_t)6 * NC));
+  CHECK_RC(d.alloc(&h->d_L, (size_t)6 * NP));
+  CHECK_RC(d.alloc(&h->d_q, (size_t)3 * NP));
+  CHECK_RC(d.alloc(&h->d_Y, (size_t)18 * NE));
+  CHECK_RC(d.alloc(&h->d_camred, h->camred_count()));
+  const size_t npart = std::max<size_t>({(size_t)h->nchunk * 27, (size_t)h->nxchunk * 36, (size_t)h->nchunk * 6, 16});
+  CHECK_RC(d.alloc(&h->d_partial, npart));
+  CHECK_RC(d.alloc(&h->d_spack, h->spack_count()));
+  const int n = 6 * NC;
+  h->lds = ((n + 1 + 7) / 8) * 8;
+  if (h->lds % 512 == 0) h->lds += 8;  // avoid power-of-two row strides
+  CHECK_RC(d.alloc(&h->d_S, NC > 0 ? (size_t)(n + 1) * h->lds : 1));
+  CHECK_RC(d.alloc(&h->d_yc, (size_t)6 * NC));
+  CHECK_RC(d.alloc(&h->d_dp, (size_t)3 * NP));
+  CHECK_RC(d.alloc(&h->d_dc, (size_t)6 * NC));
+  h->red_grid = grid_for(std::max(N, 3 * NP), 256, 1024);
+  CHECK_RC(d.alloc(&h->d_gpart, (size_t)h->red_grid * 4));
+  CHECK_RC(d.alloc(&h->d_scal, S_NSLOTS));
+  CHECK_RC(d.alloc(&h->d_flags, 4));
+  HIP_OK(hipMemsetAsync(h->d_dc, 0, sizeof(double) * std::max(1, 6 * NC), s));
+  HIP_OK(hipStreamSynchronize(s));
+
+  DevView& v = h->view;
+  v.N = N;
+  v.NP = NP;
+  v.E = h->E;
+  v.NC = NC;
+  v.NE = NE;
+  v.nplanes = h->nplanes;
+  v.obs_idx = h->d_obs_idx;
+  v.obs_xy = h->d_obs_xy;
+  v.pt_obs_ptr = h->d_pt_obs_ptr;
+  v.pt_ent_ptr = h->d_pt_ent_ptr;
+  v.ent_os = h->d_ent_os;
+  v.ent_cam = h->d_ent_cam;
+  v.ent_pt = h->d_ent_pt;
+  v.ext_col = h->d_ext_col;
+  v.intr = h->d_intr;
+  h->have_problem = true;
+  return 0;
+}
+
+extern "C" int dab_update_parameters(dab_handle* h, const double* points, const double* ext) {
+  clear_error();
+  if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
+  HIP_OK(hipSetDevice(h->device));
+  if (points) {
+    std::vector<double> pts((size_t)3 * h->NP);
+    for (int i = 0; i < h->NP; ++i)
+      for (int k = 0; k < 3; ++k) pts[3 * (size_t)i + k] = points[3 * (size_t)h->pt_of[i] + k];
+    HIP_OK(hipMemcpyAsync(h->d_points, pts.data(), pts.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+  }
+  if (ext) {
+    HIP_OK(hipMemcpyAsync(h->d_ext, ext, sizeof(double) * 6 * (size_t)h->E, hipMemcpyHostToDevice, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+  }
+  return 0;
+}
+
+extern "C" int dab_get_parameters(dab_handle* h, double* points, double* ext) {
+  clear_error();
+  if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
+  HIP_OK(hipSetDevice(h->device));
+  if (points) {
+    std::vector<double> pts((size_t)3 * h->NP);
+    HIP_OK(hipMemcpyAsync(pts.data(), h->d_points, pts.size() * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    for (int i = 0; i < h->NP; ++i)
+      for (int k = 0; k < 3; ++k) points[3 * (size_t)h->pt_of[i] + k] = pts[3 * (size_t)i + k];
+  }
+  if (ext) {
+    HIP_OK(hipMemcpyAsync(ext, h->d_ext, sizeof(double) * 6 * (size_t)h->E, hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------
+// evaluation building blocks
+// ------------------------------------------------------------------------------------
+// Residual + Jacobian at the current x and the J^T J / J^T r blocks (camera side
+// all-reduced). Leaves cost / gradient scalars in d_scal (point parts all-reduced).
+static int eval_jacobian_and_blocks(dab_handle* h, bool with_norms) {
+  hipStream_t s = h->stream;
+  const DevView& v = h->view;
+  launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
+  launch_jacobian(s, v, h->d_points, h->d_camtab, h->d_r, h->d_J);
+  launch_point_vg(s, v, h->d_r, h->d_J, h->d_V, h->d_g);
+  if (h->NC > 0) {
+    launch_cam_ug_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_cam_ent, h->d_r, h->d_J, h->d_partial);
+    launch_seg_final(s, h->NC, 27, h->d_seg_chunk, h->d_partial, h->ug());
+    if (h->ncross > 0) {
+      if (h->nxchunk > 0) {
+        launch_cross_partial(s, v, h->nxchunk, h->d_xchunk_beg, h->d_xobs, h->d_J, h->d_partial);
+        launch_seg_final(s, h->ncross, 36, h->d_xseg_chunk, h->d_partial, h->Ux());
+      } else {
+        HIP_OK(hipMemsetAsync(h->Ux(), 0, sizeof(double) * 36 * (size_t)h->ncross, s));
+      }
+    }
+    CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
+  }
+  launch_r_sumsq(s, h->N, h->d_r, h->d_gpart, h->red_grid);
+  launch_final_sum(s, h->red_grid, 2, h->d_gpart, h->d_scal + S_COST);
+  if (with_norms) {
+    launch_grad_points(s, h->NP, h->d_points, h->d_g, h->d_gpart, h->red_grid);
+    launch_final_sum(s, h->red_grid, 3, h->d_gpart, h->d_scal + S_GMAX_P, 1u);
+    launch_cam_norms(s, h->E, h->d_ext_col, h->d_ext, nullptr, h->NC > 0 ? h->ug() : nullptr,
+                     h->d_scal + S_CAM0);
+  }
+  // cross-rank: sums of cost, bad, gnorm, xnorm; max of gmax
+  CHECK_RC(h->allreduce(h->d_scal + S_COST, 2, ncclSum));
+  if (with_norms) {
+    CHECK_RC(h->allreduce(h->d_scal + S_GMAX_P, 1, ncclMax));
+    CHECK_RC(h->allreduce(h->d_scal + S_GNORM_P, 2, ncclSum));
+  }
+  return 0;
+}
+
+static int read_scalars(dab_handle* h) {
+  HIP_OK(hipMemcpyAsync(h->h_scal, h->d_scal, sizeof(double) * S_NSLOTS, hipMemcpyDeviceToHost, h->stream));
+  HIP_OK(hipMemcpyAsync(h->h_flags, h->d_flags, sizeof(int) * 4, hipMemcpyDeviceToHost, h->stream));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+// Jacobi scaling s = 1/(1+sqrt(diag(J^T J))), computed once at iteration 0.
+__global__ void k_scale_points(int NP, const double* __restrict__ V, double* __restrict__ sp, int on) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 3 * NP) return;
+  const int k = i / NP, p = i - k * NP;
+  const int vi = k == 0 ? 0 : (k == 1 ? 3 : 5);
+  sp[i] = on ? 1.0 / (1.0 + sqrt(V[(size_t)vi * NP + p])) : 1.0;
+}
+__global__ void k_scale_cams(int NC, const double* __restrict__ ug, double* __restrict__ sc, int on) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 6 * NC) return;
+  const int c = i / 6, a = i - 6 * c;
+  const int q = a * 6 - (a * (a - 1)) / 2;  // (a,a) in the packed upper layout
+  sc[i] = on ? 1.0 / (1.0 + sqrt(ug[27 * (size_t)c + q])) : 1.0;
+}
+
+static void print_header() {
+  std::printf("iter      cost      cost_change  |gradient|   |step|    tr_ratio  tr_radius  ls_iter  iter_time  total_time\n");
+}
+static void print_iter(const dab_iteration& it, double total) {
+  std::printf("%4d % 3.6e % 3.2e % 3.2e % 3.2e % 3.2e % 3.2e %4d % 3.2e % 3.2e\n", it.iteration, it.cost,
+              it.cost_change, it.gradient_max_norm, it.step_norm, it.relative_decrease, it.trust_region_radius,
+              it.linear_solver_iterations, it.iteration_time_in_seconds, total);
+  std::fflush(stdout);
+}
+
+// ------------------------------------------------------------------------------------
+// dab_solve: the trust-region LM loop
+// ------------------------------------------------------------------------------------
+extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* sum) {
+  clear_error();
+  if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
+  if (!sum) return set_error(DAB_E_INVALID, "null summary");
+  dab_options opt;
+  if (opt_in) opt = *opt_in;
+  else dab_options_init(&opt);
+  if (opt.linear_solver_type != DAB_LINEAR_SOLVER_EXPLICIT_SCHUR)
+    return set_error(DAB_E_UNSUPPORTED, "only DAB_LINEAR_SOLVER_EXPLICIT_SCHUR is available in this build");
+  HIP_OK(hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  const DevView& v = h->view;
+  const int NP = h->NP, NC = h->NC, n = 6 * NC;
+  const double t_start = now_s();
+  std::memset(sum->message, 0, sizeof(sum->message));
+  sum->iterations_written = 0;
+  sum->num_successful_steps = sum->num_unsuccessful_steps = 0;
+  sum->num_iterations = 0;
+  sum->num_residuals = 2 * h->N;
+  sum->num_parameters = 3 * NP + 6 * NC;
+  sum->num_free_points = NP;
+  sum->num_free_ext = NC;
+  sum->jacobian_evaluation_time_in_seconds = 0;
+  sum->residual_evaluation_time_in_seconds = 0;
+  sum->linear_solver_time_in_seconds = 0;
+  sum->termination_type = DAB_FAILURE;
+  const bool verbose = opt.minimizer_progress_to_stdout && h->rank == 0;
+  const bool in_global = true;  (void)in_global;
+
+  // ---- iteration 0 ----
+  double t0 = now_s();
+  CHECK_RC(eval_jacobian_and_blocks(h, true));
+  CHECK_RC(read_scalars(h));
+  {
+    const int g3 = grid_for(3 * NP, 256, 1 << 20);
+    k_scale_points<<<g3, 256, 0, s>>>(NP, h->d_V, h->d_scale_p, opt.jacobi_scaling);
+    if (NC > 0) k_scale_cams<<<grid_for(6 * NC, 256, 1 << 20), 256, 0, s>>>(NC, h->ug(), h->d_scale_c, opt.jacobi_scaling);
+  }
+  sum->jacobian_evaluation_time_in_seconds += now_s() - t0;
+  double x_cost = 0.5 * h->h_scal[S_COST];
+  bool eval_ok = h->h_scal[S_COST_BAD] == 0.0;
+  double gmax = std::max(h->h_scal[S_GMAX_P], h->h_scal[S_CAM0 + 2]);
+  double x_norm = std::sqrt(h->h_scal[S_XNORM_P] + h->h_scal[S_CAM0 + 4]);
+  sum->initial_cost = x_cost;
+  double final_cost = x_cost;
+  if (!eval_ok) {
+    std::snprintf(sum->message, sizeof(sum->message), "Residual and Jacobian evaluation failed.");
+    sum->final_cost = x_cost;
+    sum->total_time_in_seconds = now_s() - t_start;
+    return 0;
+  }
+
+  // best state (Ceres keeps parameters_ = the lowest-cost accepted x)
+  double minimum_cost = x_cost;
+  int iteration = 0;
+  double radius = opt.initial_trust_region_radius, decrease_factor = 2.0;
+  int num_invalid = 0;
+  int term = -1;
+  dab_iteration it{};
+  it.iteration = 0;
+  it.step_is_successful = 1;
+  it.step_is_valid = 1;
+  it.cost = x_cost;
+  it.gradient_max_norm = gmax;
+  double iter_start = t_start;
+  if (verbose) print_header();
+
+  for (;;) {
+    // FinalizeIterationAndCheckIfMinimizerCanContinue
+    if (it.step_is_successful) {
+      sum->num_successful_steps++;
+      if (x_cost < minimum_cost) minimum_cost = x_cost;
+    } else {
+      sum->num_unsuccessful_steps++;
+    }
+    it.trust_region_radius = radius;
+    it.iteration_time_in_seconds = now_s() - iter_start;
+    if (it.cost < final_cost) final_cost = it.cost;
+    if (sum->iterations && sum->iterations_written < sum->iterations_capacity)
+      sum->iterations[sum->iterations_written++] = it;
+    if (verbose) print_iter(it, now_s() - t_start);
+    sum->num_iterations = iteration;
+    if (now_s() - t_start >= opt.max_solver_time_in_seconds) {
+      term = DAB_NO_CONVERGENCE;
+      std::snprintf(sum->message, sizeof(sum->message), "Maximum solver time reached.");
+      break;
+    }
+    if (iteration >= opt.max_num_iterations) {
+      term = DAB_NO_CONVERGENCE;
+      std::snprintf(sum->message, sizeof(sum->message),
+                    "Maximum number of iterations reached. Number of iterations: %d.", iteration);
+      break;
+    }
+    if (it.step_is_successful && gmax <= opt.gradient_tolerance) {
+      term = DAB_CONVERGENCE;
+      std::snprintf(sum->message, sizeof(sum->message), "Gradient tolerance reached. Gradient max norm: %e <= %e",
+                    gmax, opt.gradient_tolerance);
+      break;
+    }
+    if (radius <= opt.min_trust_region_radius) {
+      term = DAB_CONVERGENCE;
+      std::snprintf(sum->message, sizeof(sum->message), "Minimum trust region radius reached.");
+      break;
+    }
+
+    iter_start = now_s();
+    iteration++;
+    const double prev_gmax = gmax;
+    it = dab_iteration{};
+    it.iteration = iteration;
+    it.linear_solver_iterations = 1;
+
+    // ---- ComputeTrustRegionStep (DENSE_SCHUR) ----
+    const double tls = now_s();
+    StepScalars sc{radius, opt.min_lm_diagonal, opt.max_lm_diagonal};
+    HIP_OK(hipMemsetAsync(h->d_flags, 0, sizeof(int) * 4, s));
+    launch_point_factor(s, v, h->d_V, h->d_g, h->d_scale_p, sc, h->d_L, h->d_q, h->d_flags);
+    if (NC > 0) {
+      launch_entry_y(s, v, h->d_J, h->d_scale_p, h->d_scale_c, h->d_L, h->d_Y);
+      launch_s_blocks(s, v, h->nblk, h->d_blk_pair_beg, h->d_pairs, h->d_Y, h->packed());
+      launch_cam_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_cam_ent, h->d_Y, h->d_q, h->d_partial);
+      launch_seg_final(s, NC, 6, h->d_seg_chunk, h->d_partial, h->ybc());
+      CHECK_RC(h->allreduce(h->d_spack, h->spack_count(), ncclSum));
+      launch_s_unpack(s, NC, h->nblk, h->d_blk_cam, h->packed(), h->ug(), h->ncross, h->d_cross_cam, h->Ux(),
+                      h->d_scale_c, sc, h->ybc(), h->d_S, h->lds);
+      if (chol_factor_solve(h->chol, s, n, h->d_S, h->lds, h->d_yc, h->d_flags + 1) != 0)
+        return set_error(DAB_E_DEVICE, "rocblas_dsyrk failed");
+    }
+    launch_backsub(s, v, h->d_L, h->d_q, h->d_Y, NC > 0 ? h->d_yc : nullptr, h->d_scale_p, h->d_dp);
+    // candidate x + delta and the model / candidate cost in one observation pass
+    launch_axpy_points(s, NP, h->d_points, h->d_dp, h->d_points_c, h->d_gpart, h->red_grid);
+    launch_final_sum(s, h->red_grid, 2, h->d_gpart, h->d_scal + S_STEP_P);
+    launch_cam_candidate(s, h->E, h->d_ext_col, h->d_ext, NC > 0 ? h->d_yc : nullptr, h->d_scale_c, h->d_ext_c,
+                         h->d_dc);
+    launch_cam_norms(s, h->E, h->d_ext_col, h->d_ext, h->d_ext_c, nullptr, h->d_scal + S_CAM0);
+    launch_cam_tables(s, h->E, h->d_ext_c, h->d_camtab_c);
+    const double tre = now_s();
+    launch_candidate(s, v, h->d_J, h->d_r, h->d_dp, h->d_dc, h->d_points_c, h->d_camtab_c, h->d_gpart,
+                     h->red_grid);
+    launch_final_sum(s, h->red_grid, 3, h->d_gpart, h->d_scal + S_MODEL);
+    CHECK_RC(h->allreduce(h->d_scal + S_MODEL, 5, ncclSum));
+    if (h->world > 1) NCCL_OK(ncclAllReduce(h->d_flags, h->d_flags, 4, ncclInt32, ncclMax, h->comm, s));
+    CHECK_RC(read_scalars(h));
+    const double tdone = now_s();
+    sum->linear_solver_time_in_seconds += tre - tls;
+    sum->residual_evaluation_time_in_seconds += tdone - tre;
+
+    const bool solve_fail = h->h_flags[0] != 0 || h->h_flags[1] != 0 || h->h_flags[2] != 0 || h->h_flags[3] != 0;
+    const double model_cost_change = h->h_scal[S_MODEL];
+    it.step_is_valid = !solve_fail && std::isfinite(model_cost_change) && model_cost_change > 0.0;
+    if (!it.step_is_valid) {
+      num_invalid++;
+      if (num_invalid >= opt.max_num_consecutive_invalid_steps) {
+        term = DAB_FAILURE;
+        std::snprintf(sum->message, sizeof(sum->message),
+                      "Number of consecutive invalid steps more than Solver::Options::max_num_consecutive_invalid_steps: %d",
+                      opt.max_num_consecutive_invalid_steps);
+        break;
+      }
+      radius = radius / decrease_factor;
+      decrease_factor *= 2.0;
+      it.cost = x_cost;
+      it.gradient_max_norm = prev_gmax;
+      it.step_is_successful = 0;
+      continue;
+    }
+    num_invalid = 0;
+    const double candidate_cost = h->h_scal[S_CAND_BAD] != 0.0 ? 1.7976931348623157e308 : 0.5 * h->h_scal[S_CAND];
+    // ParameterToleranceReached
+    it.step_norm = std::sqrt(h->h_scal[S_STEP_P] + h->h_scal[S_CAM0 + 0]);
+    if (it.step_norm <= opt.parameter_tolerance * (x_norm + opt.parameter_tolerance)) {
+      term = DAB_CONVERGENCE;
+      std::snprintf(sum->message, sizeof(sum->message), "Parameter tolerance reached. Relative step_norm: %e <= %e.",
+                    it.step_norm / (x_norm + opt.parameter_tolerance), opt.parameter_tolerance);
+      break;
+    }
+    // FunctionToleranceReached
+    it.cost_change = x_cost - candidate_cost;
+    if (std::fabs(it.cost_change) <= opt.function_tolerance * x_cost) {
+      term = DAB_CONVERGENCE;
+      std::snprintf(sum->message, sizeof(sum->message), "Function tolerance reached. |cost_change|/cost: %e <= %e",
+                    std::fabs(it.cost_change) / x_cost, opt.function_tolerance);
+      break;
+    }
+    it.relative_decrease = (x_cost - candidate_cost) / model_cost_change;
+    if (it.relative_decrease > opt.min_relative_decrease) {
+      // HandleSuccessfulStep: x <- candidate, re-evaluate J at the new point
+      const double xc_norm = std::sqrt(h->h_scal[S_XCNORM_P] + h->h_scal[S_CAM0 + 1]);
+      std::swap(h->d_points, h->d_points_c);
+      std::swap(h->d_ext, h->d_ext_c);
+      x_norm = xc_norm;
+      const double tj = now_s();
+      CHECK_RC(eval_jacobian_and_blocks(h, true));
+      CHECK_RC(read_scalars(h));
+      sum->jacobian_evaluation_time_in_seconds += now_s() - tj;
+      if (h->h_scal[S_COST_BAD] != 0.0) {
+        term = DAB_FAILURE;
+        std::snprintf(sum->message, sizeof(sum->message), "Residual and Jacobian evaluation failed.");
+        break;
+      }
+      x_cost = 0.5 * h->h_scal[S_COST];
+      gmax = std::max(h->h_scal[S_GMAX_P], h->h_scal[S_CAM0 + 2]);
+      it.step_is_successful = 1;
+      it.cost = x_cost;
+      it.gradient_max_norm = gmax;
+      radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * it.relative_decrease - 1.0, 3));
+      radius = std::min(opt.max_trust_region_radius, radius);
+      decrease_factor = 2.0;
+    } else {
+      it.step_is_successful = 0;
+      it.cost = candidate_cost;
+      it.gradient_max_norm = prev_gmax;
+      radius = radius / decrease_factor;
+      decrease_factor *= 2.0;
+    }
+  }
+
+  sum->termination_type = term;
+  sum->final_cost = final_cost;
+  (void)minimum_cost;
+  // the accepted iterate is always the lowest-cost one (steps are monotone), so the
+  // device-resident x is Ceres' parameters_; write it back (sfm.cc:47-48 semantics)
+  CHECK_RC(dab_get_parameters(h, h->prob.points, h->prob.ext));
+  sum->total_time_in_seconds = now_s() - t_start;
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------
+// evaluation entry points (filterPoint3d residual pass, parity)
+// ------------------------------------------------------------------------------------
+extern "C" int dab_eval_residuals(dab_handle* h, double* residuals, double* cost) {
+  clear_error();
+  if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
+  HIP_OK(hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
+  launch_residual(s, h->view, h->d_points, h->d_camtab, h->d_r, h->d_gpart, h->red_grid);
+  launch_final_sum(s, h->red_grid, 2, h->d_gpart, h->d_scal + S_COST);
+  CHECK_RC(read_scalars(h));
+  if (cost) *cost = 0.5 * h->h_scal[S_COST];
+  if (residuals) {
+    std::vector<double> r((size_t)2 * h->N);
+    HIP_OK(hipMemcpyAsync(r.data(), h->d_r, r.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    for (int s2 = 0; s2 < h->N; ++s2) {
+      residuals[2 * (size_t)h->perm[s2]] = r[2 * (size_t)s2];
+      residuals[2 * (size_t)h->perm[s2] + 1] = r[2 * (size_t)s2 + 1];
+    }
+  }
+  return 0;
+}
+
+extern "C" int dab_eval_jacobians(dab_handle* h, double* residuals, double* jacobians) {
+  clear_error();
+  if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
+  HIP_OK(hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
+  launch_jacobian(s, h->view, h->d_points, h->d_camtab, h->d_r, h->d_J);
+  std::vector<double> r((size_t)2 * h->N), J((size_t)h->nplanes * h->N);
+  HIP_OK(hipMemcpyAsync(r.data(), h->d_r, r.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(J.data(), h->d_J, J.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  for (int s2 = 0; s2 < h->N; ++s2) {
+    const int o = h->perm[s2];
+    if (residuals) {
+      residuals[2 * (size_t)o] = r[2 * (size_t)s2];
+      residuals[2 * (size_t)o + 1] = r[2 * (size_t)s2 + 1];
+    }
+    if (jacobians) {
+      double* out = jacobians + (size_t)o * 30;
+      const bool comp = h->prob.obs_ext1[o] >= 0;
+      for (int col = 0; col < 15; ++col)
+        for (int row = 0; row < 2; ++row) {
+          double val = 0.0;
+          if (col < 9 || comp) val = J[(size_t)(2 * col + row) * h->N + s2];
+          out[row * 15 + col] = val;
+        }
+    }
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------
+// benchmark hooks
+// ------------------------------------------------------------------------------------
+extern "C" int dab_bench_eval_pass(dab_handle* h, int with_assembly) {
+  clear_error();
+  if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
+  HIP_OK(hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  const DevView& v = h->view;
+  launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
+  HIP_OK(hipEventRecord(h->ev0, s));
+  launch_jacobian(s, v, h->d_points, h->d_camtab, h->d_r, h->d_J);
+  HIP_OK(hipEventRecord(h->ev1, s));
+  if (with_assembly) {
+    launch_point_vg(s, v, h->d_r, h->d_J, h->d_V, h->d_g);
+    if (h->NC > 0) {
+      launch_cam_ug_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_cam_ent, h->d_r, h->d_J, h->d_partial);
+      launch_seg_final(s, h->NC, 27, h->d_seg_chunk, h->d_partial, h->ug());
+      if (h->ncross > 0 && h->nxchunk > 0) {
+        launch_cross_partial(s, v, h->nxchunk, h->d_xchunk_beg, h->d_xobs, h->d_J, h->d_partial);
+        launch_seg_final(s, h->ncross, 36, h->d_xseg_chunk, h->d_partial, h->Ux());
+      }
+      CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
+    }
+    launch_r_sumsq(s, h->N, h->d_r, h->d_gpart, h->red_grid);
+    launch_final_sum(s, h->red_grid, 2, h->d_gpart, h->d_scal + S_COST);
+    CHECK_RC(h->allreduce(h->d_scal + S_COST, 2, ncclSum));
+  }
+  HIP_OK(hipEventRecord(h->ev2, s));
+  HIP_OK(hipEventSynchronize(h->ev2));
+  float a = 0.f, b = 0.f;
+  HIP_OK(hipEventElapsedTime(&a, h->ev0, h->ev1));
+  HIP_OK(hipEventElapsedTime(&b, h->ev1, h->ev2));
+  h->bench_jac_ms += a;
+  h->bench_asm_ms += b;
+  h->bench_count++;
+  return 0;
+}
+
+extern "C" int dab_sync(dab_handle* h) {
+  clear_error();
+  if (!h) return set_error(DAB_E_INVALID, "null handle");
+  HIP_OK(hipSetDevice(h->device));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int dab_bench_kernel_ms(dab_handle* h, double* jac_ms, double* assembly_ms) {
+  clear_error();
+  if (!h) return set_error(DAB_E_INVALID, "null handle");
+  const double n = h->bench_count > 0 ? h->bench_count : 1;
+  if (jac_ms) *jac_ms = h->bench_jac_ms / n;
+  if (assembly_ms) *assembly_ms = h->bench_asm_ms / n;
+  h->bench_jac_ms = h->bench_asm_ms = 0;
+  h->bench_count = 0;
+  return 0;
+}
+
+extern "C" int dab_jacobian_bytes(dab_handle* h, double* bytes) {
+  clear_error();
+  if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
+  // algorithmic bytes of one residual+Jacobian launch: per observation
+  // idx 16 + xy 16 + r 16 + J 8*(18|30); parameters once: points 24/pt, tables 256/ext,
+  // intrinsics 64 each
+  long long ncomp = 0;
+  for (int o = 0; o < h->N; ++o) ncomp += h->prob.obs_ext1[o] >= 0;
+  const double per_single = 16 + 16 + 16 + 8.0 * 18, per_comp = 16 + 16 + 16 + 8.0 * 30;
+  *bytes = (h->N - ncomp) * per_single + ncomp * per_comp + 24.0 * h->NP + 8.0 * kCamTab * h->E + 64.0 * h->NI;
+  return 0;
+}
