@@ -1,18 +1,22 @@
 // dab_kernels.hip — gfx950 kernels of the BA hot path.
 //
-// Every kernel is wave64-native and works on point-major SoA data:
-//   obs_idx  int4 (point, ext0, ext1, intr)    16 B / observation, one dwordx4 load
-//   obs_xy   double2                           16 B / observation
-//   r        double2                           16 B / observation (written)
-//   J        [plane][N] doubles, plane = 2*col + row, col in X(3) w0(3) t0(3) w1(3) t1(3)
-//            18 planes (single extrinsic) or 30 (arc∘ring): 144 / 240 B per observation.
-// Per-extrinsic rotation data is precomputed once per parameter state (launch_cam_tables)
-// so the per-observation kernels carry no transcendental: the Jacobian of
-// R(w)X with respect to w is -R [X]x J_r(w) (right Jacobian of SO(3)); in Ceres'
-// first-order branch (|w|^2 <= DBL_EPSILON, rotation.h) R = I + [w]x and the
-// derivative is -[X]x, which the table encodes as Rd = I, Jd = I.
-// All reductions are deterministic: fixed-shape wave butterflies + fixed-order block and
-// chunk sums, so results are bitwise reproducible run to run.
+// Data layout in HBM (all wave64, coalesced on the dominant streams):
+//   point-major observation streams ("s" order, observations of one point contiguous)
+//     obs_idx int4 (point, ext0, ext1, intr) 16 B, obs_xy double2 16 B, obs_ent int2 8 B
+//     r double2 16 B, Jp[6][N] planes 48 B (d r / d X, plane = 2*col + row)
+//   camera-major entry records (one per observation slot whose extrinsic is free):
+//     rec[pos][16] = d r / d(w,t) row 0 (6) | row 1 (6) | r (2) | pad   128 B
+//     Y[pos][18]   = Schur factor of the entry, per LM iteration       144 B
+//   per-point V[6][NP], g[3][NP], L[6][NP], q[NP][4]; per-camera ug[NC][27].
+// The residual+Jacobian kernel writes the records straight to their camera-major slots,
+// so every camera-side reduction (U, g_c, Schur rhs, S blocks) streams contiguous
+// records instead of gathering 8-byte words, and it reduces the point blocks V, g with a
+// deterministic segmented wave scan instead of a second pass over J.
+// Per-extrinsic rotation data is precomputed once per parameter state (k_cam_tables):
+// d(R(w)X)/dw = -R [X]x J_r(w) (right Jacobian of SO(3)); in Ceres' first-order branch
+// (|w|^2 <= DBL_EPSILON, rotation.h) R = I + [w]x and the derivative is -[X]x, encoded as
+// Rd = I, Jd = I. No transcendental runs per observation.
+// Every reduction has a fixed shape and order: results are bitwise reproducible.
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -65,23 +69,33 @@ __global__ void k_seg_final(int nseg, int K, const int* __restrict__ seg_chunk,
   out[t] = v;
 }
 
-__global__ void k_final_sum(int grid, int K, const double* __restrict__ partial,
-                            double* __restrict__ out, unsigned max_mask) {
-  const int k = threadIdx.x;
-  if (k >= K) return;
-  const bool is_max = (max_mask >> k) & 1u;
-  double v = 0.0;
-  for (int c = 0; c < grid; ++c) {
-    const double x = partial[(size_t)c * K + k];
-    v = is_max ? fmax(v, x) : v + x;
+// one block of 256 threads: strided per-thread sums in fixed order, then a fixed tree
+__global__ __launch_bounds__(256) void k_final_sum(int grid, int K, const double* __restrict__ partial,
+                                                   double* __restrict__ out, unsigned max_mask) {
+  __shared__ double sh[256];
+  const int t = threadIdx.x;
+  for (int k = 0; k < K; ++k) {
+    const bool is_max = (max_mask >> k) & 1u;
+    double v = 0.0;
+    for (int c = t; c < grid; c += 256) {
+      const double x = partial[(size_t)c * K + k];
+      v = is_max ? fmax(v, x) : v + x;
+    }
+    sh[t] = v;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+      if (t < off) sh[t] = is_max ? fmax(sh[t], sh[t + off]) : sh[t] + sh[t + off];
+      __syncthreads();
+    }
+    if (t == 0) out[k] = sh[0];
+    __syncthreads();
   }
-  out[k] = v;
 }
 
-__global__ void k_cam_norms(int E, const int* __restrict__ ext_col, const double* __restrict__ ext,
-                            const double* __restrict__ ext_c, const double* __restrict__ ug,
-                            double* __restrict__ out) {
-  // single block of 256 threads, fixed-order combine
+__global__ __launch_bounds__(256) void k_cam_norms(int E, const int* __restrict__ ext_col,
+                                                   const double* __restrict__ ext,
+                                                   const double* __restrict__ ext_c,
+                                                   const double* __restrict__ ug, double* __restrict__ out) {
   __shared__ double sh[256][5];
   double a[5] = {0, 0, 0, 0, 0};
   for (int t = threadIdx.x; t < 6 * E; t += blockDim.x) {
@@ -100,19 +114,22 @@ __global__ void k_cam_norms(int E, const int* __restrict__ ext_col, const double
 #pragma unroll
   for (int i = 0; i < 5; ++i) sh[threadIdx.x][i] = a[i];
   __syncthreads();
-  if (threadIdx.x < 5) {
-    const int i = threadIdx.x;
-    double v = 0.0;
-    for (int q = 0; q < 256; ++q) v = (i == 2) ? fmax(v, sh[q][i]) : v + sh[q][i];
-    out[i] = v;
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) {
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+        sh[threadIdx.x][i] = (i == 2) ? fmax(sh[threadIdx.x][i], sh[threadIdx.x + off][i])
+                                      : sh[threadIdx.x][i] + sh[threadIdx.x + off][i];
+    }
+    __syncthreads();
   }
+  if (threadIdx.x < 5) out[threadIdx.x] = sh[0][threadIdx.x];
 }
 
 void launch_cam_norms(hipStream_t s, int E, const int* ext_col, const double* ext, const double* ext_c,
                       const double* ug, double* out) {
   k_cam_norms<<<1, 256, 0, s>>>(E, ext_col, ext, ext_c, ug, out);
 }
-
 void launch_seg_final(hipStream_t s, int nseg, int K, const int* seg_chunk, const double* partial,
                       double* out) {
   if (nseg <= 0) return;
@@ -121,22 +138,7 @@ void launch_seg_final(hipStream_t s, int nseg, int K, const int* seg_chunk, cons
 }
 void launch_final_sum(hipStream_t s, int grid, int K, const double* partial, double* out,
                       unsigned max_mask) {
-  k_final_sum<<<1, 64, 0, s>>>(grid, K, partial, out, max_mask);
-}
-
-__global__ __launch_bounds__(256) void k_r_sumsq(int N, const double2* __restrict__ r,
-                                                 double* __restrict__ partial) {
-  double acc[2] = {0.0, 0.0};
-  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < N; s += gridDim.x * blockDim.x) {
-    const double2 v = r[s];
-    acc[0] += v.x * v.x + v.y * v.y;
-    acc[1] += (isfinite(v.x) && isfinite(v.y)) ? 0.0 : 1.0;
-  }
-  block_reduce_store<2>(acc, partial + 2 * (size_t)blockIdx.x);
-}
-
-void launch_r_sumsq(hipStream_t s, int N, const double* r, double* partial, int grid) {
-  k_r_sumsq<<<grid, 256, 0, s>>>(N, reinterpret_cast<const double2*>(r), partial);
+  k_final_sum<<<1, 256, 0, s>>>(grid, K, partial, out, max_mask);
 }
 
 // ------------------------------------------------------------------------------------
@@ -254,106 +256,241 @@ __device__ __forceinline__ void dwrot(const double a[3], const double X[3], cons
   o[2] = -(c0 * Jd[2] + c1 * Jd[5] + c2 * Jd[8]);
 }
 
-__device__ __forceinline__ void load_tab(const double* __restrict__ camtab, int e, double (&T)[30]) {
+template <int NT>
+__device__ __forceinline__ void load_tab(const double* __restrict__ camtab, int e, double (&T)[NT]) {
   const double2* p = reinterpret_cast<const double2*>(camtab + (size_t)kCamTab * e);
 #pragma unroll
-  for (int i = 0; i < 15; ++i) {
-    const double2 v = p[i];
-    T[2 * i] = v.x;
-    T[2 * i + 1] = v.y;
-  }
-}
-__device__ __forceinline__ void load_rt(const double* __restrict__ camtab, int e, double (&T)[12]) {
-  const double2* p = reinterpret_cast<const double2*>(camtab + (size_t)kCamTab * e);
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
+  for (int i = 0; i < NT / 2; ++i) {
     const double2 v = p[i];
     T[2 * i] = v.x;
     T[2 * i + 1] = v.y;
   }
 }
 
+// One observation: residual and every Jacobian row, from the camera tables.
+struct ObsJac {
+  Proj pr;
+  double jx0[3], jx1[3];    // d r / d X
+  double jw0a[3], jw0b[3];  // d r / d w0   (rows 0, 1)
+  double jw1a[3], jw1b[3];  // d r / d w1
+  double jt1a[3], jt1b[3];  // d r / d t1   (d r / d t0 = pr.A0 / pr.A1)
+};
+
+__device__ __forceinline__ void obs_jacobian(const int4 id, const double2 xy, const double X[3],
+                                             const double* __restrict__ camtab,
+                                             const double* __restrict__ K, ObsJac& o) {
+  double T0[30];
+  load_tab<30>(camtab, id.y, T0);
+  if (id.z >= 0) {
+    double T1[30];
+    load_tab<30>(camtab, id.z, T1);
+    double P2[3], P[3];
+    matvec_add(T1, X, T1 + 9, P2);
+    matvec_add(T0, P2, T0 + 9, P);
+    project(P, K, xy.x, xy.y, o.pr, true);
+    double B0a[3], B0b[3];
+    rowmat(o.pr.A0, T0, B0a);  // A R0
+    rowmat(o.pr.A1, T0, B0b);
+    rowmat(B0a, T1, o.jx0);    // A R0 R1
+    rowmat(B0b, T1, o.jx1);
+    double Ca[3], Cb[3];
+    rowmat(B0a, T1 + 12, Ca);  // A R0 Rd1
+    rowmat(B0b, T1 + 12, Cb);
+    dwrot(Ca, X, T1 + 21, o.jw1a);
+    dwrot(Cb, X, T1 + 21, o.jw1b);
+    double Da[3], Db[3];
+    rowmat(o.pr.A0, T0 + 12, Da);  // A Rd0
+    rowmat(o.pr.A1, T0 + 12, Db);
+    dwrot(Da, P2, T0 + 21, o.jw0a);
+    dwrot(Db, P2, T0 + 21, o.jw0b);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      o.jt1a[i] = B0a[i];
+      o.jt1b[i] = B0b[i];
+    }
+  } else {
+    double P[3];
+    matvec_add(T0, X, T0 + 9, P);
+    project(P, K, xy.x, xy.y, o.pr, true);
+    rowmat(o.pr.A0, T0, o.jx0);
+    rowmat(o.pr.A1, T0, o.jx1);
+    double Da[3], Db[3];
+    rowmat(o.pr.A0, T0 + 12, Da);
+    rowmat(o.pr.A1, T0 + 12, Db);
+    dwrot(Da, X, T0 + 21, o.jw0a);
+    dwrot(Db, X, T0 + 21, o.jw0b);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) o.jw1a[i] = o.jw1b[i] = o.jt1a[i] = o.jt1b[i] = 0.0;
+  }
+}
+
+__device__ __forceinline__ void store_rec(double* __restrict__ rec, int pos, const double wa[3],
+                                          const double wb[3], const double ta[3], const double tb[3],
+                                          double ru, double rv) {
+  double2* p = reinterpret_cast<double2*>(rec + (size_t)kRec * pos);
+  p[0] = make_double2(wa[0], wa[1]);
+  p[1] = make_double2(wa[2], ta[0]);
+  p[2] = make_double2(ta[1], ta[2]);
+  p[3] = make_double2(wb[0], wb[1]);
+  p[4] = make_double2(wb[2], tb[0]);
+  p[5] = make_double2(tb[1], tb[2]);
+  p[6] = make_double2(ru, rv);
+  p[7] = make_double2(0.0, 0.0);
+}
+
+// Product kernel. Block = 256 threads = 4 waves; wave windows of 64 consecutive
+// observations, grid-strided. V/g use an inclusive segmented scan keyed by point id.
 __global__ __launch_bounds__(256) void k_jacobian(DevView v, const double* __restrict__ points,
                                                   const double* __restrict__ camtab,
-                                                  double2* __restrict__ r, double* __restrict__ J) {
+                                                  double2* __restrict__ r, double* __restrict__ Jp,
+                                                  double* __restrict__ rec, double* __restrict__ V,
+                                                  double* __restrict__ g, double* __restrict__ wpart,
+                                                  double* __restrict__ partial) {
   const int N = v.N;
-  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < N; s += gridDim.x * blockDim.x) {
-    const int4 id = v.obs_idx[s];
-    const double2 xy = v.obs_xy[s];
-    const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
-    const double* K = v.intr + (size_t)kIntr * id.w;
-    double T0[30];
-    load_tab(camtab, id.y, T0);
-    Proj pr;
-    double jx0[3], jx1[3], jw0a[3], jw0b[3], jw1a[3], jw1b[3], jt1a[3], jt1b[3];
-    if (id.z >= 0) {
-      double T1[30];
-      load_tab(camtab, id.z, T1);
-      double P2[3], P[3];
-      matvec_add(T1, X, T1 + 9, P2);
-      matvec_add(T0, P2, T0 + 9, P);
-      project(P, K, xy.x, xy.y, pr, true);
-      double B0a[3], B0b[3];
-      rowmat(pr.A0, T0, B0a);  // A R0
-      rowmat(pr.A1, T0, B0b);
-      rowmat(B0a, T1, jx0);    // A R0 R1
-      rowmat(B0b, T1, jx1);
-      double Ca[3], Cb[3];
-      rowmat(B0a, T1 + 12, Ca);  // A R0 Rd1
-      rowmat(B0b, T1 + 12, Cb);
-      dwrot(Ca, X, T1 + 21, jw1a);
-      dwrot(Cb, X, T1 + 21, jw1b);
-      double Da[3], Db[3];
-      rowmat(pr.A0, T0 + 12, Da);  // A Rd0
-      rowmat(pr.A1, T0 + 12, Db);
-      dwrot(Da, P2, T0 + 21, jw0a);
-      dwrot(Db, P2, T0 + 21, jw0b);
+  const size_t Ns = (size_t)N, NPs = (size_t)v.NP;
+  const int lane = threadIdx.x & 63;
+  double acc[2] = {0.0, 0.0};
+  for (int base = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kWin; base < N; base += gridDim.x * 4 * kWin) {
+    const int s = base + lane;
+    const bool valid = s < N;
+    double c[9];
+    int pt = -1 - lane;  // never equal across invalid lanes
+    if (valid) {
+      const int4 id = v.obs_idx[s];
+      const double2 xy = v.obs_xy[s];
+      const int2 ent = v.obs_ent[s];
+      pt = id.x;
+      const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
+      ObsJac o;
+      obs_jacobian(id, xy, X, camtab, v.intr + (size_t)kIntr * id.w, o);
+      const double ru = o.pr.ru, rv = o.pr.rv;
+      r[s] = make_double2(ru, rv);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) { jt1a[i] = B0a[i]; jt1b[i] = B0b[i]; }
+      for (int k = 0; k < 3; ++k) {
+        Jp[(2 * k) * Ns + s] = o.jx0[k];
+        Jp[(2 * k + 1) * Ns + s] = o.jx1[k];
+      }
+      if (ent.x >= 0) store_rec(rec, ent.x, o.jw0a, o.jw0b, o.pr.A0, o.pr.A1, ru, rv);
+      if (ent.y >= 0) store_rec(rec, ent.y, o.jw1a, o.jw1b, o.jt1a, o.jt1b, ru, rv);
+      c[0] = o.jx0[0] * o.jx0[0] + o.jx1[0] * o.jx1[0];
+      c[1] = o.jx0[0] * o.jx0[1] + o.jx1[0] * o.jx1[1];
+      c[2] = o.jx0[0] * o.jx0[2] + o.jx1[0] * o.jx1[2];
+      c[3] = o.jx0[1] * o.jx0[1] + o.jx1[1] * o.jx1[1];
+      c[4] = o.jx0[1] * o.jx0[2] + o.jx1[1] * o.jx1[2];
+      c[5] = o.jx0[2] * o.jx0[2] + o.jx1[2] * o.jx1[2];
+      c[6] = o.jx0[0] * ru + o.jx1[0] * rv;
+      c[7] = o.jx0[1] * ru + o.jx1[1] * rv;
+      c[8] = o.jx0[2] * ru + o.jx1[2] * rv;
+      acc[0] += ru * ru + rv * rv;
+      acc[1] += (isfinite(ru) && isfinite(rv)) ? 0.0 : 1.0;
     } else {
-      double P[3];
-      matvec_add(T0, X, T0 + 9, P);
-      project(P, K, xy.x, xy.y, pr, true);
-      rowmat(pr.A0, T0, jx0);
-      rowmat(pr.A1, T0, jx1);
-      double Da[3], Db[3];
-      rowmat(pr.A0, T0 + 12, Da);
-      rowmat(pr.A1, T0 + 12, Db);
-      dwrot(Da, X, T0 + 21, jw0a);
-      dwrot(Db, X, T0 + 21, jw0b);
-    }
-    r[s] = make_double2(pr.ru, pr.rv);
-    double* Jp = J + s;
-    const size_t Ns = (size_t)N;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      Jp[(2 * c) * Ns] = jx0[c];
-      Jp[(2 * c + 1) * Ns] = jx1[c];
-      Jp[(2 * (3 + c)) * Ns] = jw0a[c];
-      Jp[(2 * (3 + c) + 1) * Ns] = jw0b[c];
-      Jp[(2 * (6 + c)) * Ns] = pr.A0[c];
-      Jp[(2 * (6 + c) + 1) * Ns] = pr.A1[c];
+      for (int k = 0; k < 9; ++k) c[k] = 0.0;
     }
-    if (id.z >= 0) {
+    // inclusive segmented scan (Hillis–Steele) within the 64-lane window
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        Jp[(2 * (9 + c)) * Ns] = jw1a[c];
-        Jp[(2 * (9 + c) + 1) * Ns] = jw1b[c];
-        Jp[(2 * (12 + c)) * Ns] = jt1a[c];
-        Jp[(2 * (12 + c) + 1) * Ns] = jt1b[c];
+    for (int off = 1; off < 64; off <<= 1) {
+      const int pu = __shfl_up(pt, off, 64);
+      const bool take = lane >= off && pu == pt;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const double vu = __shfl_up(c[k], off, 64);
+        if (take) c[k] += vu;
+      }
+    }
+    const int pn = __shfl_down(pt, 1, 64);
+    const bool tail = valid && (lane == 63 || s + 1 == N || pn != pt);
+    if (tail) {
+      const int a = v.pt_obs_ptr[pt], b = v.pt_obs_ptr[pt + 1];
+      if (a >= base && b <= base + kWin) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) V[k * NPs + pt] = c[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) g[k * NPs + pt] = c[6 + k];
+      } else {
+        const size_t w = (size_t)(base / kWin);
+        if (a < base) {  // the window's first segment
+#pragma unroll
+          for (int k = 0; k < 9; ++k) wpart[(2 * w) * 9 + k] = c[k];
+        }
+        if (b > base + kWin) {  // the window's last segment
+#pragma unroll
+          for (int k = 0; k < 9; ++k) wpart[(2 * w + 1) * 9 + k] = c[k];
+        }
       }
     }
   }
+  block_reduce_store<2>(acc, partial + 2 * (size_t)blockIdx.x);
 }
 
 void launch_jacobian(hipStream_t s, const DevView& v, const double* points, const double* camtab,
-                     double* r, double* J) {
-  if (v.N <= 0) return;
-  k_jacobian<<<grid_for(v.N, 256, 1 << 20), 256, 0, s>>>(v, points, camtab,
-                                                        reinterpret_cast<double2*>(r), J);
+                     double* r, double* Jp, double* rec, double* V, double* g, double* wpart,
+                     double* partial, int grid) {
+  k_jacobian<<<grid, 256, 0, s>>>(v, points, camtab, reinterpret_cast<double2*>(r), Jp, rec, V, g, wpart,
+                                  partial);
 }
 
-// residual at a parameter state: partial[block] = {sum r^2, nonfinite count}
+__global__ void k_point_fixup(int nstrad, const int4* __restrict__ strad, const double* __restrict__ wpart,
+                              int NP, double* __restrict__ V, double* __restrict__ g) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nstrad) return;
+  const int4 st = strad[t];  // (point, first window, last window)
+  double c[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) c[k] = wpart[(2 * (size_t)st.y + 1) * 9 + k];
+  for (int w = st.y + 1; w <= st.z; ++w)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) c[k] += wpart[(2 * (size_t)w) * 9 + k];
+  const size_t NPs = (size_t)NP;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) V[k * NPs + st.x] = c[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) g[k * NPs + st.x] = c[6 + k];
+}
+
+void launch_point_fixup(hipStream_t s, int nstrad, const int4* strad, const double* wpart, int NP,
+                        double* V, double* g) {
+  if (nstrad <= 0) return;
+  k_point_fixup<<<grid_for(nstrad, 256, 1 << 20), 256, 0, s>>>(nstrad, strad, wpart, NP, V, g);
+}
+
+// parity API: every Jacobian column as planes Jfull[2*col+row][N]
+__global__ __launch_bounds__(256) void k_jacobian_full(DevView v, const double* __restrict__ points,
+                                                       const double* __restrict__ camtab,
+                                                       double2* __restrict__ r, double* __restrict__ J) {
+  const int N = v.N;
+  const size_t Ns = (size_t)N;
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < N; s += gridDim.x * blockDim.x) {
+    const int4 id = v.obs_idx[s];
+    const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
+    ObsJac o;
+    obs_jacobian(id, v.obs_xy[s], X, camtab, v.intr + (size_t)kIntr * id.w, o);
+    r[s] = make_double2(o.pr.ru, o.pr.rv);
+    double* Jo = J + s;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      Jo[(2 * c) * Ns] = o.jx0[c];
+      Jo[(2 * c + 1) * Ns] = o.jx1[c];
+      Jo[(2 * (3 + c)) * Ns] = o.jw0a[c];
+      Jo[(2 * (3 + c) + 1) * Ns] = o.jw0b[c];
+      Jo[(2 * (6 + c)) * Ns] = o.pr.A0[c];
+      Jo[(2 * (6 + c) + 1) * Ns] = o.pr.A1[c];
+      Jo[(2 * (9 + c)) * Ns] = o.jw1a[c];
+      Jo[(2 * (9 + c) + 1) * Ns] = o.jw1b[c];
+      Jo[(2 * (12 + c)) * Ns] = o.jt1a[c];
+      Jo[(2 * (12 + c) + 1) * Ns] = o.jt1b[c];
+    }
+  }
+}
+
+void launch_jacobian_full(hipStream_t s, const DevView& v, const double* points, const double* camtab,
+                          double* r, double* Jfull) {
+  if (v.N <= 0) return;
+  k_jacobian_full<<<grid_for(v.N, 256, 1 << 20), 256, 0, s>>>(v, points, camtab,
+                                                              reinterpret_cast<double2*>(r), Jfull);
+}
+
+// residual at a parameter state
 __device__ __forceinline__ void residual_at(const DevView& v, const double* __restrict__ points,
                                             const double* __restrict__ camtab, int s, double& ru,
                                             double& rv) {
@@ -362,11 +499,11 @@ __device__ __forceinline__ void residual_at(const DevView& v, const double* __re
   const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
   const double* K = v.intr + (size_t)kIntr * id.w;
   double T0[12];
-  load_rt(camtab, id.y, T0);
+  load_tab<12>(camtab, id.y, T0);
   double P[3];
   if (id.z >= 0) {
     double T1[12], P2[3];
-    load_rt(camtab, id.z, T1);
+    load_tab<12>(camtab, id.z, T1);
     matvec_add(T1, X, T1 + 9, P2);
     matvec_add(T0, P2, T0 + 9, P);
   } else {
@@ -399,113 +536,74 @@ void launch_residual(hipStream_t s, const DevView& v, const double* points, cons
 }
 
 // ------------------------------------------------------------------------------------
-// J^T J / J^T r block assembly (row a7, normal-equation side)
+// camera-side J^T J / J^T r reductions over contiguous records (row a7)
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_point_vg(DevView v, const double2* __restrict__ r,
-                                                  const double* __restrict__ J, double* __restrict__ V,
-                                                  double* __restrict__ g) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= v.NP) return;
-  const size_t Ns = (size_t)v.N, NPs = (size_t)v.NP;
-  double a00 = 0, a01 = 0, a02 = 0, a11 = 0, a12 = 0, a22 = 0, g0 = 0, g1 = 0, g2 = 0;
-  for (int s = v.pt_obs_ptr[p]; s < v.pt_obs_ptr[p + 1]; ++s) {
-    const double2 rr = r[s];
-    const double x0 = J[0 * Ns + s], y0 = J[1 * Ns + s];
-    const double x1 = J[2 * Ns + s], y1 = J[3 * Ns + s];
-    const double x2 = J[4 * Ns + s], y2 = J[5 * Ns + s];
-    a00 += x0 * x0 + y0 * y0;
-    a01 += x0 * x1 + y0 * y1;
-    a02 += x0 * x2 + y0 * y2;
-    a11 += x1 * x1 + y1 * y1;
-    a12 += x1 * x2 + y1 * y2;
-    a22 += x2 * x2 + y2 * y2;
-    g0 += x0 * rr.x + y0 * rr.y;
-    g1 += x1 * rr.x + y1 * rr.y;
-    g2 += x2 * rr.x + y2 * rr.y;
+__device__ __forceinline__ void load_rec(const double* __restrict__ rec, int pos, double (&q)[14]) {
+  const double2* p = reinterpret_cast<const double2*>(rec + (size_t)kRec * pos);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const double2 t = p[i];
+    q[2 * i] = t.x;
+    q[2 * i + 1] = t.y;
   }
-  V[0 * NPs + p] = a00; V[1 * NPs + p] = a01; V[2 * NPs + p] = a02;
-  V[3 * NPs + p] = a11; V[4 * NPs + p] = a12; V[5 * NPs + p] = a22;
-  g[0 * NPs + p] = g0; g[1 * NPs + p] = g1; g[2 * NPs + p] = g2;
 }
 
-void launch_point_vg(hipStream_t s, const DevView& v, const double* r, const double* J, double* V,
-                     double* g) {
-  if (v.NP <= 0) return;
-  k_point_vg<<<grid_for(v.NP, 256, 1 << 20), 256, 0, s>>>(v, reinterpret_cast<const double2*>(r), J, V, g);
-}
-
-__global__ __launch_bounds__(256) void k_cam_ug_partial(DevView v, const int* __restrict__ chunk_beg,
-                                                        const int* __restrict__ cam_ent,
-                                                        const double2* __restrict__ r,
-                                                        const double* __restrict__ J,
+__global__ __launch_bounds__(256) void k_cam_ug_partial(const int* __restrict__ chunk_beg,
+                                                        const double* __restrict__ rec,
                                                         double* __restrict__ partial) {
   const int c = blockIdx.x;
   const int b = chunk_beg[c], e = chunk_beg[c + 1];
-  const size_t Ns = (size_t)v.N;
   double acc[27];
 #pragma unroll
   for (int i = 0; i < 27; ++i) acc[i] = 0.0;
   for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
-    const int os = v.ent_os[cam_ent[i]];
-    const int s = os >> 1, slot = os & 1;
-    const double2 rr = r[s];
-    double ja[6], jb[6];
-    const int col0 = 3 + 6 * slot;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-      ja[a] = J[(size_t)(2 * (col0 + a)) * Ns + s];
-      jb[a] = J[(size_t)(2 * (col0 + a) + 1) * Ns + s];
-    }
-    int q = 0;
+    double q[14];
+    load_rec(rec, i, q);
+    const double* ja = q;
+    const double* jb = q + 6;
+    int k = 0;
 #pragma unroll
     for (int a = 0; a < 6; ++a)
 #pragma unroll
-      for (int bb = a; bb < 6; ++bb) acc[q++] += ja[a] * ja[bb] + jb[a] * jb[bb];
+      for (int bb = a; bb < 6; ++bb) acc[k++] += ja[a] * ja[bb] + jb[a] * jb[bb];
 #pragma unroll
-    for (int a = 0; a < 6; ++a) acc[21 + a] += ja[a] * rr.x + jb[a] * rr.y;
+    for (int a = 0; a < 6; ++a) acc[21 + a] += ja[a] * q[12] + jb[a] * q[13];
   }
   block_reduce_store<27>(acc, partial + 27 * (size_t)c);
 }
 
-void launch_cam_ug_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
-                           const int* cam_ent, const double* r, const double* J, double* partial) {
+void launch_cam_ug_partial(hipStream_t s, int nchunk, const int* chunk_beg, const double* rec,
+                           double* partial) {
   if (nchunk <= 0) return;
-  k_cam_ug_partial<<<nchunk, 256, 0, s>>>(v, chunk_beg, cam_ent, reinterpret_cast<const double2*>(r), J,
-                                          partial);
+  k_cam_ug_partial<<<nchunk, 256, 0, s>>>(chunk_beg, rec, partial);
 }
 
 __global__ __launch_bounds__(256) void k_cross_partial(DevView v, const int* __restrict__ chunk_beg,
                                                        const int* __restrict__ xobs,
-                                                       const double* __restrict__ J,
+                                                       const double* __restrict__ rec,
                                                        double* __restrict__ partial) {
   const int c = blockIdx.x;
   const int b = chunk_beg[c], e = chunk_beg[c + 1];
-  const size_t Ns = (size_t)v.N;
   double acc[36];
 #pragma unroll
   for (int i = 0; i < 36; ++i) acc[i] = 0.0;
   for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
-    const int s = xobs[i];
-    double a0[6], a1[6], b0[6], b1[6];
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-      a0[a] = J[(size_t)(2 * (3 + a)) * Ns + s];
-      a1[a] = J[(size_t)(2 * (3 + a) + 1) * Ns + s];
-      b0[a] = J[(size_t)(2 * (9 + a)) * Ns + s];
-      b1[a] = J[(size_t)(2 * (9 + a) + 1) * Ns + s];
-    }
+    const int2 ent = v.obs_ent[xobs[i]];
+    double qa[14], qb[14];
+    load_rec(rec, ent.x, qa);
+    load_rec(rec, ent.y, qb);
 #pragma unroll
     for (int a = 0; a < 6; ++a)
 #pragma unroll
-      for (int bb = 0; bb < 6; ++bb) acc[6 * a + bb] += a0[a] * b0[bb] + a1[a] * b1[bb];
+      for (int bb = 0; bb < 6; ++bb) acc[6 * a + bb] += qa[a] * qb[bb] + qa[6 + a] * qb[6 + bb];
   }
   block_reduce_store<36>(acc, partial + 36 * (size_t)c);
 }
 
 void launch_cross_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
-                          const int* xobs, const double* J, double* partial) {
+                          const int* xobs, const double* rec, double* partial) {
   if (nchunk <= 0) return;
-  k_cross_partial<<<nchunk, 256, 0, s>>>(v, chunk_beg, xobs, J, partial);
+  k_cross_partial<<<nchunk, 256, 0, s>>>(v, chunk_beg, xobs, rec, partial);
 }
 
 // ------------------------------------------------------------------------------------
@@ -522,7 +620,7 @@ __global__ __launch_bounds__(256) void k_point_factor(DevView v, const double* _
   const double s0 = sp[p], s1 = sp[NPs + p], s2 = sp[2 * NPs + p];
   double v00 = s0 * V[p] * s0, v01 = s0 * V[NPs + p] * s1, v02 = s0 * V[2 * NPs + p] * s2;
   double v11 = s1 * V[3 * NPs + p] * s1, v12 = s1 * V[4 * NPs + p] * s2, v22 = s2 * V[5 * NPs + p] * s2;
-  auto lmd = [&](double d) {
+  auto lmd = [&](double d) {  // LM diagonal: clamp(diag(Js^T Js)) / radius
     d = fmin(fmax(d, sc.min_diag), sc.max_diag);
     const double D = sqrt(d / sc.radius);
     return D * D;
@@ -548,7 +646,8 @@ __global__ __launch_bounds__(256) void k_point_factor(DevView v, const double* _
   if (!ok) atomicOr(fail, 1);
   L[p] = l00; L[NPs + p] = l10; L[2 * NPs + p] = l20;
   L[3 * NPs + p] = l11; L[4 * NPs + p] = l21; L[5 * NPs + p] = l22;
-  q[p] = q0; q[NPs + p] = q1; q[2 * NPs + p] = q2;
+  reinterpret_cast<double2*>(q)[2 * (size_t)p] = make_double2(q0, q1);
+  reinterpret_cast<double2*>(q)[2 * (size_t)p + 1] = make_double2(q2, 0.0);
 }
 
 void launch_point_factor(hipStream_t s, const DevView& v, const double* V, const double* g,
@@ -557,29 +656,31 @@ void launch_point_factor(hipStream_t s, const DevView& v, const double* V, const
   k_point_factor<<<grid_for(v.NP, 256, 1 << 20), 256, 0, s>>>(v, V, g, scale_p, sc, L, q, fail);
 }
 
-__global__ __launch_bounds__(256) void k_entry_y(DevView v, const double* __restrict__ J,
+__global__ __launch_bounds__(256) void k_entry_y(DevView v, const double* __restrict__ Jp,
+                                                 const double* __restrict__ rec,
                                                  const double* __restrict__ sp,
                                                  const double* __restrict__ scc,
                                                  const double* __restrict__ L, double* __restrict__ Y) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= v.NE) return;
-  const int os = v.ent_os[e], s = os >> 1, slot = os & 1;
-  const int p = v.ent_pt[e], c = v.ent_cam[e];
-  const size_t Ns = (size_t)v.N, NPs = (size_t)v.NP, NEs = (size_t)v.NE;
+  const int s = v.ent_os[e] >> 1;
+  const int p = v.ent_pt[e], c = v.ent_cam[e], pos = v.ent_pos[e];
+  const size_t Ns = (size_t)v.N, NPs = (size_t)v.NP;
   const double spv[3] = {sp[p], sp[NPs + p], sp[2 * NPs + p]};
   const double l00 = L[p], l10 = L[NPs + p], l20 = L[2 * NPs + p];
   const double l11 = L[3 * NPs + p], l21 = L[4 * NPs + p], l22 = L[5 * NPs + p];
   double jp0[3], jp1[3];
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
-    jp0[b] = J[(size_t)(2 * b) * Ns + s];
-    jp1[b] = J[(size_t)(2 * b + 1) * Ns + s];
+    jp0[b] = Jp[(size_t)(2 * b) * Ns + s];
+    jp1[b] = Jp[(size_t)(2 * b + 1) * Ns + s];
   }
-  const int col0 = 3 + 6 * slot;
+  double q[14];
+  load_rec(rec, pos, q);
+  double y[18];
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
-    const double ja = J[(size_t)(2 * (col0 + a)) * Ns + s];
-    const double jb = J[(size_t)(2 * (col0 + a) + 1) * Ns + s];
+    const double ja = q[a], jb = q[6 + a];
     const double sa = scc[6 * c + a];
     const double w0 = sa * (ja * jp0[0] + jb * jp1[0]) * spv[0];
     const double w1 = sa * (ja * jp0[1] + jb * jp1[1]) * spv[1];
@@ -587,20 +688,23 @@ __global__ __launch_bounds__(256) void k_entry_y(DevView v, const double* __rest
     const double y0 = w0 / l00;
     const double y1 = (w1 - l10 * y0) / l11;
     const double y2 = (w2 - l20 * y0 - l21 * y1) / l22;
-    Y[(size_t)(3 * a) * NEs + e] = y0;
-    Y[(size_t)(3 * a + 1) * NEs + e] = y1;
-    Y[(size_t)(3 * a + 2) * NEs + e] = y2;
+    y[3 * a] = y0;
+    y[3 * a + 1] = y1;
+    y[3 * a + 2] = y2;
   }
+  double2* out = reinterpret_cast<double2*>(Y + (size_t)kYRec * pos);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) out[i] = make_double2(y[2 * i], y[2 * i + 1]);
 }
 
-void launch_entry_y(hipStream_t s, const DevView& v, const double* J, const double* scale_p,
-                    const double* scale_c, const double* L, double* Y) {
+void launch_entry_y(hipStream_t s, const DevView& v, const double* Jp, const double* rec,
+                    const double* scale_p, const double* scale_c, const double* L, double* Y) {
   if (v.NE <= 0) return;
-  k_entry_y<<<grid_for(v.NE, 256, 1 << 20), 256, 0, s>>>(v, J, scale_p, scale_c, L, Y);
+  k_entry_y<<<grid_for(v.NE, 256, 1 << 20), 256, 0, s>>>(v, Jp, rec, scale_p, scale_c, L, Y);
 }
 
 // one wave per S block; lane (a,b) < 36 accumulates -sum Y_row[a,:] . Y_col[b,:]
-__global__ __launch_bounds__(256) void k_s_blocks(int NE, int nblk, const int* __restrict__ blk_pair_beg,
+__global__ __launch_bounds__(256) void k_s_blocks(int nblk, const int* __restrict__ blk_pair_beg,
                                                   const int2* __restrict__ pairs,
                                                   const double* __restrict__ Y,
                                                   double* __restrict__ packed) {
@@ -608,48 +712,44 @@ __global__ __launch_bounds__(256) void k_s_blocks(int NE, int nblk, const int* _
   const int lane = threadIdx.x & 63;
   if (blk >= nblk || lane >= 36) return;
   const int a = lane / 6, b = lane - 6 * (lane / 6);
-  const size_t NEs = (size_t)NE;
   double acc = 0.0;
   for (int i = blk_pair_beg[blk]; i < blk_pair_beg[blk + 1]; ++i) {
     const int2 pr = pairs[i];
-    acc += Y[(size_t)(3 * a) * NEs + pr.x] * Y[(size_t)(3 * b) * NEs + pr.y] +
-           Y[(size_t)(3 * a + 1) * NEs + pr.x] * Y[(size_t)(3 * b + 1) * NEs + pr.y] +
-           Y[(size_t)(3 * a + 2) * NEs + pr.x] * Y[(size_t)(3 * b + 2) * NEs + pr.y];
+    const double* yr = Y + (size_t)kYRec * pr.x + 3 * a;
+    const double* yc = Y + (size_t)kYRec * pr.y + 3 * b;
+    acc += yr[0] * yc[0] + yr[1] * yc[1] + yr[2] * yc[2];
   }
   packed[36 * (size_t)blk + lane] = -acc;
 }
 
-void launch_s_blocks(hipStream_t s, const DevView& v, int nblk, const int* blk_pair_beg,
-                     const int2* pairs, const double* Y, double* packed) {
+void launch_s_blocks(hipStream_t s, int nblk, const int* blk_pair_beg, const int2* pairs,
+                     const double* Y, double* packed) {
   if (nblk <= 0) return;
-  k_s_blocks<<<(nblk + 3) / 4, 256, 0, s>>>(v.NE, nblk, blk_pair_beg, pairs, Y, packed);
+  k_s_blocks<<<(nblk + 3) / 4, 256, 0, s>>>(nblk, blk_pair_beg, pairs, Y, packed);
 }
 
 __global__ __launch_bounds__(256) void k_cam_rhs_partial(DevView v, const int* __restrict__ chunk_beg,
-                                                         const int* __restrict__ cam_ent,
                                                          const double* __restrict__ Y,
                                                          const double* __restrict__ q,
                                                          double* __restrict__ partial) {
   const int c = blockIdx.x;
   const int b = chunk_beg[c], e = chunk_beg[c + 1];
-  const size_t NEs = (size_t)v.NE, NPs = (size_t)v.NP;
   double acc[6] = {0, 0, 0, 0, 0, 0};
   for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
-    const int en = cam_ent[i];
-    const int p = v.ent_pt[en];
-    const double q0 = q[p], q1 = q[NPs + p], q2 = q[2 * NPs + p];
+    const int p = v.cm_pt[i];
+    const double2 qa = reinterpret_cast<const double2*>(q)[2 * (size_t)p];
+    const double q2 = q[4 * (size_t)p + 2];
+    const double* y = Y + (size_t)kYRec * i;
 #pragma unroll
-    for (int a = 0; a < 6; ++a)
-      acc[a] -= Y[(size_t)(3 * a) * NEs + en] * q0 + Y[(size_t)(3 * a + 1) * NEs + en] * q1 +
-                Y[(size_t)(3 * a + 2) * NEs + en] * q2;
+    for (int a = 0; a < 6; ++a) acc[a] -= y[3 * a] * qa.x + y[3 * a + 1] * qa.y + y[3 * a + 2] * q2;
   }
   block_reduce_store<6>(acc, partial + 6 * (size_t)c);
 }
 
 void launch_cam_rhs_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
-                            const int* cam_ent, const double* Y, const double* q, double* partial) {
+                            const double* Y, const double* q, double* partial) {
   if (nchunk <= 0) return;
-  k_cam_rhs_partial<<<nchunk, 256, 0, s>>>(v, chunk_beg, cam_ent, Y, q, partial);
+  k_cam_rhs_partial<<<nchunk, 256, 0, s>>>(v, chunk_beg, Y, q, partial);
 }
 
 // --- dense reduced camera system ------------------------------------------------------
@@ -662,26 +762,22 @@ __global__ void k_s_scatter(int nblk, const int2* __restrict__ blk_cam, const do
   S[(size_t)(6 * rc.x + a) * lds + 6 * rc.y + b] = packed[t];
 }
 __global__ void k_s_diag(int NC, const double* __restrict__ ug, const double* __restrict__ scc,
-                         StepScalars sc, const double* __restrict__ ybc,
-                         double* __restrict__ S, int lds) {
+                         StepScalars sc, const double* __restrict__ ybc, double* __restrict__ S, int lds) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= NC * 36) return;
   const int c = t / 36, ab = t - 36 * c, a = ab / 6, b = ab - 6 * (ab / 6);
   if (b > a) return;  // lower triangle of the diagonal block
-  // upper-packed index of (b,a), b <= a
-  const int q = b * 6 - (b * (b - 1)) / 2 + (a - b);
+  const int q = b * 6 - (b * (b - 1)) / 2 + (a - b);  // upper-packed index of (b, a)
   const double sa = scc[6 * c + a], sb = scc[6 * c + b];
   double u = sa * ug[27 * (size_t)c + q] * sb;
   if (a == b) {
-    double d = fmin(fmax(u, sc.min_diag), sc.max_diag);
+    const double d = fmin(fmax(u, sc.min_diag), sc.max_diag);
     const double D = sqrt(d / sc.radius);
     u += D * D;
   }
   const size_t n = (size_t)6 * NC;
   S[(size_t)(6 * c + a) * lds + 6 * c + b] += u;
-  if (b == 0) {  // rhs row: b_c = s_c g_c - sum Y q
-    S[n * lds + 6 * c + a] = sa * ug[27 * (size_t)c + 21 + a] + ybc[6 * c + a];
-  }
+  if (b == 0) S[n * lds + 6 * c + a] = sa * ug[27 * (size_t)c + 21 + a] + ybc[6 * c + a];
 }
 __global__ void k_s_cross(int ncross, const int2* __restrict__ cross_cam, const double* __restrict__ X,
                           const double* __restrict__ scc, double* __restrict__ S, int lds) {
@@ -713,17 +809,19 @@ __global__ __launch_bounds__(256) void k_backsub(DevView v, const double* __rest
                                                  double* __restrict__ dp) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= v.NP) return;
-  const size_t NPs = (size_t)v.NP, NEs = (size_t)v.NE;
-  double r0 = q[p], r1 = q[NPs + p], r2 = q[2 * NPs + p];
+  const size_t NPs = (size_t)v.NP;
+  const double2 qa = reinterpret_cast<const double2*>(q)[2 * (size_t)p];
+  double r0 = qa.x, r1 = qa.y, r2 = q[4 * (size_t)p + 2];
   if (yc) {
     for (int e = v.pt_ent_ptr[p]; e < v.pt_ent_ptr[p + 1]; ++e) {
       const int c = v.ent_cam[e];
+      const double* y = Y + (size_t)kYRec * v.ent_pos[e];
 #pragma unroll
       for (int a = 0; a < 6; ++a) {
-        const double y = yc[6 * c + a];
-        r0 -= Y[(size_t)(3 * a) * NEs + e] * y;
-        r1 -= Y[(size_t)(3 * a + 1) * NEs + e] * y;
-        r2 -= Y[(size_t)(3 * a + 2) * NEs + e] * y;
+        const double ycv = yc[6 * c + a];
+        r0 -= y[3 * a] * ycv;
+        r1 -= y[3 * a + 1] * ycv;
+        r2 -= y[3 * a + 2] * ycv;
       }
     }
   }
@@ -788,7 +886,8 @@ void launch_cam_candidate(hipStream_t s, int E, const int* ext_col, const double
   k_cam_candidate<<<grid_for(6 * E, 256, 1 << 20), 256, 0, s>>>(E, ext_col, ext, yc, scale_c, ext_c, delta_c);
 }
 
-__global__ __launch_bounds__(256) void k_candidate(DevView v, const double* __restrict__ J,
+__global__ __launch_bounds__(256) void k_candidate(DevView v, const double* __restrict__ Jp,
+                                                   const double* __restrict__ rec,
                                                    const double2* __restrict__ r,
                                                    const double* __restrict__ dp,
                                                    const double* __restrict__ dc,
@@ -799,31 +898,32 @@ __global__ __launch_bounds__(256) void k_candidate(DevView v, const double* __re
   const size_t Ns = (size_t)v.N, NPs = (size_t)v.NP;
   for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < v.N; s += gridDim.x * blockDim.x) {
     const int4 id = v.obs_idx[s];
+    const int2 ent = v.obs_ent[s];
     double m0 = 0.0, m1 = 0.0;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const double d = dp[c * NPs + id.x];
-      m0 += J[(size_t)(2 * c) * Ns + s] * d;
-      m1 += J[(size_t)(2 * c + 1) * Ns + s] * d;
+      m0 += Jp[(size_t)(2 * c) * Ns + s] * d;
+      m1 += Jp[(size_t)(2 * c + 1) * Ns + s] * d;
     }
-    const int c0 = v.ext_col[id.y];
-    if (c0 >= 0) {
+    if (ent.x >= 0) {
+      double q[14];
+      load_rec(rec, ent.x, q);
+      const double* d = dc + 6 * v.ext_col[id.y];
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
-        const double d = dc[6 * c0 + k];
-        m0 += J[(size_t)(2 * (3 + k)) * Ns + s] * d;
-        m1 += J[(size_t)(2 * (3 + k) + 1) * Ns + s] * d;
+        m0 += q[k] * d[k];
+        m1 += q[6 + k] * d[k];
       }
     }
-    if (id.z >= 0) {
-      const int c1 = v.ext_col[id.z];
-      if (c1 >= 0) {
+    if (ent.y >= 0) {
+      double q[14];
+      load_rec(rec, ent.y, q);
+      const double* d = dc + 6 * v.ext_col[id.z];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
-          const double d = dc[6 * c1 + k];
-          m0 += J[(size_t)(2 * (9 + k)) * Ns + s] * d;
-          m1 += J[(size_t)(2 * (9 + k) + 1) * Ns + s] * d;
-        }
+      for (int k = 0; k < 6; ++k) {
+        m0 += q[k] * d[k];
+        m1 += q[6 + k] * d[k];
       }
     }
     const double2 rr = r[s];
@@ -836,11 +936,11 @@ __global__ __launch_bounds__(256) void k_candidate(DevView v, const double* __re
   block_reduce_store<3>(acc, partial + 3 * (size_t)blockIdx.x);
 }
 
-void launch_candidate(hipStream_t s, const DevView& v, const double* J, const double* r,
+void launch_candidate(hipStream_t s, const DevView& v, const double* Jp, const double* rec, const double* r,
                       const double* delta_p, const double* delta_c, const double* points_c,
                       const double* camtab_c, double* partial, int grid) {
-  k_candidate<<<grid, 256, 0, s>>>(v, J, reinterpret_cast<const double2*>(r), delta_p, delta_c, points_c,
-                                   camtab_c, partial);
+  k_candidate<<<grid, 256, 0, s>>>(v, Jp, rec, reinterpret_cast<const double2*>(r), delta_p, delta_c,
+                                   points_c, camtab_c, partial);
 }
 
 __global__ __launch_bounds__(256) void k_grad_points(int NP, const double* __restrict__ x,
@@ -856,7 +956,6 @@ __global__ __launch_bounds__(256) void k_grad_points(int NP, const double* __res
     acc[1] += d * d;
     acc[2] += xv * xv;
   }
-  // max needs its own reduction
   __shared__ double shm[kRedBlock / 64];
   double m = acc[0];
 #pragma unroll

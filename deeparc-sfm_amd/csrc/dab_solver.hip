@@ -119,7 +119,7 @@ struct dab_handle {
   std::vector<int> perm;            // sorted obs -> caller's obs index
   std::vector<int> pt_of;           // local point -> caller's point id
   std::vector<int> ext_col;         // ext -> free camera column
-  int nchunk = 0, nxchunk = 0, ncross = 0, nblk = 0;
+  int nchunk = 0, nxchunk = 0, ncross = 0, nblk = 0, nwin = 0, nstrad = 0;
   long long npairs = 0;
   int lds = 0;                      // leading dim of dense S
 
@@ -128,9 +128,11 @@ struct dab_handle {
   DevView view{};
   int4* d_obs_idx = nullptr;
   double2* d_obs_xy = nullptr;
+  int2* d_obs_ent = nullptr;
+  int4* d_strad = nullptr;
   int *d_pt_obs_ptr = nullptr, *d_pt_ent_ptr = nullptr, *d_ent_os = nullptr, *d_ent_cam = nullptr,
-      *d_ent_pt = nullptr, *d_ext_col = nullptr;
-  int *d_cam_ent = nullptr, *d_chunk_beg = nullptr, *d_seg_chunk = nullptr;
+      *d_ent_pt = nullptr, *d_ent_pos = nullptr, *d_cm_pt = nullptr, *d_ext_col = nullptr;
+  int *d_chunk_beg = nullptr, *d_seg_chunk = nullptr;
   int *d_xobs = nullptr, *d_xchunk_beg = nullptr, *d_xseg_chunk = nullptr;
   int2* d_cross_cam = nullptr;
   int2 *d_pairs = nullptr, *d_blk_cam = nullptr;
@@ -138,7 +140,8 @@ struct dab_handle {
   double* d_intr = nullptr;
   double *d_points = nullptr, *d_points_c = nullptr, *d_ext = nullptr, *d_ext_c = nullptr;
   double *d_camtab = nullptr, *d_camtab_c = nullptr;
-  double *d_r = nullptr, *d_J = nullptr;
+  double *d_r = nullptr, *d_Jp = nullptr, *d_rec = nullptr, *d_wpart = nullptr;
+  double* d_Jfull = nullptr;  // parity API only (lazily allocated)
   double *d_V = nullptr, *d_g = nullptr, *d_scale_p = nullptr, *d_scale_c = nullptr;
   double *d_L = nullptr, *d_q = nullptr, *d_Y = nullptr;
   double* d_camred = nullptr;  // [Ucc NC*21 | gc NC*6 | Ux ncross*36] (all-reduced)
@@ -394,6 +397,26 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   seg_chunk[NC] = (int)chunk_beg.size();
   h->nchunk = (int)chunk_beg.size();
   chunk_beg.push_back(NE);
+  // camera-major record positions of the entries, and per observation
+  std::vector<int> ent_pos(NE), cm_pt(NE);
+  for (int i = 0; i < NE; ++i) {
+    ent_pos[cam_ent[i]] = i;
+    cm_pt[i] = ent_pt[cam_ent[i]];
+  }
+  std::vector<int2> obs_ent(N, make_int2(-1, -1));
+  for (int e = 0; e < NE; ++e) {
+    const int s2 = ent_os[e] >> 1;
+    if (ent_os[e] & 1) obs_ent[s2].y = ent_pos[e];
+    else obs_ent[s2].x = ent_pos[e];
+  }
+  // points whose observations straddle a 64-observation window (segmented V/g fix-up)
+  h->nwin = (N + kWin - 1) / kWin;
+  std::vector<int4> strad;
+  for (int pt = 0; pt < NP; ++pt) {
+    const int a = pt_obs_ptr[pt], b = pt_obs_ptr[pt + 1];
+    if (b > a && a / kWin != (b - 1) / kWin) strad.push_back(make_int4(pt, a / kWin, (b - 1) / kWin, 0));
+  }
+  h->nstrad = (int)strad.size();
 
   // arc∘ring cross blocks: composed observations whose two cameras are both free.
   // The pair table is the union over ranks so the all-reduced layout matches.
@@ -474,7 +497,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
     pairs.resize(tmp.size());
     std::vector<long long> local_keys;
     for (size_t i = 0; i < tmp.size(); ++i) {
-      pairs[i] = make_int2(tmp[i].e, tmp[i].f);
+      pairs[i] = make_int2(ent_pos[tmp[i].e], ent_pos[tmp[i].f]);  // Y records are camera-major
       if (local_keys.empty() || local_keys.back() != tmp[i].key) local_keys.push_back(tmp[i].key);
     }
     // diagonal blocks always exist; union across ranks
@@ -539,7 +562,10 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   CHECK_RC(upload(&h->d_ent_cam, d, ent_cam, s));
   CHECK_RC(upload(&h->d_ent_pt, d, ent_pt, s));
   CHECK_RC(upload(&h->d_ext_col, d, h->ext_col, s));
-  CHECK_RC(upload(&h->d_cam_ent, d, cam_ent, s));
+  CHECK_RC(upload(&h->d_ent_pos, d, ent_pos, s));
+  CHECK_RC(upload(&h->d_cm_pt, d, cm_pt, s));
+  CHECK_RC(upload(&h->d_obs_ent, d, obs_ent, s));
+  CHECK_RC(upload(&h->d_strad, d, strad, s));
   CHECK_RC(upload(&h->d_chunk_beg, d, chunk_beg, s));
   CHECK_RC(upload(&h->d_seg_chunk, d, seg_chunk, s));
   CHECK_RC(upload(&h->d_xobs, d, xobs, s));
@@ -557,14 +583,17 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   CHECK_RC(d.alloc(&h->d_camtab, (size_t)kCamTab * h->E));
   CHECK_RC(d.alloc(&h->d_camtab_c, (size_t)kCamTab * h->E));
   CHECK_RC(d.alloc(&h->d_r, (size_t)2 * N));
-  CHECK_RC(d.alloc(&h->d_J, (size_t)h->nplanes * N));
+  CHECK_RC(d.alloc(&h->d_Jp, (size_t)6 * N));
+  CHECK_RC(d.alloc(&h->d_rec, (size_t)kRec * NE));
+  CHECK_RC(d.alloc(&h->d_wpart, (size_t)18 * h->nwin));
+  h->d_Jfull = nullptr;
   CHECK_RC(d.alloc(&h->d_V, (size_t)6 * NP));
   CHECK_RC(d.alloc(&h->d_g, (size_t)3 * NP));
   CHECK_RC(d.alloc(&h->d_scale_p, (size_t)3 * NP));
   CHECK_RC(d.alloc(&h->d_scale_c, (size_t)6 * NC));
   CHECK_RC(d.alloc(&h->d_L, (size_t)6 * NP));
-  CHECK_RC(d.alloc(&h->d_q, (size_t)3 * NP));
-  CHECK_RC(d.alloc(&h->d_Y, (size_t)18 * NE));
+  CHECK_RC(d.alloc(&h->d_q, (size_t)4 * NP));
+  CHECK_RC(d.alloc(&h->d_Y, (size_t)kYRec * NE));
   CHECK_RC(d.alloc(&h->d_camred, h->camred_count()));
   const size_t npart = std::max<size_t>({(size_t)h->nchunk * 27, (size_t)h->nxchunk * 36, (size_t)h->nchunk * 6, 16});
   CHECK_RC(d.alloc(&h->d_partial, npart));
@@ -589,14 +618,17 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   v.E = h->E;
   v.NC = NC;
   v.NE = NE;
-  v.nplanes = h->nplanes;
+  v.nwin = h->nwin;
   v.obs_idx = h->d_obs_idx;
   v.obs_xy = h->d_obs_xy;
+  v.obs_ent = h->d_obs_ent;
   v.pt_obs_ptr = h->d_pt_obs_ptr;
   v.pt_ent_ptr = h->d_pt_ent_ptr;
   v.ent_os = h->d_ent_os;
   v.ent_cam = h->d_ent_cam;
   v.ent_pt = h->d_ent_pt;
+  v.ent_pos = h->d_ent_pos;
+  v.cm_pt = h->d_cm_pt;
   v.ext_col = h->d_ext_col;
   v.intr = h->d_intr;
   h->have_problem = true;
@@ -642,20 +674,23 @@ extern "C" int dab_get_parameters(dab_handle* h, double* points, double* ext) {
 // ------------------------------------------------------------------------------------
 // evaluation building blocks
 // ------------------------------------------------------------------------------------
-// Residual + Jacobian at the current x and the J^T J / J^T r blocks (camera side
-// all-reduced). Leaves cost / gradient scalars in d_scal (point parts all-reduced).
-static int eval_jacobian_and_blocks(dab_handle* h, bool with_norms) {
+// The evaluation pass proper (the benchmark "step"): residual + Jacobian kernel with the
+// fused point blocks V, g, the straddling-point fix-up, the camera blocks U, g_c (and the
+// arc∘ring cross blocks) over contiguous records, all-reduced across ranks, and the cost.
+// Expects the camera tables of the current x in d_camtab.
+static int eval_core(dab_handle* h) {
   hipStream_t s = h->stream;
   const DevView& v = h->view;
-  launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
-  launch_jacobian(s, v, h->d_points, h->d_camtab, h->d_r, h->d_J);
-  launch_point_vg(s, v, h->d_r, h->d_J, h->d_V, h->d_g);
+  launch_jacobian(s, v, h->d_points, h->d_camtab, h->d_r, h->d_Jp, h->d_rec, h->d_V, h->d_g, h->d_wpart,
+                  h->d_gpart, h->red_grid);
+  launch_point_fixup(s, h->nstrad, h->d_strad, h->d_wpart, h->NP, h->d_V, h->d_g);
+  launch_final_sum(s, h->red_grid, 2, h->d_gpart, h->d_scal + S_COST);
   if (h->NC > 0) {
-    launch_cam_ug_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_cam_ent, h->d_r, h->d_J, h->d_partial);
+    launch_cam_ug_partial(s, h->nchunk, h->d_chunk_beg, h->d_rec, h->d_partial);
     launch_seg_final(s, h->NC, 27, h->d_seg_chunk, h->d_partial, h->ug());
     if (h->ncross > 0) {
       if (h->nxchunk > 0) {
-        launch_cross_partial(s, v, h->nxchunk, h->d_xchunk_beg, h->d_xobs, h->d_J, h->d_partial);
+        launch_cross_partial(s, v, h->nxchunk, h->d_xchunk_beg, h->d_xobs, h->d_rec, h->d_partial);
         launch_seg_final(s, h->ncross, 36, h->d_xseg_chunk, h->d_partial, h->Ux());
       } else {
         HIP_OK(hipMemsetAsync(h->Ux(), 0, sizeof(double) * 36 * (size_t)h->ncross, s));
@@ -663,8 +698,15 @@ static int eval_jacobian_and_blocks(dab_handle* h, bool with_norms) {
     }
     CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
   }
-  launch_r_sumsq(s, h->N, h->d_r, h->d_gpart, h->red_grid);
-  launch_final_sum(s, h->red_grid, 2, h->d_gpart, h->d_scal + S_COST);
+  return 0;
+}
+
+// Residual + Jacobian at the current x and the J^T J / J^T r blocks (camera side
+// all-reduced). Leaves cost / gradient scalars in d_scal (point parts all-reduced).
+static int eval_jacobian_and_blocks(dab_handle* h, bool with_norms) {
+  hipStream_t s = h->stream;
+  launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
+  CHECK_RC(eval_core(h));
   if (with_norms) {
     launch_grad_points(s, h->NP, h->d_points, h->d_g, h->d_gpart, h->red_grid);
     launch_final_sum(s, h->red_grid, 3, h->d_gpart, h->d_scal + S_GMAX_P, 1u);
@@ -834,9 +876,9 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
     HIP_OK(hipMemsetAsync(h->d_flags, 0, sizeof(int) * 4, s));
     launch_point_factor(s, v, h->d_V, h->d_g, h->d_scale_p, sc, h->d_L, h->d_q, h->d_flags);
     if (NC > 0) {
-      launch_entry_y(s, v, h->d_J, h->d_scale_p, h->d_scale_c, h->d_L, h->d_Y);
-      launch_s_blocks(s, v, h->nblk, h->d_blk_pair_beg, h->d_pairs, h->d_Y, h->packed());
-      launch_cam_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_cam_ent, h->d_Y, h->d_q, h->d_partial);
+      launch_entry_y(s, v, h->d_Jp, h->d_rec, h->d_scale_p, h->d_scale_c, h->d_L, h->d_Y);
+      launch_s_blocks(s, h->nblk, h->d_blk_pair_beg, h->d_pairs, h->d_Y, h->packed());
+      launch_cam_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_Y, h->d_q, h->d_partial);
       launch_seg_final(s, NC, 6, h->d_seg_chunk, h->d_partial, h->ybc());
       CHECK_RC(h->allreduce(h->d_spack, h->spack_count(), ncclSum));
       launch_s_unpack(s, NC, h->nblk, h->d_blk_cam, h->packed(), h->ug(), h->ncross, h->d_cross_cam, h->Ux(),
@@ -853,8 +895,8 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
     launch_cam_norms(s, h->E, h->d_ext_col, h->d_ext, h->d_ext_c, nullptr, h->d_scal + S_CAM0);
     launch_cam_tables(s, h->E, h->d_ext_c, h->d_camtab_c);
     const double tre = now_s();
-    launch_candidate(s, v, h->d_J, h->d_r, h->d_dp, h->d_dc, h->d_points_c, h->d_camtab_c, h->d_gpart,
-                     h->red_grid);
+    launch_candidate(s, v, h->d_Jp, h->d_rec, h->d_r, h->d_dp, h->d_dc, h->d_points_c, h->d_camtab_c,
+                     h->d_gpart, h->red_grid);
     launch_final_sum(s, h->red_grid, 3, h->d_gpart, h->d_scal + S_MODEL);
     CHECK_RC(h->allreduce(h->d_scal + S_MODEL, 5, ncclSum));
     if (h->world > 1) NCCL_OK(ncclAllReduce(h->d_flags, h->d_flags, 4, ncclInt32, ncclMax, h->comm, s));
@@ -973,11 +1015,12 @@ extern "C" int dab_eval_jacobians(dab_handle* h, double* residuals, double* jaco
   if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
   HIP_OK(hipSetDevice(h->device));
   hipStream_t s = h->stream;
+  if (!h->d_Jfull) CHECK_RC(h->dev.alloc(&h->d_Jfull, (size_t)30 * h->N));
   launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
-  launch_jacobian(s, h->view, h->d_points, h->d_camtab, h->d_r, h->d_J);
-  std::vector<double> r((size_t)2 * h->N), J((size_t)h->nplanes * h->N);
+  launch_jacobian_full(s, h->view, h->d_points, h->d_camtab, h->d_r, h->d_Jfull);
+  std::vector<double> r((size_t)2 * h->N), J((size_t)30 * h->N);
   HIP_OK(hipMemcpyAsync(r.data(), h->d_r, r.size() * sizeof(double), hipMemcpyDeviceToHost, s));
-  HIP_OK(hipMemcpyAsync(J.data(), h->d_J, J.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(J.data(), h->d_Jfull, J.size() * sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
   for (int s2 = 0; s2 < h->N; ++s2) {
     const int o = h->perm[s2];
@@ -1010,21 +1053,21 @@ extern "C" int dab_bench_eval_pass(dab_handle* h, int with_assembly) {
   const DevView& v = h->view;
   launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
   HIP_OK(hipEventRecord(h->ev0, s));
-  launch_jacobian(s, v, h->d_points, h->d_camtab, h->d_r, h->d_J);
+  launch_jacobian(s, v, h->d_points, h->d_camtab, h->d_r, h->d_Jp, h->d_rec, h->d_V, h->d_g, h->d_wpart,
+                  h->d_gpart, h->red_grid);
   HIP_OK(hipEventRecord(h->ev1, s));
   if (with_assembly) {
-    launch_point_vg(s, v, h->d_r, h->d_J, h->d_V, h->d_g);
+    launch_point_fixup(s, h->nstrad, h->d_strad, h->d_wpart, h->NP, h->d_V, h->d_g);
+    launch_final_sum(s, h->red_grid, 2, h->d_gpart, h->d_scal + S_COST);
     if (h->NC > 0) {
-      launch_cam_ug_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_cam_ent, h->d_r, h->d_J, h->d_partial);
+      launch_cam_ug_partial(s, h->nchunk, h->d_chunk_beg, h->d_rec, h->d_partial);
       launch_seg_final(s, h->NC, 27, h->d_seg_chunk, h->d_partial, h->ug());
       if (h->ncross > 0 && h->nxchunk > 0) {
-        launch_cross_partial(s, v, h->nxchunk, h->d_xchunk_beg, h->d_xobs, h->d_J, h->d_partial);
+        launch_cross_partial(s, v, h->nxchunk, h->d_xchunk_beg, h->d_xobs, h->d_rec, h->d_partial);
         launch_seg_final(s, h->ncross, 36, h->d_xseg_chunk, h->d_partial, h->Ux());
       }
       CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
     }
-    launch_r_sumsq(s, h->N, h->d_r, h->d_gpart, h->red_grid);
-    launch_final_sum(s, h->red_grid, 2, h->d_gpart, h->d_scal + S_COST);
     CHECK_RC(h->allreduce(h->d_scal + S_COST, 2, ncclSum));
   }
   HIP_OK(hipEventRecord(h->ev2, s));
@@ -1060,12 +1103,17 @@ extern "C" int dab_bench_kernel_ms(dab_handle* h, double* jac_ms, double* assemb
 extern "C" int dab_jacobian_bytes(dab_handle* h, double* bytes) {
   clear_error();
   if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
-  // algorithmic bytes of one residual+Jacobian launch: per observation
-  // idx 16 + xy 16 + r 16 + J 8*(18|30); parameters once: points 24/pt, tables 256/ext,
-  // intrinsics 64 each
-  long long ncomp = 0;
-  for (int o = 0; o < h->N; ++o) ncomp += h->prob.obs_ext1[o] >= 0;
-  const double per_single = 16 + 16 + 16 + 8.0 * 18, per_comp = 16 + 16 + 16 + 8.0 * 30;
-  *bytes = (h->N - ncomp) * per_single + ncomp * per_comp + 24.0 * h->NP + 8.0 * kCamTab * h->E + 64.0 * h->NI;
+  // Algorithmic bytes of one residual+Jacobian launch, SURVEY §8d:
+  //   B = sum_obs (16 xy + 4 n_idx + 16 r + 16 k) + 24 N_pts + 48 N_ext + 48 N_intr
+  // with k = free columns of the observation (3 + 6 per free extrinsic) and n_idx = 2
+  // (single) or 3 (arc∘ring) index words. The kernel's own extra traffic (records padded
+  // to 128 B, camera-major positions, fused V/g) is deliberately not counted.
+  double b = 24.0 * h->NP + 48.0 * h->E + 48.0 * h->NI;
+  for (int o = 0; o < h->N; ++o) {
+    const int e0 = h->prob.obs_ext0[o], e1 = h->prob.obs_ext1[o];
+    const int k = 3 + 6 * (h->ext_col[e0] >= 0) + 6 * (e1 >= 0 && h->ext_col[e1] >= 0);
+    b += 16.0 + 4.0 * (e1 >= 0 ? 3 : 2) + 16.0 + 16.0 * k;
+  }
+  *bytes = b;
   return 0;
 }
