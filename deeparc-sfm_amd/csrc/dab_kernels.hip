@@ -276,52 +276,58 @@ struct ObsJac {
   double jt1a[3], jt1b[3];  // d r / d t1   (d r / d t0 = pr.A0 / pr.A1)
 };
 
+// The table is read in the order the math needs it (R,t -> project -> A R -> Rd -> Jd) so
+// that only one 3x3 block per camera is live at a time (register pressure sets occupancy).
 __device__ __forceinline__ void obs_jacobian(const int4 id, const double2 xy, const double X[3],
                                              const double* __restrict__ camtab,
                                              const double* __restrict__ K, ObsJac& o) {
-  double T0[30];
-  load_tab<30>(camtab, id.y, T0);
-  if (id.z >= 0) {
-    double T1[30];
-    load_tab<30>(camtab, id.z, T1);
-    double P2[3], P[3];
-    matvec_add(T1, X, T1 + 9, P2);
-    matvec_add(T0, P2, T0 + 9, P);
-    project(P, K, xy.x, xy.y, o.pr, true);
-    double B0a[3], B0b[3];
-    rowmat(o.pr.A0, T0, B0a);  // A R0
-    rowmat(o.pr.A1, T0, B0b);
-    rowmat(B0a, T1, o.jx0);    // A R0 R1
+  // One uniform flow for both forms; the branch only selects values (a select between two
+  // private arrays would force them into scratch). Q is the point the arc/single rotation
+  // acts on: X (single) or P2 = R1 X + t1 (arc∘ring).
+  const bool comp = id.z >= 0;
+  const double* __restrict__ T0 = camtab + (size_t)kCamTab * id.y;
+  const double* __restrict__ T1 = camtab + (size_t)kCamTab * (comp ? id.z : id.y);
+  double Q[3];
+  if (comp) {
+    matvec_add(T1, X, T1 + 9, Q);
+  } else {
+    Q[0] = X[0];
+    Q[1] = X[1];
+    Q[2] = X[2];
+  }
+  double P[3];
+  matvec_add(T0, Q, T0 + 9, P);
+  project(P, K, xy.x, xy.y, o.pr, true);
+  double B0a[3], B0b[3];
+  rowmat(o.pr.A0, T0, B0a);  // A R0 = d r / d Q
+  rowmat(o.pr.A1, T0, B0b);
+  if (comp) {
+    rowmat(B0a, T1, o.jx0);  // A R0 R1
     rowmat(B0b, T1, o.jx1);
     double Ca[3], Cb[3];
     rowmat(B0a, T1 + 12, Ca);  // A R0 Rd1
     rowmat(B0b, T1 + 12, Cb);
     dwrot(Ca, X, T1 + 21, o.jw1a);
     dwrot(Cb, X, T1 + 21, o.jw1b);
-    double Da[3], Db[3];
-    rowmat(o.pr.A0, T0 + 12, Da);  // A Rd0
-    rowmat(o.pr.A1, T0 + 12, Db);
-    dwrot(Da, P2, T0 + 21, o.jw0a);
-    dwrot(Db, P2, T0 + 21, o.jw0b);
+  } else {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      o.jt1a[i] = B0a[i];
-      o.jt1b[i] = B0b[i];
+      o.jx0[i] = B0a[i];
+      o.jx1[i] = B0b[i];
+      o.jw1a[i] = 0.0;
+      o.jw1b[i] = 0.0;
     }
-  } else {
-    double P[3];
-    matvec_add(T0, X, T0 + 9, P);
-    project(P, K, xy.x, xy.y, o.pr, true);
-    rowmat(o.pr.A0, T0, o.jx0);
-    rowmat(o.pr.A1, T0, o.jx1);
-    double Da[3], Db[3];
-    rowmat(o.pr.A0, T0 + 12, Da);
-    rowmat(o.pr.A1, T0 + 12, Db);
-    dwrot(Da, X, T0 + 21, o.jw0a);
-    dwrot(Db, X, T0 + 21, o.jw0b);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) o.jw1a[i] = o.jw1b[i] = o.jt1a[i] = o.jt1b[i] = 0.0;
   }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {  // d r / d t1 = A R0 (zero when single)
+    o.jt1a[i] = comp ? B0a[i] : 0.0;
+    o.jt1b[i] = comp ? B0b[i] : 0.0;
+  }
+  double Da[3], Db[3];
+  rowmat(o.pr.A0, T0 + 12, Da);  // A Rd0
+  rowmat(o.pr.A1, T0 + 12, Db);
+  dwrot(Da, Q, T0 + 21, o.jw0a);
+  dwrot(Db, Q, T0 + 21, o.jw0b);
 }
 
 __device__ __forceinline__ void store_rec(double* __restrict__ rec, int pos, const double wa[3],
@@ -340,12 +346,15 @@ __device__ __forceinline__ void store_rec(double* __restrict__ rec, int pos, con
 
 // Product kernel. Block = 256 threads = 4 waves; wave windows of 64 consecutive
 // observations, grid-strided. V/g use an inclusive segmented scan keyed by point id.
-__global__ __launch_bounds__(256) void k_jacobian(DevView v, const double* __restrict__ points,
-                                                  const double* __restrict__ camtab,
-                                                  double2* __restrict__ r, double* __restrict__ Jp,
-                                                  double* __restrict__ rec, double* __restrict__ V,
-                                                  double* __restrict__ g, double* __restrict__ wpart,
-                                                  double* __restrict__ partial) {
+// VAR (ablation only, bench knob DAB_JAC_VARIANT): bit0 skip records, bit1 skip the V/g
+// scan, bit2 skip the Jp planes. MINW: __launch_bounds__ waves per SIMD.
+template <int VAR, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_jacobian(DevView v, const double* __restrict__ points,
+                                                        const double* __restrict__ camtab,
+                                                        double2* __restrict__ r, double* __restrict__ Jp,
+                                                        double* __restrict__ rec, double* __restrict__ V,
+                                                        double* __restrict__ g, double* __restrict__ wpart,
+                                                        double* __restrict__ partial) {
   const int N = v.N;
   const size_t Ns = (size_t)N, NPs = (size_t)v.NP;
   const int lane = threadIdx.x & 63;
@@ -365,13 +374,19 @@ __global__ __launch_bounds__(256) void k_jacobian(DevView v, const double* __res
       obs_jacobian(id, xy, X, camtab, v.intr + (size_t)kIntr * id.w, o);
       const double ru = o.pr.ru, rv = o.pr.rv;
       r[s] = make_double2(ru, rv);
+      if constexpr (!(VAR & 4)) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        Jp[(2 * k) * Ns + s] = o.jx0[k];
-        Jp[(2 * k + 1) * Ns + s] = o.jx1[k];
+        for (int k = 0; k < 3; ++k) {
+          Jp[(2 * k) * Ns + s] = o.jx0[k];
+          Jp[(2 * k + 1) * Ns + s] = o.jx1[k];
+        }
       }
-      if (ent.x >= 0) store_rec(rec, ent.x, o.jw0a, o.jw0b, o.pr.A0, o.pr.A1, ru, rv);
-      if (ent.y >= 0) store_rec(rec, ent.y, o.jw1a, o.jw1b, o.jt1a, o.jt1b, ru, rv);
+      if constexpr (!(VAR & 1)) {
+        if (ent.x >= 0) store_rec(rec, ent.x, o.jw0a, o.jw0b, o.pr.A0, o.pr.A1, ru, rv);
+        if (ent.y >= 0) store_rec(rec, ent.y, o.jw1a, o.jw1b, o.jt1a, o.jt1b, ru, rv);
+      } else {
+        asm volatile("" ::"v"(o.jw0a[0]), "v"(o.jw0b[2]), "v"(o.jw1a[1]), "v"(o.jt1b[2]), "v"(ent.x));
+      }
       c[0] = o.jx0[0] * o.jx0[0] + o.jx1[0] * o.jx1[0];
       c[1] = o.jx0[0] * o.jx0[1] + o.jx1[0] * o.jx1[1];
       c[2] = o.jx0[0] * o.jx0[2] + o.jx1[0] * o.jx1[2];
@@ -386,6 +401,10 @@ __global__ __launch_bounds__(256) void k_jacobian(DevView v, const double* __res
     } else {
 #pragma unroll
       for (int k = 0; k < 9; ++k) c[k] = 0.0;
+    }
+    if constexpr ((VAR & 2) != 0) {
+      asm volatile("" ::"v"(c[0]), "v"(c[5]), "v"(c[8]));
+      continue;
     }
     // inclusive segmented scan (Hillis–Steele) within the 64-lane window
 #pragma unroll
@@ -426,8 +445,26 @@ __global__ __launch_bounds__(256) void k_jacobian(DevView v, const double* __res
 void launch_jacobian(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                      double* r, double* Jp, double* rec, double* V, double* g, double* wpart,
                      double* partial, int grid) {
-  k_jacobian<<<grid, 256, 0, s>>>(v, points, camtab, reinterpret_cast<double2*>(r), Jp, rec, V, g, wpart,
-                                  partial);
+  // bench-only ablation knob (scripts/jac_ablation.py); unset = the product kernel
+  const char* env = getenv("DAB_JAC_VARIANT");
+  const int variant = env ? atoi(env) : 0;
+  double2* r2 = reinterpret_cast<double2*>(r);
+#define JAC_LAUNCH(VAR, MINW) \
+  k_jacobian<VAR, MINW><<<grid, 256, 0, s>>>(v, points, camtab, r2, Jp, rec, V, g, wpart, partial)
+  switch (variant) {
+    case 0: JAC_LAUNCH(0, 2); break;   // product default
+    case 100: JAC_LAUNCH(0, 3); break;
+    case 200: JAC_LAUNCH(0, 4); break;
+    case 1: JAC_LAUNCH(1, 2); break;
+    case 2: JAC_LAUNCH(2, 2); break;
+    case 3: JAC_LAUNCH(3, 2); break;
+    case 7: JAC_LAUNCH(7, 2); break;
+    case 201: JAC_LAUNCH(1, 4); break;
+    case 203: JAC_LAUNCH(3, 4); break;
+    case 207: JAC_LAUNCH(7, 4); break;
+    default: JAC_LAUNCH(0, 2); break;
+  }
+#undef JAC_LAUNCH
 }
 
 __global__ void k_point_fixup(int nstrad, const int4* __restrict__ strad, const double* __restrict__ wpart,

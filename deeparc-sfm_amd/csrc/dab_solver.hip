@@ -1042,6 +1042,41 @@ extern "C" int dab_eval_jacobians(dab_handle* h, double* residuals, double* jaco
   return 0;
 }
 
+extern "C" int dab_dense_spd_solve(dab_handle* h, int n, const double* A, const double* b, double* x,
+                                   double* factor_ms) {
+  clear_error();
+  if (!h) return set_error(DAB_E_INVALID, "null handle");
+  if (n < 0 || (n > 0 && (!A || !b || !x))) return set_error(DAB_E_INVALID, "bad dense solve arguments");
+  if (n == 0) return 0;
+  HIP_OK(hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  int lds = ((n + 1 + 7) / 8) * 8;
+  if (lds % 512 == 0) lds += 8;
+  Dev tmp;
+  double *dA = nullptr, *dy = nullptr;
+  int* dflag = nullptr;
+  CHECK_RC(tmp.alloc(&dA, (size_t)(n + 1) * lds));
+  CHECK_RC(tmp.alloc(&dy, (size_t)n));
+  CHECK_RC(tmp.alloc(&dflag, 1));
+  HIP_OK(hipMemsetAsync(dA, 0, sizeof(double) * (size_t)(n + 1) * lds, s));
+  HIP_OK(hipMemsetAsync(dflag, 0, sizeof(int), s));
+  HIP_OK(hipMemcpy2DAsync(dA, lds * sizeof(double), A, n * sizeof(double), n * sizeof(double), n,
+                          hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemcpyAsync(dA + (size_t)n * lds, b, n * sizeof(double), hipMemcpyHostToDevice, s));
+  HIP_OK(hipEventRecord(h->ev0, s));
+  if (chol_factor_solve(h->chol, s, n, dA, lds, dy, dflag) != 0)
+    return set_error(DAB_E_DEVICE, "dense factorisation launch failed");
+  HIP_OK(hipEventRecord(h->ev1, s));
+  int flag = 0;
+  HIP_OK(hipMemcpyAsync(x, dy, n * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(&flag, dflag, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  float ms = 0.f;
+  HIP_OK(hipEventElapsedTime(&ms, h->ev0, h->ev1));
+  if (factor_ms) *factor_ms = ms;
+  return flag ? 1 : 0;
+}
+
 // ------------------------------------------------------------------------------------
 // benchmark hooks
 // ------------------------------------------------------------------------------------

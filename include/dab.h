@@ -191,6 +191,14 @@ int dab_get_parameters(dab_handle* h, double* points, double* ext);
 int dab_eval_residuals(dab_handle* h, double* residuals, double* cost);
 int dab_eval_jacobians(dab_handle* h, double* residuals, double* jacobians);
 
+/* Dense SPD solve A x = b on the handle's device with the library's blocked Cholesky (the
+ * reduced-camera-system factorisation of DAB_LINEAR_SOLVER_EXPLICIT_SCHUR; Eigen LLT in
+ * Ceres' DENSE_SCHUR). A: n x n row-major, only the lower triangle is read. factor_ms
+ * (nullable): device time of factorisation + solves. Returns DAB_OK, 1 when A is not
+ * numerically positive definite, or a negative error. */
+int dab_dense_spd_solve(dab_handle* h, int n, const double* A, const double* b, double* x,
+                        double* factor_ms);
+
 /* ---- benchmark hooks -------------------------------------------------------------------
  * One evaluation pass on device-resident data: residual+Jacobian kernel followed by the
  * JtJ / Jtr block assembly (per-point V,g and per-camera U,g; all-reduced across ranks).
