@@ -117,6 +117,37 @@ void launch_candidate(hipStream_t s, const DevView& v, const double* Jp, const d
 void launch_grad_points(hipStream_t s, int NP, const double* x, const double* g /*[3][NP]*/,
                         double* partial, int grid);
 
+// ---- implicit-Schur PCG (dab_pcg.hip) -------------------------------------------------------
+enum { kPcgRunning = 0, kPcgSuccess = 1, kPcgNoConvergence = 2, kPcgFailure = 3 };
+struct PcgState {
+  double rho, Q0, alpha, eta, norm_b, pad[3];
+  int iter, status, min_iter, max_iter;
+};
+// per chunk: 21 upper of sum_runs Z Z^T (Z = sum of the run's Y; run[i] = length of the
+// same-point run starting at position i, 0 inside a run) | 6 of -sum Y q_p -> partial[chunk][27]
+void launch_pcg_diag_rhs_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
+                                 const int* run, const double* Y, const double* q, double* partial);
+// per camera: Ad = s U s + D^2 [NC][36], Minv = (Ad - sum Y Y^T)^-1 [NC][36],
+// b = s g_c - sum Y q, x = 0, r = b; fail[0] |= 1 if a block is not positive definite
+void launch_pcg_setup(hipStream_t s, int NC, const double* ug, const double* scale_c, StepScalars sc,
+                      const double* red, double* Ad, double* Minv, double* bvec, double* x, double* r,
+                      int* fail);
+void launch_pcg_init(hipStream_t s, int n, const double* bvec, const int* fail, PcgState* st, double eta,
+                     int min_iter, int max_iter);
+// z = M^-1 r, rho, p = z + beta p
+void launch_pcg_direction(hipStream_t s, int NC, const double* Minv, const double* r, double* z, double* p,
+                          PcgState* st);
+// the two Y passes of S vec: t[NP][4], partial[chunk][6] (= -sum Y t per chunk)
+void launch_pcg_matvec_passes(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
+                              const double* Y, const double* vec, double* t, double* partial,
+                              const PcgState* st);
+// mode 0: q = S p, alpha, x, r, Q-test; 1: q = S p, alpha, x; 2: r = b - S x, Q-test.
+// w[NC][6] = all-reduced Y part of the product; xptr/xlist: per-camera CSR of cross blocks
+// (code = 2*k + (camera is c1)), nullable when there are none.
+void launch_pcg_update(hipStream_t s, int NC, int mode, const double* Ad, const double* w, const int* xptr,
+                       const int* xlist, const int2* xcam, const double* X, const double* scale_c,
+                       const double* bvec, const double* p, double* q, double* x, double* r, PcgState* st);
+
 // ---- dense Cholesky (dab_chol.hip) -------------------------------------------------------
 // Factor the (n+1)x(n+1) augmented lower matrix [S b; b^T *] in place (row-major, ld = lda):
 // the first n rows end as L and row n as z = L^-1 b; then solve L^T y = z into y.

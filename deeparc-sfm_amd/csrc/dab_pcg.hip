@@ -1,0 +1,518 @@
+// dab_pcg.hip — implicit-Schur preconditioned conjugate gradients on the reduced camera
+// system (DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG; SURVEY §8a row a7, "Schur + PCG").
+//
+// S = (s U s + D^2 + cross) - sum_p Y_p Y_p^T is never formed. One matrix-vector product
+// S v is two streaming passes over the camera-major Y records (144 B / entry):
+//   point pass   t_p = sum_{e in p} Y_e^T v_cam(e)            (gathers Y_e by position)
+//   camera pass  w_c = -sum_{pos in c} Y_pos t_pt(pos)         (contiguous records, chunked)
+// followed, after the cross-rank all-reduce of w, by one work-group that adds the camera
+// block diagonal / arc∘ring cross terms and runs the CG scalar recurrences. The
+// preconditioner is block Jacobi on S (Ceres' SCHUR_JACOBI): M_c = diag block of S.
+//
+// The recurrences follow Ceres' ConjugateGradientsSolver (conjugate_gradients_solver.h,
+// external, Ceres 2.x; restated, not verified in this container): x0 = 0, r = b,
+// z = M^-1 r, rho = r.z, p = z + (rho / rho_prev) p, q = S p, alpha = rho / p.q,
+// x += alpha p, r -= alpha q (r = b - S x every 10th iteration), Q1 = -x.(b + r),
+// stop when iter * (Q1 - Q0) / Q1 < eta (Nash & Sofer; eta = Solver::Options::eta) or at
+// max_num_iterations; p.q <= 0 stops with the current x; rho, beta or alpha zero/inf is a
+// linear solver failure (the LM step is then invalid).
+//
+// All CG control lives on the device (PcgState) so the host enqueues iterations in batches
+// without a round trip; every kernel returns at once after the state leaves "running".
+// Every reduction has a fixed order, so results are bitwise reproducible and identical on
+// every rank.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+
+#include "dab_kernels.h"
+
+namespace dab {
+
+namespace {
+
+constexpr int kOneWG = 1024;
+
+__device__ __forceinline__ double wg_sum(double v, double* sh) {
+  // fixed-order sum over a 1024-thread work-group, result broadcast to every thread
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i];
+  return t;
+}
+
+__device__ __forceinline__ bool zero_or_inf(double x) { return x == 0.0 || isinf(x); }
+
+// upper-packed index of (a, b), a <= b, in a symmetric 6x6
+__device__ __forceinline__ int up6(int a, int b) { return a * 6 - (a * (a - 1)) / 2 + (b - a); }
+
+}  // namespace
+
+// ---- setup ---------------------------------------------------------------------------
+
+// per chunk of camera-major positions: 21 upper entries of sum Z Z^T over same-point runs
+// (the exact diagonal S block) | 6 of -sum Y q_p
+__device__ __forceinline__ void load_y(const double* __restrict__ Y, int i, double (&y)[18]) {
+  const double2* y2 = reinterpret_cast<const double2*>(Y + (size_t)kYRec * i);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const double2 t = y2[k];
+    y[2 * k] = t.x;
+    y[2 * k + 1] = t.y;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pcg_diag_rhs_partial(DevView v, const int* __restrict__ chunk_beg,
+                                                              const int* __restrict__ run,
+                                                              const double* __restrict__ Y,
+                                                              const double* __restrict__ q,
+                                                              double* __restrict__ partial) {
+  const int c = blockIdx.x;
+  const int b = chunk_beg[c], e = chunk_beg[c + 1];
+  double acc[27];
+#pragma unroll
+  for (int i = 0; i < 27; ++i) acc[i] = 0.0;
+  for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
+    const int p = v.cm_pt[i];
+    const double2 qa = reinterpret_cast<const double2*>(q)[2 * (size_t)p];
+    const double q2 = q[4 * (size_t)p + 2];
+    double y[18];
+    load_y(Y, i, y);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[21 + a] -= y[3 * a] * qa.x + y[3 * a + 1] * qa.y + y[3 * a + 2] * q2;
+    const int len = run[i];
+    if (len == 0) continue;
+    for (int j = 1; j < len; ++j) {  // rare (rig): fold the run into Z
+      double w[18];
+      load_y(Y, i + j, w);
+#pragma unroll
+      for (int k = 0; k < 18; ++k) y[k] += w[k];
+    }
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int bb = a; bb < 6; ++bb)
+        acc[k++] += y[3 * a] * y[3 * bb] + y[3 * a + 1] * y[3 * bb + 1] + y[3 * a + 2] * y[3 * bb + 2];
+  }
+  // fixed-order block reduction
+  __shared__ double sh[kRedBlock / 64][27];
+#pragma unroll
+  for (int i = 0; i < 27; ++i) {
+    double t = acc[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+    acc[i] = t;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 27; ++i) sh[w][i] = acc[i];
+  }
+  __syncthreads();
+  if (threadIdx.x < 27) {
+    double t = sh[0][threadIdx.x];
+#pragma unroll
+    for (int q2 = 1; q2 < kRedBlock / 64; ++q2) t += sh[q2][threadIdx.x];
+    partial[27 * (size_t)c + threadIdx.x] = t;
+  }
+}
+
+// thread per camera: A_c = s U_cc s + D^2 (full 36, kept for the operator), M_c^-1 from
+// A_c - sum Y Y^T (6x6 Cholesky + inverse), b_c = s g_c - sum Y q, x = 0, r = b.
+__global__ __launch_bounds__(256) void k_pcg_setup(int NC, const double* __restrict__ ug,
+                                                   const double* __restrict__ scc, StepScalars sc,
+                                                   const double* __restrict__ red /*[NC][27]*/,
+                                                   double* __restrict__ Ad, double* __restrict__ Minv,
+                                                   double* __restrict__ bvec, double* __restrict__ x,
+                                                   double* __restrict__ r, int* __restrict__ fail) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= NC) return;
+  const double* u = ug + 27 * (size_t)c;
+  const double* rd = red + 27 * (size_t)c;
+  double s[6];
+#pragma unroll
+  for (int a = 0; a < 6; ++a) s[a] = scc[6 * c + a];
+  double A[6][6], M[6][6];
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const int lo = a < b ? a : b, hi = a < b ? b : a;
+      double val = s[a] * u[up6(lo, hi)] * s[b];
+      if (a == b) {
+        const double d = fmin(fmax(val, sc.min_diag), sc.max_diag);
+        const double D = sqrt(d / sc.radius);
+        val += D * D;
+      }
+      A[a][b] = val;
+      M[a][b] = val - rd[up6(lo, hi)];
+    }
+  double* ad = Ad + 36 * (size_t)c;
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int b = 0; b < 6; ++b) ad[6 * a + b] = A[a][b];
+  // Cholesky M = L L^T (lower, in place)
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    double d = M[j][j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) d -= M[j][k] * M[j][k];
+    ok = ok && d > 0.0;
+    const double l = sqrt(d);
+    M[j][j] = l;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      double t = M[i][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t -= M[i][k] * M[j][k];
+      M[i][j] = t / l;
+    }
+  }
+  // Li = L^-1 (lower), then M^-1 = Li^T Li
+  double Li[6][6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) Li[i][j] = 0.0;
+    Li[j][j] = 1.0 / M[j][j];
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = j; k < i; ++k) t -= M[i][k] * Li[k][j];
+      Li[i][j] = t / M[i][i];
+    }
+  }
+  double* mi = Minv + 36 * (size_t)c;
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) t += Li[k][a] * Li[k][b];
+      ok = ok && isfinite(t);
+      mi[6 * a + b] = t;
+    }
+  if (!ok) atomicOr(fail, 1);
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    const double bv = s[a] * u[21 + a] + rd[21 + a];
+    bvec[6 * c + a] = bv;
+    r[6 * c + a] = bv;
+    x[6 * c + a] = 0.0;
+  }
+}
+
+// one work-group: norm_b, status
+__global__ __launch_bounds__(kOneWG) void k_pcg_init(int n, const double* __restrict__ bvec,
+                                                     const int* __restrict__ fail, PcgState* st,
+                                                     double eta, int min_iter, int max_iter) {
+  __shared__ double sh[kOneWG / 64];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) acc += bvec[i] * bvec[i];
+  const double nb2 = wg_sum(acc, sh);
+  if (threadIdx.x == 0) {
+    st->rho = 0.0;
+    st->Q0 = 0.0;
+    st->alpha = 0.0;
+    st->eta = eta;
+    st->norm_b = sqrt(nb2);
+    st->iter = 0;
+    st->min_iter = min_iter;
+    st->max_iter = max_iter;
+    st->status = fail[0] != 0 ? kPcgFailure : (nb2 == 0.0 ? kPcgSuccess : kPcgRunning);
+    if (st->status == kPcgRunning && max_iter <= 0) st->status = kPcgNoConvergence;
+  }
+}
+
+// ---- per iteration -------------------------------------------------------------------
+
+// one work-group: z = M^-1 r, rho = r.z, p = z + beta p
+__global__ __launch_bounds__(kOneWG) void k_pcg_direction(int NC, const double* __restrict__ Minv,
+                                                          const double* __restrict__ r, double* __restrict__ z,
+                                                          double* __restrict__ p, PcgState* st) {
+  __shared__ double sh[kOneWG / 64];
+  if (st->status != kPcgRunning) return;
+  const int iter = st->iter + 1;
+  double acc = 0.0;
+  for (int c = threadIdx.x; c < NC; c += blockDim.x) {
+    const double* mi = Minv + 36 * (size_t)c;
+    double rc[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) rc[a] = r[6 * c + a];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      double t = 0.0;
+#pragma unroll
+      for (int b = 0; b < 6; ++b) t += mi[6 * a + b] * rc[b];
+      z[6 * c + a] = t;
+      acc += rc[a] * t;
+    }
+  }
+  const double rho = wg_sum(acc, sh);
+  const double rho_prev = st->rho;
+  const double beta = iter == 1 ? 0.0 : rho / rho_prev;
+  const bool bad = zero_or_inf(rho) || (iter > 1 && zero_or_inf(beta));
+  if (!bad) {
+    for (int c = threadIdx.x; c < NC; c += blockDim.x) {
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        const int i = 6 * c + a;
+        p[i] = iter == 1 ? z[i] : z[i] + beta * p[i];
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    st->iter = iter;
+    st->rho = rho;
+    if (bad) st->status = kPcgFailure;
+  }
+}
+
+// point pass: t_p = sum_e Y_e^T v_cam(e) -> t[NP][4]
+__global__ __launch_bounds__(256) void k_pcg_point_pass(DevView v, const double* __restrict__ Y,
+                                                        const double* __restrict__ vec,
+                                                        double* __restrict__ t, const PcgState* st) {
+  if (st->status != kPcgRunning) return;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= v.NP) return;
+  double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+  for (int e = v.pt_ent_ptr[p]; e < v.pt_ent_ptr[p + 1]; ++e) {
+    const int c = v.ent_cam[e];
+    const double2* y2 = reinterpret_cast<const double2*>(Y + (size_t)kYRec * v.ent_pos[e]);
+    const double2* v2 = reinterpret_cast<const double2*>(vec + 6 * (size_t)c);
+    double y[18], vc[6];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const double2 w = y2[k];
+      y[2 * k] = w.x;
+      y[2 * k + 1] = w.y;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double2 w = v2[k];
+      vc[2 * k] = w.x;
+      vc[2 * k + 1] = w.y;
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      t0 += y[3 * a] * vc[a];
+      t1 += y[3 * a + 1] * vc[a];
+      t2 += y[3 * a + 2] * vc[a];
+    }
+  }
+  reinterpret_cast<double2*>(t)[2 * (size_t)p] = make_double2(t0, t1);
+  reinterpret_cast<double2*>(t)[2 * (size_t)p + 1] = make_double2(t2, 0.0);
+}
+
+// camera pass: per chunk of positions -sum Y_pos t_pt(pos) -> partial[chunk][6]
+__global__ __launch_bounds__(256) void k_pcg_cam_pass(DevView v, const int* __restrict__ chunk_beg,
+                                                      const double* __restrict__ Y, const double* __restrict__ t,
+                                                      double* __restrict__ partial, const PcgState* st) {
+  if (st->status != kPcgRunning) return;
+  const int c = blockIdx.x;
+  const int b = chunk_beg[c], e = chunk_beg[c + 1];
+  double acc[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
+    const int p = v.cm_pt[i];
+    const double2 ta = reinterpret_cast<const double2*>(t)[2 * (size_t)p];
+    const double t2 = t[4 * (size_t)p + 2];
+    const double2* y2 = reinterpret_cast<const double2*>(Y + (size_t)kYRec * i);
+    double y[18];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const double2 w = y2[k];
+      y[2 * k] = w.x;
+      y[2 * k + 1] = w.y;
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[a] -= y[3 * a] * ta.x + y[3 * a + 1] * ta.y + y[3 * a + 2] * t2;
+  }
+  __shared__ double sh[kRedBlock / 64][6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    double x = acc[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    acc[i] = x;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) sh[w][i] = acc[i];
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    double x = sh[0][threadIdx.x];
+#pragma unroll
+    for (int q = 1; q < kRedBlock / 64; ++q) x += sh[q][threadIdx.x];
+    partial[6 * (size_t)c + threadIdx.x] = x;
+  }
+}
+
+// (A_cc + cross) vec + w for camera c, component-wise into out[6]
+__device__ __forceinline__ void apply_cam(int c, const double* __restrict__ Ad, const double* __restrict__ vec,
+                                          const double* __restrict__ w, const int* __restrict__ xptr,
+                                          const int* __restrict__ xlist, const int2* __restrict__ xcam,
+                                          const double* __restrict__ X, const double* __restrict__ scc,
+                                          double (&out)[6]) {
+  const double* ad = Ad + 36 * (size_t)c;
+  double vc[6];
+#pragma unroll
+  for (int b = 0; b < 6; ++b) vc[b] = vec[6 * c + b];
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    double t = w[6 * c + a];
+#pragma unroll
+    for (int b = 0; b < 6; ++b) t += ad[6 * a + b] * vc[b];
+    out[a] = t;
+  }
+  if (xptr) {
+    for (int j = xptr[c]; j < xptr[c + 1]; ++j) {
+      const int code = xlist[j], k = code >> 1;
+      const int2 cc = xcam[k];  // X_k = Jc0^T Jc1, block (c0, c1)
+      const double* xk = X + 36 * (size_t)k;
+      if ((code & 1) == 0) {  // c == c0: out += (s0 X s1) v_c1
+        const int o = cc.y;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          double t = 0.0;
+#pragma unroll
+          for (int b = 0; b < 6; ++b) t += xk[6 * a + b] * scc[6 * o + b] * vec[6 * o + b];
+          out[a] += scc[6 * c + a] * t;
+        }
+      } else {  // c == c1: out += (s0 X s1)^T v_c0
+        const int o = cc.x;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          double t = 0.0;
+#pragma unroll
+          for (int b = 0; b < 6; ++b) t += xk[6 * b + a] * scc[6 * o + b] * vec[6 * o + b];
+          out[a] += scc[6 * c + a] * t;
+        }
+      }
+    }
+  }
+}
+
+// one work-group. mode 0: q = S p, alpha, x += alpha p, r -= alpha q, Q-test
+//                 mode 1: q = S p, alpha, x += alpha p (r recomputed by mode 2)
+//                 mode 2: r = b - S x, Q-test
+__global__ __launch_bounds__(kOneWG) void k_pcg_update(int NC, int mode, const double* __restrict__ Ad,
+                                                       const double* __restrict__ w,
+                                                       const int* __restrict__ xptr, const int* __restrict__ xlist,
+                                                       const int2* __restrict__ xcam, const double* __restrict__ X,
+                                                       const double* __restrict__ scc, const double* __restrict__ bvec,
+                                                       const double* __restrict__ p, double* __restrict__ q,
+                                                       double* __restrict__ x, double* __restrict__ r,
+                                                       PcgState* st) {
+  __shared__ double sh[kOneWG / 64];
+  if (st->status != kPcgRunning) return;
+  int status = kPcgRunning;
+  if (mode != 2) {
+    double acc = 0.0;
+    for (int c = threadIdx.x; c < NC; c += blockDim.x) {
+      double o[6];
+      apply_cam(c, Ad, p, w, xptr, xlist, xcam, X, scc, o);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        q[6 * c + a] = o[a];
+        acc += p[6 * c + a] * o[a];
+      }
+    }
+    const double pq = wg_sum(acc, sh);
+    if (pq <= 0.0 || isinf(pq)) {
+      // Ceres: "Matrix is indefinite, no more progress can be made" — keep x
+      if (threadIdx.x == 0) st->status = kPcgNoConvergence;
+      return;
+    }
+    const double alpha = st->rho / pq;
+    if (isinf(alpha)) {
+      if (threadIdx.x == 0) st->status = kPcgFailure;
+      return;
+    }
+    for (int c = threadIdx.x; c < NC; c += blockDim.x) {
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        const int i = 6 * c + a;
+        x[i] += alpha * p[i];
+        if (mode == 0) r[i] -= alpha * q[i];
+      }
+    }
+    if (mode == 1) return;
+  } else {
+    for (int c = threadIdx.x; c < NC; c += blockDim.x) {
+      double o[6];
+      apply_cam(c, Ad, x, w, xptr, xlist, xcam, X, scc, o);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) r[6 * c + a] = bvec[6 * c + a] - o[a];
+    }
+  }
+  double acc = 0.0;
+  for (int c = threadIdx.x; c < NC; c += blockDim.x) {
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      const int i = 6 * c + a;
+      acc += x[i] * (bvec[i] + r[i]);
+    }
+  }
+  const double Q1 = -wg_sum(acc, sh);
+  if (threadIdx.x == 0) {
+    const int iter = st->iter;
+    const double zeta = iter * (Q1 - st->Q0) / Q1;
+    if (zeta < st->eta && iter >= st->min_iter) status = kPcgSuccess;
+    else if (iter >= st->max_iter) status = kPcgNoConvergence;
+    st->Q0 = Q1;
+    st->status = status;
+  }
+}
+
+// ---- launchers -------------------------------------------------------------------------
+
+void launch_pcg_diag_rhs_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
+                                 const int* run, const double* Y, const double* q, double* partial) {
+  if (nchunk <= 0) return;
+  k_pcg_diag_rhs_partial<<<nchunk, kRedBlock, 0, s>>>(v, chunk_beg, run, Y, q, partial);
+}
+
+void launch_pcg_setup(hipStream_t s, int NC, const double* ug, const double* scale_c, StepScalars sc,
+                      const double* red, double* Ad, double* Minv, double* bvec, double* x, double* r,
+                      int* fail) {
+  if (NC <= 0) return;
+  k_pcg_setup<<<grid_for(NC, 256, 1 << 20), 256, 0, s>>>(NC, ug, scale_c, sc, red, Ad, Minv, bvec, x, r, fail);
+}
+
+void launch_pcg_init(hipStream_t s, int n, const double* bvec, const int* fail, PcgState* st, double eta,
+                     int min_iter, int max_iter) {
+  k_pcg_init<<<1, kOneWG, 0, s>>>(n, bvec, fail, st, eta, min_iter, max_iter);
+}
+
+void launch_pcg_direction(hipStream_t s, int NC, const double* Minv, const double* r, double* z, double* p,
+                          PcgState* st) {
+  k_pcg_direction<<<1, kOneWG, 0, s>>>(NC, Minv, r, z, p, st);
+}
+
+void launch_pcg_matvec_passes(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
+                              const double* Y, const double* vec, double* t, double* partial,
+                              const PcgState* st) {
+  if (v.NP > 0) k_pcg_point_pass<<<grid_for(v.NP, 256, 1 << 20), 256, 0, s>>>(v, Y, vec, t, st);
+  if (nchunk > 0) k_pcg_cam_pass<<<nchunk, kRedBlock, 0, s>>>(v, chunk_beg, Y, t, partial, st);
+}
+
+void launch_pcg_update(hipStream_t s, int NC, int mode, const double* Ad, const double* w, const int* xptr,
+                       const int* xlist, const int2* xcam, const double* X, const double* scale_c,
+                       const double* bvec, const double* p, double* q, double* x, double* r, PcgState* st) {
+  k_pcg_update<<<1, kOneWG, 0, s>>>(NC, mode, Ad, w, xptr, xlist, xcam, X, scale_c, bvec, p, q, x, r, st);
+}
+
+}  // namespace dab

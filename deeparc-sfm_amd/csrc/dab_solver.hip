@@ -68,7 +68,8 @@ enum Slot {
   S_STEP_P,        // sum (x - xc)^2 over points
   S_XCNORM_P,      // sum xc^2 over points
   S_CAM0,          // 5 camera slots (launch_cam_norms)
-  S_END = S_CAM0 + 5,
+  S_TIME = S_CAM0 + 5,  // solver wall-clock (max over ranks)
+  S_END,
   S_NSLOTS = 16
 };
 
@@ -122,6 +123,10 @@ struct dab_handle {
   int nchunk = 0, nxchunk = 0, ncross = 0, nblk = 0, nwin = 0, nstrad = 0;
   long long npairs = 0;
   int lds = 0;                      // leading dim of dense S
+  bool schur_built = false;
+  bool pcg_built = false;
+  int nxlist = 0;
+  std::vector<int> h_pt_ent_ptr, h_ent_cam, h_ent_pos;  // kept for build_schur_tables
 
   // ---- device buffers ----
   Dev dev;
@@ -148,6 +153,13 @@ struct dab_handle {
   double* d_partial = nullptr; // chunk partials (max of chunk counts * 36)
   double* d_spack = nullptr;   // [packed nblk*36 | ybc NC*6] (all-reduced)
   double* d_S = nullptr;
+  // implicit-Schur PCG (lazily allocated)
+  double *d_pcg_b = nullptr, *d_pcg_r = nullptr, *d_pcg_z = nullptr, *d_pcg_p = nullptr, *d_pcg_q = nullptr,
+         *d_pcg_w = nullptr, *d_pcg_Ad = nullptr, *d_pcg_Minv = nullptr, *d_pcg_red = nullptr,
+         *d_pcg_t = nullptr;
+  PcgState* d_pcg_state = nullptr;
+  PcgState* h_pcg_state = nullptr;  // pinned
+  int *d_xptr = nullptr, *d_xlist = nullptr, *d_run = nullptr;
   double *d_yc = nullptr, *d_dp = nullptr, *d_dc = nullptr;
   double* d_gpart = nullptr;   // grid partials
   double* d_scal = nullptr;    // S_NSLOTS
@@ -160,6 +172,7 @@ struct dab_handle {
     dev.release();
     if (h_scal) (void)hipHostFree(h_scal);
     if (h_flags) (void)hipHostFree(h_flags);
+    if (h_pcg_state) (void)hipHostFree(h_pcg_state);
     if (chol) chol_destroy(chol);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -403,6 +416,19 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
     ent_pos[cam_ent[i]] = i;
     cm_pt[i] = ent_pt[cam_ent[i]];
   }
+  // runs of one point inside one camera's positions (rig: a point seen by one arc through
+  // several rings has several entries of that camera); run[i] = run length at its first
+  // position, 0 elsewhere. The diagonal S block needs (sum_run Y)(sum_run Y)^T.
+  std::vector<int> run(NE, 0);
+  for (int c = 0; c < NC; ++c) {
+    int i = cam_cnt[c];
+    while (i < cam_cnt[c + 1]) {
+      int j = i + 1;
+      while (j < cam_cnt[c + 1] && cm_pt[j] == cm_pt[i]) ++j;
+      run[i] = j - i;
+      i = j;
+    }
+  }
   std::vector<int2> obs_ent(N, make_int2(-1, -1));
   for (int e = 0; e < NE; ++e) {
     const int s2 = ent_os[e] >> 1;
@@ -468,6 +494,157 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
     xchunk_beg.push_back((int)xkeys.size());
   }
 
+  // per-camera CSR of cross blocks for the implicit operator: code = 2 k + (camera is c1)
+  std::vector<int> xptr(NC + 1, 0), xlist;
+  {
+    std::vector<std::vector<int>> per(NC);
+    for (int k = 0; k < h->ncross; ++k) {
+      per[cross_cam[k].x].push_back(2 * k);
+      per[cross_cam[k].y].push_back(2 * k + 1);
+    }
+    for (int c = 0; c < NC; ++c) {
+      xptr[c] = (int)xlist.size();
+      xlist.insert(xlist.end(), per[c].begin(), per[c].end());
+    }
+    if (NC > 0) xptr[NC] = (int)xlist.size();
+    h->nxlist = (int)xlist.size();
+  }
+
+  h->h_pt_ent_ptr = pt_ent_ptr;
+  h->h_ent_cam = ent_cam;
+  h->h_ent_pos = ent_pos;
+  h->schur_built = false;
+  h->pcg_built = false;
+  h->nblk = 0;
+  h->npairs = 0;
+
+  // intrinsics: (cx, cy, fx, fy', k0, k1) with unused distortion terms zeroed
+  std::vector<double> intr((size_t)kIntr * std::max(1, h->NI), 0.0);
+  for (int i = 0; i < h->NI; ++i) {
+    const double* K = p->intr + 6 * (size_t)i;
+    double* o = &intr[(size_t)kIntr * i];
+    o[0] = K[0];
+    o[1] = K[1];
+    o[2] = K[2];
+    o[3] = p->intr_nf[i] == 2 ? K[3] : K[2];
+    o[4] = p->intr_nk[i] >= 1 ? K[4] : 0.0;
+    o[5] = p->intr_nk[i] >= 2 ? K[5] : 0.0;
+  }
+  std::vector<double> points((size_t)3 * NP);
+  for (int i = 0; i < NP; ++i)
+    for (int k = 0; k < 3; ++k) points[3 * (size_t)i + k] = p->points[3 * (size_t)h->pt_of[i] + k];
+  std::vector<double> ext(p->ext, p->ext + 6 * (size_t)h->E);
+
+  // ---- upload ----
+  Dev& d = h->dev;
+  CHECK_RC(upload(&h->d_obs_idx, d, obs_idx, s));
+  CHECK_RC(upload(&h->d_obs_xy, d, obs_xy, s));
+  CHECK_RC(upload(&h->d_pt_obs_ptr, d, pt_obs_ptr, s));
+  CHECK_RC(upload(&h->d_pt_ent_ptr, d, pt_ent_ptr, s));
+  CHECK_RC(upload(&h->d_ent_os, d, ent_os, s));
+  CHECK_RC(upload(&h->d_ent_cam, d, ent_cam, s));
+  CHECK_RC(upload(&h->d_ent_pt, d, ent_pt, s));
+  CHECK_RC(upload(&h->d_ext_col, d, h->ext_col, s));
+  CHECK_RC(upload(&h->d_ent_pos, d, ent_pos, s));
+  CHECK_RC(upload(&h->d_cm_pt, d, cm_pt, s));
+  CHECK_RC(upload(&h->d_obs_ent, d, obs_ent, s));
+  CHECK_RC(upload(&h->d_strad, d, strad, s));
+  CHECK_RC(upload(&h->d_chunk_beg, d, chunk_beg, s));
+  CHECK_RC(upload(&h->d_seg_chunk, d, seg_chunk, s));
+  CHECK_RC(upload(&h->d_xobs, d, xobs, s));
+  CHECK_RC(upload(&h->d_xchunk_beg, d, xchunk_beg, s));
+  CHECK_RC(upload(&h->d_xseg_chunk, d, xseg_chunk, s));
+  CHECK_RC(upload(&h->d_cross_cam, d, cross_cam, s));
+  CHECK_RC(upload(&h->d_xptr, d, xptr, s));
+  CHECK_RC(upload(&h->d_run, d, run, s));
+  CHECK_RC(upload(&h->d_xlist, d, xlist, s));
+  CHECK_RC(upload(&h->d_intr, d, intr, s));
+  CHECK_RC(upload(&h->d_points, d, points, s));
+  CHECK_RC(upload(&h->d_ext, d, ext, s));
+  CHECK_RC(d.alloc(&h->d_points_c, (size_t)3 * NP));
+  CHECK_RC(d.alloc(&h->d_ext_c, (size_t)6 * h->E));
+  CHECK_RC(d.alloc(&h->d_camtab, (size_t)kCamTab * h->E));
+  CHECK_RC(d.alloc(&h->d_camtab_c, (size_t)kCamTab * h->E));
+  CHECK_RC(d.alloc(&h->d_r, (size_t)2 * N));
+  CHECK_RC(d.alloc(&h->d_Jp, (size_t)6 * N));
+  CHECK_RC(d.alloc(&h->d_rec, (size_t)kRec * NE));
+  CHECK_RC(d.alloc(&h->d_wpart, (size_t)18 * h->nwin));
+  h->d_Jfull = nullptr;
+  CHECK_RC(d.alloc(&h->d_V, (size_t)6 * NP));
+  CHECK_RC(d.alloc(&h->d_g, (size_t)3 * NP));
+  CHECK_RC(d.alloc(&h->d_scale_p, (size_t)3 * NP));
+  CHECK_RC(d.alloc(&h->d_scale_c, (size_t)6 * NC));
+  CHECK_RC(d.alloc(&h->d_L, (size_t)6 * NP));
+  CHECK_RC(d.alloc(&h->d_q, (size_t)4 * NP));
+  CHECK_RC(d.alloc(&h->d_Y, (size_t)kYRec * NE));
+  CHECK_RC(d.alloc(&h->d_camred, h->camred_count()));
+  const size_t npart = std::max<size_t>({(size_t)h->nchunk * 27, (size_t)h->nxchunk * 36, (size_t)h->nchunk * 6, 16});
+  CHECK_RC(d.alloc(&h->d_partial, npart));
+  CHECK_RC(d.alloc(&h->d_yc, (size_t)6 * NC));
+  CHECK_RC(d.alloc(&h->d_dp, (size_t)3 * NP));
+  CHECK_RC(d.alloc(&h->d_dc, (size_t)6 * NC));
+  h->red_grid = grid_for(std::max(N, 3 * NP), 256, 1024);
+  CHECK_RC(d.alloc(&h->d_gpart, (size_t)h->red_grid * 4));
+  CHECK_RC(d.alloc(&h->d_scal, S_NSLOTS));
+  CHECK_RC(d.alloc(&h->d_flags, 4));
+  HIP_OK(hipMemsetAsync(h->d_dc, 0, sizeof(double) * std::max(1, 6 * NC), s));
+  HIP_OK(hipStreamSynchronize(s));
+
+  DevView& v = h->view;
+  v.N = N;
+  v.NP = NP;
+  v.E = h->E;
+  v.NC = NC;
+  v.NE = NE;
+  v.nwin = h->nwin;
+  v.obs_idx = h->d_obs_idx;
+  v.obs_xy = h->d_obs_xy;
+  v.obs_ent = h->d_obs_ent;
+  v.pt_obs_ptr = h->d_pt_obs_ptr;
+  v.pt_ent_ptr = h->d_pt_ent_ptr;
+  v.ent_os = h->d_ent_os;
+  v.ent_cam = h->d_ent_cam;
+  v.ent_pt = h->d_ent_pt;
+  v.ent_pos = h->d_ent_pos;
+  v.cm_pt = h->d_cm_pt;
+  v.ext_col = h->d_ext_col;
+  v.intr = h->d_intr;
+  h->have_problem = true;
+  return 0;
+}
+
+
+// Explicit-Schur tables (DAB_LINEAR_SOLVER_EXPLICIT_SCHUR only), built on first use:
+// every ordered pair (e, f) of entries of one point with cam(e) >= cam(f) contributes
+// -Y_e Y_f^T to lower block (cam(e), cam(f)) of the reduced camera system S. Pairs are
+// sorted by block so each block is one deterministic segment. The block table is the
+// union over ranks so the all-reduced packed layout matches.
+static constexpr long long kMaxExplicitPairs = 200000000LL;
+static int build_schur_tables(dab_handle* h) {
+  if (h->schur_built) return 0;
+  hipStream_t s = h->stream;
+  const int NP = h->NP, NC = h->NC;
+  const std::vector<int>& pt_ent_ptr = h->h_pt_ent_ptr;
+  const std::vector<int>& ent_cam = h->h_ent_cam;
+  const std::vector<int>& ent_pos = h->h_ent_pos;
+  long long total = 0;
+  for (int pt = 0; pt < NP; ++pt) {
+    const long long m = pt_ent_ptr[pt + 1] - pt_ent_ptr[pt];
+    total += m * (m + 1) / 2 + m;  // upper bound
+  }
+  double flag = total > kMaxExplicitPairs ? 1.0 : 0.0;
+  if (h->world > 1) {  // every rank must take the same branch
+    double* d_f = nullptr;
+    CHECK_RC(h->dev.alloc(&d_f, 1));
+    HIP_OK(hipMemcpyAsync(d_f, &flag, sizeof(double), hipMemcpyHostToDevice, s));
+    CHECK_RC(h->allreduce(d_f, 1, ncclMax));
+    HIP_OK(hipMemcpyAsync(&flag, d_f, sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+  }
+  if (flag != 0.0)
+    return set_error(DAB_E_UNSUPPORTED,
+                     "reduced camera system too large for explicit Schur pair tables (" +
+                         std::to_string(total) + " pairs); use DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG");
   // reduced-camera-system blocks: ordered entry pairs (e, f) of one point with
   // cam(e) >= cam(f); block (cam(e), cam(f)) of the lower triangle of S.
   std::vector<long long> blkkeys;
@@ -476,11 +653,6 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   if (NC > 0) {
     struct PK { long long key; int e, f; };
     std::vector<PK> tmp;
-    long long total = 0;
-    for (int pt = 0; pt < NP; ++pt) {
-      const long long m = pt_ent_ptr[pt + 1] - pt_ent_ptr[pt];
-      total += m * (m + 1) / 2 + m;  // upper bound
-    }
     tmp.reserve((size_t)total);
     for (int pt = 0; pt < NP; ++pt)
       for (int e = pt_ent_ptr[pt]; e < pt_ent_ptr[pt + 1]; ++e)
@@ -535,103 +707,87 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   std::vector<int2> blk_cam(h->nblk);
   for (int b = 0; b < h->nblk; ++b) blk_cam[b] = make_int2((int)(blkkeys[b] / NC), (int)(blkkeys[b] % NC));
 
-  // intrinsics: (cx, cy, fx, fy', k0, k1) with unused distortion terms zeroed
-  std::vector<double> intr((size_t)kIntr * std::max(1, h->NI), 0.0);
-  for (int i = 0; i < h->NI; ++i) {
-    const double* K = p->intr + 6 * (size_t)i;
-    double* o = &intr[(size_t)kIntr * i];
-    o[0] = K[0];
-    o[1] = K[1];
-    o[2] = K[2];
-    o[3] = p->intr_nf[i] == 2 ? K[3] : K[2];
-    o[4] = p->intr_nk[i] >= 1 ? K[4] : 0.0;
-    o[5] = p->intr_nk[i] >= 2 ? K[5] : 0.0;
-  }
-  std::vector<double> points((size_t)3 * NP);
-  for (int i = 0; i < NP; ++i)
-    for (int k = 0; k < 3; ++k) points[3 * (size_t)i + k] = p->points[3 * (size_t)h->pt_of[i] + k];
-  std::vector<double> ext(p->ext, p->ext + 6 * (size_t)h->E);
-
-  // ---- upload ----
   Dev& d = h->dev;
-  CHECK_RC(upload(&h->d_obs_idx, d, obs_idx, s));
-  CHECK_RC(upload(&h->d_obs_xy, d, obs_xy, s));
-  CHECK_RC(upload(&h->d_pt_obs_ptr, d, pt_obs_ptr, s));
-  CHECK_RC(upload(&h->d_pt_ent_ptr, d, pt_ent_ptr, s));
-  CHECK_RC(upload(&h->d_ent_os, d, ent_os, s));
-  CHECK_RC(upload(&h->d_ent_cam, d, ent_cam, s));
-  CHECK_RC(upload(&h->d_ent_pt, d, ent_pt, s));
-  CHECK_RC(upload(&h->d_ext_col, d, h->ext_col, s));
-  CHECK_RC(upload(&h->d_ent_pos, d, ent_pos, s));
-  CHECK_RC(upload(&h->d_cm_pt, d, cm_pt, s));
-  CHECK_RC(upload(&h->d_obs_ent, d, obs_ent, s));
-  CHECK_RC(upload(&h->d_strad, d, strad, s));
-  CHECK_RC(upload(&h->d_chunk_beg, d, chunk_beg, s));
-  CHECK_RC(upload(&h->d_seg_chunk, d, seg_chunk, s));
-  CHECK_RC(upload(&h->d_xobs, d, xobs, s));
-  CHECK_RC(upload(&h->d_xchunk_beg, d, xchunk_beg, s));
-  CHECK_RC(upload(&h->d_xseg_chunk, d, xseg_chunk, s));
-  CHECK_RC(upload(&h->d_cross_cam, d, cross_cam, s));
   CHECK_RC(upload(&h->d_pairs, d, pairs, s));
   CHECK_RC(upload(&h->d_blk_cam, d, blk_cam, s));
   CHECK_RC(upload(&h->d_blk_pair_beg, d, blk_pair_beg, s));
-  CHECK_RC(upload(&h->d_intr, d, intr, s));
-  CHECK_RC(upload(&h->d_points, d, points, s));
-  CHECK_RC(upload(&h->d_ext, d, ext, s));
-  CHECK_RC(d.alloc(&h->d_points_c, (size_t)3 * NP));
-  CHECK_RC(d.alloc(&h->d_ext_c, (size_t)6 * h->E));
-  CHECK_RC(d.alloc(&h->d_camtab, (size_t)kCamTab * h->E));
-  CHECK_RC(d.alloc(&h->d_camtab_c, (size_t)kCamTab * h->E));
-  CHECK_RC(d.alloc(&h->d_r, (size_t)2 * N));
-  CHECK_RC(d.alloc(&h->d_Jp, (size_t)6 * N));
-  CHECK_RC(d.alloc(&h->d_rec, (size_t)kRec * NE));
-  CHECK_RC(d.alloc(&h->d_wpart, (size_t)18 * h->nwin));
-  h->d_Jfull = nullptr;
-  CHECK_RC(d.alloc(&h->d_V, (size_t)6 * NP));
-  CHECK_RC(d.alloc(&h->d_g, (size_t)3 * NP));
-  CHECK_RC(d.alloc(&h->d_scale_p, (size_t)3 * NP));
-  CHECK_RC(d.alloc(&h->d_scale_c, (size_t)6 * NC));
-  CHECK_RC(d.alloc(&h->d_L, (size_t)6 * NP));
-  CHECK_RC(d.alloc(&h->d_q, (size_t)4 * NP));
-  CHECK_RC(d.alloc(&h->d_Y, (size_t)kYRec * NE));
-  CHECK_RC(d.alloc(&h->d_camred, h->camred_count()));
-  const size_t npart = std::max<size_t>({(size_t)h->nchunk * 27, (size_t)h->nxchunk * 36, (size_t)h->nchunk * 6, 16});
-  CHECK_RC(d.alloc(&h->d_partial, npart));
   CHECK_RC(d.alloc(&h->d_spack, h->spack_count()));
   const int n = 6 * NC;
   h->lds = ((n + 1 + 7) / 8) * 8;
   if (h->lds % 512 == 0) h->lds += 8;  // avoid power-of-two row strides
   CHECK_RC(d.alloc(&h->d_S, NC > 0 ? (size_t)(n + 1) * h->lds : 1));
-  CHECK_RC(d.alloc(&h->d_yc, (size_t)6 * NC));
-  CHECK_RC(d.alloc(&h->d_dp, (size_t)3 * NP));
-  CHECK_RC(d.alloc(&h->d_dc, (size_t)6 * NC));
-  h->red_grid = grid_for(std::max(N, 3 * NP), 256, 1024);
-  CHECK_RC(d.alloc(&h->d_gpart, (size_t)h->red_grid * 4));
-  CHECK_RC(d.alloc(&h->d_scal, S_NSLOTS));
-  CHECK_RC(d.alloc(&h->d_flags, 4));
-  HIP_OK(hipMemsetAsync(h->d_dc, 0, sizeof(double) * std::max(1, 6 * NC), s));
   HIP_OK(hipStreamSynchronize(s));
+  h->schur_built = true;
+  return 0;
+}
 
-  DevView& v = h->view;
-  v.N = N;
-  v.NP = NP;
-  v.E = h->E;
-  v.NC = NC;
-  v.NE = NE;
-  v.nwin = h->nwin;
-  v.obs_idx = h->d_obs_idx;
-  v.obs_xy = h->d_obs_xy;
-  v.obs_ent = h->d_obs_ent;
-  v.pt_obs_ptr = h->d_pt_obs_ptr;
-  v.pt_ent_ptr = h->d_pt_ent_ptr;
-  v.ent_os = h->d_ent_os;
-  v.ent_cam = h->d_ent_cam;
-  v.ent_pt = h->d_ent_pt;
-  v.ent_pos = h->d_ent_pos;
-  v.cm_pt = h->d_cm_pt;
-  v.ext_col = h->d_ext_col;
-  v.intr = h->d_intr;
-  h->have_problem = true;
+// Implicit-Schur PCG buffers (DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG), allocated on first use.
+static int build_pcg_buffers(dab_handle* h) {
+  if (h->pcg_built) return 0;
+  Dev& d = h->dev;
+  const size_t n = (size_t)6 * h->NC;
+  for (double** b : {&h->d_pcg_b, &h->d_pcg_r, &h->d_pcg_z, &h->d_pcg_p, &h->d_pcg_q, &h->d_pcg_w})
+    CHECK_RC(d.alloc(b, n));
+  CHECK_RC(d.alloc(&h->d_pcg_Ad, 6 * n));
+  CHECK_RC(d.alloc(&h->d_pcg_Minv, 6 * n));
+  CHECK_RC(d.alloc(&h->d_pcg_red, (size_t)27 * h->NC));
+  CHECK_RC(d.alloc(&h->d_pcg_t, (size_t)4 * h->NP));
+  CHECK_RC(d.alloc(&h->d_pcg_state, 1));
+  if (!h->h_pcg_state &&
+      hipHostMalloc(reinterpret_cast<void**>(&h->h_pcg_state), sizeof(PcgState)) != hipSuccess)
+    return set_error(DAB_E_NOMEM, "pinned PCG state allocation failed");
+  h->pcg_built = true;
+  return 0;
+}
+
+// S vec (Y part) -> d_pcg_w, all-reduced across ranks
+static int pcg_matvec(dab_handle* h, const double* vec) {
+  hipStream_t s = h->stream;
+  launch_pcg_matvec_passes(s, h->view, h->nchunk, h->d_chunk_beg, h->d_Y, vec, h->d_pcg_t, h->d_partial,
+                           h->d_pcg_state);
+  launch_seg_final(s, h->NC, 6, h->d_seg_chunk, h->d_partial, h->d_pcg_w);
+  CHECK_RC(h->allreduce(h->d_pcg_w, (size_t)6 * h->NC, ncclSum));
+  return 0;
+}
+
+// Solve S y = b (scaled, damped reduced camera system) into d_yc with preconditioned CG.
+// Requires d_L, d_q (point factor) and d_Y (entry_y) of this step. Returns the number of
+// CG iterations in *iters and the final PcgState status in *status.
+static int pcg_solve(dab_handle* h, const dab_options& opt, StepScalars sc, int* iters, int* status) {
+  hipStream_t s = h->stream;
+  const DevView& v = h->view;
+  const int NC = h->NC;
+  launch_pcg_diag_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_run, h->d_Y, h->d_q, h->d_partial);
+  launch_seg_final(s, NC, 27, h->d_seg_chunk, h->d_partial, h->d_pcg_red);
+  CHECK_RC(h->allreduce(h->d_pcg_red, (size_t)27 * NC, ncclSum));
+  launch_pcg_setup(s, NC, h->ug(), h->d_scale_c, sc, h->d_pcg_red, h->d_pcg_Ad, h->d_pcg_Minv, h->d_pcg_b,
+                   h->d_yc, h->d_pcg_r, h->d_flags + 1);
+  const int max_it = std::max(0, opt.max_linear_solver_iterations);
+  launch_pcg_init(s, 6 * NC, h->d_pcg_b, h->d_flags + 1, h->d_pcg_state, opt.eta,
+                  opt.min_linear_solver_iterations, max_it);
+  const int* xptr = h->nxlist > 0 ? h->d_xptr : nullptr;
+  int done = 0, batch = 4;
+  for (;;) {
+    for (int j = 0; j < batch && done < max_it; ++j) {
+      ++done;
+      launch_pcg_direction(s, NC, h->d_pcg_Minv, h->d_pcg_r, h->d_pcg_z, h->d_pcg_p, h->d_pcg_state);
+      CHECK_RC(pcg_matvec(h, h->d_pcg_p));
+      const bool reset = done % 10 == 0;  // r = b - S x every 10th iteration
+      launch_pcg_update(s, NC, reset ? 1 : 0, h->d_pcg_Ad, h->d_pcg_w, xptr, h->d_xlist, h->d_cross_cam, h->Ux(),
+                        h->d_scale_c, h->d_pcg_b, h->d_pcg_p, h->d_pcg_q, h->d_yc, h->d_pcg_r, h->d_pcg_state);
+      if (reset) {
+        CHECK_RC(pcg_matvec(h, h->d_yc));
+        launch_pcg_update(s, NC, 2, h->d_pcg_Ad, h->d_pcg_w, xptr, h->d_xlist, h->d_cross_cam, h->Ux(),
+                          h->d_scale_c, h->d_pcg_b, h->d_pcg_p, h->d_pcg_q, h->d_yc, h->d_pcg_r, h->d_pcg_state);
+      }
+    }
+    HIP_OK(hipMemcpyAsync(h->h_pcg_state, h->d_pcg_state, sizeof(PcgState), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (h->h_pcg_state->status != kPcgRunning || done >= max_it) break;
+    batch = std::min(2 * batch, 32);
+  }
+  *iters = h->h_pcg_state->iter;
+  *status = h->h_pcg_state->status;
   return 0;
 }
 
@@ -755,6 +911,21 @@ static void print_iter(const dab_iteration& it, double total) {
   std::fflush(stdout);
 }
 
+// Wall-clock since solve start, maxed over ranks so every rank takes the
+// "Maximum solver time reached" exit on the same iteration. Returns < 0 on error.
+static double elapsed_collective(dab_handle* h, double local) {
+  if (h->world <= 1) return local;
+  hipStream_t s = h->stream;
+  h->h_scal[S_TIME] = local;
+  if (hipMemcpyAsync(h->d_scal + S_TIME, &h->h_scal[S_TIME], sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess)
+    return -1.0;
+  if (h->allreduce(h->d_scal + S_TIME, 1, ncclMax) != 0) return -1.0;
+  if (hipMemcpyAsync(&h->h_scal[S_TIME], h->d_scal + S_TIME, sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess)
+    return -1.0;
+  if (hipStreamSynchronize(s) != hipSuccess) return -1.0;
+  return h->h_scal[S_TIME];
+}
+
 // ------------------------------------------------------------------------------------
 // dab_solve: the trust-region LM loop
 // ------------------------------------------------------------------------------------
@@ -765,9 +936,12 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
   dab_options opt;
   if (opt_in) opt = *opt_in;
   else dab_options_init(&opt);
-  if (opt.linear_solver_type != DAB_LINEAR_SOLVER_EXPLICIT_SCHUR)
-    return set_error(DAB_E_UNSUPPORTED, "only DAB_LINEAR_SOLVER_EXPLICIT_SCHUR is available in this build");
+  if (opt.linear_solver_type != DAB_LINEAR_SOLVER_EXPLICIT_SCHUR &&
+      opt.linear_solver_type != DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)
+    return set_error(DAB_E_INVALID, "unknown linear_solver_type");
+  const bool use_pcg = opt.linear_solver_type == DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG;
   HIP_OK(hipSetDevice(h->device));
+  CHECK_RC(use_pcg ? build_pcg_buffers(h) : build_schur_tables(h));
   hipStream_t s = h->stream;
   const DevView& v = h->view;
   const int NP = h->NP, NC = h->NC, n = 6 * NC;
@@ -840,7 +1014,9 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
       sum->iterations[sum->iterations_written++] = it;
     if (verbose) print_iter(it, now_s() - t_start);
     sum->num_iterations = iteration;
-    if (now_s() - t_start >= opt.max_solver_time_in_seconds) {
+    const double elapsed = elapsed_collective(h, now_s() - t_start);
+    if (elapsed < 0) return set_error(DAB_E_DEVICE, "solver-time all-reduce failed");
+    if (elapsed >= opt.max_solver_time_in_seconds) {
       term = DAB_NO_CONVERGENCE;
       std::snprintf(sum->message, sizeof(sum->message), "Maximum solver time reached.");
       break;
@@ -875,7 +1051,14 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
     StepScalars sc{radius, opt.min_lm_diagonal, opt.max_lm_diagonal};
     HIP_OK(hipMemsetAsync(h->d_flags, 0, sizeof(int) * 4, s));
     launch_point_factor(s, v, h->d_V, h->d_g, h->d_scale_p, sc, h->d_L, h->d_q, h->d_flags);
-    if (NC > 0) {
+    bool pcg_fail = false;
+    if (NC > 0 && use_pcg) {
+      launch_entry_y(s, v, h->d_Jp, h->d_rec, h->d_scale_p, h->d_scale_c, h->d_L, h->d_Y);
+      int cg_iters = 0, cg_status = 0;
+      CHECK_RC(pcg_solve(h, opt, sc, &cg_iters, &cg_status));
+      it.linear_solver_iterations = cg_iters;
+      pcg_fail = cg_status == kPcgFailure;
+    } else if (NC > 0) {
       launch_entry_y(s, v, h->d_Jp, h->d_rec, h->d_scale_p, h->d_scale_c, h->d_L, h->d_Y);
       launch_s_blocks(s, h->nblk, h->d_blk_pair_beg, h->d_pairs, h->d_Y, h->packed());
       launch_cam_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_Y, h->d_q, h->d_partial);
@@ -884,7 +1067,7 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
       launch_s_unpack(s, NC, h->nblk, h->d_blk_cam, h->packed(), h->ug(), h->ncross, h->d_cross_cam, h->Ux(),
                       h->d_scale_c, sc, h->ybc(), h->d_S, h->lds);
       if (chol_factor_solve(h->chol, s, n, h->d_S, h->lds, h->d_yc, h->d_flags + 1) != 0)
-        return set_error(DAB_E_DEVICE, "rocblas_dsyrk failed");
+        return set_error(DAB_E_DEVICE, "dense Cholesky launch failed");
     }
     launch_backsub(s, v, h->d_L, h->d_q, h->d_Y, NC > 0 ? h->d_yc : nullptr, h->d_scale_p, h->d_dp);
     // candidate x + delta and the model / candidate cost in one observation pass
@@ -905,7 +1088,8 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
     sum->linear_solver_time_in_seconds += tre - tls;
     sum->residual_evaluation_time_in_seconds += tdone - tre;
 
-    const bool solve_fail = h->h_flags[0] != 0 || h->h_flags[1] != 0 || h->h_flags[2] != 0 || h->h_flags[3] != 0;
+    const bool solve_fail = pcg_fail || h->h_flags[0] != 0 || h->h_flags[1] != 0 || h->h_flags[2] != 0 ||
+                            h->h_flags[3] != 0;
     const double model_cost_change = h->h_scal[S_MODEL];
     it.step_is_valid = !solve_fail && std::isfinite(model_cost_change) && model_cost_change > 0.0;
     if (!it.step_is_valid) {

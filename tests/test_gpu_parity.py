@@ -101,6 +101,37 @@ def test_lm_rig_matches_oracle(pkg, orc, gpu):
     assert_same_trajectory(g, o, prob, ref)
 
 
+@pytest.mark.parametrize("kind", ["bal", "rig"])
+def test_lm_pcg_matches_oracle(pkg, orc, gpu, kind):
+    """IMPLICIT_SCHUR_PCG: the GPU implicit operator vs the oracle's CG on the explicit S.
+    Same recurrences; only summation order differs, so CG iteration counts and the LM
+    trajectory agree (costs 1e-8 relative)."""
+    if kind == "bal":
+        prob = pkg.synth(kind=0, num_cameras=50, num_points=3000, obs_per_point=6, seed=31)
+    else:
+        prob = pkg.synth(kind=1, num_arcs=6, num_rings=14, num_points=2500, obs_per_point=8, seed=32)
+    g, o, ref = run_both(pkg, orc, prob, max_num_iterations=15,
+                         linear_solver_type=pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)
+    assert_same_trajectory(g, o, prob, ref, tol_cost=1e-8, tol_x=1e-6)
+    gi = [it["linear_solver_iterations"] for it in g["iterations"]]
+    oi = [it["linear_solver_iterations"] for it in o["iterations"]]
+    assert gi == oi
+    assert max(gi) > 1
+    assert g["final_cost"] < 0.05 * g["initial_cost"]
+
+
+def test_lm_pcg_reaches_dense_schur_minimum(pkg, gpu):
+    prob = pkg.synth(kind=1, num_arcs=5, num_rings=12, num_points=2000, obs_per_point=7, seed=33)
+    res = []
+    for lst in (pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR, pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG):
+        p = prob.copy()
+        s = pkg.Solver(0)
+        s.set_problem(p)
+        res.append(s.solve(pkg.options(max_num_iterations=50, linear_solver_type=lst))["final_cost"])
+        s.close()
+    assert res[1] == pytest.approx(res[0], rel=1e-4)
+
+
 def test_lm_freeze_camera_matches_oracle(pkg, orc, gpu):
     prob = pkg.synth(kind=1, num_arcs=4, num_rings=10, num_points=2000, obs_per_point=6, seed=23)
     prob.freeze_camera = True  # solve(..., freeze_camera=true), sfm.cc:111

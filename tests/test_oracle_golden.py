@@ -53,3 +53,19 @@ def test_rotation_helpers(orc):
         R = orc.aa_to_rotmat(c["aa"])
         if th * th > 2.220446049250313e-16:
             np.testing.assert_allclose(R, c["R_colmajor"], rtol=0, atol=1e-15)
+
+
+def test_oracle_pcg_reaches_dense_schur_minimum(pkg, orc):
+    """The oracle's CG step (implicit-Schur PCG restatement) converges to the same
+    minimum as its exact dense-Schur step on a small rig problem."""
+    prob = pkg.synth(kind=1, num_arcs=4, num_rings=8, num_points=400, obs_per_point=6, seed=41)
+    out = {}
+    for name, lst in (("dense", pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR),
+                      ("pcg", pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)):
+        p = prob.copy()
+        out[name] = orc.solve(pkg, p, pkg.options(max_num_iterations=40, num_threads=4,
+                                                  linear_solver_type=lst))
+    assert out["pcg"]["final_cost"] == pytest.approx(out["dense"]["final_cost"], rel=1e-4)
+    assert out["pcg"]["final_cost"] < 0.05 * out["pcg"]["initial_cost"]
+    cg = [it["linear_solver_iterations"] for it in out["pcg"]["iterations"][1:]]
+    assert max(cg) > 1 and all(c <= 500 for c in cg)
