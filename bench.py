@@ -71,7 +71,16 @@ def main():
             buf[:] = torch.tensor(list(pkg.Solver.unique_id()), dtype=torch.uint8)
         dist.broadcast(buf, 0)
         uid = bytes(buf.tolist())
-    solver = pkg.Solver(local_rank, rank, world, uid)
+    # DAB_BENCH_DEVICE pins every rank to one device (multi-rank rehearsal on a 1-GPU box)
+    device = int(os.environ.get("DAB_BENCH_DEVICE", local_rank))
+    host_ar = None
+    if world > 1 and os.environ.get("DAB_BENCH_HOST_COLLECTIVE") == "1":
+        import torch
+
+        def host_ar(arr, op):  # rehearsal only: library collectives staged through gloo
+            dist.all_reduce(torch.from_numpy(arr),
+                            op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+    solver = pkg.Solver(device, rank, world, uid, host_allreduce=host_ar)
     solver.set_problem(prob)
     n_obs = prob.num_obs
 

@@ -86,6 +86,9 @@ class DabSynthConfig(C.Structure):
     ]
 
 
+# int (*)(double* buf, int64_t count, int op, void* user): op 0 = sum, 1 = max
+HostAllreduceFn = C.CFUNCTYPE(C.c_int, _dp, C.c_int64, C.c_int, C.c_void_p)
+
 # name -> (restype, argtypes); every symbol include/dab.h declares
 SIGNATURES = {
     "dab_abi_version": (C.c_int, []),
@@ -95,6 +98,8 @@ SIGNATURES = {
     "dab_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "dab_create_dist": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint8),
                                   C.POINTER(C.c_void_p)]),
+    "dab_create_dist_host": (C.c_int, [C.c_int, C.c_int, C.c_int, HostAllreduceFn, C.c_void_p,
+                                       C.POINTER(C.c_void_p)]),
     "dab_destroy": (C.c_int, [C.c_void_p]),
     "dab_set_problem": (C.c_int, [C.c_void_p, C.POINTER(DabProblem)]),
     "dab_update_parameters": (C.c_int, [C.c_void_p, _dp, _dp]),

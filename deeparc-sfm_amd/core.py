@@ -61,6 +61,24 @@ class Problem:
                        self.obs_intr[m], self.points, self.ext, self.intr, self.intr_nf,
                        self.intr_nk, self.ext_const, self.freeze_camera)
 
+    def point_owner(self, world):
+        """Owner rank of every point for a world-size sharding (partition by
+        point, so V, V^-1 and the back-substitution stay GPU-local): contiguous point-id
+        ranges whose observation counts are balanced. Cameras are replicated."""
+        npts = int(self.points.shape[0])
+        cnt = np.bincount(self.obs_point, minlength=npts).astype(np.int64)
+        total = int(cnt.sum())
+        start = np.cumsum(cnt) - cnt
+        return np.minimum(start * world // max(total, 1), world - 1).astype(np.int32)
+
+    def shard(self, rank, world):
+        """The observations of the points owned by `rank` (parameter arrays shared, the
+        gauge / ext_const of the global problem kept)."""
+        if world <= 1:
+            return self
+        owner = self.point_owner(world)
+        return self.subset(owner[self.obs_point] == rank)
+
     def as_c(self):
         """dab_problem view of the arrays (valid while self is alive)."""
         p = DabProblem()
@@ -155,12 +173,28 @@ def summary_to_dict(s, its):
 
 
 class Solver:
-    """One libdab handle (one GPU). For multi-GPU pass rank/world/unique_id."""
+    """One libdab handle (one GPU). For multi-GPU pass rank/world/unique_id (RCCL).
 
-    def __init__(self, device=0, rank=0, world_size=1, unique_id=None):
+    host_allreduce (rehearsal only): a callable(np.ndarray, op) that all-reduces the array
+    in place across ranks (op "sum" | "max"), e.g. over gloo; the library then stages its
+    collectives through host memory instead of RCCL, so several ranks may share one GPU."""
+
+    def __init__(self, device=0, rank=0, world_size=1, unique_id=None, host_allreduce=None):
         self.lib = load_library()
         h = C.c_void_p()
-        if world_size > 1:
+        self._cb = None
+        if world_size > 1 and host_allreduce is not None:
+            def _cb(buf, count, op, user):
+                try:
+                    arr = np.ctypeslib.as_array(buf, shape=(int(count),))
+                    host_allreduce(arr, "max" if op == 1 else "sum")
+                    return 0
+                except Exception:  # reported to the library as a collective failure
+                    return 1
+            self._cb = _abi.HostAllreduceFn(_cb)
+            check(self.lib.dab_create_dist_host(device, rank, world_size, self._cb, None, C.byref(h)),
+                  self.lib)
+        elif world_size > 1:
             buf = (C.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
             check(self.lib.dab_create_dist(device, rank, world_size, buf, C.byref(h)), self.lib)
         else:

@@ -173,6 +173,7 @@ struct dab_handle {
     if (h_scal) (void)hipHostFree(h_scal);
     if (h_flags) (void)hipHostFree(h_flags);
     if (h_pcg_state) (void)hipHostFree(h_pcg_state);
+    if (h_stage) (void)hipHostFree(h_stage);
     if (chol) chol_destroy(chol);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -188,9 +189,56 @@ struct dab_handle {
   double* ybc() { return d_spack + (size_t)36 * nblk; }
   size_t spack_count() const { return (size_t)36 * nblk + (size_t)6 * NC; }
 
+  // host-staged collective (dab_create_dist_host): rehearsal path, not the product path
+  dab_host_allreduce_fn host_cb = nullptr;
+  void* host_user = nullptr;
+  double* h_stage = nullptr;  // pinned
+  size_t stage_cap = 0;
+
+  int stage(size_t n) {
+    if (n <= stage_cap) return 0;
+    if (h_stage) (void)hipHostFree(h_stage);
+    h_stage = nullptr;
+    stage_cap = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&h_stage), n * sizeof(double)) != hipSuccess)
+      return set_error(DAB_E_NOMEM, "pinned staging allocation failed");
+    stage_cap = n;
+    return 0;
+  }
+  int host_allreduce(double* buf, size_t n, int op) {
+    CHECK_RC(stage(n));
+    HIP_OK(hipMemcpyAsync(h_stage, buf, n * sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    if (host_cb(h_stage, (int64_t)n, op, host_user) != 0)
+      return set_error(DAB_E_COMM, "host all-reduce callback failed");
+    HIP_OK(hipMemcpyAsync(buf, h_stage, n * sizeof(double), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    return 0;
+  }
+
   int allreduce(double* buf, size_t n, ncclRedOp_t op) {
     if (world <= 1 || n == 0) return 0;
+    if (host_cb) return host_allreduce(buf, n, op == ncclMax ? 1 : 0);
     NCCL_OK(ncclAllReduce(buf, buf, n, ncclDouble, op, comm, stream));
+    return 0;
+  }
+  // max over ranks of small int flag arrays
+  int allreduce_max_i32(int* buf, int n) {
+    if (world <= 1 || n == 0) return 0;
+    if (!host_cb) {
+      NCCL_OK(ncclAllReduce(buf, buf, n, ncclInt32, ncclMax, comm, stream));
+      return 0;
+    }
+    int tmp[16];
+    if (n > 16) return set_error(DAB_E_INVALID, "flag all-reduce too large");
+    CHECK_RC(stage(n));
+    HIP_OK(hipMemcpyAsync(tmp, buf, n * sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    for (int i = 0; i < n; ++i) h_stage[i] = tmp[i];
+    if (host_cb(h_stage, n, 1, host_user) != 0) return set_error(DAB_E_COMM, "host all-reduce callback failed");
+    for (int i = 0; i < n; ++i) tmp[i] = (int)h_stage[i];
+    HIP_OK(hipMemcpyAsync(buf, tmp, n * sizeof(int), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipStreamSynchronize(stream));
     return 0;
   }
 };
@@ -265,6 +313,20 @@ extern "C" int dab_create_dist(int device, int rank, int world_size, const uint8
       return set_error(DAB_E_COMM, msg);
     }
   }
+  return 0;
+}
+
+extern "C" int dab_create_dist_host(int device, int rank, int world_size, dab_host_allreduce_fn cb, void* user,
+                                    dab_handle** out) {
+  clear_error();
+  if (world_size < 1 || rank < 0 || rank >= world_size) return set_error(DAB_E_INVALID, "bad rank/world");
+  if (world_size > 1 && !cb) return set_error(DAB_E_INVALID, "null all-reduce callback");
+  CHECK_RC(create_common(device, out));
+  dab_handle* h = *out;
+  h->rank = rank;
+  h->world = world_size;
+  h->host_cb = cb;
+  h->host_user = user;
   return 0;
 }
 
@@ -1082,7 +1144,7 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
                      h->d_gpart, h->red_grid);
     launch_final_sum(s, h->red_grid, 3, h->d_gpart, h->d_scal + S_MODEL);
     CHECK_RC(h->allreduce(h->d_scal + S_MODEL, 5, ncclSum));
-    if (h->world > 1) NCCL_OK(ncclAllReduce(h->d_flags, h->d_flags, 4, ncclInt32, ncclMax, h->comm, s));
+    CHECK_RC(h->allreduce_max_i32(h->d_flags, 4));
     CHECK_RC(read_scalars(h));
     const double tdone = now_s();
     sum->linear_solver_time_in_seconds += tre - tls;

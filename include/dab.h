@@ -169,6 +169,14 @@ int dab_create(int device, dab_handle** out);
 int dab_comm_unique_id(uint8_t out_id[128]);
 int dab_create_dist(int device, int rank, int world_size, const uint8_t unique_id[128],
                     dab_handle** out);
+/* Host-staged collective, for rehearsing the multi-rank path where RCCL cannot run
+ * (several ranks sharing one GPU; CI). Every all-reduce copies the device buffer to
+ * host memory and calls cb(buf, count, op, user), which must reduce it in place across
+ * the ranks (op 0 = sum, 1 = max; e.g. over gloo) and return 0. Not the product path:
+ * one process per GPU uses dab_create_dist (RCCL over xGMI). */
+typedef int (*dab_host_allreduce_fn)(double* buf, int64_t count, int op, void* user);
+int dab_create_dist_host(int device, int rank, int world_size, dab_host_allreduce_fn cb, void* user,
+                         dab_handle** out);
 int dab_destroy(dab_handle* h);
 
 /* ---- problem upload / solve ------------------------------------------------------------

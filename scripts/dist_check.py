@@ -1,0 +1,97 @@
+"""Multi-rank check of the RCCL path on whatever GPUs the box has.
+
+Launch: python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1
+        --master-port P scripts/dist_check.py [--device D]
+Every rank solves its point shard of one global problem through dab_create_dist; rank 0
+also solves the global problem on one handle and compares the LM trajectories (explicit
+Schur and PCG). With --device D every rank uses device D (ranks sharing one GPU; RCCL
+refuses that, so pair it with --host-collective, which stages the library's collectives
+through gloo and exercises every other part of the sharded path).
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--device", type=int, default=-1)
+    ap.add_argument("--host-collective", action="store_true",
+                    help="stage the library's all-reduces through gloo (ranks sharing a GPU)")
+    a = ap.parse_args()
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dev = a.device if a.device >= 0 else int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    import _pkgload
+
+    pkg = _pkgload.load()
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    buf = torch.zeros(128, dtype=torch.uint8)
+    if rank == 0:
+        buf[:] = torch.tensor(list(pkg.Solver.unique_id()), dtype=torch.uint8)
+    dist.broadcast(buf, 0)
+    uid = bytes(buf.tolist())
+    def gloo_allreduce(arr, op):
+        t = torch.from_numpy(arr)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+
+    out = {}
+    for kind in ("bal", "rig"):
+        if kind == "bal":
+            glob = pkg.synth(kind=0, num_cameras=40, num_points=4000, obs_per_point=6, seed=61)
+        else:
+            glob = pkg.synth(kind=1, num_arcs=5, num_rings=12, num_points=3000, obs_per_point=7, seed=62)
+        owner = glob.point_owner(world)
+        for lst in (pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR, pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG):
+            opts = pkg.options(max_num_iterations=12, linear_solver_type=lst)
+            ref = None
+            if rank == 0:
+                g1 = glob.copy()
+                s1 = pkg.Solver(dev)
+                s1.set_problem(g1)
+                ref = (s1.solve(opts), g1.points.copy(), g1.ext.copy())
+                s1.close()
+            dist.barrier()
+            mine = glob.copy().shard(rank, world)
+            s = pkg.Solver(dev, rank, world, uid, host_allreduce=gloo_allreduce if a.host_collective else None)
+            s.set_problem(mine)
+            summ = s.solve(opts)
+            s.close()
+            pts = torch.from_numpy(np.where((owner == rank)[:, None], mine.points, 0.0))
+            dist.all_reduce(pts)
+            ext = torch.from_numpy(mine.ext.copy())
+            dist.all_reduce(ext, op=dist.ReduceOp.MAX)
+            ext_min = torch.from_numpy(mine.ext.copy())
+            dist.all_reduce(ext_min, op=dist.ReduceOp.MIN)
+            if rank == 0:
+                rs, rp, re = ref
+                ca = [it["cost"] for it in summ["iterations"]]
+                cb = [it["cost"] for it in rs["iterations"]]
+                n = min(len(ca), len(cb))
+                out[f"{kind}_{lst}"] = dict(
+                    iters=(summ["num_iterations"], rs["num_iterations"]),
+                    term=(summ["termination"], rs["termination"]),
+                    max_rel_cost=float(max(abs(x - y) / abs(y) for x, y in zip(ca[:n], cb[:n]))),
+                    final=(summ["final_cost"], rs["final_cost"]),
+                    dpts=float(np.abs(pts.numpy() - rp).max()),
+                    dext=float(np.abs(ext.numpy() - re).max()),
+                    ext_ranks_equal=bool(torch.equal(ext, ext_min)))
+    if rank == 0:
+        print(json.dumps(out, indent=1))
+        bad = [k for k, v in out.items()
+               if v["iters"][0] != v["iters"][1] or v["max_rel_cost"] > 1e-8 or v["dpts"] > 1e-6
+               or v["dext"] > 1e-6 or not v["ext_ranks_equal"]]
+        print("DIST_CHECK", "FAIL " + ",".join(bad) if bad else "OK")
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

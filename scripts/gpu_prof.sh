@@ -1,11 +1,20 @@
 #!/bin/bash
-# GPU box: parity tests, then the bench under rocprofv3 --kernel-trace --stats.
+# GPU box: HBM traffic (two separate PMC passes), the bench line, then the bench under
+# rocprofv3 --kernel-trace --stats. Every GPU step has its own time limit; the script stops
+# at the first failure. Outputs under gpurun_out/prof_<tag>/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
+TAG=${TAG:-r01}
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -q -m gpu -x > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench.log 2>&1
-rc=$?; echo "bench rc=$rc"; tail -2 gpurun_out/bench.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu ${PROF_ARGS} > gpurun_out/prof.log 2>&1
-rc=$?; echo "prof rc=$rc"; exit $rc
+SHORT="--steps 10 --warmup 3 --no-cpu --no-lm"
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 bench.py $SHORT ${PROF_ARGS} > $OUT/fetch.log 2>&1 || { echo "fetch pass failed"; tail -20 $OUT/fetch.log; exit 1; }
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 bench.py $SHORT ${PROF_ARGS} > $OUT/write.log 2>&1 || { echo "write pass failed"; tail -20 $OUT/write.log; exit 1; }
+python3 scripts/traffic.py $OUT/fetch $OUT/write profiles/traffic_latest.json > $OUT/traffic.txt 2>&1 || { cat $OUT/traffic.txt; exit 1; }
+cp profiles/traffic_latest.json $OUT/
+head -25 $OUT/traffic.txt
+timeout -k 10 600 python3 bench.py ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -20 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --no-cpu ${PROF_ARGS} > $OUT/trace.log 2>&1 || { echo "trace pass failed"; tail -20 $OUT/trace.log; exit 1; }
+find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
+head -30 $OUT/kernel_stats.csv

@@ -1,0 +1,25 @@
+"""Sharded multi-rank path on the GPU: two ranks on one device, the library's collectives
+staged through gloo (dab_create_dist_host; RCCL refuses two ranks per GPU). Each rank
+solves its point shard; the LM trajectories (explicit Schur and PCG, BAL and rig) must
+match the single-handle solve of the global problem (costs 1e-8 relative, parameters 1e-6)."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_two_ranks_match_single_handle(gpu):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "scripts", "dist_check.py"), "--device", "0", "--host-collective"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "DIST_CHECK OK" in p.stdout, p.stdout[-3000:]
