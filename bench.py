@@ -2,8 +2,9 @@
 
 metric (BASELINE.json): "M observations/sec residual+Jacobian; wall-clock/LM-iter".
   step  = one evaluation pass over the rank's shard with inputs resident in HBM:
-          residual + analytic-Jacobian kernel, then the J^T J / J^T r block assembly
-          (per-point V, g; per-camera U, g_c all-reduced over RCCL when N > 1).
+          residual + analytic Jacobian of every observation, reduced on chip into the
+          J^T J / J^T r blocks (matrix-free: point side k_eval_points -> V, g; camera
+          side k_eval_cams -> U, g_c, all-reduced over RCCL when N > 1).
   value = observations processed by all ranks / max-over-ranks wall time, in M obs/s.
   workload: BASELINE config 3 shape per GPU (1k cameras / 100k points / 1M obs, fp64);
           at N GPUs every rank holds a 1M-obs shard of one N-shard global problem that
@@ -11,7 +12,7 @@ metric (BASELINE.json): "M observations/sec residual+Jacobian; wall-clock/LM-ite
   lm_iter_ms: wall-clock per LM iteration on the same problem, measured in the same run
           (median over the timed iterations): lm_* with the exact dense-Schur step
           (the reference's DENSE_SCHUR), lm_pcg_* with implicit-Schur PCG.
-  roofline: residual+Jacobian kernel, algorithmic bytes / HIP-event kernel time.
+  roofline: k_eval_points (point side of the pass), algorithmic bytes / HIP-event time.
   cpu_baseline: the C oracle (Ceres-semantics restatement, OpenMP) on the box's host
           cores, rank 0 at N=1 only, bounded sample.
 """
@@ -189,15 +190,15 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (SURVEY §8d generator; reference data files are stripped)",
             "config": {"workload": args.config + " per GPU: 1000 cameras, 100000 points, "
-                       "1000000 observations, BAL-shaped, eval pass = residual+Jacobian + JtJ "
-                       "block assembly", "global_obs": world * n_obs,
+                       "1000000 observations, BAL-shaped, eval pass = residual+Jacobian reduced "
+                       "into the JtJ/Jtr blocks", "global_obs": world * n_obs,
                        "parallelism": f"point-sharded x{world}, RCCL all-reduce of camera blocks"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_jacobian", "kernel_ms": jac_ms,
+                         "kernel": "k_eval_points", "kernel_ms": jac_ms,
                          "algorithmic_bytes_per_launch": jac_bytes},
-            "jacobian_kernel_mobs_per_s": n_obs / (jac_ms * 1e-3) / 1e6,
-            "assembly_ms": asm_ms,
+            "point_kernel_mobs_per_s": n_obs / (jac_ms * 1e-3) / 1e6,
+            "camera_side_ms": asm_ms,
             "cpu_baseline": cpu,
         }
         if lm:

@@ -8,26 +8,27 @@ namespace dab {
 
 constexpr int kCamTab = 32;   // doubles per extrinsic table: R(9) t(3) Rd(9) Jd(9) pad(2)
 constexpr int kIntr = 8;      // doubles per intrinsic: cx cy fx fy k0 k1 0 0
-constexpr int kRec = 16;      // doubles per camera-entry record: Jc row0(6) row1(6) r(2) pad(2)
 constexpr int kYRec = 18;     // doubles per Y_e record (6x3)
 constexpr int kRedBlock = 256;
-constexpr int kChunk = 1024;  // max elements per reduction chunk
-constexpr int kWin = 64;      // observations per wave window (segmented point reduction)
+constexpr int kChunk = 256;   // max elements per reduction chunk (one per thread)
+constexpr int kSlotBit = 1 << 30;  // cm_idx.w flag: the entry is the ring (slot 1) camera
 
 // Device-side problem view. Observations are point-major ("s" order). An "entry" is an
 // observation slot whose extrinsic is free; entries have a point-major index e and a
-// camera-major position pos (records live at pos).
+// camera-major position pos (Y records live at pos). cm_idx / cm_xy are a static
+// camera-major copy of the observation inputs, so camera-side passes stream them.
 struct DevView {
-  int N;          // observations
+  int N;          // observation slots (SELL-64 layout, padding slots have point -1)
   int NP;         // points (local, referenced)
   int E;          // extrinsics
   int NC;         // free cameras
   int NE;         // entries
-  int nwin;       // ceil(N / kWin)
+  int nslice;     // SELL-64 slices (64 points each)
   const int4* obs_idx;      // (point, ext0, ext1, intr)
   const double2* obs_xy;
-  const int2* obs_ent;      // camera-major positions of slot 0 / slot 1 entries (-1: none)
-  const int* pt_obs_ptr;    // [NP+1]
+  const int4* cm_idx;       // [NE] obs_idx of the entry's observation, w |= kSlotBit for slot 1
+  const double2* cm_xy;     // [NE]
+  const int* slice_off;     // [nslice+1] first slot of each slice (slice length = 64 x longest track)
   const int* pt_ent_ptr;    // [NP+1]
   const int* ent_os;        // [NE] s*2+slot (point-major)
   const int* ent_cam;       // [NE]
@@ -40,30 +41,24 @@ struct DevView {
 
 // camera tables for all extrinsics from ext[E][6]
 void launch_cam_tables(hipStream_t s, int E, const double* ext, double* camtab);
-// Product residual + Jacobian pass (row a1-a4 + the point half of a7's assembly):
-//   r[N] (double2), Jp[6][N] (d r / d X planes, plane = 2*col + row),
-//   rec[pos][kRec] camera-entry records (d r / d (w,t) and r), point V[6][NP], g[3][NP]
-//   (segmented wave reduction; straddling points through wpart + launch_point_fixup),
-//   partial[grid][2] = {sum r^2, non-finite}.
-void launch_jacobian(hipStream_t s, const DevView& v, const double* points, const double* camtab,
-                     double* r, double* Jp, double* rec, double* V, double* g, double* wpart,
-                     double* partial, int grid);
-// straddling points: strad[k] = (p, first window, last window)
-void launch_point_fixup(hipStream_t s, int nstrad, const int4* strad, const double* wpart, int NP,
-                        double* V, double* g);
+// Point side of the evaluation pass (rows a1-a4, matrix-free): residual + d r / d X per
+// observation reduced into V[6][NP], g[3][NP] (one SELL slice per block, lane = point,
+// wps = 4 | 8 | 16 waves per slice), partial[grid][2] = {sum r^2, non-finite}.
+void launch_eval_points(hipStream_t s, const DevView& v, const double* points, const double* camtab, double* V,
+                        double* g, double* partial, int grid, int wps);
 // Full Jacobian planes (parity API): Jfull[30][N], r[N]
 void launch_jacobian_full(hipStream_t s, const DevView& v, const double* points,
                           const double* camtab, double* r, double* Jfull);
 // residual only, with per-block partial sums of r^2 and a non-finite count
 void launch_residual(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                      double* r_out /*nullable*/, double* partial /*[grid][2]*/, int grid);
-// camera-major reductions over records
+// camera side of the evaluation pass (matrix-free, camera-major inputs):
 //  U/g: per entry 21 (Jc^T Jc upper) + 6 (Jc^T r) -> partial[chunk][27]
-void launch_cam_ug_partial(hipStream_t s, int nchunk, const int* chunk_beg, const double* rec,
-                           double* partial);
-//  cross blocks Jc0^T Jc1 over composed observations -> partial[chunk][36]
-void launch_cross_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
-                          const int* xobs, const double* rec, double* partial);
+void launch_eval_cams(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const double* points,
+                      const double* camtab, double* partial);
+//  arc∘ring cross blocks Jc0^T Jc1 over composed observations (pair-major copy) -> partial[chunk][36]
+void launch_eval_cross(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
+                       const double2* x_xy, const double* points, const double* camtab, double* partial);
 //  final: seg_out[seg][K] = sum of partial chunks [seg_chunk[seg], seg_chunk[seg+1])
 void launch_seg_final(hipStream_t s, int nseg, int K, const int* seg_chunk, const double* partial,
                       double* out);
@@ -80,12 +75,13 @@ void launch_cam_norms(hipStream_t s, int E, const int* ext_col, const double* ex
 struct StepScalars {
   double radius, min_diag, max_diag;
 };
-// point factor: Vs = s V s + D^2, L = chol(Vs) -> L[6][NP], q = L^-1 (s g) -> q[NP][4]
+// point factor: Vs = s V s + D^2 = L L^T -> PU[NP][6] = diag(s) L^-T (upper: 00 01 02 11
+// 12 22), q = L^-1 (s g) -> q[NP][4]
 void launch_point_factor(hipStream_t s, const DevView& v, const double* V, const double* g,
-                         const double* scale_p, StepScalars sc, double* L, double* q, int* fail);
-// entry Y_e = (s_c ∘ Jc^T Jp ∘ s_p) L^-T -> Y[pos][kYRec]
-void launch_entry_y(hipStream_t s, const DevView& v, const double* Jp, const double* rec,
-                    const double* scale_p, const double* scale_c, const double* L, double* Y);
+                         const double* scale_p, StepScalars sc, double* PU, double* q, int* fail);
+// entry Y_pos = (s_c ∘ Jc^T Jp) PU_p -> Y[pos][kYRec] (re-evaluated, camera-major)
+void launch_entry_y(hipStream_t s, const DevView& v, const double* points, const double* camtab,
+                    const double* scale_c, const double* PU, double* Y);
 // S blocks (Y part): packed[blk][36] = - sum_pairs Y_row Y_col^T (pairs hold positions)
 void launch_s_blocks(hipStream_t s, int nblk, const int* blk_pair_beg, const int2* pairs,
                      const double* Y, double* packed);
@@ -99,8 +95,8 @@ void launch_s_unpack(hipStream_t s, int NC, int nblk, const int2* blk_cam, const
                      const double* ug, int ncross, const int2* cross_cam,
                      const double* Ucross /*[ncross][36]*/, const double* scale_c, StepScalars sc,
                      const double* ybc /*[NC][6]*/, double* S, int lds);
-// y_p = L^-T (q - sum_e Y_e^T y_c); delta_p = -y_p * s_p -> dp[3][NP]
-void launch_backsub(hipStream_t s, const DevView& v, const double* L, const double* q,
+// delta_p = -PU (q - sum_e Y_e^T y_c) -> dp[3][NP]
+void launch_backsub(hipStream_t s, const DevView& v, const double* PU, const double* q,
                     const double* Y, const double* yc, const double* scale_p, double* delta_p);
 // x_c = x + delta for points; partial[grid][2] = {sum (x-xc)^2, sum xc^2}
 void launch_axpy_points(hipStream_t s, int NP, const double* x, const double* d, double* xc,
@@ -110,9 +106,9 @@ void launch_cam_candidate(hipStream_t s, int E, const int* ext_col, const double
                           double* delta_c);
 // model cost change + candidate cost in one observation pass:
 //  partial[grid][3] = { sum -(m.(r+m/2)), sum rc^2, nonfinite }
-void launch_candidate(hipStream_t s, const DevView& v, const double* Jp, const double* rec,
-                      const double* r, const double* delta_p, const double* delta_c,
-                      const double* points_c, const double* camtab_c, double* partial, int grid);
+void launch_candidate(hipStream_t s, const DevView& v, const double* points, const double* camtab,
+                      const double* delta_p, const double* delta_c, const double* camtab_c, double* partial,
+                      int grid);
 // gradient norms over points: partial[grid][3] = {max |x-(x-g)|, sum (x-(x-g))^2, sum x^2}
 void launch_grad_points(hipStream_t s, int NP, const double* x, const double* g /*[3][NP]*/,
                         double* partial, int grid);

@@ -2,16 +2,16 @@
 //
 // Data layout in HBM (all wave64, coalesced on the dominant streams):
 //   point-major observation streams ("s" order, observations of one point contiguous)
-//     obs_idx int4 (point, ext0, ext1, intr) 16 B, obs_xy double2 16 B, obs_ent int2 8 B
-//     r double2 16 B, Jp[6][N] planes 48 B (d r / d X, plane = 2*col + row)
-//   camera-major entry records (one per observation slot whose extrinsic is free):
-//     rec[pos][16] = d r / d(w,t) row 0 (6) | row 1 (6) | r (2) | pad   128 B
+//     obs_idx int4 (point, ext0, ext1, intr) 16 B, obs_xy double2 16 B
+//   camera-major entry inputs (one per observation slot whose extrinsic is free, static):
+//     cm_idx int4 16 B, cm_xy double2 16 B
 //     Y[pos][18]   = Schur factor of the entry, per LM iteration       144 B
-//   per-point V[6][NP], g[3][NP], L[6][NP], q[NP][4]; per-camera ug[NC][27].
-// The residual+Jacobian kernel writes the records straight to their camera-major slots,
-// so every camera-side reduction (U, g_c, Schur rhs, S blocks) streams contiguous
-// records instead of gathering 8-byte words, and it reduces the point blocks V, g with a
-// deterministic segmented wave scan instead of a second pass over J.
+//   per-point V[6][NP], g[3][NP], PU[NP][6], q[NP][4]; per-camera ug[NC][27].
+// Matrix-free: the Jacobian is never stored. Each pass re-evaluates the rows it needs
+// from the 32-B inputs (point side in point-major order, camera side from the
+// camera-major copy) and reduces them on chip: V, g by a deterministic segmented wave
+// scan, U, g_c by fixed-shape chunk reductions. Per observation that moves ~32 B instead
+// of writing and re-reading a 144-240 B Jacobian.
 // Per-extrinsic rotation data is precomputed once per parameter state (k_cam_tables):
 // d(R(w)X)/dw = -R [X]x J_r(w) (right Jacobian of SO(3)); in Ceres' first-order branch
 // (|w|^2 <= DBL_EPSILON, rotation.h) R = I + [w]x and the derivative is -[X]x, encoded as
@@ -20,8 +20,10 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <cstdlib>
 
 #include "dab_kernels.h"
+#include "dab_wave.h"
 
 namespace dab {
 
@@ -38,17 +40,11 @@ int grid_for(int n, int block, int cap) {
 template <int K>
 __device__ __forceinline__ void block_reduce_store(double (&acc)[K], double* __restrict__ out) {
   __shared__ double sh[kRedBlock / 64][K];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < K; ++i) {
-    double v = acc[i];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    acc[i] = v;
-  }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) {
-#pragma unroll
-    for (int i = 0; i < K; ++i) sh[w][i] = acc[i];
+    const double v = wave_sum_lane63(acc[i]);
+    if (lane == 63) sh[w][i] = v;
   }
   __syncthreads();
   if (threadIdx.x < K) {
@@ -276,219 +272,238 @@ struct ObsJac {
   double jt1a[3], jt1b[3];  // d r / d t1   (d r / d t0 = pr.A0 / pr.A1)
 };
 
-// The table is read in the order the math needs it (R,t -> project -> A R -> Rd -> Jd) so
-// that only one 3x3 block per camera is live at a time (register pressure sets occupancy).
-__device__ __forceinline__ void obs_jacobian(const int4 id, const double2 xy, const double X[3],
-                                             const double* __restrict__ camtab,
-                                             const double* __restrict__ K, ObsJac& o) {
-  // One uniform flow for both forms; the branch only selects values (a select between two
-  // private arrays would force them into scratch). Q is the point the arc/single rotation
-  // acts on: X (single) or P2 = R1 X + t1 (arc∘ring).
+// Table rows come in with 16-byte vector loads into registers: in BAL-shaped problems
+// every lane of a wave reads a different camera, so the number of load instructions
+// (not bytes) is what the L2 sees. R,t first (needed for the residual), Rd/Jd only by the
+// passes that want camera rows.
+template <int OFF, int NT>
+__device__ __forceinline__ void load_tab_at(const double* __restrict__ camtab, int e, double (&T)[NT]) {
+  const double2* p = reinterpret_cast<const double2*>(camtab + (size_t)kCamTab * e + OFF);
+#pragma unroll
+  for (int i = 0; i < NT / 2; ++i) {
+    const double2 v = p[i];
+    T[2 * i] = v.x;
+    T[2 * i + 1] = v.y;
+  }
+}
+__device__ __forceinline__ void load_intr(const double* __restrict__ intr, int i, double (&K)[6]) {
+  const double2* p = reinterpret_cast<const double2*>(intr + (size_t)kIntr * i);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double2 v = p[k];
+    K[2 * k] = v.x;
+    K[2 * k + 1] = v.y;
+  }
+}
+
+// Residual and the Jacobian rows of one observation that a pass needs, from the camera
+// tables. JP: d r / d X (2x3). SLOT 0: d r / d (w0, t0); SLOT 1: d r / d (w1, t1) of the
+// ring camera of an arc∘ring observation; SLOT 2: both (jc0/jc1 = slot 0 rows, jd0/jd1 =
+// slot 1 rows); SLOT -1: no camera rows. Q is the point the arc/single rotation acts on:
+// X (single) or P2 = R1 X + t1 (arc∘ring).
+template <bool JP, int SLOT>
+__device__ __forceinline__ void obs_rows(const int4 id, const double2 xy, const double X[3],
+                                         const double* __restrict__ camtab, const double* __restrict__ intr,
+                                         double& ru, double& rv, double jx0[3], double jx1[3], double jc0[6],
+                                         double jc1[6], double jd0[6] = nullptr, double jd1[6] = nullptr) {
   const bool comp = id.z >= 0;
-  const double* __restrict__ T0 = camtab + (size_t)kCamTab * id.y;
-  const double* __restrict__ T1 = camtab + (size_t)kCamTab * (comp ? id.z : id.y);
-  double Q[3];
+  double A[12];  // R0 | t0
+  load_tab_at<0, 12>(camtab, id.y, A);
+  double Kr[6];
+  load_intr(intr, id.w, Kr);
+  double Q[3], B[12];  // B = R1 | t1 (arc∘ring only)
   if (comp) {
-    matvec_add(T1, X, T1 + 9, Q);
+    load_tab_at<0, 12>(camtab, id.z, B);
+    matvec_add(B, X, B + 9, Q);
   } else {
     Q[0] = X[0];
     Q[1] = X[1];
     Q[2] = X[2];
   }
   double P[3];
-  matvec_add(T0, Q, T0 + 9, P);
-  project(P, K, xy.x, xy.y, o.pr, true);
-  double B0a[3], B0b[3];
-  rowmat(o.pr.A0, T0, B0a);  // A R0 = d r / d Q
-  rowmat(o.pr.A1, T0, B0b);
-  if (comp) {
-    rowmat(B0a, T1, o.jx0);  // A R0 R1
-    rowmat(B0b, T1, o.jx1);
-    double Ca[3], Cb[3];
-    rowmat(B0a, T1 + 12, Ca);  // A R0 Rd1
-    rowmat(B0b, T1 + 12, Cb);
-    dwrot(Ca, X, T1 + 21, o.jw1a);
-    dwrot(Cb, X, T1 + 21, o.jw1b);
-  } else {
+  matvec_add(A, Q, A + 9, P);
+  Proj pr;
+  project(P, Kr, xy.x, xy.y, pr, true);
+  ru = pr.ru;
+  rv = pr.rv;
+  if constexpr (SLOT == 0 || SLOT == 2) {
+    double D[18];  // Rd0 | Jd0
+    load_tab_at<12, 18>(camtab, id.y, D);
+    double Da[3], Db[3];
+    rowmat(pr.A0, D, Da);
+    rowmat(pr.A1, D, Db);
+    dwrot(Da, Q, D + 9, jc0);
+    dwrot(Db, Q, D + 9, jc1);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      o.jx0[i] = B0a[i];
-      o.jx1[i] = B0b[i];
-      o.jw1a[i] = 0.0;
-      o.jw1b[i] = 0.0;
+      jc0[3 + i] = pr.A0[i];
+      jc1[3 + i] = pr.A1[i];
     }
   }
+  if constexpr (JP || SLOT >= 1) {
+    double B0a[3], B0b[3];
+    rowmat(pr.A0, A, B0a);  // A R0
+    rowmat(pr.A1, A, B0b);
+    if constexpr (SLOT >= 1) {
+      double* o0 = SLOT == 1 ? jc0 : jd0;
+      double* o1 = SLOT == 1 ? jc1 : jd1;
+      if (comp) {
+        double D[18];  // Rd1 | Jd1
+        load_tab_at<12, 18>(camtab, id.z, D);
+        double Ca[3], Cb[3];
+        rowmat(B0a, D, Ca);
+        rowmat(B0b, D, Cb);
+        dwrot(Ca, X, D + 9, o0);
+        dwrot(Cb, X, D + 9, o1);
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {  // d r / d t1 = A R0 (zero when single)
-    o.jt1a[i] = comp ? B0a[i] : 0.0;
-    o.jt1b[i] = comp ? B0b[i] : 0.0;
-  }
-  double Da[3], Db[3];
-  rowmat(o.pr.A0, T0 + 12, Da);  // A Rd0
-  rowmat(o.pr.A1, T0 + 12, Db);
-  dwrot(Da, Q, T0 + 21, o.jw0a);
-  dwrot(Db, Q, T0 + 21, o.jw0b);
-}
-
-__device__ __forceinline__ void store_rec(double* __restrict__ rec, int pos, const double wa[3],
-                                          const double wb[3], const double ta[3], const double tb[3],
-                                          double ru, double rv) {
-  double2* p = reinterpret_cast<double2*>(rec + (size_t)kRec * pos);
-  p[0] = make_double2(wa[0], wa[1]);
-  p[1] = make_double2(wa[2], ta[0]);
-  p[2] = make_double2(ta[1], ta[2]);
-  p[3] = make_double2(wb[0], wb[1]);
-  p[4] = make_double2(wb[2], tb[0]);
-  p[5] = make_double2(tb[1], tb[2]);
-  p[6] = make_double2(ru, rv);
-  p[7] = make_double2(0.0, 0.0);
-}
-
-// Product kernel. Block = 256 threads = 4 waves; wave windows of 64 consecutive
-// observations, grid-strided. V/g use an inclusive segmented scan keyed by point id.
-// VAR (ablation only, bench knob DAB_JAC_VARIANT): bit0 skip records, bit1 skip the V/g
-// scan, bit2 skip the Jp planes. MINW: __launch_bounds__ waves per SIMD.
-template <int VAR, int MINW>
-__global__ __launch_bounds__(256, MINW) void k_jacobian(DevView v, const double* __restrict__ points,
-                                                        const double* __restrict__ camtab,
-                                                        double2* __restrict__ r, double* __restrict__ Jp,
-                                                        double* __restrict__ rec, double* __restrict__ V,
-                                                        double* __restrict__ g, double* __restrict__ wpart,
-                                                        double* __restrict__ partial) {
-  const int N = v.N;
-  const size_t Ns = (size_t)N, NPs = (size_t)v.NP;
-  const int lane = threadIdx.x & 63;
-  double acc[2] = {0.0, 0.0};
-  for (int base = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kWin; base < N; base += gridDim.x * 4 * kWin) {
-    const int s = base + lane;
-    const bool valid = s < N;
-    double c[9];
-    int pt = -1 - lane;  // never equal across invalid lanes
-    if (valid) {
-      const int4 id = v.obs_idx[s];
-      const double2 xy = v.obs_xy[s];
-      const int2 ent = v.obs_ent[s];
-      pt = id.x;
-      const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
-      ObsJac o;
-      obs_jacobian(id, xy, X, camtab, v.intr + (size_t)kIntr * id.w, o);
-      const double ru = o.pr.ru, rv = o.pr.rv;
-      r[s] = make_double2(ru, rv);
-      if constexpr (!(VAR & 4)) {
+        for (int i = 0; i < 3; ++i) {
+          o0[3 + i] = B0a[i];
+          o1[3 + i] = B0b[i];
+        }
+      } else {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          Jp[(2 * k) * Ns + s] = o.jx0[k];
-          Jp[(2 * k + 1) * Ns + s] = o.jx1[k];
+        for (int i = 0; i < 6; ++i) {
+          o0[i] = 0.0;
+          o1[i] = 0.0;
         }
       }
-      if constexpr (!(VAR & 1)) {
-        if (ent.x >= 0) store_rec(rec, ent.x, o.jw0a, o.jw0b, o.pr.A0, o.pr.A1, ru, rv);
-        if (ent.y >= 0) store_rec(rec, ent.y, o.jw1a, o.jw1b, o.jt1a, o.jt1b, ru, rv);
+    }
+    if constexpr (JP) {
+      if (comp) {
+        rowmat(B0a, B, jx0);
+        rowmat(B0b, B, jx1);
       } else {
-        asm volatile("" ::"v"(o.jw0a[0]), "v"(o.jw0b[2]), "v"(o.jw1a[1]), "v"(o.jt1b[2]), "v"(ent.x));
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          jx0[i] = B0a[i];
+          jx1[i] = B0b[i];
+        }
       }
-      c[0] = o.jx0[0] * o.jx0[0] + o.jx1[0] * o.jx1[0];
-      c[1] = o.jx0[0] * o.jx0[1] + o.jx1[0] * o.jx1[1];
-      c[2] = o.jx0[0] * o.jx0[2] + o.jx1[0] * o.jx1[2];
-      c[3] = o.jx0[1] * o.jx0[1] + o.jx1[1] * o.jx1[1];
-      c[4] = o.jx0[1] * o.jx0[2] + o.jx1[1] * o.jx1[2];
-      c[5] = o.jx0[2] * o.jx0[2] + o.jx1[2] * o.jx1[2];
-      c[6] = o.jx0[0] * ru + o.jx1[0] * rv;
-      c[7] = o.jx0[1] * ru + o.jx1[1] * rv;
-      c[8] = o.jx0[2] * ru + o.jx1[2] * rv;
+    }
+  }
+}
+
+// Every row of one observation (parity API, cross blocks, candidate pass).
+__device__ __forceinline__ void obs_jacobian(const int4 id, const double2 xy, const double X[3],
+                                             const double* __restrict__ camtab,
+                                             const double* __restrict__ intr, ObsJac& o) {
+  double c0[6], c1[6], d0[6], d1[6];
+  obs_rows<true, 2>(id, xy, X, camtab, intr, o.pr.ru, o.pr.rv, o.jx0, o.jx1, c0, c1, d0, d1);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    o.jw0a[i] = c0[i];
+    o.jw0b[i] = c1[i];
+    o.pr.A0[i] = c0[3 + i];
+    o.pr.A1[i] = c1[3 + i];
+    o.jw1a[i] = d0[i];
+    o.jw1b[i] = d1[i];
+    o.jt1a[i] = d0[3 + i];
+    o.jt1b[i] = d1[3 + i];
+  }
+}
+
+// Point side of the evaluation pass (rows a1-a4 + the point half of a7), matrix-free:
+// residual and d r / d X per observation, reduced straight into V = Jp^T Jp (6) and
+// g_p = Jp^T r (3). Nothing per observation is written: every later pass re-evaluates
+// the rows it needs from the inputs (32 B per observation; the Jacobian is 144-240 B).
+// One block per SELL-64 slice: lane l owns point 64 sl + l (its X loaded once), wave w of
+// the WPS waves takes the slice's observation rows k = w, w + WPS, ... (coalesced 64-slot
+// rows), and the per-wave sums are combined in LDS in a fixed order: no cross-lane scan.
+template <int WPS, int VAR = 0>
+__global__ __launch_bounds__(64 * WPS) void k_eval_points(DevView v, const double* __restrict__ points,
+                                                          const double* __restrict__ camtab,
+                                                          double* __restrict__ V, double* __restrict__ g,
+                                                          double* __restrict__ partial) {
+  __shared__ double sh[WPS > 1 ? WPS - 1 : 1][9][64];
+  __shared__ double shp[WPS][2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const size_t NPs = (size_t)v.NP;
+  double acc[2] = {0.0, 0.0};
+  for (int sl = blockIdx.x; sl < v.nslice; sl += gridDim.x) {
+    const int p = 64 * sl + lane;
+    const int off = v.slice_off[sl], len = (v.slice_off[sl + 1] - off) >> 6;
+    double X[3] = {0.0, 0.0, 0.0};
+    if (p < v.NP) {
+      X[0] = points[3 * (size_t)p];
+      X[1] = points[3 * (size_t)p + 1];
+      X[2] = points[3 * (size_t)p + 2];
+    }
+    double c[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) c[k] = 0.0;
+    for (int k = w; k < len; k += WPS) {
+      const int s = off + 64 * k + lane;
+      int4 id = v.obs_idx[s];
+      if (id.x < 0) continue;  // padding slot
+      const double2 xy = v.obs_xy[s];
+      double ru, rv, jx0[3], jx1[3];
+      if constexpr (VAR == 1) {  // ablation: loads only
+        ru = xy.x + id.y;
+        rv = xy.y + id.w;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) jx0[q] = jx1[q] = X[q];
+      } else {
+        if constexpr (VAR == 2) id.y = id.w = 0;  // ablation: one camera (uniform table loads)
+        obs_rows<true, -1>(id, xy, X, camtab, v.intr, ru, rv, jx0, jx1, nullptr, nullptr);
+      }
+      c[0] += jx0[0] * jx0[0] + jx1[0] * jx1[0];
+      c[1] += jx0[0] * jx0[1] + jx1[0] * jx1[1];
+      c[2] += jx0[0] * jx0[2] + jx1[0] * jx1[2];
+      c[3] += jx0[1] * jx0[1] + jx1[1] * jx1[1];
+      c[4] += jx0[1] * jx0[2] + jx1[1] * jx1[2];
+      c[5] += jx0[2] * jx0[2] + jx1[2] * jx1[2];
+      c[6] += jx0[0] * ru + jx1[0] * rv;
+      c[7] += jx0[1] * ru + jx1[1] * rv;
+      c[8] += jx0[2] * ru + jx1[2] * rv;
       acc[0] += ru * ru + rv * rv;
       acc[1] += (isfinite(ru) && isfinite(rv)) ? 0.0 : 1.0;
-    } else {
-#pragma unroll
-      for (int k = 0; k < 9; ++k) c[k] = 0.0;
     }
-    if constexpr ((VAR & 2) != 0) {
-      asm volatile("" ::"v"(c[0]), "v"(c[5]), "v"(c[8]));
-      continue;
-    }
-    // inclusive segmented scan (Hillis–Steele) within the 64-lane window
+    if (WPS > 1) {
+      if (w > 0) {
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int pu = __shfl_up(pt, off, 64);
-      const bool take = lane >= off && pu == pt;
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        const double vu = __shfl_up(c[k], off, 64);
-        if (take) c[k] += vu;
+        for (int k = 0; k < 9; ++k) sh[w - 1][k][lane] = c[k];
       }
+      __syncthreads();
     }
-    const int pn = __shfl_down(pt, 1, 64);
-    const bool tail = valid && (lane == 63 || s + 1 == N || pn != pt);
-    if (tail) {
-      const int a = v.pt_obs_ptr[pt], b = v.pt_obs_ptr[pt + 1];
-      if (a >= base && b <= base + kWin) {
+    if (w == 0 && p < v.NP) {
+      if (WPS > 1) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) V[k * NPs + pt] = c[k];
+        for (int k = 0; k < 9; ++k) {
+          double t = c[k];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) g[k * NPs + pt] = c[6 + k];
-      } else {
-        const size_t w = (size_t)(base / kWin);
-        if (a < base) {  // the window's first segment
-#pragma unroll
-          for (int k = 0; k < 9; ++k) wpart[(2 * w) * 9 + k] = c[k];
-        }
-        if (b > base + kWin) {  // the window's last segment
-#pragma unroll
-          for (int k = 0; k < 9; ++k) wpart[(2 * w + 1) * 9 + k] = c[k];
+          for (int q = 0; q < WPS - 1; ++q) t += sh[q][k][lane];
+          c[k] = t;
         }
       }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) V[k * NPs + p] = c[k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) g[k * NPs + p] = c[6 + k];
     }
+    if (WPS > 1) __syncthreads();
   }
-  block_reduce_store<2>(acc, partial + 2 * (size_t)blockIdx.x);
-}
-
-void launch_jacobian(hipStream_t s, const DevView& v, const double* points, const double* camtab,
-                     double* r, double* Jp, double* rec, double* V, double* g, double* wpart,
-                     double* partial, int grid) {
-  // bench-only ablation knob (scripts/jac_ablation.py); unset = the product kernel
-  const char* env = getenv("DAB_JAC_VARIANT");
-  const int variant = env ? atoi(env) : 0;
-  double2* r2 = reinterpret_cast<double2*>(r);
-#define JAC_LAUNCH(VAR, MINW) \
-  k_jacobian<VAR, MINW><<<grid, 256, 0, s>>>(v, points, camtab, r2, Jp, rec, V, g, wpart, partial)
-  switch (variant) {
-    case 0: JAC_LAUNCH(0, 2); break;   // product default
-    case 100: JAC_LAUNCH(0, 3); break;
-    case 200: JAC_LAUNCH(0, 4); break;
-    case 1: JAC_LAUNCH(1, 2); break;
-    case 2: JAC_LAUNCH(2, 2); break;
-    case 3: JAC_LAUNCH(3, 2); break;
-    case 7: JAC_LAUNCH(7, 2); break;
-    case 201: JAC_LAUNCH(1, 4); break;
-    case 203: JAC_LAUNCH(3, 4); break;
-    case 207: JAC_LAUNCH(7, 4); break;
-    default: JAC_LAUNCH(0, 2); break;
+  // per-block cost partials: wave sums, then a fixed-order sum over the waves
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double t = wave_sum_lane63(acc[i]);
+    if (lane == 63) shp[w][i] = t;
   }
-#undef JAC_LAUNCH
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    double t = shp[0][threadIdx.x];
+#pragma unroll
+    for (int q = 1; q < WPS; ++q) t += shp[q][threadIdx.x];
+    partial[2 * (size_t)blockIdx.x + threadIdx.x] = t;
+  }
 }
 
-__global__ void k_point_fixup(int nstrad, const int4* __restrict__ strad, const double* __restrict__ wpart,
-                              int NP, double* __restrict__ V, double* __restrict__ g) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nstrad) return;
-  const int4 st = strad[t];  // (point, first window, last window)
-  double c[9];
-#pragma unroll
-  for (int k = 0; k < 9; ++k) c[k] = wpart[(2 * (size_t)st.y + 1) * 9 + k];
-  for (int w = st.y + 1; w <= st.z; ++w)
-#pragma unroll
-    for (int k = 0; k < 9; ++k) c[k] += wpart[(2 * (size_t)w) * 9 + k];
-  const size_t NPs = (size_t)NP;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) V[k * NPs + st.x] = c[k];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) g[k * NPs + st.x] = c[6 + k];
-}
-
-void launch_point_fixup(hipStream_t s, int nstrad, const int4* strad, const double* wpart, int NP,
-                        double* V, double* g) {
-  if (nstrad <= 0) return;
-  k_point_fixup<<<grid_for(nstrad, 256, 1 << 20), 256, 0, s>>>(nstrad, strad, wpart, NP, V, g);
+void launch_eval_points(hipStream_t s, const DevView& v, const double* points, const double* camtab, double* V,
+                        double* g, double* partial, int grid, int wps) {
+  if (wps == 41) k_eval_points<4, 1><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);  // ablations
+  else if (wps == 42) k_eval_points<4, 2><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);
+  else if (wps == 4) k_eval_points<4><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);
+  else if (wps == 16) k_eval_points<16><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
+  else k_eval_points<8><<<grid, 512, 0, s>>>(v, points, camtab, V, g, partial);
 }
 
 // parity API: every Jacobian column as planes Jfull[2*col+row][N]
@@ -499,9 +514,10 @@ __global__ __launch_bounds__(256) void k_jacobian_full(DevView v, const double* 
   const size_t Ns = (size_t)N;
   for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < N; s += gridDim.x * blockDim.x) {
     const int4 id = v.obs_idx[s];
+    if (id.x < 0) continue;  // padding slot
     const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
     ObsJac o;
-    obs_jacobian(id, v.obs_xy[s], X, camtab, v.intr + (size_t)kIntr * id.w, o);
+    obs_jacobian(id, v.obs_xy[s], X, camtab, v.intr, o);
     r[s] = make_double2(o.pr.ru, o.pr.rv);
     double* Jo = J + s;
 #pragma unroll
@@ -558,6 +574,7 @@ __global__ __launch_bounds__(256) void k_residual(DevView v, const double* __res
                                                   double* __restrict__ partial) {
   double acc[2] = {0.0, 0.0};
   for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < v.N; s += gridDim.x * blockDim.x) {
+    if (v.obs_idx[s].x < 0) continue;  // padding slot
     double ru, rv;
     residual_at(v, points, camtab, s, ru, rv);
     if (rout) rout[s] = make_double2(ru, rv);
@@ -573,62 +590,68 @@ void launch_residual(hipStream_t s, const DevView& v, const double* points, cons
 }
 
 // ------------------------------------------------------------------------------------
-// camera-side J^T J / J^T r reductions over contiguous records (row a7)
+// camera-side J^T J / J^T r reductions, matrix-free (row a7)
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ void load_rec(const double* __restrict__ rec, int pos, double (&q)[14]) {
-  const double2* p = reinterpret_cast<const double2*>(rec + (size_t)kRec * pos);
-#pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    const double2 t = p[i];
-    q[2 * i] = t.x;
-    q[2 * i + 1] = t.y;
-  }
-}
-
-__global__ __launch_bounds__(256) void k_cam_ug_partial(const int* __restrict__ chunk_beg,
-                                                        const double* __restrict__ rec,
-                                                        double* __restrict__ partial) {
+// One block per chunk of camera-major entry positions (one camera per chunk): the
+// entry's observation is re-evaluated from its camera-major input copy (cm_idx, cm_xy,
+// 32 B, contiguous) and its camera rows reduced into U (21 upper) | g_c (6).
+__global__ __launch_bounds__(256) void k_eval_cams(DevView v, const int* __restrict__ chunk_beg,
+                                                   const double* __restrict__ points,
+                                                   const double* __restrict__ camtab,
+                                                   double* __restrict__ partial) {
   const int c = blockIdx.x;
   const int b = chunk_beg[c], e = chunk_beg[c + 1];
   double acc[27];
 #pragma unroll
   for (int i = 0; i < 27; ++i) acc[i] = 0.0;
   for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
-    double q[14];
-    load_rec(rec, i, q);
-    const double* ja = q;
-    const double* jb = q + 6;
+    int4 id = v.cm_idx[i];
+    const bool slot1 = (id.w & kSlotBit) != 0;
+    id.w &= ~kSlotBit;
+    const double2 xy = v.cm_xy[i];
+    const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
+    double ru, rv, ja[6], jb[6];
+    if (slot1) obs_rows<false, 1>(id, xy, X, camtab, v.intr, ru, rv, nullptr, nullptr, ja, jb);
+    else obs_rows<false, 0>(id, xy, X, camtab, v.intr, ru, rv, nullptr, nullptr, ja, jb);
     int k = 0;
 #pragma unroll
     for (int a = 0; a < 6; ++a)
 #pragma unroll
       for (int bb = a; bb < 6; ++bb) acc[k++] += ja[a] * ja[bb] + jb[a] * jb[bb];
 #pragma unroll
-    for (int a = 0; a < 6; ++a) acc[21 + a] += ja[a] * q[12] + jb[a] * q[13];
+    for (int a = 0; a < 6; ++a) acc[21 + a] += ja[a] * ru + jb[a] * rv;
   }
   block_reduce_store<27>(acc, partial + 27 * (size_t)c);
 }
 
-void launch_cam_ug_partial(hipStream_t s, int nchunk, const int* chunk_beg, const double* rec,
-                           double* partial) {
+void launch_eval_cams(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const double* points,
+                      const double* camtab, double* partial) {
   if (nchunk <= 0) return;
-  k_cam_ug_partial<<<nchunk, 256, 0, s>>>(chunk_beg, rec, partial);
+  k_eval_cams<<<nchunk, 256, 0, s>>>(v, chunk_beg, points, camtab, partial);
 }
 
-__global__ __launch_bounds__(256) void k_cross_partial(DevView v, const int* __restrict__ chunk_beg,
-                                                       const int* __restrict__ xobs,
-                                                       const double* __restrict__ rec,
-                                                       double* __restrict__ partial) {
+// arc∘ring cross blocks Jc0^T Jc1, one block per chunk of composed observations sorted
+// by camera pair, re-evaluated from their pair-major input copy.
+__global__ __launch_bounds__(256) void k_eval_cross(DevView v, const int* __restrict__ chunk_beg,
+                                                    const int4* __restrict__ x_idx,
+                                                    const double2* __restrict__ x_xy,
+                                                    const double* __restrict__ points,
+                                                    const double* __restrict__ camtab,
+                                                    double* __restrict__ partial) {
   const int c = blockIdx.x;
   const int b = chunk_beg[c], e = chunk_beg[c + 1];
   double acc[36];
 #pragma unroll
   for (int i = 0; i < 36; ++i) acc[i] = 0.0;
   for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
-    const int2 ent = v.obs_ent[xobs[i]];
-    double qa[14], qb[14];
-    load_rec(rec, ent.x, qa);
-    load_rec(rec, ent.y, qb);
+    const int4 id = x_idx[i];
+    const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
+    ObsJac o;
+    obs_jacobian(id, x_xy[i], X, camtab, v.intr, o);
+    const double qa[12] = {o.jw0a[0], o.jw0a[1], o.jw0a[2], o.pr.A0[0], o.pr.A0[1], o.pr.A0[2],
+                           o.jw0b[0], o.jw0b[1], o.jw0b[2], o.pr.A1[0], o.pr.A1[1], o.pr.A1[2]};
+    const double qb[12] = {o.jw1a[0], o.jw1a[1], o.jw1a[2], o.jt1a[0], o.jt1a[1], o.jt1a[2],
+                           o.jw1b[0], o.jw1b[1], o.jw1b[2], o.jt1b[0], o.jt1b[1], o.jt1b[2]};
 #pragma unroll
     for (int a = 0; a < 6; ++a)
 #pragma unroll
@@ -637,10 +660,10 @@ __global__ __launch_bounds__(256) void k_cross_partial(DevView v, const int* __r
   block_reduce_store<36>(acc, partial + 36 * (size_t)c);
 }
 
-void launch_cross_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
-                          const int* xobs, const double* rec, double* partial) {
+void launch_eval_cross(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
+                       const double2* x_xy, const double* points, const double* camtab, double* partial) {
   if (nchunk <= 0) return;
-  k_cross_partial<<<nchunk, 256, 0, s>>>(v, chunk_beg, xobs, rec, partial);
+  k_eval_cross<<<nchunk, 256, 0, s>>>(v, chunk_beg, x_idx, x_xy, points, camtab, partial);
 }
 
 // ------------------------------------------------------------------------------------
@@ -681,8 +704,18 @@ __global__ __launch_bounds__(256) void k_point_factor(DevView v, const double* _
   const double q2 = (gs2 - l20 * q0 - l21 * q1) / l22;
   ok = ok && isfinite(q0) && isfinite(q1) && isfinite(q2);
   if (!ok) atomicOr(fail, 1);
-  L[p] = l00; L[NPs + p] = l10; L[2 * NPs + p] = l20;
-  L[3 * NPs + p] = l11; L[4 * NPs + p] = l21; L[5 * NPs + p] = l22;
+  // PU = diag(s) L^-T: L^-1 = [[a, 0, 0], [b, c, 0], [d, e, f]]
+  const double ia = 1.0 / l00, ic = 1.0 / l11, iff = 1.0 / l22;
+  const double ib = -l10 * ia * ic;
+  const double ie = -l21 * ic * iff;
+  const double id = -(l20 * ia + l21 * ib) * iff;
+  double* pu = L + 6 * (size_t)p;  // (00, 01, 02, 11, 12, 22) of diag(s) L^-T
+  pu[0] = s0 * ia;
+  pu[1] = s0 * ib;
+  pu[2] = s0 * id;
+  pu[3] = s1 * ic;
+  pu[4] = s1 * ie;
+  pu[5] = s2 * iff;
   reinterpret_cast<double2*>(q)[2 * (size_t)p] = make_double2(q0, q1);
   reinterpret_cast<double2*>(q)[2 * (size_t)p + 1] = make_double2(q2, 0.0);
 }
@@ -693,51 +726,45 @@ void launch_point_factor(hipStream_t s, const DevView& v, const double* V, const
   k_point_factor<<<grid_for(v.NP, 256, 1 << 20), 256, 0, s>>>(v, V, g, scale_p, sc, L, q, fail);
 }
 
-__global__ __launch_bounds__(256) void k_entry_y(DevView v, const double* __restrict__ Jp,
-                                                 const double* __restrict__ rec,
-                                                 const double* __restrict__ sp,
+// Y_pos = (s_c ∘ Jc^T Jp) PU_p for the entry at camera-major position pos, re-evaluated
+// from the camera-major input copy: contiguous inputs, contiguous 144 B record writes.
+__global__ __launch_bounds__(256) void k_entry_y(DevView v, const double* __restrict__ points,
+                                                 const double* __restrict__ camtab,
                                                  const double* __restrict__ scc,
-                                                 const double* __restrict__ L, double* __restrict__ Y) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= v.NE) return;
-  const int s = v.ent_os[e] >> 1;
-  const int p = v.ent_pt[e], c = v.ent_cam[e], pos = v.ent_pos[e];
-  const size_t Ns = (size_t)v.N, NPs = (size_t)v.NP;
-  const double spv[3] = {sp[p], sp[NPs + p], sp[2 * NPs + p]};
-  const double l00 = L[p], l10 = L[NPs + p], l20 = L[2 * NPs + p];
-  const double l11 = L[3 * NPs + p], l21 = L[4 * NPs + p], l22 = L[5 * NPs + p];
-  double jp0[3], jp1[3];
-#pragma unroll
-  for (int b = 0; b < 3; ++b) {
-    jp0[b] = Jp[(size_t)(2 * b) * Ns + s];
-    jp1[b] = Jp[(size_t)(2 * b + 1) * Ns + s];
-  }
-  double q[14];
-  load_rec(rec, pos, q);
+                                                 const double* __restrict__ PU, double* __restrict__ Y) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= v.NE) return;
+  int4 id = v.cm_idx[i];
+  const bool slot1 = (id.w & kSlotBit) != 0;
+  id.w &= ~kSlotBit;
+  const int c = v.ext_col[slot1 ? id.z : id.y];
+  const double2 xy = v.cm_xy[i];
+  const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
+  double ru, rv, jx0[3], jx1[3], ja[6], jb[6];
+  if (slot1) obs_rows<true, 1>(id, xy, X, camtab, v.intr, ru, rv, jx0, jx1, ja, jb);
+  else obs_rows<true, 0>(id, xy, X, camtab, v.intr, ru, rv, jx0, jx1, ja, jb);
+  const double* pu = PU + 6 * (size_t)id.x;
+  const double u00 = pu[0], u01 = pu[1], u02 = pu[2], u11 = pu[3], u12 = pu[4], u22 = pu[5];
   double y[18];
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
-    const double ja = q[a], jb = q[6 + a];
     const double sa = scc[6 * c + a];
-    const double w0 = sa * (ja * jp0[0] + jb * jp1[0]) * spv[0];
-    const double w1 = sa * (ja * jp0[1] + jb * jp1[1]) * spv[1];
-    const double w2 = sa * (ja * jp0[2] + jb * jp1[2]) * spv[2];
-    const double y0 = w0 / l00;
-    const double y1 = (w1 - l10 * y0) / l11;
-    const double y2 = (w2 - l20 * y0 - l21 * y1) / l22;
-    y[3 * a] = y0;
-    y[3 * a + 1] = y1;
-    y[3 * a + 2] = y2;
+    const double w0 = ja[a] * jx0[0] + jb[a] * jx1[0];
+    const double w1 = ja[a] * jx0[1] + jb[a] * jx1[1];
+    const double w2 = ja[a] * jx0[2] + jb[a] * jx1[2];
+    y[3 * a] = sa * (w0 * u00);
+    y[3 * a + 1] = sa * (w0 * u01 + w1 * u11);
+    y[3 * a + 2] = sa * (w0 * u02 + w1 * u12 + w2 * u22);
   }
-  double2* out = reinterpret_cast<double2*>(Y + (size_t)kYRec * pos);
+  double2* out = reinterpret_cast<double2*>(Y + (size_t)kYRec * i);
 #pragma unroll
-  for (int i = 0; i < 9; ++i) out[i] = make_double2(y[2 * i], y[2 * i + 1]);
+  for (int k = 0; k < 9; ++k) out[k] = make_double2(y[2 * k], y[2 * k + 1]);
 }
 
-void launch_entry_y(hipStream_t s, const DevView& v, const double* Jp, const double* rec,
-                    const double* scale_p, const double* scale_c, const double* L, double* Y) {
+void launch_entry_y(hipStream_t s, const DevView& v, const double* points, const double* camtab,
+                    const double* scale_c, const double* PU, double* Y) {
   if (v.NE <= 0) return;
-  k_entry_y<<<grid_for(v.NE, 256, 1 << 20), 256, 0, s>>>(v, Jp, rec, scale_p, scale_c, L, Y);
+  k_entry_y<<<grid_for(v.NE, 256, 1 << 20), 256, 0, s>>>(v, points, camtab, scale_c, PU, Y);
 }
 
 // one wave per S block; lane (a,b) < 36 accumulates -sum Y_row[a,:] . Y_col[b,:]
@@ -862,15 +889,11 @@ __global__ __launch_bounds__(256) void k_backsub(DevView v, const double* __rest
       }
     }
   }
-  const double l00 = L[p], l10 = L[NPs + p], l20 = L[2 * NPs + p];
-  const double l11 = L[3 * NPs + p], l21 = L[4 * NPs + p], l22 = L[5 * NPs + p];
-  const double y2 = r2 / l22;
-  const double y1 = (r1 - l21 * y2) / l11;
-  const double y0 = (r0 - l10 * y1 - l20 * y2) / l00;
-  // step = -y (Ceres solves J y = r then negates), delta = step * scale
-  dp[p] = -y0 * sp[p];
-  dp[NPs + p] = -y1 * sp[NPs + p];
-  dp[2 * NPs + p] = -y2 * sp[2 * NPs + p];
+  // delta_p = -diag(s) L^-T (q - sum_e Y_e^T y_c) = -PU (...)   (step = -y, Ceres)
+  const double* pu = L + 6 * (size_t)p;
+  dp[p] = -(pu[0] * r0 + pu[1] * r1 + pu[2] * r2);
+  dp[NPs + p] = -(pu[3] * r1 + pu[4] * r2);
+  dp[2 * NPs + p] = -(pu[5] * r2);
 }
 
 void launch_backsub(hipStream_t s, const DevView& v, const double* L, const double* q, const double* Y,
@@ -923,61 +946,90 @@ void launch_cam_candidate(hipStream_t s, int E, const int* ext_col, const double
   k_cam_candidate<<<grid_for(6 * E, 256, 1 << 20), 256, 0, s>>>(E, ext_col, ext, yc, scale_c, ext_c, delta_c);
 }
 
-__global__ __launch_bounds__(256) void k_candidate(DevView v, const double* __restrict__ Jp,
-                                                   const double* __restrict__ rec,
-                                                   const double2* __restrict__ r,
+// Model cost change -(J delta).(r + J delta / 2) and the candidate residual at x + delta
+// in one observation pass; J and r at x are re-evaluated (bitwise what the evaluation
+// pass saw), the candidate point is formed as x + delta exactly as k_axpy_points does.
+__global__ __launch_bounds__(256) void k_candidate(DevView v, const double* __restrict__ points,
+                                                   const double* __restrict__ camtab,
                                                    const double* __restrict__ dp,
                                                    const double* __restrict__ dc,
-                                                   const double* __restrict__ points_c,
                                                    const double* __restrict__ camtab_c,
                                                    double* __restrict__ partial) {
   double acc[3] = {0.0, 0.0, 0.0};
-  const size_t Ns = (size_t)v.N, NPs = (size_t)v.NP;
+  const size_t NPs = (size_t)v.NP;
   for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < v.N; s += gridDim.x * blockDim.x) {
     const int4 id = v.obs_idx[s];
-    const int2 ent = v.obs_ent[s];
-    double m0 = 0.0, m1 = 0.0;
+    if (id.x < 0) continue;  // padding slot
+    const double2 xy = v.obs_xy[s];
+    const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
+    const double d3[3] = {dp[id.x], dp[NPs + id.x], dp[2 * NPs + id.x]};
+    const double* K = v.intr + (size_t)kIntr * id.w;
+    double m0 = 0.0, m1 = 0.0, ru, rv;
+    {
+      ObsJac o;
+      obs_jacobian(id, xy, X, camtab, v.intr, o);
+      ru = o.pr.ru;
+      rv = o.pr.rv;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const double d = dp[c * NPs + id.x];
-      m0 += Jp[(size_t)(2 * c) * Ns + s] * d;
-      m1 += Jp[(size_t)(2 * c + 1) * Ns + s] * d;
-    }
-    if (ent.x >= 0) {
-      double q[14];
-      load_rec(rec, ent.x, q);
-      const double* d = dc + 6 * v.ext_col[id.y];
+      for (int c = 0; c < 3; ++c) {
+        m0 += o.jx0[c] * d3[c];
+        m1 += o.jx1[c] * d3[c];
+      }
+      const int c0 = v.ext_col[id.y];
+      if (c0 >= 0) {
+        const double* d = dc + 6 * c0;
 #pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        m0 += q[k] * d[k];
-        m1 += q[6 + k] * d[k];
+        for (int k = 0; k < 3; ++k) {
+          m0 += o.jw0a[k] * d[k];
+          m1 += o.jw0b[k] * d[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          m0 += o.pr.A0[k] * d[3 + k];
+          m1 += o.pr.A1[k] * d[3 + k];
+        }
+      }
+      const int c1 = id.z >= 0 ? v.ext_col[id.z] : -1;
+      if (c1 >= 0) {
+        const double* d = dc + 6 * c1;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          m0 += o.jw1a[k] * d[k];
+          m1 += o.jw1b[k] * d[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          m0 += o.jt1a[k] * d[3 + k];
+          m1 += o.jt1b[k] * d[3 + k];
+        }
       }
     }
-    if (ent.y >= 0) {
-      double q[14];
-      load_rec(rec, ent.y, q);
-      const double* d = dc + 6 * v.ext_col[id.z];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        m0 += q[k] * d[k];
-        m1 += q[6 + k] * d[k];
-      }
+    acc[0] += -(m0 * (ru + m0 / 2.0) + m1 * (rv + m1 / 2.0));
+    // candidate residual at (x + delta)
+    const double Xc[3] = {X[0] + d3[0], X[1] + d3[1], X[2] + d3[2]};
+    double T0[12];
+    load_tab<12>(camtab_c, id.y, T0);
+    double P[3];
+    if (id.z >= 0) {
+      double T1[12], P2[3];
+      load_tab<12>(camtab_c, id.z, T1);
+      matvec_add(T1, Xc, T1 + 9, P2);
+      matvec_add(T0, P2, T0 + 9, P);
+    } else {
+      matvec_add(T0, Xc, T0 + 9, P);
     }
-    const double2 rr = r[s];
-    acc[0] += -(m0 * (rr.x + m0 / 2.0) + m1 * (rr.y + m1 / 2.0));
-    double ru, rv;
-    residual_at(v, points_c, camtab_c, s, ru, rv);
-    acc[1] += ru * ru + rv * rv;
-    acc[2] += (isfinite(ru) && isfinite(rv)) ? 0.0 : 1.0;
+    Proj pc;
+    project(P, K, xy.x, xy.y, pc, false);
+    acc[1] += pc.ru * pc.ru + pc.rv * pc.rv;
+    acc[2] += (isfinite(pc.ru) && isfinite(pc.rv)) ? 0.0 : 1.0;
   }
   block_reduce_store<3>(acc, partial + 3 * (size_t)blockIdx.x);
 }
 
-void launch_candidate(hipStream_t s, const DevView& v, const double* Jp, const double* rec, const double* r,
-                      const double* delta_p, const double* delta_c, const double* points_c,
-                      const double* camtab_c, double* partial, int grid) {
-  k_candidate<<<grid, 256, 0, s>>>(v, Jp, rec, reinterpret_cast<const double2*>(r), delta_p, delta_c,
-                                   points_c, camtab_c, partial);
+void launch_candidate(hipStream_t s, const DevView& v, const double* points, const double* camtab,
+                      const double* delta_p, const double* delta_c, const double* camtab_c, double* partial,
+                      int grid) {
+  k_candidate<<<grid, 256, 0, s>>>(v, points, camtab, delta_p, delta_c, camtab_c, partial);
 }
 
 __global__ __launch_bounds__(256) void k_grad_points(int NP, const double* __restrict__ x,

@@ -26,6 +26,7 @@
 #include <cfloat>
 
 #include "dab_kernels.h"
+#include "dab_wave.h"
 
 namespace dab {
 
@@ -35,11 +36,10 @@ constexpr int kOneWG = 1024;
 
 __device__ __forceinline__ double wg_sum(double v, double* sh) {
   // fixed-order sum over a 1024-thread work-group, result broadcast to every thread
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  v = wave_sum_lane63(v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   __syncthreads();
-  if (lane == 0) sh[w] = v;
+  if (lane == 63) sh[w] = v;
   __syncthreads();
   double t = 0.0;
   for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i];
@@ -102,17 +102,11 @@ __global__ __launch_bounds__(256) void k_pcg_diag_rhs_partial(DevView v, const i
   }
   // fixed-order block reduction
   __shared__ double sh[kRedBlock / 64][27];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < 27; ++i) {
-    double t = acc[i];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
-    acc[i] = t;
-  }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) {
-#pragma unroll
-    for (int i = 0; i < 27; ++i) sh[w][i] = acc[i];
+    const double t = wave_sum_lane63(acc[i]);
+    if (lane == 63) sh[w][i] = t;
   }
   __syncthreads();
   if (threadIdx.x < 27) {
@@ -339,17 +333,11 @@ __global__ __launch_bounds__(256) void k_pcg_cam_pass(DevView v, const int* __re
     for (int a = 0; a < 6; ++a) acc[a] -= y[3 * a] * ta.x + y[3 * a + 1] * ta.y + y[3 * a + 2] * t2;
   }
   __shared__ double sh[kRedBlock / 64][6];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    double x = acc[i];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-    acc[i] = x;
-  }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) {
-#pragma unroll
-    for (int i = 0; i < 6; ++i) sh[w][i] = acc[i];
+    const double x = wave_sum_lane63(acc[i]);
+    if (lane == 63) sh[w][i] = x;
   }
   __syncthreads();
   if (threadIdx.x < 6) {

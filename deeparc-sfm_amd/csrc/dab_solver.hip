@@ -21,6 +21,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -120,7 +121,8 @@ struct dab_handle {
   std::vector<int> perm;            // sorted obs -> caller's obs index
   std::vector<int> pt_of;           // local point -> caller's point id
   std::vector<int> ext_col;         // ext -> free camera column
-  int nchunk = 0, nxchunk = 0, ncross = 0, nblk = 0, nwin = 0, nstrad = 0;
+  int nchunk = 0, nxchunk = 0, ncross = 0, nblk = 0, nslice = 0;
+  int NS = 0;  // observation slots (SELL-64, incl. padding)
   long long npairs = 0;
   int lds = 0;                      // leading dim of dense S
   bool schur_built = false;
@@ -133,19 +135,21 @@ struct dab_handle {
   DevView view{};
   int4* d_obs_idx = nullptr;
   double2* d_obs_xy = nullptr;
-  int2* d_obs_ent = nullptr;
-  int4* d_strad = nullptr;
-  int *d_pt_obs_ptr = nullptr, *d_pt_ent_ptr = nullptr, *d_ent_os = nullptr, *d_ent_cam = nullptr,
+  int4* d_cm_idx = nullptr;
+  double2* d_cm_xy = nullptr;
+  int4* d_x_idx = nullptr;
+  double2* d_x_xy = nullptr;
+  int *d_slice_off = nullptr, *d_pt_ent_ptr = nullptr, *d_ent_os = nullptr, *d_ent_cam = nullptr,
       *d_ent_pt = nullptr, *d_ent_pos = nullptr, *d_cm_pt = nullptr, *d_ext_col = nullptr;
   int *d_chunk_beg = nullptr, *d_seg_chunk = nullptr;
-  int *d_xobs = nullptr, *d_xchunk_beg = nullptr, *d_xseg_chunk = nullptr;
+  int *d_xchunk_beg = nullptr, *d_xseg_chunk = nullptr;
   int2* d_cross_cam = nullptr;
   int2 *d_pairs = nullptr, *d_blk_cam = nullptr;
   int* d_blk_pair_beg = nullptr;
   double* d_intr = nullptr;
   double *d_points = nullptr, *d_points_c = nullptr, *d_ext = nullptr, *d_ext_c = nullptr;
   double *d_camtab = nullptr, *d_camtab_c = nullptr;
-  double *d_r = nullptr, *d_Jp = nullptr, *d_rec = nullptr, *d_wpart = nullptr;
+  double* d_r = nullptr;
   double* d_Jfull = nullptr;  // parity API only (lazily allocated)
   double *d_V = nullptr, *d_g = nullptr, *d_scale_p = nullptr, *d_scale_c = nullptr;
   double *d_L = nullptr, *d_q = nullptr, *d_Y = nullptr;
@@ -167,6 +171,8 @@ struct dab_handle {
   double* h_scal = nullptr;    // pinned
   int* h_flags = nullptr;      // pinned
   int red_grid = 1;
+  int eval_grid = 1;  // k_eval_points blocks (one SELL slice per block)
+  int eval_wps = 4;   // waves per slice (DAB_EVAL_WPS tuning knob)
 
   ~dab_handle() {
     dev.release();
@@ -392,12 +398,15 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
       h->any_compose = true;
     }
   }
+  // device point order: referenced points by observation count, descending (stable by
+  // id), so that the 64 points of one wave slice have similar track lengths (SELL-64)
+  std::vector<int> pcount(p->num_points, 0);
+  for (int o = 0; o < N; ++o) pcount[p->obs_point[o]]++;
   h->pt_of.clear();
   for (int i = 0; i < p->num_points; ++i)
-    if (pref[i]) {
-      pt_local[i] = (int)h->pt_of.size();
-      h->pt_of.push_back(i);
-    }
+    if (pref[i]) h->pt_of.push_back(i);
+  std::stable_sort(h->pt_of.begin(), h->pt_of.end(), [&](int a, int b) { return pcount[a] > pcount[b]; });
+  for (int l = 0; l < (int)h->pt_of.size(); ++l) pt_local[h->pt_of[l]] = l;
   h->NP = (int)h->pt_of.size();
   // the free camera set must agree on every rank
   if (h->world > 1) {
@@ -420,29 +429,49 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   const int NP = h->NP, NC = h->NC;
   h->nplanes = h->any_compose ? 30 : 18;
 
-  // point-major observation order (stable)
+  // Observation slots, SELL-64: slice sl holds local points [64 sl, 64 sl + 64); the k-th
+  // observation (caller order) of the slice's lane-l point sits at slice_off[sl] + 64 k + l,
+  // slices padded to their longest track (padding slots: point -1). One wave walks a
+  // slice with every load coalesced and reduces V, g per lane with no cross-lane work.
   std::vector<int> cnt(NP + 1, 0);
   for (int o = 0; o < N; ++o) cnt[pt_local[p->obs_point[o]] + 1]++;
   for (int i = 0; i < NP; ++i) cnt[i + 1] += cnt[i];
-  std::vector<int> pt_obs_ptr = cnt;
-  h->perm.assign(N, 0);
+  std::vector<int> by_pt(N);
   {
     std::vector<int> fill(cnt.begin(), cnt.end() - 1);
-    for (int o = 0; o < N; ++o) h->perm[fill[pt_local[p->obs_point[o]]]++] = o;
+    for (int o = 0; o < N; ++o) by_pt[fill[pt_local[p->obs_point[o]]]++] = o;
   }
-  std::vector<int4> obs_idx(N);
-  std::vector<double2> obs_xy(N);
-  for (int s2 = 0; s2 < N; ++s2) {
-    const int o = h->perm[s2];
-    obs_idx[s2] = make_int4(pt_local[p->obs_point[o]], p->obs_ext0[o], p->obs_ext1[o], p->obs_intr[o]);
-    obs_xy[s2] = make_double2(p->obs_xy[2 * (size_t)o], p->obs_xy[2 * (size_t)o + 1]);
+  h->nslice = (NP + 63) / 64;
+  std::vector<int> slice_off(h->nslice + 1, 0);
+  for (int sl = 0; sl < h->nslice; ++sl) {
+    const int p0 = 64 * sl;
+    const int len = cnt[p0 + 1] - cnt[p0];  // longest track of the slice (sorted)
+    slice_off[sl + 1] = slice_off[sl] + 64 * len;
+  }
+  const int NS = slice_off[h->nslice];
+  h->NS = NS;
+  h->perm.assign(NS, -1);
+  std::vector<int4> obs_idx(NS, make_int4(-1, 0, -1, 0));
+  std::vector<double2> obs_xy(NS, make_double2(0.0, 0.0));
+  std::vector<std::vector<int>> pt_slots(NP);
+  for (int pt = 0; pt < NP; ++pt) {
+    const int sl = pt / 64, lane = pt % 64;
+    for (int k = 0; k < cnt[pt + 1] - cnt[pt]; ++k) {
+      const int slot = slice_off[sl] + 64 * k + lane;
+      const int o = by_pt[cnt[pt] + k];
+      h->perm[slot] = o;
+      obs_idx[slot] = make_int4(pt, p->obs_ext0[o], p->obs_ext1[o], p->obs_intr[o]);
+      obs_xy[slot] = make_double2(p->obs_xy[2 * (size_t)o], p->obs_xy[2 * (size_t)o + 1]);
+    }
   }
   // entries (observation slots on free cameras), point-major
   std::vector<int> ent_os, ent_cam, ent_pt, pt_ent_ptr(NP + 1, 0);
   ent_os.reserve((size_t)N * (h->any_compose ? 2 : 1));
   for (int pt = 0; pt < NP; ++pt) {
     pt_ent_ptr[pt] = (int)ent_os.size();
-    for (int s2 = pt_obs_ptr[pt]; s2 < pt_obs_ptr[pt + 1]; ++s2) {
+    const int sl = pt / 64, lane = pt % 64;
+    for (int k = 0; k < cnt[pt + 1] - cnt[pt]; ++k) {
+      const int s2 = slice_off[sl] + 64 * k + lane;
       for (int slot = 0; slot < 2; ++slot) {
         const int e = slot ? obs_idx[s2].z : obs_idx[s2].y;
         if (e < 0 || h->ext_col[e] < 0) continue;
@@ -464,10 +493,13 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
     std::vector<int> fill(cam_cnt.begin(), cam_cnt.end() - 1);
     for (int e = 0; e < NE; ++e) cam_ent[fill[ent_cam[e]]++] = e;
   }
+  // entries per reduction chunk (one block each); DAB_CHUNK is a tuning knob
+  const char* chunk_env = getenv("DAB_CHUNK");
+  const int chunk = std::max(64, chunk_env ? atoi(chunk_env) : kChunk);
   std::vector<int> chunk_beg, seg_chunk(NC + 1, 0);
   for (int c = 0; c < NC; ++c) {
     seg_chunk[c] = (int)chunk_beg.size();
-    for (int b = cam_cnt[c]; b < cam_cnt[c + 1]; b += kChunk) chunk_beg.push_back(b);
+    for (int b = cam_cnt[c]; b < cam_cnt[c + 1]; b += chunk) chunk_beg.push_back(b);
   }
   seg_chunk[NC] = (int)chunk_beg.size();
   h->nchunk = (int)chunk_beg.size();
@@ -491,35 +523,30 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
       i = j;
     }
   }
-  std::vector<int2> obs_ent(N, make_int2(-1, -1));
-  for (int e = 0; e < NE; ++e) {
-    const int s2 = ent_os[e] >> 1;
-    if (ent_os[e] & 1) obs_ent[s2].y = ent_pos[e];
-    else obs_ent[s2].x = ent_pos[e];
+  // static camera-major copy of the entries' observation inputs (matrix-free camera passes)
+  std::vector<int4> cm_idx(NE);
+  std::vector<double2> cm_xy(NE);
+  for (int i = 0; i < NE; ++i) {
+    const int e = cam_ent[i], s2 = ent_os[e] >> 1;
+    int4 id = obs_idx[s2];
+    if (ent_os[e] & 1) id.w |= kSlotBit;
+    cm_idx[i] = id;
+    cm_xy[i] = obs_xy[s2];
   }
-  // points whose observations straddle a 64-observation window (segmented V/g fix-up)
-  h->nwin = (N + kWin - 1) / kWin;
-  std::vector<int4> strad;
-  for (int pt = 0; pt < NP; ++pt) {
-    const int a = pt_obs_ptr[pt], b = pt_obs_ptr[pt + 1];
-    if (b > a && a / kWin != (b - 1) / kWin) strad.push_back(make_int4(pt, a / kWin, (b - 1) / kWin, 0));
-  }
-  h->nstrad = (int)strad.size();
-
   // arc∘ring cross blocks: composed observations whose two cameras are both free.
   // The pair table is the union over ranks so the all-reduced layout matches.
   std::vector<long long> xkeys;
-  for (int s2 = 0; s2 < N; ++s2) {
+  for (int s2 = 0; s2 < NS; ++s2) {
     const int e0 = obs_idx[s2].y, e1 = obs_idx[s2].z;
-    if (e1 < 0) continue;
+    if (e1 < 0 || obs_idx[s2].x < 0) continue;
     const int c0 = h->ext_col[e0], c1 = e1 >= 0 ? h->ext_col[e1] : -1;
     if (c0 < 0 || c1 < 0) continue;
-    xkeys.push_back(((long long)c0 * NC + c1) * (long long)N + s2);
+    xkeys.push_back(((long long)c0 * NC + c1) * (long long)NS + s2);
   }
   std::sort(xkeys.begin(), xkeys.end());
   std::vector<long long> pairkeys;  // unique (c0*NC+c1)
   for (long long k : xkeys) {
-    const long long pk = k / N;
+    const long long pk = k / NS;
     if (pairkeys.empty() || pairkeys.back() != pk) pairkeys.push_back(pk);
   }
   if (h->world > 1 && h->any_compose && NC > 0) {
@@ -539,17 +566,21 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   h->ncross = (int)pairkeys.size();
   std::vector<int2> cross_cam(h->ncross);
   for (int k = 0; k < h->ncross; ++k) cross_cam[k] = make_int2((int)(pairkeys[k] / NC), (int)(pairkeys[k] % NC));
-  std::vector<int> xobs(xkeys.size()), xchunk_beg, xseg_chunk(h->ncross + 1, 0);
+  std::vector<int> xchunk_beg, xseg_chunk(h->ncross + 1, 0);
+  std::vector<int4> x_idx(xkeys.size());
+  std::vector<double2> x_xy(xkeys.size());
   {
     size_t i = 0;
     for (int k = 0; k < h->ncross; ++k) {
       xseg_chunk[k] = (int)xchunk_beg.size();
       const size_t b = i;
-      while (i < xkeys.size() && xkeys[i] / N == pairkeys[k]) {
-        xobs[i] = (int)(xkeys[i] % N);
+      while (i < xkeys.size() && xkeys[i] / NS == pairkeys[k]) {
+        const int s2 = (int)(xkeys[i] % NS);
+        x_idx[i] = obs_idx[s2];
+        x_xy[i] = obs_xy[s2];
         ++i;
       }
-      for (size_t q = b; q < i; q += kChunk) xchunk_beg.push_back((int)q);
+      for (size_t q = b; q < i; q += chunk) xchunk_beg.push_back((int)q);
     }
     xseg_chunk[h->ncross] = (int)xchunk_beg.size();
     h->nxchunk = (int)xchunk_beg.size();
@@ -601,7 +632,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   Dev& d = h->dev;
   CHECK_RC(upload(&h->d_obs_idx, d, obs_idx, s));
   CHECK_RC(upload(&h->d_obs_xy, d, obs_xy, s));
-  CHECK_RC(upload(&h->d_pt_obs_ptr, d, pt_obs_ptr, s));
+  CHECK_RC(upload(&h->d_slice_off, d, slice_off, s));
   CHECK_RC(upload(&h->d_pt_ent_ptr, d, pt_ent_ptr, s));
   CHECK_RC(upload(&h->d_ent_os, d, ent_os, s));
   CHECK_RC(upload(&h->d_ent_cam, d, ent_cam, s));
@@ -609,11 +640,12 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   CHECK_RC(upload(&h->d_ext_col, d, h->ext_col, s));
   CHECK_RC(upload(&h->d_ent_pos, d, ent_pos, s));
   CHECK_RC(upload(&h->d_cm_pt, d, cm_pt, s));
-  CHECK_RC(upload(&h->d_obs_ent, d, obs_ent, s));
-  CHECK_RC(upload(&h->d_strad, d, strad, s));
+  CHECK_RC(upload(&h->d_cm_idx, d, cm_idx, s));
+  CHECK_RC(upload(&h->d_cm_xy, d, cm_xy, s));
   CHECK_RC(upload(&h->d_chunk_beg, d, chunk_beg, s));
   CHECK_RC(upload(&h->d_seg_chunk, d, seg_chunk, s));
-  CHECK_RC(upload(&h->d_xobs, d, xobs, s));
+  CHECK_RC(upload(&h->d_x_idx, d, x_idx, s));
+  CHECK_RC(upload(&h->d_x_xy, d, x_xy, s));
   CHECK_RC(upload(&h->d_xchunk_beg, d, xchunk_beg, s));
   CHECK_RC(upload(&h->d_xseg_chunk, d, xseg_chunk, s));
   CHECK_RC(upload(&h->d_cross_cam, d, cross_cam, s));
@@ -627,10 +659,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   CHECK_RC(d.alloc(&h->d_ext_c, (size_t)6 * h->E));
   CHECK_RC(d.alloc(&h->d_camtab, (size_t)kCamTab * h->E));
   CHECK_RC(d.alloc(&h->d_camtab_c, (size_t)kCamTab * h->E));
-  CHECK_RC(d.alloc(&h->d_r, (size_t)2 * N));
-  CHECK_RC(d.alloc(&h->d_Jp, (size_t)6 * N));
-  CHECK_RC(d.alloc(&h->d_rec, (size_t)kRec * NE));
-  CHECK_RC(d.alloc(&h->d_wpart, (size_t)18 * h->nwin));
+  CHECK_RC(d.alloc(&h->d_r, (size_t)2 * NS));
   h->d_Jfull = nullptr;
   CHECK_RC(d.alloc(&h->d_V, (size_t)6 * NP));
   CHECK_RC(d.alloc(&h->d_g, (size_t)3 * NP));
@@ -645,24 +674,30 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   CHECK_RC(d.alloc(&h->d_yc, (size_t)6 * NC));
   CHECK_RC(d.alloc(&h->d_dp, (size_t)3 * NP));
   CHECK_RC(d.alloc(&h->d_dc, (size_t)6 * NC));
-  h->red_grid = grid_for(std::max(N, 3 * NP), 256, 1024);
-  CHECK_RC(d.alloc(&h->d_gpart, (size_t)h->red_grid * 4));
+  h->red_grid = grid_for(std::max(h->NS, 3 * NP), 256, 1024);
+  h->eval_grid = std::max(1, h->nslice);
+  {
+    const char* env = getenv("DAB_EVAL_WPS");
+    h->eval_wps = env ? atoi(env) : 4;
+  }
+  CHECK_RC(d.alloc(&h->d_gpart, (size_t)std::max(h->red_grid, h->eval_grid) * 4));
   CHECK_RC(d.alloc(&h->d_scal, S_NSLOTS));
   CHECK_RC(d.alloc(&h->d_flags, 4));
   HIP_OK(hipMemsetAsync(h->d_dc, 0, sizeof(double) * std::max(1, 6 * NC), s));
   HIP_OK(hipStreamSynchronize(s));
 
   DevView& v = h->view;
-  v.N = N;
+  v.N = h->NS;
   v.NP = NP;
   v.E = h->E;
   v.NC = NC;
   v.NE = NE;
-  v.nwin = h->nwin;
+  v.nslice = h->nslice;
   v.obs_idx = h->d_obs_idx;
   v.obs_xy = h->d_obs_xy;
-  v.obs_ent = h->d_obs_ent;
-  v.pt_obs_ptr = h->d_pt_obs_ptr;
+  v.cm_idx = h->d_cm_idx;
+  v.cm_xy = h->d_cm_xy;
+  v.slice_off = h->d_slice_off;
   v.pt_ent_ptr = h->d_pt_ent_ptr;
   v.ent_os = h->d_ent_os;
   v.ent_cam = h->d_ent_cam;
@@ -892,23 +927,25 @@ extern "C" int dab_get_parameters(dab_handle* h, double* points, double* ext) {
 // ------------------------------------------------------------------------------------
 // evaluation building blocks
 // ------------------------------------------------------------------------------------
-// The evaluation pass proper (the benchmark "step"): residual + Jacobian kernel with the
-// fused point blocks V, g, the straddling-point fix-up, the camera blocks U, g_c (and the
-// arc∘ring cross blocks) over contiguous records, all-reduced across ranks, and the cost.
-// Expects the camera tables of the current x in d_camtab.
-static int eval_core(dab_handle* h) {
+// The evaluation pass proper (the benchmark "step"), matrix-free: the point-side kernel
+// (residual + d r / d X reduced into V, g, cost), the
+// camera-side kernel (U, g_c from the camera-major inputs) and the arc∘ring cross blocks,
+// all-reduced across ranks. Expects the camera tables of the current x in d_camtab.
+static void eval_points(dab_handle* h) {
+  hipStream_t s = h->stream;
+  launch_eval_points(s, h->view, h->d_points, h->d_camtab, h->d_V, h->d_g, h->d_gpart, h->eval_grid, h->eval_wps);
+}
+static int eval_rest(dab_handle* h) {
   hipStream_t s = h->stream;
   const DevView& v = h->view;
-  launch_jacobian(s, v, h->d_points, h->d_camtab, h->d_r, h->d_Jp, h->d_rec, h->d_V, h->d_g, h->d_wpart,
-                  h->d_gpart, h->red_grid);
-  launch_point_fixup(s, h->nstrad, h->d_strad, h->d_wpart, h->NP, h->d_V, h->d_g);
-  launch_final_sum(s, h->red_grid, 2, h->d_gpart, h->d_scal + S_COST);
+  launch_final_sum(s, h->eval_grid, 2, h->d_gpart, h->d_scal + S_COST);
   if (h->NC > 0) {
-    launch_cam_ug_partial(s, h->nchunk, h->d_chunk_beg, h->d_rec, h->d_partial);
+    launch_eval_cams(s, v, h->nchunk, h->d_chunk_beg, h->d_points, h->d_camtab, h->d_partial);
     launch_seg_final(s, h->NC, 27, h->d_seg_chunk, h->d_partial, h->ug());
     if (h->ncross > 0) {
       if (h->nxchunk > 0) {
-        launch_cross_partial(s, v, h->nxchunk, h->d_xchunk_beg, h->d_xobs, h->d_rec, h->d_partial);
+        launch_eval_cross(s, v, h->nxchunk, h->d_xchunk_beg, h->d_x_idx, h->d_x_xy, h->d_points, h->d_camtab,
+                          h->d_partial);
         launch_seg_final(s, h->ncross, 36, h->d_xseg_chunk, h->d_partial, h->Ux());
       } else {
         HIP_OK(hipMemsetAsync(h->Ux(), 0, sizeof(double) * 36 * (size_t)h->ncross, s));
@@ -917,6 +954,10 @@ static int eval_core(dab_handle* h) {
     CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
   }
   return 0;
+}
+static int eval_core(dab_handle* h) {
+  eval_points(h);
+  return eval_rest(h);
 }
 
 // Residual + Jacobian at the current x and the J^T J / J^T r blocks (camera side
@@ -1115,13 +1156,13 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
     launch_point_factor(s, v, h->d_V, h->d_g, h->d_scale_p, sc, h->d_L, h->d_q, h->d_flags);
     bool pcg_fail = false;
     if (NC > 0 && use_pcg) {
-      launch_entry_y(s, v, h->d_Jp, h->d_rec, h->d_scale_p, h->d_scale_c, h->d_L, h->d_Y);
+      launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, h->d_Y);
       int cg_iters = 0, cg_status = 0;
       CHECK_RC(pcg_solve(h, opt, sc, &cg_iters, &cg_status));
       it.linear_solver_iterations = cg_iters;
       pcg_fail = cg_status == kPcgFailure;
     } else if (NC > 0) {
-      launch_entry_y(s, v, h->d_Jp, h->d_rec, h->d_scale_p, h->d_scale_c, h->d_L, h->d_Y);
+      launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, h->d_Y);
       launch_s_blocks(s, h->nblk, h->d_blk_pair_beg, h->d_pairs, h->d_Y, h->packed());
       launch_cam_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_Y, h->d_q, h->d_partial);
       launch_seg_final(s, NC, 6, h->d_seg_chunk, h->d_partial, h->ybc());
@@ -1140,8 +1181,7 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
     launch_cam_norms(s, h->E, h->d_ext_col, h->d_ext, h->d_ext_c, nullptr, h->d_scal + S_CAM0);
     launch_cam_tables(s, h->E, h->d_ext_c, h->d_camtab_c);
     const double tre = now_s();
-    launch_candidate(s, v, h->d_Jp, h->d_rec, h->d_r, h->d_dp, h->d_dc, h->d_points_c, h->d_camtab_c,
-                     h->d_gpart, h->red_grid);
+    launch_candidate(s, v, h->d_points, h->d_camtab, h->d_dp, h->d_dc, h->d_camtab_c, h->d_gpart, h->red_grid);
     launch_final_sum(s, h->red_grid, 3, h->d_gpart, h->d_scal + S_MODEL);
     CHECK_RC(h->allreduce(h->d_scal + S_MODEL, 5, ncclSum));
     CHECK_RC(h->allreduce_max_i32(h->d_flags, 4));
@@ -1245,12 +1285,14 @@ extern "C" int dab_eval_residuals(dab_handle* h, double* residuals, double* cost
   CHECK_RC(read_scalars(h));
   if (cost) *cost = 0.5 * h->h_scal[S_COST];
   if (residuals) {
-    std::vector<double> r((size_t)2 * h->N);
+    std::vector<double> r((size_t)2 * h->NS);
     HIP_OK(hipMemcpyAsync(r.data(), h->d_r, r.size() * sizeof(double), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    for (int s2 = 0; s2 < h->N; ++s2) {
-      residuals[2 * (size_t)h->perm[s2]] = r[2 * (size_t)s2];
-      residuals[2 * (size_t)h->perm[s2] + 1] = r[2 * (size_t)s2 + 1];
+    for (int s2 = 0; s2 < h->NS; ++s2) {
+      const int o = h->perm[s2];
+      if (o < 0) continue;
+      residuals[2 * (size_t)o] = r[2 * (size_t)s2];
+      residuals[2 * (size_t)o + 1] = r[2 * (size_t)s2 + 1];
     }
   }
   return 0;
@@ -1261,15 +1303,16 @@ extern "C" int dab_eval_jacobians(dab_handle* h, double* residuals, double* jaco
   if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
   HIP_OK(hipSetDevice(h->device));
   hipStream_t s = h->stream;
-  if (!h->d_Jfull) CHECK_RC(h->dev.alloc(&h->d_Jfull, (size_t)30 * h->N));
+  if (!h->d_Jfull) CHECK_RC(h->dev.alloc(&h->d_Jfull, (size_t)30 * h->NS));
   launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
   launch_jacobian_full(s, h->view, h->d_points, h->d_camtab, h->d_r, h->d_Jfull);
-  std::vector<double> r((size_t)2 * h->N), J((size_t)30 * h->N);
+  std::vector<double> r((size_t)2 * h->NS), J((size_t)30 * h->NS);
   HIP_OK(hipMemcpyAsync(r.data(), h->d_r, r.size() * sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_OK(hipMemcpyAsync(J.data(), h->d_Jfull, J.size() * sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
-  for (int s2 = 0; s2 < h->N; ++s2) {
+  for (int s2 = 0; s2 < h->NS; ++s2) {
     const int o = h->perm[s2];
+    if (o < 0) continue;
     if (residuals) {
       residuals[2 * (size_t)o] = r[2 * (size_t)s2];
       residuals[2 * (size_t)o + 1] = r[2 * (size_t)s2 + 1];
@@ -1280,7 +1323,7 @@ extern "C" int dab_eval_jacobians(dab_handle* h, double* residuals, double* jaco
       for (int col = 0; col < 15; ++col)
         for (int row = 0; row < 2; ++row) {
           double val = 0.0;
-          if (col < 9 || comp) val = J[(size_t)(2 * col + row) * h->N + s2];
+          if (col < 9 || comp) val = J[(size_t)(2 * col + row) * h->NS + s2];
           out[row * 15 + col] = val;
         }
     }
@@ -1331,24 +1374,12 @@ extern "C" int dab_bench_eval_pass(dab_handle* h, int with_assembly) {
   if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
   HIP_OK(hipSetDevice(h->device));
   hipStream_t s = h->stream;
-  const DevView& v = h->view;
   launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
   HIP_OK(hipEventRecord(h->ev0, s));
-  launch_jacobian(s, v, h->d_points, h->d_camtab, h->d_r, h->d_Jp, h->d_rec, h->d_V, h->d_g, h->d_wpart,
-                  h->d_gpart, h->red_grid);
+  eval_points(h);
   HIP_OK(hipEventRecord(h->ev1, s));
   if (with_assembly) {
-    launch_point_fixup(s, h->nstrad, h->d_strad, h->d_wpart, h->NP, h->d_V, h->d_g);
-    launch_final_sum(s, h->red_grid, 2, h->d_gpart, h->d_scal + S_COST);
-    if (h->NC > 0) {
-      launch_cam_ug_partial(s, h->nchunk, h->d_chunk_beg, h->d_rec, h->d_partial);
-      launch_seg_final(s, h->NC, 27, h->d_seg_chunk, h->d_partial, h->ug());
-      if (h->ncross > 0 && h->nxchunk > 0) {
-        launch_cross_partial(s, v, h->nxchunk, h->d_xchunk_beg, h->d_xobs, h->d_rec, h->d_partial);
-        launch_seg_final(s, h->ncross, 36, h->d_xseg_chunk, h->d_partial, h->Ux());
-      }
-      CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
-    }
+    CHECK_RC(eval_rest(h));
     CHECK_RC(h->allreduce(h->d_scal + S_COST, 2, ncclSum));
   }
   HIP_OK(hipEventRecord(h->ev2, s));
@@ -1384,17 +1415,15 @@ extern "C" int dab_bench_kernel_ms(dab_handle* h, double* jac_ms, double* assemb
 extern "C" int dab_jacobian_bytes(dab_handle* h, double* bytes) {
   clear_error();
   if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
-  // Algorithmic bytes of one residual+Jacobian launch, SURVEY §8d:
-  //   B = sum_obs (16 xy + 4 n_idx + 16 r + 16 k) + 24 N_pts + 48 N_ext + 48 N_intr
-  // with k = free columns of the observation (3 + 6 per free extrinsic) and n_idx = 2
-  // (single) or 3 (arc∘ring) index words. The kernel's own extra traffic (records padded
-  // to 128 B, camera-major positions, fused V/g) is deliberately not counted.
-  double b = 24.0 * h->NP + 48.0 * h->E + 48.0 * h->NI;
-  for (int o = 0; o < h->N; ++o) {
-    const int e0 = h->prob.obs_ext0[o], e1 = h->prob.obs_ext1[o];
-    const int k = 3 + 6 * (h->ext_col[e0] >= 0) + 6 * (e1 >= 0 && h->ext_col[e1] >= 0);
-    b += 16.0 + 4.0 * (e1 >= 0 ? 3 : 2) + 16.0 + 16.0 * k;
-  }
+  // Algorithmic bytes of one launch of the point-side evaluation kernel (k_eval_points,
+  // matrix-free residual + Jacobian reduced into V, g): the SURVEY §8d input terms
+  // (16 xy + 4 n_idx per observation, n_idx = 2 single / 3 arc∘ring; 24 per point,
+  // 48 per intrinsic) plus what the kernel must read and write instead of the stored
+  // Jacobian: the R, t part of each camera table (96 B) and V, g per point (72 B).
+  // The Jacobian itself never reaches HBM, so its 16 k bytes per observation are not
+  // counted (they are not moved).
+  double b = (24.0 + 72.0) * h->NP + 96.0 * h->E + 48.0 * h->NI;
+  for (int o = 0; o < h->N; ++o) b += 16.0 + 4.0 * (h->prob.obs_ext1[o] >= 0 ? 3 : 2);
   *bytes = b;
   return 0;
 }

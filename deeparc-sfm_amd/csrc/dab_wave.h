@@ -1,0 +1,45 @@
+// dab_wave.h — wave64 reductions and segmented scans on DPP lane moves (gfx9 DPP
+// controls: quad_perm, row_shr, row_bcast:15/31). These replace ds_bpermute-based
+// shuffles in every reduction of the hot path: a DPP move is a VALU modifier, a shuffle
+// is an LDS round trip. All orders are fixed, so results are bitwise reproducible.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <climits>
+
+namespace dab {
+
+// value of lane (i - shift pattern) per DPP control; lanes without a source keep `old`
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
+__device__ __forceinline__ double dpp_f64(double v, double old) {
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), CTRL, ROW_MASK, BANK_MASK,
+                                             false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), CTRL, ROW_MASK, BANK_MASK,
+                                             false);
+  return __hiloint2double(hi, lo);
+}
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
+__device__ __forceinline__ int dpp_i32(int v, int old) {
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, ROW_MASK, BANK_MASK, false);
+}
+
+// Sum over the 64 lanes; the total is in lane 63 (other lanes hold partials). Inside a
+// row every source lane exists (xor 1, xor 2, half-row mirror, row mirror), so those
+// moves need no `old` operand; only the two row broadcasts are masked.
+template <int CTRL>
+__device__ __forceinline__ double dpp_full_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_sum_lane63(double v) {
+  v += dpp_full_f64<0xb1>(v);        // quad_perm [1,0,3,2]
+  v += dpp_full_f64<0x4e>(v);        // quad_perm [2,3,0,1]
+  v += dpp_full_f64<0x141>(v);       // row_half_mirror
+  v += dpp_full_f64<0x140>(v);       // row_mirror: every lane holds its row sum
+  v += dpp_f64<0x142, 0xa>(v, 0.0);  // row_bcast:15 -> rows 1, 3
+  v += dpp_f64<0x143, 0xc>(v, 0.0);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+}  // namespace dab

@@ -1,0 +1,30 @@
+"""Tuning sweep of the evaluation pass (camera chunk size) on one config."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import _pkgload  # noqa: E402
+
+pkg = _pkgload.load()
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c3_1kcam"
+prob = pkg.synth(**pkg.CONFIGS[cfg])
+for wps, chunk in ((4, 2048), (41, 2048), (42, 2048)):
+    os.environ["DAB_CHUNK"] = str(chunk)
+    os.environ["DAB_EVAL_WPS"] = str(wps)
+    s = pkg.Solver(0)
+    s.set_problem(prob)
+    for _ in range(5):
+        s.bench_eval_pass(True)
+    s.sync()
+    s.bench_kernel_ms()
+    t0 = time.perf_counter()
+    for _ in range(30):
+        s.bench_eval_pass(True)
+    s.sync()
+    dt = (time.perf_counter() - t0) / 30
+    j, a = s.bench_kernel_ms()
+    print(f"{cfg} wps={wps} chunk={chunk}: step {dt * 1e3:.3f} ms, points kernel {j * 1e3:.1f} us, rest {a * 1e3:.1f} us, "
+          f"{prob.num_obs / dt / 1e6:.0f} M obs/s", flush=True)
+    s.close()
