@@ -38,7 +38,7 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--config", default="c3_1kcam")
     ap.add_argument("--n-obs", type=int, default=1000000)
-    ap.add_argument("--kernel", default="k_jacobian<")
+    ap.add_argument("--kernel", default="k_eval_points<")
     a = ap.parse_args()
     fetch, write = load(a.fetch_dir, "FETCH_SIZE"), load(a.write_dir, "WRITE_SIZE")
     table = {}
