@@ -10,7 +10,7 @@ constexpr int kCamTab = 32;   // doubles per extrinsic table: R(9) t(3) Rd(9) Jd
 constexpr int kIntr = 8;      // doubles per intrinsic: cx cy fx fy k0 k1 0 0
 constexpr int kYRec = 18;     // doubles per Y_e record (6x3)
 constexpr int kRedBlock = 256;
-constexpr int kChunk = 256;   // max elements per reduction chunk (one per thread)
+constexpr int kChunk = 4096;  // max entries per reduction chunk (C3: one chunk per camera)
 constexpr int kSlotBit = 1 << 30;  // cm_idx.w flag: the entry is the ring (slot 1) camera
 
 // Device-side problem view. Observations are point-major ("s" order). An "entry" is an
@@ -23,6 +23,7 @@ struct DevView {
   int E;          // extrinsics
   int NC;         // free cameras
   int NE;         // entries
+  int NI;         // intrinsics
   int nslice;     // SELL-64 slices (64 points each)
   const int4* obs_idx;      // (point, ext0, ext1, intr)
   const double2* obs_xy;
@@ -43,9 +44,11 @@ struct DevView {
 void launch_cam_tables(hipStream_t s, int E, const double* ext, double* camtab);
 // Point side of the evaluation pass (rows a1-a4, matrix-free): residual + d r / d X per
 // observation reduced into V[6][NP], g[3][NP] (one SELL slice per block, lane = point,
-// wps = 4 | 8 | 16 waves per slice), partial[grid][2] = {sum r^2, non-finite}.
+// wps = 4 | 8 | 16 waves per slice with global tables, 0 = LDS-staged tables with a
+// persistent grid), partial[grid][2] = {sum r^2, non-finite}.
 void launch_eval_points(hipStream_t s, const DevView& v, const double* points, const double* camtab, double* V,
                         double* g, double* partial, int grid, int wps);
+bool eval_points_lds_fits(int E);
 // Full Jacobian planes (parity API): Jfull[30][N], r[N]
 void launch_jacobian_full(hipStream_t s, const DevView& v, const double* points,
                           const double* camtab, double* r, double* Jfull);

@@ -37,20 +37,33 @@ int grid_for(int n, int block, int cap) {
 // ------------------------------------------------------------------------------------
 // reductions
 // ------------------------------------------------------------------------------------
+// Fixed-order sum of K per-thread values over a 256-thread block: four full-mask DPP
+// steps give every lane its 16-lane row sum, the 16 row sums go through LDS, and K
+// threads add them in order. About 13 VALU per value and wave, against ~22 for a
+// full-wave DPP reduction.
+__device__ __forceinline__ double row_sum16(double v) {
+  v += dpp_full_f64<0xb1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_full_f64<0x4e>(v);   // quad_perm [2,3,0,1]
+  v += dpp_full_f64<0x141>(v);  // row_half_mirror
+  v += dpp_full_f64<0x140>(v);  // row_mirror
+  return v;
+}
 template <int K>
 __device__ __forceinline__ void block_reduce_store(double (&acc)[K], double* __restrict__ out) {
-  __shared__ double sh[kRedBlock / 64][K];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int R = kRedBlock / 16;  // rows per block
+  __shared__ double sh[K][R];
+  const int lane = threadIdx.x & 63;
+  const int row = threadIdx.x >> 4;
 #pragma unroll
   for (int i = 0; i < K; ++i) {
-    const double v = wave_sum_lane63(acc[i]);
-    if (lane == 63) sh[w][i] = v;
+    const double v = row_sum16(acc[i]);
+    if ((lane & 15) == 15) sh[i][row] = v;
   }
   __syncthreads();
   if (threadIdx.x < K) {
-    double v = sh[0][threadIdx.x];
+    double v = sh[threadIdx.x][0];
 #pragma unroll
-    for (int q = 1; q < kRedBlock / 64; ++q) v += sh[q][threadIdx.x];
+    for (int q = 1; q < R; ++q) v += sh[threadIdx.x][q];
     out[threadIdx.x] = v;
   }
 }
@@ -296,24 +309,63 @@ __device__ __forceinline__ void load_intr(const double* __restrict__ intr, int i
   }
 }
 
+// Where a pass reads the per-camera tables from: global memory (L2-resident), or R,t
+// (and K when it fits) staged once per work-group in LDS.
+struct GlobalTabs {
+  const double* __restrict__ camtab;
+  const double* __restrict__ intr;
+  __device__ __forceinline__ void rt(int e, double (&T)[12]) const { load_tab_at<0, 12>(camtab, e, T); }
+  __device__ __forceinline__ void dj(int e, double (&T)[18]) const { load_tab_at<12, 18>(camtab, e, T); }
+  __device__ __forceinline__ void k(int i, double (&K)[6]) const { load_intr(intr, i, K); }
+};
+template <bool K_IN_LDS>
+struct LdsTabs {
+  const double* rt_s;  // LDS [E][12]: R t
+  const double* k_s;   // LDS [NI][6] when K_IN_LDS
+  const double* __restrict__ camtab;
+  const double* __restrict__ intr;
+  __device__ __forceinline__ void rt(int e, double (&T)[12]) const {
+    const double2* p = reinterpret_cast<const double2*>(rt_s + 12 * e);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const double2 v = p[i];
+      T[2 * i] = v.x;
+      T[2 * i + 1] = v.y;
+    }
+  }
+  __device__ __forceinline__ void dj(int e, double (&T)[18]) const { load_tab_at<12, 18>(camtab, e, T); }
+  __device__ __forceinline__ void k(int i, double (&K)[6]) const {
+    if constexpr (K_IN_LDS) {
+      const double2* p = reinterpret_cast<const double2*>(k_s + 6 * i);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const double2 v = p[q];
+        K[2 * q] = v.x;
+        K[2 * q + 1] = v.y;
+      }
+    } else {
+      load_intr(intr, i, K);
+    }
+  }
+};
+
 // Residual and the Jacobian rows of one observation that a pass needs, from the camera
 // tables. JP: d r / d X (2x3). SLOT 0: d r / d (w0, t0); SLOT 1: d r / d (w1, t1) of the
 // ring camera of an arc∘ring observation; SLOT 2: both (jc0/jc1 = slot 0 rows, jd0/jd1 =
 // slot 1 rows); SLOT -1: no camera rows. Q is the point the arc/single rotation acts on:
 // X (single) or P2 = R1 X + t1 (arc∘ring).
-template <bool JP, int SLOT>
-__device__ __forceinline__ void obs_rows(const int4 id, const double2 xy, const double X[3],
-                                         const double* __restrict__ camtab, const double* __restrict__ intr,
+template <bool JP, int SLOT, class Tabs>
+__device__ __forceinline__ void obs_rows(const int4 id, const double2 xy, const double X[3], const Tabs& tb,
                                          double& ru, double& rv, double jx0[3], double jx1[3], double jc0[6],
                                          double jc1[6], double jd0[6] = nullptr, double jd1[6] = nullptr) {
   const bool comp = id.z >= 0;
   double A[12];  // R0 | t0
-  load_tab_at<0, 12>(camtab, id.y, A);
+  tb.rt(id.y, A);
   double Kr[6];
-  load_intr(intr, id.w, Kr);
+  tb.k(id.w, Kr);
   double Q[3], B[12];  // B = R1 | t1 (arc∘ring only)
   if (comp) {
-    load_tab_at<0, 12>(camtab, id.z, B);
+    tb.rt(id.z, B);
     matvec_add(B, X, B + 9, Q);
   } else {
     Q[0] = X[0];
@@ -328,7 +380,7 @@ __device__ __forceinline__ void obs_rows(const int4 id, const double2 xy, const 
   rv = pr.rv;
   if constexpr (SLOT == 0 || SLOT == 2) {
     double D[18];  // Rd0 | Jd0
-    load_tab_at<12, 18>(camtab, id.y, D);
+    tb.dj(id.y, D);
     double Da[3], Db[3];
     rowmat(pr.A0, D, Da);
     rowmat(pr.A1, D, Db);
@@ -349,7 +401,7 @@ __device__ __forceinline__ void obs_rows(const int4 id, const double2 xy, const 
       double* o1 = SLOT == 1 ? jc1 : jd1;
       if (comp) {
         double D[18];  // Rd1 | Jd1
-        load_tab_at<12, 18>(camtab, id.z, D);
+        tb.dj(id.z, D);
         double Ca[3], Cb[3];
         rowmat(B0a, D, Ca);
         rowmat(B0b, D, Cb);
@@ -388,7 +440,7 @@ __device__ __forceinline__ void obs_jacobian(const int4 id, const double2 xy, co
                                              const double* __restrict__ camtab,
                                              const double* __restrict__ intr, ObsJac& o) {
   double c0[6], c1[6], d0[6], d1[6];
-  obs_rows<true, 2>(id, xy, X, camtab, intr, o.pr.ru, o.pr.rv, o.jx0, o.jx1, c0, c1, d0, d1);
+  obs_rows<true, 2>(id, xy, X, GlobalTabs{camtab, intr}, o.pr.ru, o.pr.rv, o.jx0, o.jx1, c0, c1, d0, d1);
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     o.jw0a[i] = c0[i];
@@ -406,21 +458,23 @@ __device__ __forceinline__ void obs_jacobian(const int4 id, const double2 xy, co
 // residual and d r / d X per observation, reduced straight into V = Jp^T Jp (6) and
 // g_p = Jp^T r (3). Nothing per observation is written: every later pass re-evaluates
 // the rows it needs from the inputs (32 B per observation; the Jacobian is 144-240 B).
-// One block per SELL-64 slice: lane l owns point 64 sl + l (its X loaded once), wave w of
-// the WPS waves takes the slice's observation rows k = w, w + WPS, ... (coalesced 64-slot
-// rows), and the per-wave sums are combined in LDS in a fixed order: no cross-lane scan.
-template <int WPS, int VAR = 0>
-__global__ __launch_bounds__(64 * WPS) void k_eval_points(DevView v, const double* __restrict__ points,
-                                                          const double* __restrict__ camtab,
-                                                          double* __restrict__ V, double* __restrict__ g,
-                                                          double* __restrict__ partial) {
-  __shared__ double sh[WPS > 1 ? WPS - 1 : 1][9][64];
-  __shared__ double shp[WPS][2];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+// One SELL-64 slice: lane l owns point 64 sl + l (its X loaded once), wave w of the WPS
+// waves takes the slice's observation rows k = w, w + WPS, ... (coalesced 64-slot rows),
+// and the per-wave sums are combined in LDS (sh[WPS-1][9][64]) in a fixed order: no
+// cross-lane scan. Every wave of the work-group calls this the same number of times
+// (sl >= nslice: no work, barriers only).
+template <int WPS, int VAR, class Tabs>
+__device__ __forceinline__ void eval_slice(const DevView& v, const double* __restrict__ points, const Tabs& tabs,
+                                           double* __restrict__ V, double* __restrict__ g, int sl, int w,
+                                           double (*sh)[9][64], double (&acc)[2]) {
+  const int lane = threadIdx.x & 63;
   const size_t NPs = (size_t)v.NP;
-  double acc[2] = {0.0, 0.0};
-  for (int sl = blockIdx.x; sl < v.nslice; sl += gridDim.x) {
-    const int p = 64 * sl + lane;
+  const bool live = sl < v.nslice;
+  const int p = 64 * sl + lane;
+  double c[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) c[k] = 0.0;
+  if (live) {
     const int off = v.slice_off[sl], len = (v.slice_off[sl + 1] - off) >> 6;
     double X[3] = {0.0, 0.0, 0.0};
     if (p < v.NP) {
@@ -428,14 +482,22 @@ __global__ __launch_bounds__(64 * WPS) void k_eval_points(DevView v, const doubl
       X[1] = points[3 * (size_t)p + 1];
       X[2] = points[3 * (size_t)p + 2];
     }
-    double c[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) c[k] = 0.0;
+    // rows are software-pipelined: the next row's inputs are in flight while this
+    // row computes (each wave walks only len / WPS rows, so latency dominates)
+    int4 id_n = make_int4(-1, 0, -1, 0);
+    double2 xy_n = make_double2(0.0, 0.0);
+    if (w < len) {
+      id_n = v.obs_idx[off + 64 * w + lane];
+      xy_n = v.obs_xy[off + 64 * w + lane];
+    }
     for (int k = w; k < len; k += WPS) {
-      const int s = off + 64 * k + lane;
-      int4 id = v.obs_idx[s];
+      int4 id = id_n;
+      const double2 xy = xy_n;
+      if (k + WPS < len) {
+        id_n = v.obs_idx[off + 64 * (k + WPS) + lane];
+        xy_n = v.obs_xy[off + 64 * (k + WPS) + lane];
+      }
       if (id.x < 0) continue;  // padding slot
-      const double2 xy = v.obs_xy[s];
       double ru, rv, jx0[3], jx1[3];
       if constexpr (VAR == 1) {  // ablation: loads only
         ru = xy.x + id.y;
@@ -444,45 +506,52 @@ __global__ __launch_bounds__(64 * WPS) void k_eval_points(DevView v, const doubl
         for (int q = 0; q < 3; ++q) jx0[q] = jx1[q] = X[q];
       } else {
         if constexpr (VAR == 2) id.y = id.w = 0;  // ablation: one camera (uniform table loads)
-        obs_rows<true, -1>(id, xy, X, camtab, v.intr, ru, rv, jx0, jx1, nullptr, nullptr);
+        obs_rows<true, -1>(id, xy, X, tabs, ru, rv, jx0, jx1, nullptr, nullptr);
       }
-      c[0] += jx0[0] * jx0[0] + jx1[0] * jx1[0];
-      c[1] += jx0[0] * jx0[1] + jx1[0] * jx1[1];
-      c[2] += jx0[0] * jx0[2] + jx1[0] * jx1[2];
-      c[3] += jx0[1] * jx0[1] + jx1[1] * jx1[1];
-      c[4] += jx0[1] * jx0[2] + jx1[1] * jx1[2];
-      c[5] += jx0[2] * jx0[2] + jx1[2] * jx1[2];
-      c[6] += jx0[0] * ru + jx1[0] * rv;
-      c[7] += jx0[1] * ru + jx1[1] * rv;
-      c[8] += jx0[2] * ru + jx1[2] * rv;
-      acc[0] += ru * ru + rv * rv;
+      // accumulate as two fused multiply-adds per entry (row 0, then row 1)
+      c[0] = fma(jx1[0], jx1[0], fma(jx0[0], jx0[0], c[0]));
+      c[1] = fma(jx1[0], jx1[1], fma(jx0[0], jx0[1], c[1]));
+      c[2] = fma(jx1[0], jx1[2], fma(jx0[0], jx0[2], c[2]));
+      c[3] = fma(jx1[1], jx1[1], fma(jx0[1], jx0[1], c[3]));
+      c[4] = fma(jx1[1], jx1[2], fma(jx0[1], jx0[2], c[4]));
+      c[5] = fma(jx1[2], jx1[2], fma(jx0[2], jx0[2], c[5]));
+      c[6] = fma(jx1[0], rv, fma(jx0[0], ru, c[6]));
+      c[7] = fma(jx1[1], rv, fma(jx0[1], ru, c[7]));
+      c[8] = fma(jx1[2], rv, fma(jx0[2], ru, c[8]));
+      acc[0] = fma(rv, rv, fma(ru, ru, acc[0]));
       acc[1] += (isfinite(ru) && isfinite(rv)) ? 0.0 : 1.0;
     }
-    if (WPS > 1) {
-      if (w > 0) {
-#pragma unroll
-        for (int k = 0; k < 9; ++k) sh[w - 1][k][lane] = c[k];
-      }
-      __syncthreads();
-    }
-    if (w == 0 && p < v.NP) {
-      if (WPS > 1) {
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-          double t = c[k];
-#pragma unroll
-          for (int q = 0; q < WPS - 1; ++q) t += sh[q][k][lane];
-          c[k] = t;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 6; ++k) V[k * NPs + p] = c[k];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) g[k * NPs + p] = c[6 + k];
-    }
-    if (WPS > 1) __syncthreads();
   }
-  // per-block cost partials: wave sums, then a fixed-order sum over the waves
+  if constexpr (WPS > 1) {
+    if (w > 0) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) sh[w - 1][k][lane] = c[k];
+    }
+    __syncthreads();
+  }
+  if (live && w == 0 && p < v.NP) {
+    if constexpr (WPS > 1) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        double t = c[k];
+#pragma unroll
+        for (int q = 0; q < WPS - 1; ++q) t += sh[q][k][lane];
+        c[k] = t;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) V[k * NPs + p] = c[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) g[k * NPs + p] = c[6 + k];
+  }
+  if constexpr (WPS > 1) __syncthreads();
+}
+
+// cost partials of a work-group of NW waves: wave sums, then a fixed-order sum
+template <int NW>
+__device__ __forceinline__ void store_cost_partial(double (&acc)[2], double* __restrict__ partial) {
+  __shared__ double shp[NW][2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const double t = wave_sum_lane63(acc[i]);
@@ -492,19 +561,79 @@ __global__ __launch_bounds__(64 * WPS) void k_eval_points(DevView v, const doubl
   if (threadIdx.x < 2) {
     double t = shp[0][threadIdx.x];
 #pragma unroll
-    for (int q = 1; q < WPS; ++q) t += shp[q][threadIdx.x];
+    for (int q = 1; q < NW; ++q) t += shp[q][threadIdx.x];
     partial[2 * (size_t)blockIdx.x + threadIdx.x] = t;
   }
 }
 
+// tables from global memory: one block per slice, grid-strided
+template <int WPS, int VAR = 0>
+__global__ __launch_bounds__(64 * WPS) void k_eval_points(DevView v, const double* __restrict__ points,
+                                                          const double* __restrict__ camtab,
+                                                          double* __restrict__ V, double* __restrict__ g,
+                                                          double* __restrict__ partial) {
+  __shared__ double sh[WPS > 1 ? WPS - 1 : 1][9][64];
+  const GlobalTabs tabs{camtab, v.intr};
+  double acc[2] = {0.0, 0.0};
+  const int rounds = (v.nslice + gridDim.x - 1) / gridDim.x;
+  for (int r = 0; r < rounds; ++r)
+    eval_slice<WPS, VAR>(v, points, tabs, V, g, r * gridDim.x + blockIdx.x, threadIdx.x >> 6, sh, acc);
+  store_cost_partial<WPS>(acc, partial);
+}
+
+// Tables staged in LDS (camera count <= kLdsCams): R,t of every extrinsic (and K of every
+// intrinsic when <= kLdsIntr) are copied once per work-group, so the per-lane table reads
+// of BAL-shaped data (every lane a different camera) become ds_read_b128 instead of
+// 64-line L2 gathers. Persistent: one 1024-thread work-group per CU, four slices in flight.
+constexpr int kLdsCams = 1024, kLdsIntr = 128;
+template <bool K_IN_LDS>
+__global__ __launch_bounds__(1024) void k_eval_points_lds(DevView v, const double* __restrict__ points,
+                                                          const double* __restrict__ camtab,
+                                                          double* __restrict__ V, double* __restrict__ g,
+                                                          double* __restrict__ partial) {
+  __shared__ double rt_s[kLdsCams * 12];
+  __shared__ double k_s[K_IN_LDS ? kLdsIntr * 6 : 2];
+  __shared__ double sh[4][3][9][64];
+  for (int i = threadIdx.x; i < v.E * 6; i += blockDim.x) {
+    const int e = i / 6, q = i - 6 * (i / 6);
+    reinterpret_cast<double2*>(rt_s)[i] = reinterpret_cast<const double2*>(camtab + (size_t)kCamTab * e)[q];
+  }
+  if constexpr (K_IN_LDS) {
+    for (int i = threadIdx.x; i < v.NI * 3; i += blockDim.x) {
+      const int n = i / 3, q = i - 3 * (i / 3);
+      reinterpret_cast<double2*>(k_s)[i] = reinterpret_cast<const double2*>(v.intr + (size_t)kIntr * n)[q];
+    }
+  }
+  __syncthreads();
+  const LdsTabs<K_IN_LDS> tabs{rt_s, k_s, camtab, v.intr};
+  const int wave = threadIdx.x >> 6, grp = wave >> 2, w = wave & 3;
+  double acc[2] = {0.0, 0.0};
+  const int per_round = 4 * gridDim.x;
+  const int rounds = (v.nslice + per_round - 1) / per_round;
+  for (int r = 0; r < rounds; ++r)
+    eval_slice<4, 0>(v, points, tabs, V, g, (r * gridDim.x + blockIdx.x) * 4 + grp, w, sh[grp], acc);
+  store_cost_partial<16>(acc, partial);
+}
+
 void launch_eval_points(hipStream_t s, const DevView& v, const double* points, const double* camtab, double* V,
                         double* g, double* partial, int grid, int wps) {
-  if (wps == 41) k_eval_points<4, 1><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);  // ablations
-  else if (wps == 42) k_eval_points<4, 2><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);
-  else if (wps == 4) k_eval_points<4><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);
-  else if (wps == 16) k_eval_points<16><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
-  else k_eval_points<8><<<grid, 512, 0, s>>>(v, points, camtab, V, g, partial);
+  if (wps == 0) {  // LDS-staged tables; grid = persistent work-groups
+    if (v.NI <= kLdsIntr) k_eval_points_lds<true><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
+    else k_eval_points_lds<false><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
+  } else if (wps == 41) {  // ablations
+    k_eval_points<4, 1><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);
+  } else if (wps == 42) {
+    k_eval_points<4, 2><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);
+  } else if (wps == 16) {
+    k_eval_points<16><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
+  } else if (wps == 8) {
+    k_eval_points<8><<<grid, 512, 0, s>>>(v, points, camtab, V, g, partial);
+  } else {
+    k_eval_points<4><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);
+  }
 }
+
+bool eval_points_lds_fits(int E) { return E <= kLdsCams; }
 
 // parity API: every Jacobian column as planes Jfull[2*col+row][N]
 __global__ __launch_bounds__(256) void k_jacobian_full(DevView v, const double* __restrict__ points,
@@ -601,25 +730,49 @@ __global__ __launch_bounds__(256) void k_eval_cams(DevView v, const int* __restr
                                                    double* __restrict__ partial) {
   const int c = blockIdx.x;
   const int b = chunk_beg[c], e = chunk_beg[c + 1];
+  const GlobalTabs tabs{camtab, v.intr};
   double acc[27];
 #pragma unroll
   for (int i = 0; i < 27; ++i) acc[i] = 0.0;
-  for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
-    int4 id = v.cm_idx[i];
+  // software-pipelined: the next entry's inputs (and its point) load while this one computes
+  int i = b + threadIdx.x;
+  int4 id_n = make_int4(0, 0, -1, 0);
+  double2 xy_n = make_double2(0.0, 0.0);
+  double X_n[3] = {0.0, 0.0, 0.0};
+  if (i < e) {
+    id_n = v.cm_idx[i];
+    xy_n = v.cm_xy[i];
+    X_n[0] = points[3 * (size_t)id_n.x];
+    X_n[1] = points[3 * (size_t)id_n.x + 1];
+    X_n[2] = points[3 * (size_t)id_n.x + 2];
+  }
+  for (; i < e; i += blockDim.x) {
+    int4 id = id_n;
+    const double2 xy = xy_n;
+    const double X[3] = {X_n[0], X_n[1], X_n[2]};
+    const int in = i + blockDim.x;
+    if (in < e) {
+      id_n = v.cm_idx[in];
+      xy_n = v.cm_xy[in];
+      X_n[0] = points[3 * (size_t)id_n.x];
+      X_n[1] = points[3 * (size_t)id_n.x + 1];
+      X_n[2] = points[3 * (size_t)id_n.x + 2];
+    }
     const bool slot1 = (id.w & kSlotBit) != 0;
     id.w &= ~kSlotBit;
-    const double2 xy = v.cm_xy[i];
-    const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
     double ru, rv, ja[6], jb[6];
-    if (slot1) obs_rows<false, 1>(id, xy, X, camtab, v.intr, ru, rv, nullptr, nullptr, ja, jb);
-    else obs_rows<false, 0>(id, xy, X, camtab, v.intr, ru, rv, nullptr, nullptr, ja, jb);
+    if (slot1) obs_rows<false, 1>(id, xy, X, tabs, ru, rv, nullptr, nullptr, ja, jb);
+    else obs_rows<false, 0>(id, xy, X, tabs, ru, rv, nullptr, nullptr, ja, jb);
     int k = 0;
 #pragma unroll
     for (int a = 0; a < 6; ++a)
 #pragma unroll
-      for (int bb = a; bb < 6; ++bb) acc[k++] += ja[a] * ja[bb] + jb[a] * jb[bb];
+      for (int bb = a; bb < 6; ++bb) {
+        acc[k] = fma(jb[a], jb[bb], fma(ja[a], ja[bb], acc[k]));
+        ++k;
+      }
 #pragma unroll
-    for (int a = 0; a < 6; ++a) acc[21 + a] += ja[a] * ru + jb[a] * rv;
+    for (int a = 0; a < 6; ++a) acc[21 + a] = fma(jb[a], rv, fma(ja[a], ru, acc[21 + a]));
   }
   block_reduce_store<27>(acc, partial + 27 * (size_t)c);
 }
@@ -741,8 +894,8 @@ __global__ __launch_bounds__(256) void k_entry_y(DevView v, const double* __rest
   const double2 xy = v.cm_xy[i];
   const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
   double ru, rv, jx0[3], jx1[3], ja[6], jb[6];
-  if (slot1) obs_rows<true, 1>(id, xy, X, camtab, v.intr, ru, rv, jx0, jx1, ja, jb);
-  else obs_rows<true, 0>(id, xy, X, camtab, v.intr, ru, rv, jx0, jx1, ja, jb);
+  if (slot1) obs_rows<true, 1>(id, xy, X, GlobalTabs{camtab, v.intr}, ru, rv, jx0, jx1, ja, jb);
+  else obs_rows<true, 0>(id, xy, X, GlobalTabs{camtab, v.intr}, ru, rv, jx0, jx1, ja, jb);
   const double* pu = PU + 6 * (size_t)id.x;
   const double u00 = pu[0], u01 = pu[1], u02 = pu[2], u11 = pu[3], u12 = pu[4], u22 = pu[5];
   double y[18];

@@ -172,7 +172,7 @@ struct dab_handle {
   int* h_flags = nullptr;      // pinned
   int red_grid = 1;
   int eval_grid = 1;  // k_eval_points blocks (one SELL slice per block)
-  int eval_wps = 4;   // waves per slice (DAB_EVAL_WPS tuning knob)
+  int eval_wps = 0;   // 0: LDS tables; else waves per slice (DAB_EVAL_WPS tuning knob)
 
   ~dab_handle() {
     dev.release();
@@ -675,10 +675,16 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   CHECK_RC(d.alloc(&h->d_dp, (size_t)3 * NP));
   CHECK_RC(d.alloc(&h->d_dc, (size_t)6 * NC));
   h->red_grid = grid_for(std::max(h->NS, 3 * NP), 256, 1024);
-  h->eval_grid = std::max(1, h->nslice);
   {
+    // point-side kernel: LDS-staged camera tables when they fit (persistent grid, one
+    // 1024-thread work-group per CU), else global tables (one block per slice).
     const char* env = getenv("DAB_EVAL_WPS");
-    h->eval_wps = env ? atoi(env) : 4;
+    h->eval_wps = env ? atoi(env) : (eval_points_lds_fits(h->E) ? 0 : 4);
+    int ncu = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, h->device) == hipSuccess && prop.multiProcessorCount > 0)
+      ncu = prop.multiProcessorCount;
+    h->eval_grid = h->eval_wps == 0 ? std::max(1, std::min(ncu, (h->nslice + 3) / 4)) : std::max(1, h->nslice);
   }
   CHECK_RC(d.alloc(&h->d_gpart, (size_t)std::max(h->red_grid, h->eval_grid) * 4));
   CHECK_RC(d.alloc(&h->d_scal, S_NSLOTS));
@@ -691,6 +697,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   v.NP = NP;
   v.E = h->E;
   v.NC = NC;
+  v.NI = h->NI;
   v.NE = NE;
   v.nslice = h->nslice;
   v.obs_idx = h->d_obs_idx;

@@ -4,6 +4,7 @@ B="python3 bench.py --no-cpu --no-lm --steps 5 --warmup 1"
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_FLAT SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT" \
            "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TA_BUSY_avr TD_BUSY_avr"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $set -d gpurun_out/pmc/p$i -o run --output-format csv -- $B > gpurun_out/pmc/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/pmc/p$i.log; }
@@ -15,7 +16,8 @@ for f in glob.glob("gpurun_out/pmc/p*/**/*counter_collection.csv", recursive=Tru
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("dab::", "")
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-for k in ("k_eval_points", "k_eval_cams"):
+for k in sorted(agg):
+    if not k.startswith("k_eval"): continue
     print(k)
     for c, v in sorted(agg[k].items()):
         print(f"   {c:28s} {sum(v)/len(v):14.1f}")
