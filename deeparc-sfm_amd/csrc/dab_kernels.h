@@ -55,6 +55,9 @@ void launch_jacobian_full(hipStream_t s, const DevView& v, const double* points,
 // residual only, with per-block partial sums of r^2 and a non-finite count
 void launch_residual(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                      double* r_out /*nullable*/, double* partial /*[grid][2]*/, int grid);
+// filterPoint3d masks (DeepArcManager.cc:332-424): slot_keep[N slots], pt_keep[NP]
+void launch_filter(hipStream_t s, const DevView& v, const double* points, const double* camtab, double eb,
+                   const double c[3], double radius, unsigned char* slot_keep, unsigned char* pt_keep);
 // camera side of the evaluation pass (matrix-free, camera-major inputs):
 //  U/g: per entry 21 (Jc^T Jc upper) + 6 (Jc^T r) -> partial[chunk][27]
 void launch_eval_cams(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const double* points,

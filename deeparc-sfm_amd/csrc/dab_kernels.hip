@@ -718,6 +718,50 @@ void launch_residual(hipStream_t s, const DevView& v, const double* points, cons
   k_residual<<<grid, 256, 0, s>>>(v, points, camtab, reinterpret_cast<double2*>(r_out), partial);
 }
 
+// filterPoint3d (DeepArcManager.cc:332-424) masks, one SELL slice per 64-lane block:
+// lane = point, its slots walked in order. keep(slot) = !(mse < eb); a point lives when
+// one of its slots is kept and !(|X - c|^2 > radius/2); a dead point drops its slots.
+__global__ __launch_bounds__(64) void k_filter(DevView v, const double* __restrict__ points,
+                                               const double* __restrict__ camtab, double eb, double c0,
+                                               double c1, double c2, double half_r,
+                                               unsigned char* __restrict__ slot_keep,
+                                               unsigned char* __restrict__ pt_keep) {
+  const int sl = blockIdx.x, lane = threadIdx.x;
+  const int p = 64 * sl + lane;
+  const int off = v.slice_off[sl], len = (v.slice_off[sl + 1] - off) >> 6;
+  bool alive = false;
+  for (int k = 0; k < len; ++k) {
+    const int s = off + 64 * k + lane;
+    unsigned char keep = 0;
+    if (v.obs_idx[s].x >= 0) {
+      double ru, rv;
+      residual_at(v, points, camtab, s, ru, rv);
+      const double mse = (ru * ru + rv * rv) / 2.0;
+      keep = (mse < eb) ? 0 : 1;
+    }
+    slot_keep[s] = keep;
+    alive = alive || keep;
+  }
+  if (p >= v.NP) return;
+  double d2 = 0.0;
+  const double c[3] = {c0, c1, c2};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double d = points[3 * (size_t)p + i] - c[i];
+    d2 += d * d;
+  }
+  alive = alive && !(d2 > half_r);
+  pt_keep[p] = alive ? 1 : 0;
+  if (!alive)
+    for (int k = 0; k < len; ++k) slot_keep[off + 64 * k + lane] = 0;
+}
+
+void launch_filter(hipStream_t s, const DevView& v, const double* points, const double* camtab, double eb,
+                   const double c[3], double radius, unsigned char* slot_keep, unsigned char* pt_keep) {
+  if (v.nslice <= 0) return;
+  k_filter<<<v.nslice, 64, 0, s>>>(v, points, camtab, eb, c[0], c[1], c[2], radius / 2, slot_keep, pt_keep);
+}
+
 // ------------------------------------------------------------------------------------
 // camera-side J^T J / J^T r reductions, matrix-free (row a7)
 // ------------------------------------------------------------------------------------

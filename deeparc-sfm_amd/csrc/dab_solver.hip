@@ -1338,6 +1338,41 @@ extern "C" int dab_eval_jacobians(dab_handle* h, double* residuals, double* jaco
   return 0;
 }
 
+extern "C" int dab_filter(dab_handle* h, double error_boundary, const double center[3], double radius,
+                          uint8_t* obs_keep, uint8_t* point_keep, int32_t* n_obs_kept, int32_t* n_points_kept) {
+  clear_error();
+  if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
+  if (!center) return set_error(DAB_E_INVALID, "null hemisphere center");
+  HIP_OK(hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  Dev tmp;
+  unsigned char *d_slot = nullptr, *d_pt = nullptr;
+  CHECK_RC(tmp.alloc(&d_slot, (size_t)std::max(1, h->NS)));
+  CHECK_RC(tmp.alloc(&d_pt, (size_t)std::max(1, h->NP)));
+  launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
+  launch_filter(s, h->view, h->d_points, h->d_camtab, error_boundary, center, radius, d_slot, d_pt);
+  std::vector<unsigned char> slot((size_t)h->NS), pt((size_t)h->NP);
+  if (h->NS > 0) HIP_OK(hipMemcpyAsync(slot.data(), d_slot, slot.size(), hipMemcpyDeviceToHost, s));
+  if (h->NP > 0) HIP_OK(hipMemcpyAsync(pt.data(), d_pt, pt.size(), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  int32_t no = 0, np = 0;
+  if (obs_keep) std::memset(obs_keep, 0, (size_t)h->N);
+  for (int s2 = 0; s2 < h->NS; ++s2) {
+    const int o = h->perm[s2];
+    if (o < 0) continue;
+    if (obs_keep) obs_keep[o] = slot[s2];
+    no += slot[s2];
+  }
+  if (point_keep) std::memset(point_keep, 0, (size_t)h->prob.num_points);
+  for (int i = 0; i < h->NP; ++i) {
+    if (point_keep) point_keep[h->pt_of[i]] = pt[i];
+    np += pt[i];
+  }
+  if (n_obs_kept) *n_obs_kept = no;
+  if (n_points_kept) *n_points_kept = np;
+  return 0;
+}
+
 extern "C" int dab_dense_spd_solve(dab_handle* h, int n, const double* A, const double* b, double* x,
                                    double* factor_ms) {
   clear_error();

@@ -1,0 +1,107 @@
+// DabScene.cc — DeepArcManager <-> dab_problem marshalling (see DabScene.hh).
+#include "DabScene.hh"
+
+#include <cstdlib>
+#include <unordered_map>
+
+void dab_check(int rc) {
+  if (rc != 0) throw dab_last_error();
+}
+
+DabHandle::DabHandle() {
+  const char* env = std::getenv("DAB_DEVICE");
+  dab_check(dab_create(env ? std::atoi(env) : 0, &h));
+}
+DabHandle::~DabHandle() {
+  if (h) dab_destroy(h);
+}
+
+void DabScene::build(DeepArcManager& m, bool freeze_camera) {
+  std::vector<ParameterBlock*>& blocks = *m.parameters();
+  std::vector<Point3d*>& pts = *m.point3ds();
+  std::vector<Extrinsic*>& exts = *m.extrinsics();
+  std::vector<Intrinsic*>& ks = *m.intrinsics();
+  std::unordered_map<Point3d*, int> pid;
+  std::unordered_map<Extrinsic*, int> eid;
+  std::unordered_map<Intrinsic*, int> kid;
+  for (size_t i = 0; i < pts.size(); ++i) pid[pts[i]] = (int)i;
+  for (size_t i = 0; i < exts.size(); ++i) eid[exts[i]] = (int)i;
+  for (size_t i = 0; i < ks.size(); ++i) kid[ks[i]] = (int)i;
+  auto find = [](auto& map, auto* key) {
+    auto it = map.find(key);
+    if (it == map.end()) throw "Parameter block references a parameter outside the manager";
+    return it->second;
+  };
+  const size_t N = blocks.size();
+  xy.resize(2 * N);
+  obs_point.resize(N);
+  obs_ext0.resize(N);
+  obs_ext1.resize(N);
+  obs_intr.resize(N);
+  ext_const.assign(exts.size(), 0);
+  for (size_t o = 0; o < N; ++o) {
+    ParameterBlock* b = blocks[o];
+    xy[2 * o] = b->point2d()->x();
+    xy[2 * o + 1] = b->point2d()->y();
+    obs_point[o] = find(pid, b->point3d());
+    obs_intr[o] = find(kid, b->intrinsic());
+    obs_ext0[o] = find(eid, b->first_extrinsic());
+    Extrinsic* e1 = b->second_extrinsic();
+    obs_ext1[o] = e1 ? find(eid, e1) : -1;
+    // gauge: the extrinsic of a (0,0) block is constant (sfm.cc:50-53)
+    if (b->pos_arc() == 0 && b->pos_ring() == 0) ext_const[obs_ext0[o]] = 1;
+  }
+  points.resize(3 * pts.size());
+  for (size_t i = 0; i < pts.size(); ++i)
+    for (int k = 0; k < 3; ++k) points[3 * i + k] = pts[i]->position()[k];
+  ext.resize(6 * exts.size());
+  for (size_t i = 0; i < exts.size(); ++i)
+    for (int k = 0; k < 3; ++k) {
+      ext[6 * i + k] = exts[i]->rotation()[k];
+      ext[6 * i + 3 + k] = exts[i]->translation()[k];
+    }
+  intr.assign(6 * ks.size(), 0.0);
+  intr_nf.resize(ks.size());
+  intr_nk.resize(ks.size());
+  for (size_t i = 0; i < ks.size(); ++i) {
+    Intrinsic* k = ks[i];
+    intr_nf[i] = k->focal_size();
+    intr_nk[i] = k->distrotion_size();
+    double* o = &intr[6 * i];
+    o[0] = k->center()[0];
+    o[1] = k->center()[1];
+    o[2] = k->focal()[0];
+    o[3] = intr_nf[i] == 2 ? k->focal()[1] : 0.0;
+    o[4] = intr_nk[i] >= 1 ? k->distrotion()[0] : 0.0;
+    o[5] = intr_nk[i] >= 2 ? k->distrotion()[1] : 0.0;
+  }
+  problem = dab_problem{};
+  problem.num_obs = (int32_t)N;
+  problem.num_points = (int32_t)pts.size();
+  problem.num_ext = (int32_t)exts.size();
+  problem.num_intr = (int32_t)ks.size();
+  problem.obs_xy = xy.data();
+  problem.obs_point = obs_point.data();
+  problem.obs_ext0 = obs_ext0.data();
+  problem.obs_ext1 = obs_ext1.data();
+  problem.obs_intr = obs_intr.data();
+  problem.points = points.data();
+  problem.ext = ext.data();
+  problem.intr = intr.data();
+  problem.intr_nf = intr_nf.data();
+  problem.intr_nk = intr_nk.data();
+  problem.ext_const = ext_const.data();
+  problem.freeze_camera = freeze_camera ? 1 : 0;
+}
+
+void DabScene::write_back(DeepArcManager& m) {
+  std::vector<Point3d*>& pts = *m.point3ds();
+  std::vector<Extrinsic*>& exts = *m.extrinsics();
+  for (size_t i = 0; i < pts.size(); ++i)
+    for (int k = 0; k < 3; ++k) pts[i]->position()[k] = points[3 * i + k];
+  for (size_t i = 0; i < exts.size(); ++i)
+    for (int k = 0; k < 3; ++k) {
+      exts[i]->rotation()[k] = ext[6 * i + k];
+      exts[i]->translation()[k] = ext[6 * i + 3 + k];
+    }
+}

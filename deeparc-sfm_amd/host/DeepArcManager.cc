@@ -1,0 +1,316 @@
+// DeepArcManager.cc — .deeparc I/O, PLY export, camera centres and filterPoint3d with the
+// reference's semantics (src/DeepArcManager.cc), including its quirks Q1, Q2, Q4, Q6, Q7
+// (SURVEY App. C). The residuals behind filterPoint3d come from the GPU (dab_filter).
+#include "DeepArcManager.hh"
+
+#include <cstdio>
+#include <fstream>
+#include <iostream>
+#include <unordered_map>
+
+#include "../csrc/rotation.h"
+#include "DabScene.hh"
+
+namespace {
+
+// The reference reads with operator>> and indexes with .at(); a short or inconsistent
+// file throws here instead of reading garbage.
+template <class T>
+T take(std::ifstream& f) {
+  T v{};
+  if (!(f >> v)) throw "Malformed .deeparc file";
+  return v;
+}
+
+void fmt6(FILE* f, double v) { std::fprintf(f, "%.6f", v); }  // std::fixed, setprecision(6)
+void fmtg(FILE* f, double v) { std::fprintf(f, "%g", v); }    // default ostream format
+
+}  // namespace
+
+void Extrinsic::rotationMatrix(double R[9]) { dab::AngleAxisToRotationMatrix(rotation_, R); }
+
+DeepArcManager::~DeepArcManager() { clear(); }
+
+void DeepArcManager::clear() {
+  for (ParameterBlock* b : params_) delete b;
+  for (Point3d* p : point3d_) delete p;
+  for (Intrinsic* k : intrinsics_) delete k;
+  for (Extrinsic* e : extrinsics_) delete e;
+  for (Camera* c : camera_) delete c;
+  for (auto& a : hemisphere_)
+    for (auto& r : a.second) delete r.second;
+  params_.clear();
+  point3d_.clear();
+  intrinsics_.clear();
+  extrinsics_.clear();
+  camera_.clear();
+  hemisphere_.clear();
+}
+
+bool DeepArcManager::read(std::string filename) {
+  std::ifstream f(filename);
+  if (f.fail()) {
+    std::cout << "Cannot read " << filename << std::endl;
+    throw "Cannot read input file";
+  }
+  clear();
+  (void)take<double>(f);  // version
+  const int n_blocks = take<int>(f), n_intr = take<int>(f), n_arc = take<int>(f), n_ring = take<int>(f),
+            n_points = take<int>(f);
+  if (n_blocks < 0 || n_intr < 0 || n_arc < 0 || n_ring < 0 || n_points < 0) throw "Malformed .deeparc file";
+  share_extrinsic_ = n_ring != 0;
+  arc_size_ = n_arc;
+  ring_size_ = n_ring;
+  const int n_ext = share_extrinsic_ ? n_arc + n_ring - 1 : n_arc;
+
+  // observation lines: pos_arc pos_ring point_id x y
+  for (int i = 0; i < n_blocks; ++i) {
+    const int a = take<int>(f), r = take<int>(f), pid = take<int>(f);
+    const double x = take<double>(f), y = take<double>(f);
+    params_.push_back(new ParameterBlock(a, r, pid, new Point2d(x, y)));
+  }
+  // intrinsics: cx cy nf f[nf] nk k[nk]; the principal point truncates to int (Q1)
+  for (int i = 0; i < n_intr; ++i) {
+    Intrinsic* k = new Intrinsic();
+    intrinsics_.push_back(k);
+    k->id(i);
+    const double cx = take<double>(f), cy = take<double>(f);
+    k->center((int)cx, (int)cy);
+    double v[2];
+    const int nf = take<int>(f);
+    if (nf < 0 || nf > 2) throw "Malformed .deeparc file";
+    for (int j = 0; j < nf; ++j) v[j] = take<double>(f);
+    k->focal(nf, v);
+    const int nk = take<int>(f);
+    if (nk < 0 || nk > 2) throw "Malformed .deeparc file";
+    for (int j = 0; j < nk; ++j) v[j] = take<double>(f);
+    k->distrotion(nk, v);
+  }
+  // extrinsics: tx ty tz nr r[nr]; 3 = angle-axis, 4 = quaternion (w,x,y,z),
+  // 9 = column-major rotation matrix (Ceres conventions, DeepArcManager.cc:133-147)
+  for (int i = 0; i < n_ext; ++i) {
+    Extrinsic* e = new Extrinsic();
+    extrinsics_.push_back(e);
+    e->id(i);
+    const double tx = take<double>(f), ty = take<double>(f), tz = take<double>(f);
+    e->translation(tx, ty, tz);
+    const int nr = take<int>(f);
+    if (nr != 3 && nr != 4 && nr != 9) throw "Malformed .deeparc file";
+    double rot[9], aa[3];
+    for (int j = 0; j < nr; ++j) rot[j] = take<double>(f);
+    if (nr == 9) dab::RotationMatrixToAngleAxis(rot, aa);
+    else if (nr == 4) dab::QuaternionToAngleAxis(rot, aa);
+    e->rotation(nr == 3 ? rot : aa);
+  }
+  // points: x y z r g b, colour read as double and truncated (Q2)
+  for (int i = 0; i < n_points; ++i) {
+    const double x = take<double>(f), y = take<double>(f), z = take<double>(f);
+    const double r = take<double>(f), g = take<double>(f), b = take<double>(f);
+    point3d_.push_back(new Point3d(x, y, z, (int)r, (int)g, (int)b));
+  }
+
+  auto need = [](bool ok) {
+    if (!ok) throw "Malformed .deeparc file: index out of range";
+  };
+  if (share_extrinsic_) {
+    // arc a -> extrinsic a (id a); ring r -> extrinsic 0 (r = 0) or n_arc + r - 1 (id r)
+    need(n_intr >= n_arc && n_ext >= 1);
+    for (int a = 0; a < n_arc; ++a) {
+      extrinsics_[a]->id(a);
+      for (int r = 0; r < n_ring; ++r) {
+        Extrinsic* ring = extrinsics_[ringExtrinsicIndex(r, n_arc)];
+        ring->id(r);
+        hemisphere_[a][r] = new Camera(intrinsics_[a], extrinsics_[a], ring);
+      }
+    }
+  } else {
+    // one camera per distinct extrinsic id, first intrinsic seen (std::map order)
+    std::map<int, int> ext_intr;
+    for (ParameterBlock* b : params_) ext_intr.insert({b->extrinsic_id(), b->intrinsic_id()});
+    for (const auto& ei : ext_intr) {
+      need(ei.first >= 0 && ei.first < n_ext && ei.second >= 0 && ei.second < n_intr);
+      camera_.push_back(new Camera(intrinsics_[ei.second], extrinsics_[ei.first]));
+    }
+  }
+  for (ParameterBlock* b : params_) {
+    need(b->intrinsic_id() >= 0 && b->intrinsic_id() < n_intr);
+    need(b->point3d_id() >= 0 && b->point3d_id() < n_points);
+    b->intrinsic(intrinsics_[b->intrinsic_id()]);
+    b->point3d(point3d_[b->point3d_id()]);
+    if (share_extrinsic_) {
+      need(b->pos_arc() < n_ext && b->pos_ring() >= 0 && b->pos_ring() < n_ring);
+      b->arc(extrinsics_[b->pos_arc()]);
+      b->ring(extrinsics_[ringExtrinsicIndex(b->pos_ring(), n_arc)]);
+      b->share_extrinsic(true);
+    } else {
+      need(b->extrinsic_id() >= 0 && b->extrinsic_id() < n_ext);
+      b->extrinsic(extrinsics_[b->extrinsic_id()]);
+      b->share_extrinsic(false);
+    }
+  }
+  return true;
+}
+
+std::vector<double> DeepArcManager::cameraPosition(Extrinsic* e) {
+  // C = -R^T t
+  double R[9];
+  e->rotationMatrix(R);
+  const double* t = e->translation();
+  std::vector<double> c(3);
+  for (int i = 0; i < 3; ++i) c[i] = -(R[3 * i] * t[0] + R[3 * i + 1] * t[1] + R[3 * i + 2] * t[2]);
+  return c;
+}
+
+std::vector<double> DeepArcManager::cameraPosition(Extrinsic* arc, Extrinsic* ring) {
+  // P = R_arc (R_ring X + t_ring) + t_arc = 0  =>  C = -R_ring^T t_ring - R_ring^T R_arc^T t_arc
+  double Ra[9], Rr[9];
+  arc->rotationMatrix(Ra);
+  ring->rotationMatrix(Rr);
+  const double *ta = arc->translation(), *tr = ring->translation();
+  double u[3];  // R_arc^T t_arc (column-major: R^T row i = column i)
+  for (int i = 0; i < 3; ++i) u[i] = Ra[3 * i] * ta[0] + Ra[3 * i + 1] * ta[1] + Ra[3 * i + 2] * ta[2];
+  std::vector<double> c(3);
+  for (int i = 0; i < 3; ++i) {
+    const double a = Rr[3 * i] * tr[0] + Rr[3 * i + 1] * tr[1] + Rr[3 * i + 2] * tr[2];
+    const double b = Rr[3 * i] * u[0] + Rr[3 * i + 1] * u[1] + Rr[3 * i + 2] * u[2];
+    c[i] = -a - b;
+  }
+  return c;
+}
+
+std::vector<std::vector<double> > DeepArcManager::getCameraCenter() {
+  std::vector<std::vector<double> > out;
+  if (!share_extrinsic_) return out;  // ring_size_ = 0: the arc x ring loop is empty (Q6)
+  for (int a = 0; a < arc_size_; ++a)
+    for (int r = 0; r < ring_size_; ++r) {
+      Camera* cam = hemisphere_[a][r];
+      if (r == 0) out.push_back(cameraPosition(cam->arc()));
+      else if (a == 0) out.push_back(cameraPosition(cam->ring()));
+      else out.push_back(cameraPosition(cam->arc(), cam->ring()));
+    }
+  return out;
+}
+
+void DeepArcManager::writePly(std::string filename) {
+  FILE* f = std::fopen(filename.c_str(), "w");
+  if (!f) throw "Cannot write output file";
+  const int n_cam = share_extrinsic_ ? arc_size_ * ring_size_ : (int)camera_.size();
+  std::fprintf(f,
+               "ply\nformat ascii 1.0\nelement vertex %d\nproperty float x\nproperty float y\n"
+               "property float z\nproperty uchar red\nproperty uchar green\nproperty uchar blue\n"
+               "end_header\n",
+               (int)point3d_.size() + n_cam);
+  auto put = [&](const std::vector<double>& c, const char* colour) {
+    for (int i = 0; i < 3; ++i) {
+      fmtg(f, c[i]);
+      std::fputc(' ', f);
+    }
+    std::fputs(colour, f);
+  };
+  if (share_extrinsic_) {
+    // arc-only and ring-only cameras green, composed ones magenta
+    for (int a = 0; a < arc_size_; ++a)
+      for (int r = 0; r < ring_size_; ++r) {
+        Camera* cam = hemisphere_[a][r];
+        if (r == 0) put(cameraPosition(cam->arc()), "0 255 0\n");
+        else if (a == 0) put(cameraPosition(cam->ring()), "0 255 0\n");
+        else put(cameraPosition(cam->arc(), cam->ring()), "255 0 255\n");
+      }
+  } else {
+    for (Camera* cam : camera_) put(cameraPosition(cam->extrinsic()), "0 255 0\n");
+  }
+  for (Point3d* p : point3d_) {
+    for (int i = 0; i < 3; ++i) {
+      fmtg(f, p->position()[i]);
+      std::fputc(' ', f);
+    }
+    std::fprintf(f, "%d %d %d\n", p->r(), p->g(), p->b());
+  }
+  std::fclose(f);
+}
+
+void DeepArcManager::write(std::string filename) {
+  FILE* f = std::fopen(filename.c_str(), "w");
+  if (!f) throw "Cannot write output file";
+  for (int i = 0; i < (int)point3d_.size(); ++i) point3d_[i]->id(i);  // re-index points
+  std::fprintf(f, "0.010000\n%d %d ", (int)params_.size(), (int)intrinsics_.size());
+  if (share_extrinsic_) std::fprintf(f, "%d %d ", arc_size_, ring_size_);
+  else std::fprintf(f, "%d 0 ", (int)camera_.size());
+  std::fprintf(f, "%d\n", (int)point3d_.size());
+  for (ParameterBlock* b : params_) {
+    const int cam = share_extrinsic_ ? b->ring()->id() : b->extrinsic()->id();
+    std::fprintf(f, "%d %d %d ", b->intrinsic()->id(), cam, b->point3d()->id());
+    fmt6(f, b->point2d()->x());
+    std::fputc(' ', f);
+    fmt6(f, b->point2d()->y());
+    std::fputc('\n', f);
+  }
+  for (Intrinsic* k : intrinsics_) {
+    fmt6(f, k->center()[0]);
+    std::fputc(' ', f);
+    fmt6(f, k->center()[1]);
+    std::fprintf(f, " %d", k->focal_size());
+    for (int j = 0; j < k->focal_size(); ++j) {
+      std::fputc(' ', f);
+      fmt6(f, k->focal()[j]);
+    }
+    std::fprintf(f, " %d", k->distrotion_size());
+    for (int j = 0; j < k->distrotion_size(); ++j) {
+      std::fputc(' ', f);
+      fmt6(f, k->distrotion()[j]);
+    }
+    std::fputc('\n', f);
+  }
+  for (Extrinsic* e : extrinsics_) {  // always angle-axis (Q7)
+    for (int j = 0; j < 3; ++j) {
+      fmt6(f, e->translation()[j]);
+      std::fputc(' ', f);
+    }
+    std::fputs("3", f);
+    for (int j = 0; j < 3; ++j) {
+      std::fputc(' ', f);
+      fmt6(f, e->rotation()[j]);
+    }
+    std::fputc('\n', f);
+  }
+  for (Point3d* p : point3d_) {
+    for (int j = 0; j < 3; ++j) {
+      fmt6(f, p->position()[j]);
+      std::fputc(' ', f);
+    }
+    std::fprintf(f, "%d %d %d\n", p->r(), p->g(), p->b());
+  }
+  std::fclose(f);
+}
+
+void DeepArcManager::filterPoint3d(double error_boundary, double* hemisphere_center, double hemisphere_radius) {
+  // device: residual per observation, the mse test, the empty-point and hemisphere tests
+  std::vector<uint8_t> keep_obs(params_.size(), 1), keep_pt(point3d_.size(), 1);
+  if (!params_.empty()) {
+    DabScene scene;
+    scene.build(*this, false);
+    DabHandle dh;
+    dab_check(dab_set_problem(dh.h, &scene.problem));
+    dab_check(dab_filter(dh.h, error_boundary, hemisphere_center, hemisphere_radius, keep_obs.data(),
+                         keep_pt.data(), nullptr, nullptr));
+  } else {
+    std::fill(keep_pt.begin(), keep_pt.end(), 0);  // no observations: every point is empty
+  }
+  // host: drop blocks, then points, preserving the survivors' order (std::remove_if)
+  size_t w = 0;
+  for (size_t i = 0; i < params_.size(); ++i) {
+    if (keep_obs[i]) params_[w++] = params_[i];
+    else delete params_[i];  // unlinks from its point
+  }
+  params_.resize(w);
+  w = 0;
+  for (size_t i = 0; i < point3d_.size(); ++i) {
+    if (keep_pt[i]) {
+      point3d_[w++] = point3d_[i];
+    } else {
+      for (ParameterBlock* b : point3d_[i]->total_link()) b->point3d(nullptr);  // none remain
+      delete point3d_[i];
+    }
+  }
+  point3d_.resize(w);
+}

@@ -1,0 +1,112 @@
+// Geometry.hh — the reference's parameter containers (src/Point/*.hh, src/Camera/*.hh)
+// with the same public accessors, so host code written against the reference compiles
+// against this library. Storage layout matches the reference: every block is a small
+// double array that the solver writes back in place (sfm.cc:47-48 semantics).
+#pragma once
+#include <algorithm>
+#include <set>
+
+class ParameterBlock;
+
+// Point/Point2d.hh
+class Point2d {
+ public:
+  Point2d(double x, double y) : x_(x), y_(y) {}
+  double x() { return x_; }
+  double y() { return y_; }
+
+ private:
+  double x_, y_;
+};
+
+// Point/Point3d.hh. Colour is stored as int: the loader reads doubles and truncates
+// (quirk Q2, DeepArcManager.cc:155-160).
+class Point3d {
+ public:
+  Point3d(double x, double y, double z, int r = 255, int g = 255, int b = 255)
+      : require_remove_(false), r_(r), g_(g), b_(b), id_(-1), position_{x, y, z} {}
+  int r() { return r_; }
+  int g() { return g_; }
+  int b() { return b_; }
+  int id() { return id_; }
+  void id(int v) { id_ = v; }
+  double* position() { return position_; }
+  void require_remove(bool v) { require_remove_ = v; }
+  bool require_remove() { return require_remove_; }
+  // observation links (ParameterBlock::point3d keeps them current)
+  void link(ParameterBlock* b) { blocks_.insert(b); }
+  void unlink(ParameterBlock* b) { blocks_.erase(b); }
+  std::set<ParameterBlock*> total_link() { return blocks_; }
+  bool empty() { return blocks_.empty(); }
+
+ private:
+  bool require_remove_;
+  int r_, g_, b_, id_;
+  double position_[3];
+  std::set<ParameterBlock*> blocks_;
+};
+
+// Camera/Intrinsic.hh. center() takes ints: the principal point is truncated on load
+// (quirk Q1, Intrinsic.hh:24-27).
+class Intrinsic {
+ public:
+  double* focal() { return focal_; }
+  double* center() { return center_; }
+  double* distrotion() { return distortion_; }
+  int focal_size() { return focal_size_; }
+  int distrotion_size() { return distortion_size_; }
+  int id() { return id_; }
+  void id(int v) { id_ = v; }
+  void focal(int n, const double* f) {
+    focal_size_ = n;
+    std::copy(f, f + n, focal_);
+  }
+  void distrotion(int n, const double* k) {
+    distortion_size_ = n;
+    std::copy(k, k + n, distortion_);
+  }
+  void center(int cx, int cy) {
+    center_[0] = cx;
+    center_[1] = cy;
+  }
+
+ private:
+  double focal_[2] = {0, 0}, center_[2] = {0, 0}, distortion_[2] = {0, 0};
+  int focal_size_ = 0, distortion_size_ = 0, id_ = -1;
+};
+
+// Camera/Extrinsic.hh: angle-axis rotation + translation, P = R(w) X + t.
+class Extrinsic {
+ public:
+  double* rotation() { return rotation_; }
+  double* translation() { return translation_; }
+  int id() { return id_; }
+  void id(int v) { id_ = v; }
+  void rotation(const double* w) { std::copy(w, w + 3, rotation_); }
+  void translation(double x, double y, double z) {
+    translation_[0] = x;
+    translation_[1] = y;
+    translation_[2] = z;
+  }
+  // R(w) column-major (ceres::AngleAxisToRotationMatrix, Extrinsic.hh:12-17)
+  void rotationMatrix(double R[9]);
+
+ private:
+  double rotation_[3] = {0, 0, 0}, translation_[3] = {0, 0, 0};
+  int id_ = -1;
+};
+
+// Camera/Camera.hh
+class Camera {
+ public:
+  Camera(Intrinsic* k, Extrinsic* e) : intrinsic_(k), extrinsic_(e) {}
+  Camera(Intrinsic* k, Extrinsic* arc, Extrinsic* ring) : intrinsic_(k), arc_(arc), ring_(ring) {}
+  Intrinsic* intrinsic() { return intrinsic_; }
+  Extrinsic* extrinsic() { return extrinsic_; }
+  Extrinsic* arc() { return arc_; }
+  Extrinsic* ring() { return ring_; }
+
+ private:
+  Intrinsic* intrinsic_ = nullptr;
+  Extrinsic *extrinsic_ = nullptr, *arc_ = nullptr, *ring_ = nullptr;
+};

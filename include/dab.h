@@ -16,6 +16,8 @@
  *   ceres::Solve + Summary::FullReport  sfm.cc:72-74     dab_solve + dab_summary
  *   SnavelyReprojectionError::operator()(double)         dab_eval_residuals
  *     DeepArcManager.cc:335-346 (filterPoint3d)
+ *   DeepArcManager::filterPoint3d DeepArcManager.cc:     dab_filter (device residuals +
+ *     332-424                                              drop masks)
  *   DynamicAutoDiffCostFunction::Evaluate (jacobians)    dab_eval_jacobians
  *     snavely_reprojection_error.hh:11-14
  *
@@ -198,6 +200,19 @@ int dab_get_parameters(dab_handle* h, double* points, double* ext);
  * cost: 0.5 * sum r^2. Any pointer may be NULL. */
 int dab_eval_residuals(dab_handle* h, double* residuals, double* cost);
 int dab_eval_jacobians(dab_handle* h, double* residuals, double* jacobians);
+
+/* DeepArcManager::filterPoint3d (DeepArcManager.cc:332-424) on the device, at the
+ * parameters currently on the handle (after dab_solve: the optimised ones):
+ *   1. an observation is dropped when mse = (r0^2 + r1^2) / 2 < error_boundary
+ *      (quirk Q4: the *small*-error ones, exactly as the reference);
+ *   2. a point with no remaining observation is dropped (Point3d::empty);
+ *   3. a remaining point is dropped when |X - center|^2 > radius / 2 (radius is the
+ *      fitted *squared* radius, hemisphere_radius.hh:26), and so are its observations.
+ * obs_keep[num_obs] and point_keep[num_points] (caller order; 1 = kept) may be NULL;
+ * unreferenced points are reported as dropped. Counts of kept items in *n_obs_kept /
+ * *n_points_kept (nullable). The handle's problem is not modified. */
+int dab_filter(dab_handle* h, double error_boundary, const double center[3], double radius,
+               uint8_t* obs_keep, uint8_t* point_keep, int32_t* n_obs_kept, int32_t* n_points_kept);
 
 /* Dense SPD solve A x = b on the handle's device with the library's blocked Cholesky (the
  * reduced-camera-system factorisation of DAB_LINEAR_SOLVER_EXPLICIT_SCHUR; Eigen LLT in

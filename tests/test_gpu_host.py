@@ -1,0 +1,122 @@
+"""Host adapter on the GPU: solve() / filterPoint3d / the sfm.cc main() loop through the
+C++ DeepArcManager over libdab, against the oracle restatement (oracle/deeparc_ref.py over
+the C oracle's LM). Tolerances: per-iteration LM cost 1e-9 relative, parameters 1e-7;
+filter masks exact (identical survivors); pipeline counts exact, parameters 1e-6."""
+import os
+
+import numpy as np
+import pytest
+
+from golden_util import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def host(pkg):
+    import importlib
+    return importlib.import_module(pkg.__name__ + ".host_api")
+
+
+@pytest.fixture(scope="module")
+def ref(orc):
+    import deeparc_ref
+    return deeparc_ref
+
+
+def scene_params(ref_scene):
+    pts = np.array([p["X"] for p in ref_scene["points"]]).reshape(-1, 3)
+    ext = np.array([e["w"] + e["t"] for e in ref_scene["ext"]]).reshape(-1, 6)
+    return pts, ext
+
+
+@pytest.mark.parametrize("kind", ["rig", "bal"])
+@pytest.mark.parametrize("freeze", [False, True])
+def test_solve_matches_oracle(pkg, host, ref, gpu, kind, freeze):
+    path = os.path.join(GOLDEN, "tiny_%s.deeparc" % kind)
+    m = host.DeepArcManager()
+    m.read(path)
+    g = host.solve(m, max_iteration=30, freeze_camera=freeze)
+    s = ref.read_deeparc(path)
+    o = ref.solve_scene(pkg, s, max_iteration=30, freeze_camera=freeze)
+    assert g["termination"] == o["termination"] and g["num_iterations"] == o["num_iterations"]
+    for a, b in zip(g["iterations"], o["iterations"]):
+        assert abs(a["cost"] - b["cost"]) <= 1e-9 * abs(b["cost"]), (a, b)
+    pts, ext = scene_params(s)
+    xyz, _ = m.points()
+    cams, _ = m.cameras()
+    np.testing.assert_allclose(xyz, pts, rtol=0, atol=1e-7)
+    np.testing.assert_allclose(cams, ext, rtol=0, atol=1e-7)
+
+
+@pytest.mark.parametrize("kind", ["rig", "bal"])
+@pytest.mark.parametrize("bound", [5.0, 0.5, 1e9, -1.0])
+def test_filter_matches_oracle(pkg, host, ref, gpu, kind, bound, tmp_path):
+    path = os.path.join(GOLDEN, "tiny_%s.deeparc" % kind)
+    m = host.DeepArcManager()
+    m.read(path)
+    host.solve(m, max_iteration=10)
+    m.write(str(tmp_path / "solved.deeparc"))
+    # the oracle filters the same parameter values (read back at full precision)
+    s = ref.read_deeparc(path)
+    xyz, _ = m.points()
+    cams, _ = m.cameras()
+    for i, p in enumerate(s["points"]):
+        p["X"] = list(xyz[i])
+    for i, e in enumerate(s["ext"]):
+        e["w"], e["t"] = list(cams[i, :3]), list(cams[i, 3:])
+    center, radius = ref.hemisphere_fit(ref.camera_centers(s))
+    if kind == "bal":
+        center, radius = [0.0, 0.0, 0.0], 1e6  # no centres (Q6): keep the cut inactive
+    m.filterPoint3d(bound, center, radius)
+    ref.filter_point3d(pkg, s, bound, center, radius)
+    a, r, pi, xy = m.blocks()
+    assert len(a) == len(s["blocks"])
+    np.testing.assert_array_equal(a, [b[0] for b in s["blocks"]])
+    np.testing.assert_array_equal(r, [b[1] for b in s["blocks"]])
+    np.testing.assert_array_equal(pi, [b[5] for b in s["blocks"]])
+    np.testing.assert_array_equal(xy, np.array([[b[3], b[4]] for b in s["blocks"]]).reshape(-1, 2))
+    xyz2, _ = m.points()
+    np.testing.assert_array_equal(xyz2, np.array([p["X"] for p in s["points"]]).reshape(-1, 3))
+    if bound == 1e9:
+        assert len(a) == 0 and xyz2.shape[0] == 0  # everything has mse < 1e9 (quirk Q4)
+    if bound == -1.0:
+        assert len(a) > 0
+
+
+def test_pipeline_matches_oracle(pkg, host, ref, gpu, tmp_path):
+    """sfm.cc main() on a small synthetic rig: same rounds, survivors and parameters."""
+    import gen_deeparc_fixtures as gen
+    prob = pkg.synth(kind=1, num_arcs=4, num_rings=8, num_points=600, obs_per_point=6, seed=81,
+                     pixel_noise=3.0)
+    path = tmp_path / "rig.deeparc"
+    path.write_text(gen.problem_to_deeparc(prob, True, 4, 8, [3], np.random.default_rng(0)))
+    out = tmp_path / "out.deeparc"
+    rep = host.run_pipeline(str(path), str(out), max_iteration=50)
+    s, orep = ref.run_pipeline(pkg, str(path), max_iteration=50)
+    assert rep["rounds"] == orep["rounds"]
+    assert (rep["blocks"], rep["points"]) == (orep["blocks"], orep["points"])
+    np.testing.assert_allclose(rep["hemisphere_center"], orep["hemisphere_center"], rtol=1e-9, atol=1e-12)
+    m = host.DeepArcManager()
+    m.read(str(out))
+    xyz, _ = m.points()
+    np.testing.assert_allclose(xyz, np.array([p["X"] for p in s["points"]]).reshape(-1, 3), rtol=0, atol=2e-6)
+
+
+def test_pipeline_config1_full_size(pkg, host, gpu, tmp_path):
+    """BASELINE config 1 shape (rig 8 x 36, 20k points, m = 8) end to end on the GPU:
+    properties only (the CPU oracle takes minutes at this size)."""
+    import gen_deeparc_fixtures as gen
+    prob = pkg.synth(**pkg.CONFIGS["c1_rig_8x36"])
+    path = tmp_path / "c1.deeparc"
+    path.write_text(gen.problem_to_deeparc(prob, True, 8, 36, [3, 4, 9], np.random.default_rng(1)))
+    out = tmp_path / "c1_out.deeparc"
+    rep = host.run_pipeline(str(path), str(out), ply_prefix=str(tmp_path / "c1_"), max_iteration=100)
+    assert rep["rounds"] >= 1
+    m = host.DeepArcManager()
+    m.read(str(out))
+    sz = m.sizes()
+    assert (sz["blocks"], sz["points"]) == (rep["blocks"], rep["points"])
+    assert os.path.exists(str(tmp_path / "c1_clear.ply"))
+    # the hemisphere of a rig on a unit hemisphere: squared radius near 1
+    assert 0.5 < rep["hemisphere_radius"] < 2.0
