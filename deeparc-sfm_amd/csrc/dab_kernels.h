@@ -8,7 +8,15 @@ namespace dab {
 
 constexpr int kCamTab = 32;   // doubles per extrinsic table: R(9) t(3) Rd(9) Jd(9) pad(2)
 constexpr int kIntr = 8;      // doubles per intrinsic: cx cy fx fy k0 k1 0 0
-constexpr int kYRec = 18;     // doubles per Y_e record (6x3)
+constexpr int kYRec = 18;     // elements per Y_e record (6x3), fp64 or fp32 (pcg_fp32)
+
+// Y records of one LM step, in both layouts: cm = camera-major positions (streams for the
+// camera-side passes), pm = point-major entries (streams for the point-side passes).
+struct YBufs {
+  void* cm;
+  void* pm;
+  bool f32;
+};
 constexpr int kRedBlock = 256;
 constexpr int kChunk = 4096;  // max entries per reduction chunk (C3: one chunk per camera)
 constexpr int kSlotBit = 1 << 30;  // cm_idx.w flag: the entry is the ring (slot 1) camera
@@ -36,6 +44,7 @@ struct DevView {
   const int* ent_pt;        // [NE]
   const int* ent_pos;       // [NE] camera-major position
   const int* cm_pt;         // [NE] point of the entry at camera-major position
+  const int* cm_ent;        // [NE] point-major entry index of the camera-major position
   const int* ext_col;       // [E] free camera index or -1
   const double* intr;       // [NI][kIntr]
 };
@@ -85,9 +94,9 @@ struct StepScalars {
 // 12 22), q = L^-1 (s g) -> q[NP][4]
 void launch_point_factor(hipStream_t s, const DevView& v, const double* V, const double* g,
                          const double* scale_p, StepScalars sc, double* PU, double* q, int* fail);
-// entry Y_pos = (s_c ∘ Jc^T Jp) PU_p -> Y[pos][kYRec] (re-evaluated, camera-major)
+// entry Y = (s_c ∘ Jc^T Jp) PU_p (re-evaluated) -> Y.cm[pos], Y.pm[e]
 void launch_entry_y(hipStream_t s, const DevView& v, const double* points, const double* camtab,
-                    const double* scale_c, const double* PU, double* Y);
+                    const double* scale_c, const double* PU, YBufs Y);
 // S blocks (Y part): packed[blk][36] = - sum_pairs Y_row Y_col^T (pairs hold positions)
 void launch_s_blocks(hipStream_t s, int nblk, const int* blk_pair_beg, const int2* pairs,
                      const double* Y, double* packed);
@@ -102,8 +111,8 @@ void launch_s_unpack(hipStream_t s, int NC, int nblk, const int2* blk_cam, const
                      const double* Ucross /*[ncross][36]*/, const double* scale_c, StepScalars sc,
                      const double* ybc /*[NC][6]*/, double* S, int lds);
 // delta_p = -PU (q - sum_e Y_e^T y_c) -> dp[3][NP]
-void launch_backsub(hipStream_t s, const DevView& v, const double* PU, const double* q,
-                    const double* Y, const double* yc, const double* scale_p, double* delta_p);
+void launch_backsub(hipStream_t s, const DevView& v, const double* PU, const double* q, YBufs Y,
+                    const double* yc, double* delta_p);
 // x_c = x + delta for points; partial[grid][2] = {sum (x-xc)^2, sum xc^2}
 void launch_axpy_points(hipStream_t s, int NP, const double* x, const double* d, double* xc,
                         double* partial, int grid);
@@ -128,7 +137,7 @@ struct PcgState {
 // per chunk: 21 upper of sum_runs Z Z^T (Z = sum of the run's Y; run[i] = length of the
 // same-point run starting at position i, 0 inside a run) | 6 of -sum Y q_p -> partial[chunk][27]
 void launch_pcg_diag_rhs_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
-                                 const int* run, const double* Y, const double* q, double* partial);
+                                 const int* run, YBufs Y, const double* q, double* partial);
 // per camera: Ad = s U s + D^2 [NC][36], Minv = (Ad - sum Y Y^T)^-1 [NC][36],
 // b = s g_c - sum Y q, x = 0, r = b; fail[0] |= 1 if a block is not positive definite
 void launch_pcg_setup(hipStream_t s, int NC, const double* ug, const double* scale_c, StepScalars sc,
@@ -140,9 +149,8 @@ void launch_pcg_init(hipStream_t s, int n, const double* bvec, const int* fail, 
 void launch_pcg_direction(hipStream_t s, int NC, const double* Minv, const double* r, double* z, double* p,
                           PcgState* st);
 // the two Y passes of S vec: t[NP][4], partial[chunk][6] (= -sum Y t per chunk)
-void launch_pcg_matvec_passes(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
-                              const double* Y, const double* vec, double* t, double* partial,
-                              const PcgState* st);
+void launch_pcg_matvec_passes(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, YBufs Y,
+                              const double* vec, double* t, double* partial, const PcgState* st);
 // mode 0: q = S p, alpha, x, r, Q-test; 1: q = S p, alpha, x; 2: r = b - S x, Q-test.
 // w[NC][6] = all-reduced Y part of the product; xptr/xlist: per-camera CSR of cross blocks
 // (code = 2*k + (camera is c1)), nullable when there are none.

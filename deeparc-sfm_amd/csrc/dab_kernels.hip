@@ -923,12 +923,15 @@ void launch_point_factor(hipStream_t s, const DevView& v, const double* V, const
   k_point_factor<<<grid_for(v.NP, 256, 1 << 20), 256, 0, s>>>(v, V, g, scale_p, sc, L, q, fail);
 }
 
-// Y_pos = (s_c ∘ Jc^T Jp) PU_p for the entry at camera-major position pos, re-evaluated
-// from the camera-major input copy: contiguous inputs, contiguous 144 B record writes.
+// Y = (s_c ∘ Jc^T Jp) PU_p for the entry at camera-major position pos, re-evaluated from
+// the camera-major input copy, stored in both layouts (camera-major at pos, point-major at
+// the entry's point-major index) in the step's precision.
+template <class YT>
 __global__ __launch_bounds__(256) void k_entry_y(DevView v, const double* __restrict__ points,
                                                  const double* __restrict__ camtab,
                                                  const double* __restrict__ scc,
-                                                 const double* __restrict__ PU, double* __restrict__ Y) {
+                                                 const double* __restrict__ PU, YT* __restrict__ Ycm,
+                                                 YT* __restrict__ Ypm) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= v.NE) return;
   int4 id = v.cm_idx[i];
@@ -953,15 +956,18 @@ __global__ __launch_bounds__(256) void k_entry_y(DevView v, const double* __rest
     y[3 * a + 1] = sa * (w0 * u01 + w1 * u11);
     y[3 * a + 2] = sa * (w0 * u02 + w1 * u12 + w2 * u22);
   }
-  double2* out = reinterpret_cast<double2*>(Y + (size_t)kYRec * i);
-#pragma unroll
-  for (int k = 0; k < 9; ++k) out[k] = make_double2(y[2 * k], y[2 * k + 1]);
+  store_yrec(Ycm, i, y);
+  store_yrec(Ypm, v.cm_ent[i], y);
 }
 
 void launch_entry_y(hipStream_t s, const DevView& v, const double* points, const double* camtab,
-                    const double* scale_c, const double* PU, double* Y) {
+                    const double* scale_c, const double* PU, YBufs Y) {
   if (v.NE <= 0) return;
-  k_entry_y<<<grid_for(v.NE, 256, 1 << 20), 256, 0, s>>>(v, points, camtab, scale_c, PU, Y);
+  const int g = grid_for(v.NE, 256, 1 << 20);
+  if (Y.f32)
+    k_entry_y<float><<<g, 256, 0, s>>>(v, points, camtab, scale_c, PU, (float*)Y.cm, (float*)Y.pm);
+  else
+    k_entry_y<double><<<g, 256, 0, s>>>(v, points, camtab, scale_c, PU, (double*)Y.cm, (double*)Y.pm);
 }
 
 // one wave per S block; lane (a,b) < 36 accumulates -sum Y_row[a,:] . Y_col[b,:]
@@ -1062,12 +1068,11 @@ void launch_s_unpack(hipStream_t s, int NC, int nblk, const int2* blk_cam, const
     k_s_cross<<<grid_for(ncross * 36, 256, 1 << 20), 256, 0, s>>>(ncross, cross_cam, Ucross, scale_c, S, lds);
 }
 
-__global__ __launch_bounds__(256) void k_backsub(DevView v, const double* __restrict__ L,
-                                                 const double* __restrict__ q,
-                                                 const double* __restrict__ Y,
-                                                 const double* __restrict__ yc,
-                                                 const double* __restrict__ sp,
-                                                 double* __restrict__ dp) {
+// delta_p = -PU (q - sum_e Y_e^T y_c), the point's records read contiguously (point-major)
+template <class YT>
+__global__ __launch_bounds__(256) void k_backsub(DevView v, const double* __restrict__ PU,
+                                                 const double* __restrict__ q, const YT* __restrict__ Ypm,
+                                                 const double* __restrict__ yc, double* __restrict__ dp) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= v.NP) return;
   const size_t NPs = (size_t)v.NP;
@@ -1076,7 +1081,8 @@ __global__ __launch_bounds__(256) void k_backsub(DevView v, const double* __rest
   if (yc) {
     for (int e = v.pt_ent_ptr[p]; e < v.pt_ent_ptr[p + 1]; ++e) {
       const int c = v.ent_cam[e];
-      const double* y = Y + (size_t)kYRec * v.ent_pos[e];
+      double y[18];
+      load_yrec(Ypm, e, y);
 #pragma unroll
       for (int a = 0; a < 6; ++a) {
         const double ycv = yc[6 * c + a];
@@ -1086,17 +1092,19 @@ __global__ __launch_bounds__(256) void k_backsub(DevView v, const double* __rest
       }
     }
   }
-  // delta_p = -diag(s) L^-T (q - sum_e Y_e^T y_c) = -PU (...)   (step = -y, Ceres)
-  const double* pu = L + 6 * (size_t)p;
+  // step = -y (Ceres solves J y = r then negates); delta = step * s = -PU (...)
+  const double* pu = PU + 6 * (size_t)p;
   dp[p] = -(pu[0] * r0 + pu[1] * r1 + pu[2] * r2);
   dp[NPs + p] = -(pu[3] * r1 + pu[4] * r2);
   dp[2 * NPs + p] = -(pu[5] * r2);
 }
 
-void launch_backsub(hipStream_t s, const DevView& v, const double* L, const double* q, const double* Y,
-                    const double* yc, const double* scale_p, double* delta_p) {
+void launch_backsub(hipStream_t s, const DevView& v, const double* PU, const double* q, YBufs Y,
+                    const double* yc, double* delta_p) {
   if (v.NP <= 0) return;
-  k_backsub<<<grid_for(v.NP, 256, 1 << 20), 256, 0, s>>>(v, L, q, Y, yc, scale_p, delta_p);
+  const int g = grid_for(v.NP, 256, 1 << 20);
+  if (Y.f32) k_backsub<float><<<g, 256, 0, s>>>(v, PU, q, (const float*)Y.pm, yc, delta_p);
+  else k_backsub<double><<<g, 256, 0, s>>>(v, PU, q, (const double*)Y.pm, yc, delta_p);
 }
 
 __global__ __launch_bounds__(256) void k_axpy_points(int NP, const double* __restrict__ x,

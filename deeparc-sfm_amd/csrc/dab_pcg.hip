@@ -57,19 +57,10 @@ __device__ __forceinline__ int up6(int a, int b) { return a * 6 - (a * (a - 1)) 
 
 // per chunk of camera-major positions: 21 upper entries of sum Z Z^T over same-point runs
 // (the exact diagonal S block) | 6 of -sum Y q_p
-__device__ __forceinline__ void load_y(const double* __restrict__ Y, int i, double (&y)[18]) {
-  const double2* y2 = reinterpret_cast<const double2*>(Y + (size_t)kYRec * i);
-#pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    const double2 t = y2[k];
-    y[2 * k] = t.x;
-    y[2 * k + 1] = t.y;
-  }
-}
-
+template <class YT>
 __global__ __launch_bounds__(256) void k_pcg_diag_rhs_partial(DevView v, const int* __restrict__ chunk_beg,
                                                               const int* __restrict__ run,
-                                                              const double* __restrict__ Y,
+                                                              const YT* __restrict__ Y,
                                                               const double* __restrict__ q,
                                                               double* __restrict__ partial) {
   const int c = blockIdx.x;
@@ -82,14 +73,14 @@ __global__ __launch_bounds__(256) void k_pcg_diag_rhs_partial(DevView v, const i
     const double2 qa = reinterpret_cast<const double2*>(q)[2 * (size_t)p];
     const double q2 = q[4 * (size_t)p + 2];
     double y[18];
-    load_y(Y, i, y);
+    load_yrec(Y, i, y);
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[21 + a] -= y[3 * a] * qa.x + y[3 * a + 1] * qa.y + y[3 * a + 2] * q2;
     const int len = run[i];
     if (len == 0) continue;
     for (int j = 1; j < len; ++j) {  // rare (rig): fold the run into Z
       double w[18];
-      load_y(Y, i + j, w);
+      load_yrec(Y, i + j, w);
 #pragma unroll
       for (int k = 0; k < 18; ++k) y[k] += w[k];
     }
@@ -273,8 +264,9 @@ __global__ __launch_bounds__(kOneWG) void k_pcg_direction(int NC, const double* 
   }
 }
 
-// point pass: t_p = sum_e Y_e^T v_cam(e) -> t[NP][4]
-__global__ __launch_bounds__(256) void k_pcg_point_pass(DevView v, const double* __restrict__ Y,
+// point pass: t_p = sum_e Y_e^T v_cam(e) -> t[NP][4] (point-major records, contiguous)
+template <class YT>
+__global__ __launch_bounds__(256) void k_pcg_point_pass(DevView v, const YT* __restrict__ Ypm,
                                                         const double* __restrict__ vec,
                                                         double* __restrict__ t, const PcgState* st) {
   if (st->status != kPcgRunning) return;
@@ -283,15 +275,10 @@ __global__ __launch_bounds__(256) void k_pcg_point_pass(DevView v, const double*
   double t0 = 0.0, t1 = 0.0, t2 = 0.0;
   for (int e = v.pt_ent_ptr[p]; e < v.pt_ent_ptr[p + 1]; ++e) {
     const int c = v.ent_cam[e];
-    const double2* y2 = reinterpret_cast<const double2*>(Y + (size_t)kYRec * v.ent_pos[e]);
+    double y[18];
+    load_yrec(Ypm, e, y);
     const double2* v2 = reinterpret_cast<const double2*>(vec + 6 * (size_t)c);
-    double y[18], vc[6];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-      const double2 w = y2[k];
-      y[2 * k] = w.x;
-      y[2 * k + 1] = w.y;
-    }
+    double vc[6];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const double2 w = v2[k];
@@ -310,8 +297,9 @@ __global__ __launch_bounds__(256) void k_pcg_point_pass(DevView v, const double*
 }
 
 // camera pass: per chunk of positions -sum Y_pos t_pt(pos) -> partial[chunk][6]
+template <class YT>
 __global__ __launch_bounds__(256) void k_pcg_cam_pass(DevView v, const int* __restrict__ chunk_beg,
-                                                      const double* __restrict__ Y, const double* __restrict__ t,
+                                                      const YT* __restrict__ Y, const double* __restrict__ t,
                                                       double* __restrict__ partial, const PcgState* st) {
   if (st->status != kPcgRunning) return;
   const int c = blockIdx.x;
@@ -321,14 +309,8 @@ __global__ __launch_bounds__(256) void k_pcg_cam_pass(DevView v, const int* __re
     const int p = v.cm_pt[i];
     const double2 ta = reinterpret_cast<const double2*>(t)[2 * (size_t)p];
     const double t2 = t[4 * (size_t)p + 2];
-    const double2* y2 = reinterpret_cast<const double2*>(Y + (size_t)kYRec * i);
     double y[18];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-      const double2 w = y2[k];
-      y[2 * k] = w.x;
-      y[2 * k + 1] = w.y;
-    }
+    load_yrec(Y, i, y);
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[a] -= y[3 * a] * ta.x + y[3 * a + 1] * ta.y + y[3 * a + 2] * t2;
   }
@@ -468,9 +450,13 @@ __global__ __launch_bounds__(kOneWG) void k_pcg_update(int NC, int mode, const d
 // ---- launchers -------------------------------------------------------------------------
 
 void launch_pcg_diag_rhs_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
-                                 const int* run, const double* Y, const double* q, double* partial) {
+                                 const int* run, YBufs Y, const double* q, double* partial) {
   if (nchunk <= 0) return;
-  k_pcg_diag_rhs_partial<<<nchunk, kRedBlock, 0, s>>>(v, chunk_beg, run, Y, q, partial);
+  if (Y.f32)
+    k_pcg_diag_rhs_partial<float><<<nchunk, kRedBlock, 0, s>>>(v, chunk_beg, run, (const float*)Y.cm, q, partial);
+  else
+    k_pcg_diag_rhs_partial<double><<<nchunk, kRedBlock, 0, s>>>(v, chunk_beg, run, (const double*)Y.cm, q,
+                                                                partial);
 }
 
 void launch_pcg_setup(hipStream_t s, int NC, const double* ug, const double* scale_c, StepScalars sc,
@@ -490,11 +476,18 @@ void launch_pcg_direction(hipStream_t s, int NC, const double* Minv, const doubl
   k_pcg_direction<<<1, kOneWG, 0, s>>>(NC, Minv, r, z, p, st);
 }
 
-void launch_pcg_matvec_passes(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
-                              const double* Y, const double* vec, double* t, double* partial,
-                              const PcgState* st) {
-  if (v.NP > 0) k_pcg_point_pass<<<grid_for(v.NP, 256, 1 << 20), 256, 0, s>>>(v, Y, vec, t, st);
-  if (nchunk > 0) k_pcg_cam_pass<<<nchunk, kRedBlock, 0, s>>>(v, chunk_beg, Y, t, partial, st);
+void launch_pcg_matvec_passes(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, YBufs Y,
+                              const double* vec, double* t, double* partial, const PcgState* st) {
+  const int g = grid_for(v.NP, 256, 1 << 20);
+  if (Y.f32) {
+    if (v.NP > 0) k_pcg_point_pass<float><<<g, 256, 0, s>>>(v, (const float*)Y.pm, vec, t, st);
+    if (nchunk > 0)
+      k_pcg_cam_pass<float><<<nchunk, kRedBlock, 0, s>>>(v, chunk_beg, (const float*)Y.cm, t, partial, st);
+  } else {
+    if (v.NP > 0) k_pcg_point_pass<double><<<g, 256, 0, s>>>(v, (const double*)Y.pm, vec, t, st);
+    if (nchunk > 0)
+      k_pcg_cam_pass<double><<<nchunk, kRedBlock, 0, s>>>(v, chunk_beg, (const double*)Y.cm, t, partial, st);
+  }
 }
 
 void launch_pcg_update(hipStream_t s, int NC, int mode, const double* Ad, const double* w, const int* xptr,

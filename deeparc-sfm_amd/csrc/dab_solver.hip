@@ -152,7 +152,9 @@ struct dab_handle {
   double* d_r = nullptr;
   double* d_Jfull = nullptr;  // parity API only (lazily allocated)
   double *d_V = nullptr, *d_g = nullptr, *d_scale_p = nullptr, *d_scale_c = nullptr;
-  double *d_L = nullptr, *d_q = nullptr, *d_Y = nullptr;
+  double *d_L = nullptr, *d_q = nullptr, *d_Y = nullptr, *d_Yp = nullptr;  // Y camera-/point-major
+  float *d_Y32c = nullptr, *d_Y32p = nullptr;                                 // pcg_fp32 (lazy)
+  int* d_cm_ent = nullptr;
   double* d_camred = nullptr;  // [Ucc NC*21 | gc NC*6 | Ux ncross*36] (all-reduced)
   double* d_partial = nullptr; // chunk partials (max of chunk counts * 36)
   double* d_spack = nullptr;   // [packed nblk*36 | ybc NC*6] (all-reduced)
@@ -640,6 +642,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   CHECK_RC(upload(&h->d_ext_col, d, h->ext_col, s));
   CHECK_RC(upload(&h->d_ent_pos, d, ent_pos, s));
   CHECK_RC(upload(&h->d_cm_pt, d, cm_pt, s));
+  CHECK_RC(upload(&h->d_cm_ent, d, cam_ent, s));
   CHECK_RC(upload(&h->d_cm_idx, d, cm_idx, s));
   CHECK_RC(upload(&h->d_cm_xy, d, cm_xy, s));
   CHECK_RC(upload(&h->d_chunk_beg, d, chunk_beg, s));
@@ -668,6 +671,8 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   CHECK_RC(d.alloc(&h->d_L, (size_t)6 * NP));
   CHECK_RC(d.alloc(&h->d_q, (size_t)4 * NP));
   CHECK_RC(d.alloc(&h->d_Y, (size_t)kYRec * NE));
+  CHECK_RC(d.alloc(&h->d_Yp, (size_t)kYRec * NE));
+  h->d_Y32c = h->d_Y32p = nullptr;
   CHECK_RC(d.alloc(&h->d_camred, h->camred_count()));
   const size_t npart = std::max<size_t>({(size_t)h->nchunk * 27, (size_t)h->nxchunk * 36, (size_t)h->nchunk * 6, 16});
   CHECK_RC(d.alloc(&h->d_partial, npart));
@@ -711,6 +716,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   v.ent_pt = h->d_ent_pt;
   v.ent_pos = h->d_ent_pos;
   v.cm_pt = h->d_cm_pt;
+  v.cm_ent = h->d_cm_ent;
   v.ext_col = h->d_ext_col;
   v.intr = h->d_intr;
   h->have_problem = true;
@@ -845,9 +851,9 @@ static int build_pcg_buffers(dab_handle* h) {
 }
 
 // S vec (Y part) -> d_pcg_w, all-reduced across ranks
-static int pcg_matvec(dab_handle* h, const double* vec) {
+static int pcg_matvec(dab_handle* h, YBufs yb, const double* vec) {
   hipStream_t s = h->stream;
-  launch_pcg_matvec_passes(s, h->view, h->nchunk, h->d_chunk_beg, h->d_Y, vec, h->d_pcg_t, h->d_partial,
+  launch_pcg_matvec_passes(s, h->view, h->nchunk, h->d_chunk_beg, yb, vec, h->d_pcg_t, h->d_partial,
                            h->d_pcg_state);
   launch_seg_final(s, h->NC, 6, h->d_seg_chunk, h->d_partial, h->d_pcg_w);
   CHECK_RC(h->allreduce(h->d_pcg_w, (size_t)6 * h->NC, ncclSum));
@@ -857,11 +863,11 @@ static int pcg_matvec(dab_handle* h, const double* vec) {
 // Solve S y = b (scaled, damped reduced camera system) into d_yc with preconditioned CG.
 // Requires d_L, d_q (point factor) and d_Y (entry_y) of this step. Returns the number of
 // CG iterations in *iters and the final PcgState status in *status.
-static int pcg_solve(dab_handle* h, const dab_options& opt, StepScalars sc, int* iters, int* status) {
+static int pcg_solve(dab_handle* h, const dab_options& opt, StepScalars sc, YBufs yb, int* iters, int* status) {
   hipStream_t s = h->stream;
   const DevView& v = h->view;
   const int NC = h->NC;
-  launch_pcg_diag_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_run, h->d_Y, h->d_q, h->d_partial);
+  launch_pcg_diag_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_run, yb, h->d_q, h->d_partial);
   launch_seg_final(s, NC, 27, h->d_seg_chunk, h->d_partial, h->d_pcg_red);
   CHECK_RC(h->allreduce(h->d_pcg_red, (size_t)27 * NC, ncclSum));
   launch_pcg_setup(s, NC, h->ug(), h->d_scale_c, sc, h->d_pcg_red, h->d_pcg_Ad, h->d_pcg_Minv, h->d_pcg_b,
@@ -875,12 +881,12 @@ static int pcg_solve(dab_handle* h, const dab_options& opt, StepScalars sc, int*
     for (int j = 0; j < batch && done < max_it; ++j) {
       ++done;
       launch_pcg_direction(s, NC, h->d_pcg_Minv, h->d_pcg_r, h->d_pcg_z, h->d_pcg_p, h->d_pcg_state);
-      CHECK_RC(pcg_matvec(h, h->d_pcg_p));
+      CHECK_RC(pcg_matvec(h, yb, h->d_pcg_p));
       const bool reset = done % 10 == 0;  // r = b - S x every 10th iteration
       launch_pcg_update(s, NC, reset ? 1 : 0, h->d_pcg_Ad, h->d_pcg_w, xptr, h->d_xlist, h->d_cross_cam, h->Ux(),
                         h->d_scale_c, h->d_pcg_b, h->d_pcg_p, h->d_pcg_q, h->d_yc, h->d_pcg_r, h->d_pcg_state);
       if (reset) {
-        CHECK_RC(pcg_matvec(h, h->d_yc));
+        CHECK_RC(pcg_matvec(h, yb, h->d_yc));
         launch_pcg_update(s, NC, 2, h->d_pcg_Ad, h->d_pcg_w, xptr, h->d_xlist, h->d_cross_cam, h->Ux(),
                           h->d_scale_c, h->d_pcg_b, h->d_pcg_p, h->d_pcg_q, h->d_yc, h->d_pcg_r, h->d_pcg_state);
       }
@@ -1052,6 +1058,14 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
   const bool use_pcg = opt.linear_solver_type == DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG;
   HIP_OK(hipSetDevice(h->device));
   CHECK_RC(use_pcg ? build_pcg_buffers(h) : build_schur_tables(h));
+  // Y records of each step: fp64 (both layouts), or fp32 for the mixed-precision PCG
+  // (Jacobians, residuals, V/U/g, the CG vectors and scalars stay fp64)
+  const bool y32 = use_pcg && opt.pcg_fp32 != 0;
+  if (y32 && !h->d_Y32c) {
+    CHECK_RC(h->dev.alloc(&h->d_Y32c, (size_t)kYRec * std::max(1, h->NE)));
+    CHECK_RC(h->dev.alloc(&h->d_Y32p, (size_t)kYRec * std::max(1, h->NE)));
+  }
+  const YBufs yb = y32 ? YBufs{h->d_Y32c, h->d_Y32p, true} : YBufs{h->d_Y, h->d_Yp, false};
   hipStream_t s = h->stream;
   const DevView& v = h->view;
   const int NP = h->NP, NC = h->NC, n = 6 * NC;
@@ -1163,13 +1177,13 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
     launch_point_factor(s, v, h->d_V, h->d_g, h->d_scale_p, sc, h->d_L, h->d_q, h->d_flags);
     bool pcg_fail = false;
     if (NC > 0 && use_pcg) {
-      launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, h->d_Y);
+      launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, yb);
       int cg_iters = 0, cg_status = 0;
-      CHECK_RC(pcg_solve(h, opt, sc, &cg_iters, &cg_status));
+      CHECK_RC(pcg_solve(h, opt, sc, yb, &cg_iters, &cg_status));
       it.linear_solver_iterations = cg_iters;
       pcg_fail = cg_status == kPcgFailure;
     } else if (NC > 0) {
-      launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, h->d_Y);
+      launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, yb);
       launch_s_blocks(s, h->nblk, h->d_blk_pair_beg, h->d_pairs, h->d_Y, h->packed());
       launch_cam_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_Y, h->d_q, h->d_partial);
       launch_seg_final(s, NC, 6, h->d_seg_chunk, h->d_partial, h->ybc());
@@ -1179,7 +1193,7 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
       if (chol_factor_solve(h->chol, s, n, h->d_S, h->lds, h->d_yc, h->d_flags + 1) != 0)
         return set_error(DAB_E_DEVICE, "dense Cholesky launch failed");
     }
-    launch_backsub(s, v, h->d_L, h->d_q, h->d_Y, NC > 0 ? h->d_yc : nullptr, h->d_scale_p, h->d_dp);
+    launch_backsub(s, v, h->d_L, h->d_q, yb, NC > 0 ? h->d_yc : nullptr, h->d_dp);
     // candidate x + delta and the model / candidate cost in one observation pass
     launch_axpy_points(s, NP, h->d_points, h->d_dp, h->d_points_c, h->d_gpart, h->red_grid);
     launch_final_sum(s, h->red_grid, 2, h->d_gpart, h->d_scal + S_STEP_P);

@@ -132,6 +132,27 @@ def test_lm_pcg_reaches_dense_schur_minimum(pkg, gpu):
     assert res[1] == pytest.approx(res[0], rel=1e-4)
 
 
+@pytest.mark.parametrize("kind", ["bal", "rig"])
+def test_lm_pcg_fp32_reaches_same_minimum(pkg, gpu, kind):
+    """Mixed-precision PCG (fp32 Schur factors Y, fp64 everything else): the same LM
+    reaches the fp64 minimum (final cost 1e-6 relative); its CG iteration counts may
+    differ, so only the endpoint is compared."""
+    if kind == "bal":
+        prob = pkg.synth(kind=0, num_cameras=50, num_points=3000, obs_per_point=6, seed=34)
+    else:
+        prob = pkg.synth(kind=1, num_arcs=6, num_rings=14, num_points=2500, obs_per_point=8, seed=35)
+    res = []
+    for f32 in (0, 1):
+        p = prob.copy()
+        s = pkg.Solver(0)
+        s.set_problem(p)
+        res.append(s.solve(pkg.options(max_num_iterations=50, pcg_fp32=f32,
+                                       linear_solver_type=pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)))
+        s.close()
+    assert res[1]["final_cost"] == pytest.approx(res[0]["final_cost"], rel=1e-6)
+    assert res[1]["termination"] == "CONVERGENCE"
+
+
 def test_lm_freeze_camera_matches_oracle(pkg, orc, gpu):
     prob = pkg.synth(kind=1, num_arcs=4, num_rings=10, num_points=2000, obs_per_point=6, seed=23)
     prob.freeze_camera = True  # solve(..., freeze_camera=true), sfm.cc:111
