@@ -10,8 +10,10 @@ constexpr int kCamTab = 32;   // doubles per extrinsic table: R(9) t(3) Rd(9) Jd
 constexpr int kIntr = 8;      // doubles per intrinsic: cx cy fx fy k0 k1 0 0
 constexpr int kYRec = 18;     // elements per Y_e record (6x3), fp64 or fp32 (pcg_fp32)
 
-// Y records of one LM step, in both layouts: cm = camera-major positions (streams for the
-// camera-side passes), pm = point-major entries (streams for the point-side passes).
+// Y records of one LM step, planar (element j of record i at j * stride + i), in two
+// layouts: cm[18][NE] by camera-major position (camera-side passes) and pm[2][18][NS] by
+// observation slot, one record set per extrinsic slot of the observation (point-side
+// passes walk the SELL slots with lane = point). fp64, or fp32 for pcg_fp32.
 struct YBufs {
   void* cm;
   void* pm;
@@ -44,7 +46,6 @@ struct DevView {
   const int* ent_pt;        // [NE]
   const int* ent_pos;       // [NE] camera-major position
   const int* cm_pt;         // [NE] point of the entry at camera-major position
-  const int* cm_ent;        // [NE] point-major entry index of the camera-major position
   const int* ext_col;       // [E] free camera index or -1
   const double* intr;       // [NI][kIntr]
 };
@@ -94,12 +95,14 @@ struct StepScalars {
 // 12 22), q = L^-1 (s g) -> q[NP][4]
 void launch_point_factor(hipStream_t s, const DevView& v, const double* V, const double* g,
                          const double* scale_p, StepScalars sc, double* PU, double* q, int* fail);
-// entry Y = (s_c ∘ Jc^T Jp) PU_p (re-evaluated) -> Y.cm[pos], Y.pm[e]
+// entry Y = (s_c ∘ Jc^T Jp) PU_p (re-evaluated) -> Y.cm (camera-major pass) and Y.pm
+// (slot pass; with_pm = false skips it)
 void launch_entry_y(hipStream_t s, const DevView& v, const double* points, const double* camtab,
-                    const double* scale_c, const double* PU, YBufs Y);
-// S blocks (Y part): packed[blk][36] = - sum_pairs Y_row Y_col^T (pairs hold positions)
+                    const double* scale_c, const double* PU, YBufs Y, bool with_pm);
+// S blocks (Y part): packed[blk][36] = - sum_pairs Y_row Y_col^T (pairs hold positions;
+// Y = the fp64 camera-major planes, stride NE)
 void launch_s_blocks(hipStream_t s, int nblk, const int* blk_pair_beg, const int2* pairs,
-                     const double* Y, double* packed);
+                     const double* Y, int NE, double* packed);
 // camera rhs partial: per position -Y q_p -> partial[chunk][6]
 void launch_cam_rhs_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
                             const double* Y, const double* q, double* partial);

@@ -923,15 +923,30 @@ void launch_point_factor(hipStream_t s, const DevView& v, const double* V, const
   k_point_factor<<<grid_for(v.NP, 256, 1 << 20), 256, 0, s>>>(v, V, g, scale_p, sc, L, q, fail);
 }
 
-// Y = (s_c ∘ Jc^T Jp) PU_p for the entry at camera-major position pos, re-evaluated from
-// the camera-major input copy, stored in both layouts (camera-major at pos, point-major at
-// the entry's point-major index) in the step's precision.
+// Y = (s_c ∘ Jc^T Jp) PU_p. Two passes re-evaluate the rows so that both layouts are
+// written with coalesced stores: camera-major (thread per position) and by observation
+// slot (thread per SELL slot, both extrinsic slots of the observation).
+__device__ __forceinline__ void make_y(const double (&ja)[6], const double (&jb)[6], const double (&jx0)[3],
+                                       const double (&jx1)[3], const double* __restrict__ sc,
+                                       const double* __restrict__ pu, double (&y)[18]) {
+  const double u00 = pu[0], u01 = pu[1], u02 = pu[2], u11 = pu[3], u12 = pu[4], u22 = pu[5];
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    const double sa = sc[a];
+    const double w0 = ja[a] * jx0[0] + jb[a] * jx1[0];
+    const double w1 = ja[a] * jx0[1] + jb[a] * jx1[1];
+    const double w2 = ja[a] * jx0[2] + jb[a] * jx1[2];
+    y[3 * a] = sa * (w0 * u00);
+    y[3 * a + 1] = sa * (w0 * u01 + w1 * u11);
+    y[3 * a + 2] = sa * (w0 * u02 + w1 * u12 + w2 * u22);
+  }
+}
+
 template <class YT>
 __global__ __launch_bounds__(256) void k_entry_y(DevView v, const double* __restrict__ points,
                                                  const double* __restrict__ camtab,
                                                  const double* __restrict__ scc,
-                                                 const double* __restrict__ PU, YT* __restrict__ Ycm,
-                                                 YT* __restrict__ Ypm) {
+                                                 const double* __restrict__ PU, YT* __restrict__ Ycm) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= v.NE) return;
   int4 id = v.cm_idx[i];
@@ -943,56 +958,74 @@ __global__ __launch_bounds__(256) void k_entry_y(DevView v, const double* __rest
   double ru, rv, jx0[3], jx1[3], ja[6], jb[6];
   if (slot1) obs_rows<true, 1>(id, xy, X, GlobalTabs{camtab, v.intr}, ru, rv, jx0, jx1, ja, jb);
   else obs_rows<true, 0>(id, xy, X, GlobalTabs{camtab, v.intr}, ru, rv, jx0, jx1, ja, jb);
-  const double* pu = PU + 6 * (size_t)id.x;
-  const double u00 = pu[0], u01 = pu[1], u02 = pu[2], u11 = pu[3], u12 = pu[4], u22 = pu[5];
   double y[18];
-#pragma unroll
-  for (int a = 0; a < 6; ++a) {
-    const double sa = scc[6 * c + a];
-    const double w0 = ja[a] * jx0[0] + jb[a] * jx1[0];
-    const double w1 = ja[a] * jx0[1] + jb[a] * jx1[1];
-    const double w2 = ja[a] * jx0[2] + jb[a] * jx1[2];
-    y[3 * a] = sa * (w0 * u00);
-    y[3 * a + 1] = sa * (w0 * u01 + w1 * u11);
-    y[3 * a + 2] = sa * (w0 * u02 + w1 * u12 + w2 * u22);
+  make_y(ja, jb, jx0, jx1, scc + 6 * c, PU + 6 * (size_t)id.x, y);
+  store_yplane(Ycm, (size_t)v.NE, (size_t)i, y);
+}
+
+template <class YT>
+__global__ __launch_bounds__(256) void k_entry_y_slots(DevView v, const double* __restrict__ points,
+                                                       const double* __restrict__ camtab,
+                                                       const double* __restrict__ scc,
+                                                       const double* __restrict__ PU, YT* __restrict__ Ypm) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= v.N) return;
+  const int4 id = v.obs_idx[s];
+  if (id.x < 0) return;  // padding slot
+  const int c0 = v.ext_col[id.y], c1 = id.z >= 0 ? v.ext_col[id.z] : -1;
+  if (c0 < 0 && c1 < 0) return;
+  const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
+  double ru, rv, jx0[3], jx1[3], ja[6], jb[6], da[6], db[6];
+  obs_rows<true, 2>(id, v.obs_xy[s], X, GlobalTabs{camtab, v.intr}, ru, rv, jx0, jx1, ja, jb, da, db);
+  const double* pu = PU + 6 * (size_t)id.x;
+  const size_t NS = (size_t)v.N;
+  double y[18];
+  if (c0 >= 0) {
+    make_y(ja, jb, jx0, jx1, scc + 6 * c0, pu, y);
+    store_yplane(Ypm, NS, (size_t)s, y);
   }
-  store_yrec(Ycm, i, y);
-  store_yrec(Ypm, v.cm_ent[i], y);
+  if (c1 >= 0) {
+    make_y(da, db, jx0, jx1, scc + 6 * c1, pu, y);
+    store_yplane(Ypm + 18 * NS, NS, (size_t)s, y);
+  }
 }
 
 void launch_entry_y(hipStream_t s, const DevView& v, const double* points, const double* camtab,
-                    const double* scale_c, const double* PU, YBufs Y) {
+                    const double* scale_c, const double* PU, YBufs Y, bool with_pm) {
   if (v.NE <= 0) return;
-  const int g = grid_for(v.NE, 256, 1 << 20);
-  if (Y.f32)
-    k_entry_y<float><<<g, 256, 0, s>>>(v, points, camtab, scale_c, PU, (float*)Y.cm, (float*)Y.pm);
-  else
-    k_entry_y<double><<<g, 256, 0, s>>>(v, points, camtab, scale_c, PU, (double*)Y.cm, (double*)Y.pm);
+  const int g = grid_for(v.NE, 256, 1 << 20), gs = grid_for(v.N, 256, 1 << 20);
+  if (Y.f32) {
+    k_entry_y<float><<<g, 256, 0, s>>>(v, points, camtab, scale_c, PU, (float*)Y.cm);
+    if (with_pm) k_entry_y_slots<float><<<gs, 256, 0, s>>>(v, points, camtab, scale_c, PU, (float*)Y.pm);
+  } else {
+    k_entry_y<double><<<g, 256, 0, s>>>(v, points, camtab, scale_c, PU, (double*)Y.cm);
+    if (with_pm) k_entry_y_slots<double><<<gs, 256, 0, s>>>(v, points, camtab, scale_c, PU, (double*)Y.pm);
+  }
 }
 
 // one wave per S block; lane (a,b) < 36 accumulates -sum Y_row[a,:] . Y_col[b,:]
 __global__ __launch_bounds__(256) void k_s_blocks(int nblk, const int* __restrict__ blk_pair_beg,
                                                   const int2* __restrict__ pairs,
-                                                  const double* __restrict__ Y,
+                                                  const double* __restrict__ Y, int NE,
                                                   double* __restrict__ packed) {
   const int blk = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (blk >= nblk || lane >= 36) return;
   const int a = lane / 6, b = lane - 6 * (lane / 6);
+  const size_t st = (size_t)NE;
   double acc = 0.0;
   for (int i = blk_pair_beg[blk]; i < blk_pair_beg[blk + 1]; ++i) {
     const int2 pr = pairs[i];
-    const double* yr = Y + (size_t)kYRec * pr.x + 3 * a;
-    const double* yc = Y + (size_t)kYRec * pr.y + 3 * b;
-    acc += yr[0] * yc[0] + yr[1] * yc[1] + yr[2] * yc[2];
+    acc += Y[(3 * a) * st + pr.x] * Y[(3 * b) * st + pr.y] + Y[(3 * a + 1) * st + pr.x] * Y[(3 * b + 1) * st + pr.y] +
+           Y[(3 * a + 2) * st + pr.x] * Y[(3 * b + 2) * st + pr.y];
   }
   packed[36 * (size_t)blk + lane] = -acc;
 }
 
 void launch_s_blocks(hipStream_t s, int nblk, const int* blk_pair_beg, const int2* pairs,
-                     const double* Y, double* packed) {
+                     const double* Y, int NE, double* packed) {
   if (nblk <= 0) return;
-  k_s_blocks<<<(nblk + 3) / 4, 256, 0, s>>>(nblk, blk_pair_beg, pairs, Y, packed);
+  k_s_blocks<<<(nblk + 3) / 4, 256, 0, s>>>(nblk, blk_pair_beg, pairs, Y, NE, packed);
 }
 
 __global__ __launch_bounds__(256) void k_cam_rhs_partial(DevView v, const int* __restrict__ chunk_beg,
@@ -1006,7 +1039,8 @@ __global__ __launch_bounds__(256) void k_cam_rhs_partial(DevView v, const int* _
     const int p = v.cm_pt[i];
     const double2 qa = reinterpret_cast<const double2*>(q)[2 * (size_t)p];
     const double q2 = q[4 * (size_t)p + 2];
-    const double* y = Y + (size_t)kYRec * i;
+    double y[18];
+    load_yplane(Y, (size_t)v.NE, (size_t)i, y);
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[a] -= y[3 * a] * qa.x + y[3 * a + 1] * qa.y + y[3 * a + 2] * q2;
   }
@@ -1068,35 +1102,46 @@ void launch_s_unpack(hipStream_t s, int NC, int nblk, const int2* blk_cam, const
     k_s_cross<<<grid_for(ncross * 36, 256, 1 << 20), 256, 0, s>>>(ncross, cross_cam, Ucross, scale_c, S, lds);
 }
 
-// delta_p = -PU (q - sum_e Y_e^T y_c), the point's records read contiguously (point-major)
+// delta_p = -PU (q - sum_e Y_e^T y_c): lane = point, walking its SELL observation slots
+// (coalesced planar Y records of both extrinsic slots)
 template <class YT>
 __global__ __launch_bounds__(256) void k_backsub(DevView v, const double* __restrict__ PU,
                                                  const double* __restrict__ q, const YT* __restrict__ Ypm,
                                                  const double* __restrict__ yc, double* __restrict__ dp) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= v.NP) return;
-  const size_t NPs = (size_t)v.NP;
+  const size_t NPs = (size_t)v.NP, NS = (size_t)v.N;
   const double2 qa = reinterpret_cast<const double2*>(q)[2 * (size_t)p];
-  double r0 = qa.x, r1 = qa.y, r2 = q[4 * (size_t)p + 2];
+  double r[3] = {qa.x, qa.y, q[4 * (size_t)p + 2]};
   if (yc) {
-    for (int e = v.pt_ent_ptr[p]; e < v.pt_ent_ptr[p + 1]; ++e) {
-      const int c = v.ent_cam[e];
-      double y[18];
-      load_yrec(Ypm, e, y);
+    const int sl = p >> 6, lane = p & 63;
+    const int off = v.slice_off[sl], len = (v.slice_off[sl + 1] - off) >> 6;
+    for (int k = 0; k < len; ++k) {
+      const int s = off + 64 * k + lane;
+      const int4 id = v.obs_idx[s];
+      if (id.x < 0) continue;
 #pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        const double ycv = yc[6 * c + a];
-        r0 -= y[3 * a] * ycv;
-        r1 -= y[3 * a + 1] * ycv;
-        r2 -= y[3 * a + 2] * ycv;
+      for (int slot = 0; slot < 2; ++slot) {
+        const int e = slot ? id.z : id.y;
+        const int c = e >= 0 ? v.ext_col[e] : -1;
+        if (c < 0) continue;
+        double y[18];
+        load_yplane(Ypm + slot * 18 * NS, NS, (size_t)s, y);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          const double ycv = yc[6 * c + a];
+          r[0] -= y[3 * a] * ycv;
+          r[1] -= y[3 * a + 1] * ycv;
+          r[2] -= y[3 * a + 2] * ycv;
+        }
       }
     }
   }
   // step = -y (Ceres solves J y = r then negates); delta = step * s = -PU (...)
   const double* pu = PU + 6 * (size_t)p;
-  dp[p] = -(pu[0] * r0 + pu[1] * r1 + pu[2] * r2);
-  dp[NPs + p] = -(pu[3] * r1 + pu[4] * r2);
-  dp[2 * NPs + p] = -(pu[5] * r2);
+  dp[p] = -(pu[0] * r[0] + pu[1] * r[1] + pu[2] * r[2]);
+  dp[NPs + p] = -(pu[3] * r[1] + pu[4] * r[2]);
+  dp[2 * NPs + p] = -(pu[5] * r[2]);
 }
 
 void launch_backsub(hipStream_t s, const DevView& v, const double* PU, const double* q, YBufs Y,

@@ -73,14 +73,14 @@ __global__ __launch_bounds__(256) void k_pcg_diag_rhs_partial(DevView v, const i
     const double2 qa = reinterpret_cast<const double2*>(q)[2 * (size_t)p];
     const double q2 = q[4 * (size_t)p + 2];
     double y[18];
-    load_yrec(Y, i, y);
+    load_yplane(Y, (size_t)v.NE, (size_t)i, y);
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[21 + a] -= y[3 * a] * qa.x + y[3 * a + 1] * qa.y + y[3 * a + 2] * q2;
     const int len = run[i];
     if (len == 0) continue;
     for (int j = 1; j < len; ++j) {  // rare (rig): fold the run into Z
       double w[18];
-      load_yrec(Y, i + j, w);
+      load_yplane(Y, (size_t)v.NE, (size_t)(i + j), w);
 #pragma unroll
       for (int k = 0; k < 18; ++k) y[k] += w[k];
     }
@@ -264,7 +264,8 @@ __global__ __launch_bounds__(kOneWG) void k_pcg_direction(int NC, const double* 
   }
 }
 
-// point pass: t_p = sum_e Y_e^T v_cam(e) -> t[NP][4] (point-major records, contiguous)
+// point pass: t_p = sum_e Y_e^T v_cam(e) -> t[NP][4]; lane = point over its SELL slots
+// (coalesced planar records of both extrinsic slots)
 template <class YT>
 __global__ __launch_bounds__(256) void k_pcg_point_pass(DevView v, const YT* __restrict__ Ypm,
                                                         const double* __restrict__ vec,
@@ -272,24 +273,35 @@ __global__ __launch_bounds__(256) void k_pcg_point_pass(DevView v, const YT* __r
   if (st->status != kPcgRunning) return;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= v.NP) return;
+  const size_t NS = (size_t)v.N;
+  const int sl = p >> 6, lane = p & 63;
+  const int off = v.slice_off[sl], len = (v.slice_off[sl + 1] - off) >> 6;
   double t0 = 0.0, t1 = 0.0, t2 = 0.0;
-  for (int e = v.pt_ent_ptr[p]; e < v.pt_ent_ptr[p + 1]; ++e) {
-    const int c = v.ent_cam[e];
-    double y[18];
-    load_yrec(Ypm, e, y);
-    const double2* v2 = reinterpret_cast<const double2*>(vec + 6 * (size_t)c);
-    double vc[6];
+  for (int k = 0; k < len; ++k) {
+    const int s = off + 64 * k + lane;
+    const int4 id = v.obs_idx[s];
+    if (id.x < 0) continue;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const double2 w = v2[k];
-      vc[2 * k] = w.x;
-      vc[2 * k + 1] = w.y;
-    }
+    for (int slot = 0; slot < 2; ++slot) {
+      const int e = slot ? id.z : id.y;
+      const int c = e >= 0 ? v.ext_col[e] : -1;
+      if (c < 0) continue;
+      double y[18];
+      load_yplane(Ypm + slot * 18 * NS, NS, (size_t)s, y);
+      const double2* v2 = reinterpret_cast<const double2*>(vec + 6 * (size_t)c);
+      double vc[6];
 #pragma unroll
-    for (int a = 0; a < 6; ++a) {
-      t0 += y[3 * a] * vc[a];
-      t1 += y[3 * a + 1] * vc[a];
-      t2 += y[3 * a + 2] * vc[a];
+      for (int q = 0; q < 3; ++q) {
+        const double2 w = v2[q];
+        vc[2 * q] = w.x;
+        vc[2 * q + 1] = w.y;
+      }
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        t0 += y[3 * a] * vc[a];
+        t1 += y[3 * a + 1] * vc[a];
+        t2 += y[3 * a + 2] * vc[a];
+      }
     }
   }
   reinterpret_cast<double2*>(t)[2 * (size_t)p] = make_double2(t0, t1);
@@ -310,7 +322,7 @@ __global__ __launch_bounds__(256) void k_pcg_cam_pass(DevView v, const int* __re
     const double2 ta = reinterpret_cast<const double2*>(t)[2 * (size_t)p];
     const double t2 = t[4 * (size_t)p + 2];
     double y[18];
-    load_yrec(Y, i, y);
+    load_yplane(Y, (size_t)v.NE, (size_t)i, y);
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[a] -= y[3 * a] * ta.x + y[3 * a + 1] * ta.y + y[3 * a + 2] * t2;
   }

@@ -154,7 +154,6 @@ struct dab_handle {
   double *d_V = nullptr, *d_g = nullptr, *d_scale_p = nullptr, *d_scale_c = nullptr;
   double *d_L = nullptr, *d_q = nullptr, *d_Y = nullptr, *d_Yp = nullptr;  // Y camera-/point-major
   float *d_Y32c = nullptr, *d_Y32p = nullptr;                                 // pcg_fp32 (lazy)
-  int* d_cm_ent = nullptr;
   double* d_camred = nullptr;  // [Ucc NC*21 | gc NC*6 | Ux ncross*36] (all-reduced)
   double* d_partial = nullptr; // chunk partials (max of chunk counts * 36)
   double* d_spack = nullptr;   // [packed nblk*36 | ybc NC*6] (all-reduced)
@@ -642,7 +641,6 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   CHECK_RC(upload(&h->d_ext_col, d, h->ext_col, s));
   CHECK_RC(upload(&h->d_ent_pos, d, ent_pos, s));
   CHECK_RC(upload(&h->d_cm_pt, d, cm_pt, s));
-  CHECK_RC(upload(&h->d_cm_ent, d, cam_ent, s));
   CHECK_RC(upload(&h->d_cm_idx, d, cm_idx, s));
   CHECK_RC(upload(&h->d_cm_xy, d, cm_xy, s));
   CHECK_RC(upload(&h->d_chunk_beg, d, chunk_beg, s));
@@ -671,7 +669,8 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   CHECK_RC(d.alloc(&h->d_L, (size_t)6 * NP));
   CHECK_RC(d.alloc(&h->d_q, (size_t)4 * NP));
   CHECK_RC(d.alloc(&h->d_Y, (size_t)kYRec * NE));
-  CHECK_RC(d.alloc(&h->d_Yp, (size_t)kYRec * NE));
+  const size_t npm = (size_t)kYRec * std::max(1, h->NS) * (h->any_compose ? 2 : 1);
+  CHECK_RC(d.alloc(&h->d_Yp, npm));
   h->d_Y32c = h->d_Y32p = nullptr;
   CHECK_RC(d.alloc(&h->d_camred, h->camred_count()));
   const size_t npart = std::max<size_t>({(size_t)h->nchunk * 27, (size_t)h->nxchunk * 36, (size_t)h->nchunk * 6, 16});
@@ -716,7 +715,6 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   v.ent_pt = h->d_ent_pt;
   v.ent_pos = h->d_ent_pos;
   v.cm_pt = h->d_cm_pt;
-  v.cm_ent = h->d_cm_ent;
   v.ext_col = h->d_ext_col;
   v.intr = h->d_intr;
   h->have_problem = true;
@@ -1063,7 +1061,7 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
   const bool y32 = use_pcg && opt.pcg_fp32 != 0;
   if (y32 && !h->d_Y32c) {
     CHECK_RC(h->dev.alloc(&h->d_Y32c, (size_t)kYRec * std::max(1, h->NE)));
-    CHECK_RC(h->dev.alloc(&h->d_Y32p, (size_t)kYRec * std::max(1, h->NE)));
+    CHECK_RC(h->dev.alloc(&h->d_Y32p, (size_t)kYRec * std::max(1, h->NS) * (h->any_compose ? 2 : 1)));
   }
   const YBufs yb = y32 ? YBufs{h->d_Y32c, h->d_Y32p, true} : YBufs{h->d_Y, h->d_Yp, false};
   hipStream_t s = h->stream;
@@ -1177,14 +1175,14 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
     launch_point_factor(s, v, h->d_V, h->d_g, h->d_scale_p, sc, h->d_L, h->d_q, h->d_flags);
     bool pcg_fail = false;
     if (NC > 0 && use_pcg) {
-      launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, yb);
+      launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, yb, true);
       int cg_iters = 0, cg_status = 0;
       CHECK_RC(pcg_solve(h, opt, sc, yb, &cg_iters, &cg_status));
       it.linear_solver_iterations = cg_iters;
       pcg_fail = cg_status == kPcgFailure;
     } else if (NC > 0) {
-      launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, yb);
-      launch_s_blocks(s, h->nblk, h->d_blk_pair_beg, h->d_pairs, h->d_Y, h->packed());
+      launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, yb, true);
+      launch_s_blocks(s, h->nblk, h->d_blk_pair_beg, h->d_pairs, h->d_Y, h->NE, h->packed());
       launch_cam_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_Y, h->d_q, h->d_partial);
       launch_seg_final(s, NC, 6, h->d_seg_chunk, h->d_partial, h->ybc());
       CHECK_RC(h->allreduce(h->d_spack, h->spack_count(), ncclSum));

@@ -42,34 +42,17 @@ __device__ __forceinline__ double wave_sum_lane63(double v) {
   return v;
 }
 
-// One 18-element Y record (6x3, row a = camera component) into fp64 registers.
-__device__ __forceinline__ void load_yrec(const double* __restrict__ Y, size_t i, double (&y)[18]) {
-  const double2* p = reinterpret_cast<const double2*>(Y + 18 * i);
+// Y records are planar: element j of record i at Y[j * stride + i], so every pass over
+// them (one lane per record) issues fully coalesced loads and stores.
+template <class YT>
+__device__ __forceinline__ void load_yplane(const YT* __restrict__ Y, size_t stride, size_t i, double (&y)[18]) {
 #pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    const double2 t = p[k];
-    y[2 * k] = t.x;
-    y[2 * k + 1] = t.y;
-  }
+  for (int j = 0; j < 18; ++j) y[j] = (double)Y[j * stride + i];
 }
-__device__ __forceinline__ void load_yrec(const float* __restrict__ Y, size_t i, double (&y)[18]) {
-  const float2* p = reinterpret_cast<const float2*>(Y + 18 * i);
+template <class YT>
+__device__ __forceinline__ void store_yplane(YT* __restrict__ Y, size_t stride, size_t i, const double (&y)[18]) {
 #pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    const float2 t = p[k];
-    y[2 * k] = t.x;
-    y[2 * k + 1] = t.y;
-  }
-}
-__device__ __forceinline__ void store_yrec(double* __restrict__ Y, size_t i, const double (&y)[18]) {
-  double2* p = reinterpret_cast<double2*>(Y + 18 * i);
-#pragma unroll
-  for (int k = 0; k < 9; ++k) p[k] = make_double2(y[2 * k], y[2 * k + 1]);
-}
-__device__ __forceinline__ void store_yrec(float* __restrict__ Y, size_t i, const double (&y)[18]) {
-  float2* p = reinterpret_cast<float2*>(Y + 18 * i);
-#pragma unroll
-  for (int k = 0; k < 9; ++k) p[k] = make_float2((float)y[2 * k], (float)y[2 * k + 1]);
+  for (int j = 0; j < 18; ++j) Y[j * stride + i] = (YT)y[j];
 }
 
 }  // namespace dab
