@@ -76,8 +76,9 @@ void launch_eval_cams(hipStream_t s, const DevView& v, int nchunk, const int* ch
 void launch_eval_cross(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
                        const double2* x_xy, const double* points, const double* camtab, double* partial);
 //  final: seg_out[seg][K] = sum of partial chunks [seg_chunk[seg], seg_chunk[seg+1])
+//  (max_chunks = the largest number of chunks of one segment: > 8 uses a block per segment)
 void launch_seg_final(hipStream_t s, int nseg, int K, const int* seg_chunk, const double* partial,
-                      double* out);
+                      double* out, int max_chunks = 1);
 // generic grid-level sum of partial[grid][K] -> out[K] (single block, fixed order); the
 // components whose bit is set in max_mask are combined with max instead of +.
 void launch_final_sum(hipStream_t s, int grid, int K, const double* partial, double* out,

@@ -139,9 +139,34 @@ void launch_cam_norms(hipStream_t s, int E, const int* ext_col, const double* ex
                       const double* ug, double* out) {
   k_cam_norms<<<1, 256, 0, s>>>(E, ext_col, ext, ext_c, ug, out);
 }
+// segments with many chunks: one 256-thread block per segment, thread (k, stripe) sums the
+// stripe's chunks of component k, the stripes are added in order
+__global__ __launch_bounds__(256) void k_seg_final_block(int K, const int* __restrict__ seg_chunk,
+                                                          const double* __restrict__ partial,
+                                                          double* __restrict__ out) {
+  __shared__ double sh[256];
+  const int seg = blockIdx.x;
+  const int stripes = 256 / K;
+  const int k = threadIdx.x % K, stripe = threadIdx.x / K;
+  double v = 0.0;
+  if (stripe < stripes)
+    for (int c = seg_chunk[seg] + stripe; c < seg_chunk[seg + 1]; c += stripes) v += partial[(size_t)c * K + k];
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  if (threadIdx.x < K) {
+    double t = sh[threadIdx.x];
+    for (int q = 1; q < stripes; ++q) t += sh[q * K + threadIdx.x];
+    out[(size_t)seg * K + threadIdx.x] = t;
+  }
+}
+
 void launch_seg_final(hipStream_t s, int nseg, int K, const int* seg_chunk, const double* partial,
-                      double* out) {
+                      double* out, int max_chunks) {
   if (nseg <= 0) return;
+  if (max_chunks > 8) {
+    k_seg_final_block<<<nseg, 256, 0, s>>>(K, seg_chunk, partial, out);
+    return;
+  }
   const int n = nseg * K;
   k_seg_final<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(nseg, K, seg_chunk, partial, out);
 }
@@ -618,8 +643,10 @@ __global__ __launch_bounds__(1024) void k_eval_points_lds(DevView v, const doubl
 void launch_eval_points(hipStream_t s, const DevView& v, const double* points, const double* camtab, double* V,
                         double* g, double* partial, int grid, int wps) {
   if (wps == 0) {  // LDS-staged tables; grid = persistent work-groups
-    if (v.NI <= kLdsIntr) k_eval_points_lds<true><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
-    else k_eval_points_lds<false><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
+    if (v.NI <= kLdsIntr)
+      k_eval_points_lds<true><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
+    else
+      k_eval_points_lds<false><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
   } else if (wps == 41) {  // ablations
     k_eval_points<4, 1><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);
   } else if (wps == 42) {

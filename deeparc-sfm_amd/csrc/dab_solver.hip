@@ -18,6 +18,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -108,10 +109,15 @@ struct dab_handle {
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
   CholCtx* chol = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
+  // multi-GPU: the camera-block all-reduce runs on its own stream, overlapping the
+  // point-side kernel (ev_cam: camera blocks ready; ev_comm: all-reduce done)
+  hipStream_t comm_stream = nullptr;
+  hipEvent_t ev_cam = nullptr, ev_comm = nullptr;
   // bench bookkeeping
   double bench_jac_ms = 0, bench_asm_ms = 0;
-  int bench_count = 0;
+  int bench_count = 0, bench_pending = 0;
+  std::vector<std::array<hipEvent_t, 4>> bench_ev;  // per-step events (dab_bench_eval_pass)
 
   // ---- host-side problem structure ----
   bool have_problem = false;
@@ -122,6 +128,7 @@ struct dab_handle {
   std::vector<int> pt_of;           // local point -> caller's point id
   std::vector<int> ext_col;         // ext -> free camera column
   int nchunk = 0, nxchunk = 0, ncross = 0, nblk = 0, nslice = 0;
+  int max_seg_chunks = 1, max_xseg_chunks = 1;  // largest chunk count of one camera / cross pair
   int NS = 0;  // observation slots (SELL-64, incl. padding)
   long long npairs = 0;
   int lds = 0;                      // leading dim of dense S
@@ -156,6 +163,7 @@ struct dab_handle {
   float *d_Y32c = nullptr, *d_Y32p = nullptr;                                 // pcg_fp32 (lazy)
   double* d_camred = nullptr;  // [Ucc NC*21 | gc NC*6 | Ux ncross*36] (all-reduced)
   double* d_partial = nullptr; // chunk partials (max of chunk counts * 36)
+  double* d_xpartial = nullptr; // cross-block chunk partials
   double* d_spack = nullptr;   // [packed nblk*36 | ybc NC*6] (all-reduced)
   double* d_S = nullptr;
   // implicit-Schur PCG (lazily allocated)
@@ -185,6 +193,12 @@ struct dab_handle {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (ev2) (void)hipEventDestroy(ev2);
+    if (ev3) (void)hipEventDestroy(ev3);
+    for (auto& e : bench_ev)
+      for (hipEvent_t x : e) (void)hipEventDestroy(x);
+    if (ev_cam) (void)hipEventDestroy(ev_cam);
+    if (ev_comm) (void)hipEventDestroy(ev_comm);
+    if (comm_stream) (void)hipStreamDestroy(comm_stream);
     if (comm) ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -272,7 +286,10 @@ static int create_common(int device, dab_handle** out) {
     return set_error(DAB_E_DEVICE, "rocblas handle creation failed");
   }
   if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
-      hipEventCreate(&h->ev2) != hipSuccess) {
+      hipEventCreate(&h->ev2) != hipSuccess || hipEventCreate(&h->ev3) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_cam, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_comm, hipEventDisableTiming) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking) != hipSuccess) {
     delete h;
     return set_error(DAB_E_DEVICE, "hipEventCreate failed");
   }
@@ -504,6 +521,8 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   }
   seg_chunk[NC] = (int)chunk_beg.size();
   h->nchunk = (int)chunk_beg.size();
+  h->max_seg_chunks = 1;
+  for (int c = 0; c < NC; ++c) h->max_seg_chunks = std::max(h->max_seg_chunks, seg_chunk[c + 1] - seg_chunk[c]);
   chunk_beg.push_back(NE);
   // camera-major record positions of the entries, and per observation
   std::vector<int> ent_pos(NE), cm_pt(NE);
@@ -585,6 +604,9 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
     }
     xseg_chunk[h->ncross] = (int)xchunk_beg.size();
     h->nxchunk = (int)xchunk_beg.size();
+    h->max_xseg_chunks = 1;
+    for (int k = 0; k < h->ncross; ++k)
+      h->max_xseg_chunks = std::max(h->max_xseg_chunks, xseg_chunk[k + 1] - xseg_chunk[k]);
     xchunk_beg.push_back((int)xkeys.size());
   }
 
@@ -675,6 +697,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   CHECK_RC(d.alloc(&h->d_camred, h->camred_count()));
   const size_t npart = std::max<size_t>({(size_t)h->nchunk * 27, (size_t)h->nxchunk * 36, (size_t)h->nchunk * 6, 16});
   CHECK_RC(d.alloc(&h->d_partial, npart));
+  CHECK_RC(d.alloc(&h->d_xpartial, (size_t)std::max(1, h->nxchunk) * 36));
   CHECK_RC(d.alloc(&h->d_yc, (size_t)6 * NC));
   CHECK_RC(d.alloc(&h->d_dp, (size_t)3 * NP));
   CHECK_RC(d.alloc(&h->d_dc, (size_t)6 * NC));
@@ -851,9 +874,10 @@ static int build_pcg_buffers(dab_handle* h) {
 // S vec (Y part) -> d_pcg_w, all-reduced across ranks
 static int pcg_matvec(dab_handle* h, YBufs yb, const double* vec) {
   hipStream_t s = h->stream;
-  launch_pcg_matvec_passes(s, h->view, h->nchunk, h->d_chunk_beg, yb, vec, h->d_pcg_t, h->d_partial,
-                           h->d_pcg_state);
-  launch_seg_final(s, h->NC, 6, h->d_seg_chunk, h->d_partial, h->d_pcg_w);
+  const bool direct = h->nchunk == h->NC;
+  launch_pcg_matvec_passes(s, h->view, h->nchunk, h->d_chunk_beg, yb, vec, h->d_pcg_t,
+                           direct ? h->d_pcg_w : h->d_partial, h->d_pcg_state);
+  if (!direct) launch_seg_final(s, h->NC, 6, h->d_seg_chunk, h->d_partial, h->d_pcg_w, h->max_seg_chunks);
   CHECK_RC(h->allreduce(h->d_pcg_w, (size_t)6 * h->NC, ncclSum));
   return 0;
 }
@@ -865,8 +889,10 @@ static int pcg_solve(dab_handle* h, const dab_options& opt, StepScalars sc, YBuf
   hipStream_t s = h->stream;
   const DevView& v = h->view;
   const int NC = h->NC;
-  launch_pcg_diag_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_run, yb, h->d_q, h->d_partial);
-  launch_seg_final(s, NC, 27, h->d_seg_chunk, h->d_partial, h->d_pcg_red);
+  const bool direct = h->nchunk == h->NC;
+  launch_pcg_diag_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_run, yb, h->d_q,
+                              direct ? h->d_pcg_red : h->d_partial);
+  if (!direct) launch_seg_final(s, NC, 27, h->d_seg_chunk, h->d_partial, h->d_pcg_red, h->max_seg_chunks);
   CHECK_RC(h->allreduce(h->d_pcg_red, (size_t)27 * NC, ncclSum));
   launch_pcg_setup(s, NC, h->ug(), h->d_scale_c, sc, h->d_pcg_red, h->d_pcg_Ad, h->d_pcg_Minv, h->d_pcg_b,
                    h->d_yc, h->d_pcg_r, h->d_flags + 1);
@@ -938,37 +964,46 @@ extern "C" int dab_get_parameters(dab_handle* h, double* points, double* ext) {
 // ------------------------------------------------------------------------------------
 // evaluation building blocks
 // ------------------------------------------------------------------------------------
-// The evaluation pass proper (the benchmark "step"), matrix-free: the point-side kernel
-// (residual + d r / d X reduced into V, g, cost), the
-// camera-side kernel (U, g_c from the camera-major inputs) and the arc∘ring cross blocks,
-// all-reduced across ranks. Expects the camera tables of the current x in d_camtab.
-static void eval_points(dab_handle* h) {
-  hipStream_t s = h->stream;
-  launch_eval_points(s, h->view, h->d_points, h->d_camtab, h->d_V, h->d_g, h->d_gpart, h->eval_grid, h->eval_wps);
-}
-static int eval_rest(dab_handle* h) {
+// The evaluation pass proper (the benchmark "step"), matrix-free. The camera side goes
+// first (k_eval_cams -> U, g_c; k_eval_cross -> arc∘ring blocks) so that, on several
+// GPUs, its RCCL all-reduce runs on comm_stream while the point-side kernel
+// (k_eval_points -> V, g, cost) runs on the main stream. Expects the camera tables of
+// the current x in d_camtab. ev_mid / ev_end (nullable) bracket the point kernel.
+static int eval_pass(dab_handle* h, hipEvent_t ev_mid = nullptr, hipEvent_t ev_end = nullptr) {
   hipStream_t s = h->stream;
   const DevView& v = h->view;
-  launch_final_sum(s, h->eval_grid, 2, h->d_gpart, h->d_scal + S_COST);
+  bool overlapped = false;
   if (h->NC > 0) {
-    launch_eval_cams(s, v, h->nchunk, h->d_chunk_beg, h->d_points, h->d_camtab, h->d_partial);
-    launch_seg_final(s, h->NC, 27, h->d_seg_chunk, h->d_partial, h->ug());
+    // one chunk per camera: the chunk kernels write the camera rows directly
+    const bool direct = h->nchunk == h->NC;
+    launch_eval_cams(s, v, h->nchunk, h->d_chunk_beg, h->d_points, h->d_camtab, direct ? h->ug() : h->d_partial);
+    if (!direct) launch_seg_final(s, h->NC, 27, h->d_seg_chunk, h->d_partial, h->ug(), h->max_seg_chunks);
     if (h->ncross > 0) {
       if (h->nxchunk > 0) {
         launch_eval_cross(s, v, h->nxchunk, h->d_xchunk_beg, h->d_x_idx, h->d_x_xy, h->d_points, h->d_camtab,
-                          h->d_partial);
-        launch_seg_final(s, h->ncross, 36, h->d_xseg_chunk, h->d_partial, h->Ux());
+                          h->d_xpartial);
+        launch_seg_final(s, h->ncross, 36, h->d_xseg_chunk, h->d_xpartial, h->Ux(), h->max_xseg_chunks);
       } else {
         HIP_OK(hipMemsetAsync(h->Ux(), 0, sizeof(double) * 36 * (size_t)h->ncross, s));
       }
     }
-    CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
+    if (h->world > 1 && h->comm && !h->host_cb) {
+      HIP_OK(hipEventRecord(h->ev_cam, s));
+      HIP_OK(hipStreamWaitEvent(h->comm_stream, h->ev_cam, 0));
+      NCCL_OK(ncclAllReduce(h->d_camred, h->d_camred, h->camred_count(), ncclDouble, ncclSum, h->comm,
+                            h->comm_stream));
+      HIP_OK(hipEventRecord(h->ev_comm, h->comm_stream));
+      overlapped = true;
+    } else {
+      CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
+    }
   }
+  if (ev_mid) HIP_OK(hipEventRecord(ev_mid, s));
+  launch_eval_points(s, h->view, h->d_points, h->d_camtab, h->d_V, h->d_g, h->d_gpart, h->eval_grid, h->eval_wps);
+  if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
+  launch_final_sum(s, h->eval_grid, 2, h->d_gpart, h->d_scal + S_COST);
+  if (overlapped) HIP_OK(hipStreamWaitEvent(s, h->ev_comm, 0));
   return 0;
-}
-static int eval_core(dab_handle* h) {
-  eval_points(h);
-  return eval_rest(h);
 }
 
 // Residual + Jacobian at the current x and the J^T J / J^T r blocks (camera side
@@ -976,7 +1011,7 @@ static int eval_core(dab_handle* h) {
 static int eval_jacobian_and_blocks(dab_handle* h, bool with_norms) {
   hipStream_t s = h->stream;
   launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
-  CHECK_RC(eval_core(h));
+  CHECK_RC(eval_pass(h));
   if (with_norms) {
     launch_grad_points(s, h->NP, h->d_points, h->d_g, h->d_gpart, h->red_grid);
     launch_final_sum(s, h->red_grid, 3, h->d_gpart, h->d_scal + S_GMAX_P, 1u);
@@ -1184,7 +1219,7 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
       launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, yb, true);
       launch_s_blocks(s, h->nblk, h->d_blk_pair_beg, h->d_pairs, h->d_Y, h->NE, h->packed());
       launch_cam_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_Y, h->d_q, h->d_partial);
-      launch_seg_final(s, NC, 6, h->d_seg_chunk, h->d_partial, h->ybc());
+      launch_seg_final(s, NC, 6, h->d_seg_chunk, h->d_partial, h->ybc(), h->max_seg_chunks);
       CHECK_RC(h->allreduce(h->d_spack, h->spack_count(), ncclSum));
       launch_s_unpack(s, NC, h->nblk, h->d_blk_cam, h->packed(), h->ug(), h->ncross, h->d_cross_cam, h->Ux(),
                       h->d_scale_c, sc, h->ybc(), h->d_S, h->lds);
@@ -1423,27 +1458,52 @@ extern "C" int dab_dense_spd_solve(dab_handle* h, int n, const double* A, const 
 // ------------------------------------------------------------------------------------
 // benchmark hooks
 // ------------------------------------------------------------------------------------
+// accumulate the timings of the recorded bench steps (waits for the last one)
+static int collect_bench_events(dab_handle* h) {
+  if (h->bench_pending == 0) return 0;
+  HIP_OK(hipEventSynchronize(h->bench_ev[h->bench_pending - 1][3]));
+  for (int i = 0; i < h->bench_pending; ++i) {
+    const auto& ev = h->bench_ev[i];
+    float a = 0.f, b = 0.f, c = 0.f;
+    HIP_OK(hipEventElapsedTime(&a, ev[0], ev[1]));  // camera side (+ all-reduce issue)
+    HIP_OK(hipEventElapsedTime(&b, ev[1], ev[2]));  // point kernel
+    HIP_OK(hipEventElapsedTime(&c, ev[2], ev[3]));  // cost sum + all-reduce join
+    h->bench_jac_ms += b;
+    h->bench_asm_ms += a + c;
+    h->bench_count++;
+  }
+  h->bench_pending = 0;
+  return 0;
+}
+
 extern "C" int dab_bench_eval_pass(dab_handle* h, int with_assembly) {
   clear_error();
   if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
   HIP_OK(hipSetDevice(h->device));
   hipStream_t s = h->stream;
-  launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
-  HIP_OK(hipEventRecord(h->ev0, s));
-  eval_points(h);
-  HIP_OK(hipEventRecord(h->ev1, s));
-  if (with_assembly) {
-    CHECK_RC(eval_rest(h));
-    CHECK_RC(h->allreduce(h->d_scal + S_COST, 2, ncclSum));
+  // per-step events from a pool: nothing here waits for the device, so back-to-back
+  // steps queue like the solver's own passes; dab_bench_kernel_ms reads them afterwards
+  if (h->bench_pending >= (int)h->bench_ev.size()) {
+    if (h->bench_pending >= 4096) CHECK_RC(collect_bench_events(h));
+    while ((int)h->bench_ev.size() <= h->bench_pending) {
+      std::array<hipEvent_t, 4> e{};
+      for (auto& x : e) HIP_OK(hipEventCreate(&x));
+      h->bench_ev.push_back(e);
+    }
   }
-  HIP_OK(hipEventRecord(h->ev2, s));
-  HIP_OK(hipEventSynchronize(h->ev2));
-  float a = 0.f, b = 0.f;
-  HIP_OK(hipEventElapsedTime(&a, h->ev0, h->ev1));
-  HIP_OK(hipEventElapsedTime(&b, h->ev1, h->ev2));
-  h->bench_jac_ms += a;
-  h->bench_asm_ms += b;
-  h->bench_count++;
+  const auto& ev = h->bench_ev[h->bench_pending++];
+  launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
+  HIP_OK(hipEventRecord(ev[0], s));
+  if (with_assembly) {
+    CHECK_RC(eval_pass(h, ev[1], ev[2]));
+    CHECK_RC(h->allreduce(h->d_scal + S_COST, 2, ncclSum));
+  } else {
+    HIP_OK(hipEventRecord(ev[1], s));
+    launch_eval_points(s, h->view, h->d_points, h->d_camtab, h->d_V, h->d_g, h->d_gpart, h->eval_grid,
+                       h->eval_wps);
+    HIP_OK(hipEventRecord(ev[2], s));
+  }
+  HIP_OK(hipEventRecord(ev[3], s));
   return 0;
 }
 
@@ -1458,6 +1518,7 @@ extern "C" int dab_sync(dab_handle* h) {
 extern "C" int dab_bench_kernel_ms(dab_handle* h, double* jac_ms, double* assembly_ms) {
   clear_error();
   if (!h) return set_error(DAB_E_INVALID, "null handle");
+  CHECK_RC(collect_bench_events(h));
   const double n = h->bench_count > 0 ? h->bench_count : 1;
   if (jac_ms) *jac_ms = h->bench_jac_ms / n;
   if (assembly_ms) *assembly_ms = h->bench_asm_ms / n;
