@@ -11,7 +11,10 @@ metric (BASELINE.json): "M observations/sec residual+Jacobian; wall-clock/LM-ite
           shares the camera set (weak scaling).
   lm_iter_ms: wall-clock per LM iteration on the same problem, measured in the same run
           (median over the timed iterations): lm_* with the exact dense-Schur step
-          (the reference's DENSE_SCHUR), lm_pcg_* with implicit-Schur PCG.
+          (the reference's DENSE_SCHUR), lm_pcg_* with implicit-Schur PCG, lm_pcg32_* with
+          the mixed-precision PCG (fp32 Schur factors).
+  rig_*:  BASELINE config 5 (rig 16 x 64, 1M points, 10M observations) point-sharded over
+          the N ranks (strong scaling), mixed-precision PCG, wall-clock per LM iteration.
   roofline: k_eval_points (point side of the pass), algorithmic bytes / HIP-event time.
   cpu_baseline: the C oracle (Ceres-semantics restatement, OpenMP) on the box's host
           cores, rank 0 at N=1 only, bounded sample.
@@ -37,6 +40,8 @@ def parse():
     ap.add_argument("--lm-iters", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-lm", action="store_true")
+    ap.add_argument("--no-rig", action="store_true", help="skip the config-5 rig LM measurement")
+    ap.add_argument("--rig-config", default="c5_rig_16x64")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return ap.parse_args()
 
@@ -63,15 +68,18 @@ def main():
         # gauge rule of the global problem: every shard holds camera-0 observations
         prob.ext_const[0] = 1
 
-    # communicator: rank 0 creates the RCCL id, gloo broadcasts it
-    uid = None
-    if world > 1:
+    # communicator: rank 0 creates the RCCL id, gloo broadcasts it (a fresh id per handle)
+    def make_uid():
+        if world <= 1:
+            return None
         import torch
         buf = torch.zeros(128, dtype=torch.uint8)
         if rank == 0:
             buf[:] = torch.tensor(list(pkg.Solver.unique_id()), dtype=torch.uint8)
         dist.broadcast(buf, 0)
-        uid = bytes(buf.tolist())
+        return bytes(buf.tolist())
+
+    uid = make_uid()
     # DAB_BENCH_DEVICE pins every rank to one device (multi-rank rehearsal on a 1-GPU box)
     device = int(os.environ.get("DAB_BENCH_DEVICE", local_rank))
     host_ar = None
@@ -123,11 +131,12 @@ def main():
     lm = {}
     if not args.no_lm:
         pts0, ext0 = prob.points.copy(), prob.ext.copy()
-        for tag, lst in (("lm", pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR),
-                         ("lm_pcg", pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)):
+        for tag, lst, f32 in (("lm", pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR, 0),
+                              ("lm_pcg", pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG, 0),
+                              ("lm_pcg32", pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG, 1)):
             opts = pkg.options(max_num_iterations=args.lm_iters, function_tolerance=0.0,
                                gradient_tolerance=0.0, parameter_tolerance=0.0,
-                               linear_solver_type=lst)
+                               linear_solver_type=lst, pcg_fp32=f32)
             solver.update_parameters(pts0, ext0)
             barrier()
             t1 = time.perf_counter()
@@ -147,6 +156,33 @@ def main():
             })
         prob.points[:], prob.ext[:] = pts0, ext0
         solver.update_parameters(pts0, ext0)
+
+    # ---- BASELINE config 5: the 10M-observation rig, point-sharded over the N ranks
+    # (strong scaling), mixed-precision PCG step (fp32 Schur factors). Wall-clock per LM
+    # iteration, median over the iterations, max over ranks.
+    rig = {}
+    if not args.no_rig and not args.no_lm:
+        rcfg = dict(pkg.CONFIGS[args.rig_config])
+        gprob = pkg.synth(**rcfg)
+        rprob = gprob.shard(rank, world)
+        rsolver = pkg.Solver(device, rank, world, make_uid(), host_allreduce=host_ar)
+        t_set = time.perf_counter()
+        rsolver.set_problem(rprob)
+        t_set = time.perf_counter() - t_set
+        barrier()
+        opts = pkg.options(max_num_iterations=args.lm_iters, function_tolerance=0.0, gradient_tolerance=0.0,
+                           parameter_tolerance=0.0, linear_solver_type=pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG,
+                           pcg_fp32=1)
+        summ = rsolver.solve(opts)
+        its = [it["time"] for it in summ["iterations"][1:]]
+        rig = {"rig_config": args.rig_config, "rig_global_obs": gprob.num_obs,
+               "rig_lm_pcg32_iter_ms_median": max_over_ranks(1e3 * float(np.median(its))) if its else None,
+               "rig_lm_iterations": summ["num_iterations"],
+               "rig_lm_linear_iterations": [it["linear_solver_iterations"] for it in summ["iterations"][1:]],
+               "rig_initial_cost": summ["initial_cost"], "rig_final_cost": summ["final_cost"],
+               "rig_set_problem_s": max_over_ranks(t_set)}
+        rsolver.close()
+        del gprob, rprob
 
     # ---- CPU baseline (oracle), rank 0 at N=1 only ----
     cpu = None
@@ -203,6 +239,8 @@ def main():
         }
         if lm:
             line.update(lm)
+        if rig:
+            line.update(rig)
         print(json.dumps(line), flush=True)
     solver.close()
     if dist is not None:
