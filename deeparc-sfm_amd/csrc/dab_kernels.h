@@ -147,20 +147,20 @@ void launch_pcg_diag_rhs_partial(hipStream_t s, const DevView& v, int nchunk, co
 void launch_pcg_setup(hipStream_t s, int NC, const double* ug, const double* scale_c, StepScalars sc,
                       const double* red, double* Ad, double* Minv, double* bvec, double* x, double* r,
                       int* fail);
-void launch_pcg_init(hipStream_t s, int n, const double* bvec, const int* fail, PcgState* st, double eta,
-                     int min_iter, int max_iter);
-// z = M^-1 r, rho, p = z + beta p
-void launch_pcg_direction(hipStream_t s, int NC, const double* Minv, const double* r, double* z, double* p,
-                          PcgState* st);
+// norm_b, status, and the first direction (z = M^-1 r, rho, p = z; iteration 1)
+void launch_pcg_init(hipStream_t s, int NC, const double* bvec, const int* fail, PcgState* st, double eta,
+                     int min_iter, int max_iter, const double* Minv, const double* r, double* z, double* p);
 // the two Y passes of S vec: t[NP][4], partial[chunk][6] (= -sum Y t per chunk)
 void launch_pcg_matvec_passes(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, YBufs Y,
                               const double* vec, double* t, double* partial, const PcgState* st);
 // mode 0: q = S p, alpha, x, r, Q-test; 1: q = S p, alpha, x; 2: r = b - S x, Q-test.
+// Modes 0 and 2 end with the next direction (z = M^-1 r, rho, beta, p) when still running.
 // w[NC][6] = all-reduced Y part of the product; xptr/xlist: per-camera CSR of cross blocks
 // (code = 2*k + (camera is c1)), nullable when there are none.
 void launch_pcg_update(hipStream_t s, int NC, int mode, const double* Ad, const double* w, const int* xptr,
                        const int* xlist, const int2* xcam, const double* X, const double* scale_c,
-                       const double* bvec, const double* p, double* q, double* x, double* r, PcgState* st);
+                       const double* bvec, double* p, double* q, double* x, double* r, PcgState* st,
+                       const double* Minv, double* z);
 
 // ---- dense Cholesky (dab_chol.hip) -------------------------------------------------------
 // Factor the (n+1)x(n+1) augmented lower matrix [S b; b^T *] in place (row-major, ld = lda):

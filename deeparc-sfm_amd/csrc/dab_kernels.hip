@@ -607,46 +607,54 @@ __global__ __launch_bounds__(64 * WPS) void k_eval_points(DevView v, const doubl
 }
 
 // Tables staged in LDS (camera count <= kLdsCams): R,t of every extrinsic (and K of every
-// intrinsic when <= kLdsIntr) are copied once per work-group, so the per-lane table reads
-// of BAL-shaped data (every lane a different camera) become ds_read_b128 instead of
-// 64-line L2 gathers. Persistent: one 1024-thread work-group per CU, four slices in flight.
-constexpr int kLdsCams = 1024, kLdsIntr = 128;
-template <bool K_IN_LDS>
+// intrinsic when there are at most KI of them) are copied once per work-group, so the
+// per-lane table reads of BAL-shaped data (every lane a different camera) become
+// ds_read_b128 instead of 64-line L2 gathers. Persistent: one 1024-thread work-group per
+// CU, 16 / WPS slices in flight (WPS waves each, rows split, LDS-combined).
+constexpr int kLdsCams = 1024;
+template <int KI, int WPS>
 __global__ __launch_bounds__(1024) void k_eval_points_lds(DevView v, const double* __restrict__ points,
                                                           const double* __restrict__ camtab,
                                                           double* __restrict__ V, double* __restrict__ g,
                                                           double* __restrict__ partial) {
+  constexpr int G = 16 / WPS;  // slices in flight per work-group
   __shared__ double rt_s[kLdsCams * 12];
-  __shared__ double k_s[K_IN_LDS ? kLdsIntr * 6 : 2];
-  __shared__ double sh[4][3][9][64];
+  __shared__ double k_s[KI > 0 ? KI * 6 : 2];
+  __shared__ double sh[G][WPS > 1 ? WPS - 1 : 1][9][64];
   for (int i = threadIdx.x; i < v.E * 6; i += blockDim.x) {
     const int e = i / 6, q = i - 6 * (i / 6);
     reinterpret_cast<double2*>(rt_s)[i] = reinterpret_cast<const double2*>(camtab + (size_t)kCamTab * e)[q];
   }
-  if constexpr (K_IN_LDS) {
+  if constexpr (KI > 0) {
     for (int i = threadIdx.x; i < v.NI * 3; i += blockDim.x) {
       const int n = i / 3, q = i - 3 * (i / 3);
       reinterpret_cast<double2*>(k_s)[i] = reinterpret_cast<const double2*>(v.intr + (size_t)kIntr * n)[q];
     }
   }
   __syncthreads();
-  const LdsTabs<K_IN_LDS> tabs{rt_s, k_s, camtab, v.intr};
-  const int wave = threadIdx.x >> 6, grp = wave >> 2, w = wave & 3;
+  const LdsTabs<(KI > 0)> tabs{rt_s, k_s, camtab, v.intr};
+  const int wave = threadIdx.x >> 6, grp = wave / WPS, w = wave % WPS;
   double acc[2] = {0.0, 0.0};
-  const int per_round = 4 * gridDim.x;
+  const int per_round = G * gridDim.x;
   const int rounds = (v.nslice + per_round - 1) / per_round;
   for (int r = 0; r < rounds; ++r)
-    eval_slice<4, 0>(v, points, tabs, V, g, (r * gridDim.x + blockIdx.x) * 4 + grp, w, sh[grp], acc);
+    eval_slice<WPS, 0>(v, points, tabs, V, g, (r * gridDim.x + blockIdx.x) * G + grp, w, sh[grp], acc);
   store_cost_partial<16>(acc, partial);
 }
 
+// LDS variants (all <= 160 KiB): wps 0 = 4 waves/slice, K staged when NI <= 128;
+// wps -1 = 1 wave/slice with every intrinsic staged (NI <= 1024); wps -2 = 2 waves/slice
 void launch_eval_points(hipStream_t s, const DevView& v, const double* points, const double* camtab, double* V,
                         double* g, double* partial, int grid, int wps) {
   if (wps == 0) {  // LDS-staged tables; grid = persistent work-groups
-    if (v.NI <= kLdsIntr)
-      k_eval_points_lds<true><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
-    else
-      k_eval_points_lds<false><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
+    if (v.NI <= 128) k_eval_points_lds<128, 4><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
+    else k_eval_points_lds<0, 4><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
+  } else if (wps == -1) {
+    if (v.NI <= 1024) k_eval_points_lds<1024, 1><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
+    else k_eval_points_lds<0, 1><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
+  } else if (wps == -2) {
+    if (v.NI <= 128) k_eval_points_lds<128, 2><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
+    else k_eval_points_lds<0, 2><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
   } else if (wps == 41) {  // ablations
     k_eval_points<4, 1><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);
   } else if (wps == 42) {

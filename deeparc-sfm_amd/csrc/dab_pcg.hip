@@ -197,37 +197,10 @@ __global__ __launch_bounds__(256) void k_pcg_setup(int NC, const double* __restr
   }
 }
 
-// one work-group: norm_b, status
-__global__ __launch_bounds__(kOneWG) void k_pcg_init(int n, const double* __restrict__ bvec,
-                                                     const int* __restrict__ fail, PcgState* st,
-                                                     double eta, int min_iter, int max_iter) {
-  __shared__ double sh[kOneWG / 64];
-  double acc = 0.0;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) acc += bvec[i] * bvec[i];
-  const double nb2 = wg_sum(acc, sh);
-  if (threadIdx.x == 0) {
-    st->rho = 0.0;
-    st->Q0 = 0.0;
-    st->alpha = 0.0;
-    st->eta = eta;
-    st->norm_b = sqrt(nb2);
-    st->iter = 0;
-    st->min_iter = min_iter;
-    st->max_iter = max_iter;
-    st->status = fail[0] != 0 ? kPcgFailure : (nb2 == 0.0 ? kPcgSuccess : kPcgRunning);
-    if (st->status == kPcgRunning && max_iter <= 0) st->status = kPcgNoConvergence;
-  }
-}
-
-// ---- per iteration -------------------------------------------------------------------
-
-// one work-group: z = M^-1 r, rho = r.z, p = z + beta p
-__global__ __launch_bounds__(kOneWG) void k_pcg_direction(int NC, const double* __restrict__ Minv,
-                                                          const double* __restrict__ r, double* __restrict__ z,
-                                                          double* __restrict__ p, PcgState* st) {
-  __shared__ double sh[kOneWG / 64];
-  if (st->status != kPcgRunning) return;
-  const int iter = st->iter + 1;
+// One work-group: z = M^-1 r, rho = r.z, p = z + (rho / rho_prev) p for iteration `iter`
+// (p = z when iter == 1). Every thread must call it (block-wide reductions).
+__device__ void pcg_direction(int NC, const double* __restrict__ Minv, const double* __restrict__ r,
+                              double* __restrict__ z, double* __restrict__ p, PcgState* st, int iter, double* sh) {
   double acc = 0.0;
   for (int c = threadIdx.x; c < NC; c += blockDim.x) {
     const double* mi = Minv + 36 * (size_t)c;
@@ -264,6 +237,38 @@ __global__ __launch_bounds__(kOneWG) void k_pcg_direction(int NC, const double* 
   }
 }
 
+// one work-group: norm_b, status
+__global__ __launch_bounds__(kOneWG) void k_pcg_init(int NC, const double* __restrict__ bvec,
+                                                     const int* __restrict__ fail, PcgState* st,
+                                                     double eta, int min_iter, int max_iter,
+                                                     const double* __restrict__ Minv, const double* __restrict__ r,
+                                                     double* __restrict__ z, double* __restrict__ p) {
+  __shared__ double sh[kOneWG / 64];
+  __shared__ int s_status;
+  const int n = 6 * NC;
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) acc += bvec[i] * bvec[i];
+  const double nb2 = wg_sum(acc, sh);
+  if (threadIdx.x == 0) {
+    st->rho = 0.0;
+    st->Q0 = 0.0;
+    st->alpha = 0.0;
+    st->eta = eta;
+    st->norm_b = sqrt(nb2);
+    st->iter = 0;
+    st->min_iter = min_iter;
+    st->max_iter = max_iter;
+    st->status = fail[0] != 0 ? kPcgFailure : (nb2 == 0.0 ? kPcgSuccess : kPcgRunning);
+    if (st->status == kPcgRunning && max_iter <= 0) st->status = kPcgNoConvergence;
+    s_status = st->status;
+  }
+  __syncthreads();
+  if (s_status == kPcgRunning) pcg_direction(NC, Minv, r, z, p, st, 1, sh);  // iteration 1
+}
+
+// ---- per iteration -------------------------------------------------------------------
+
+// one work-group: z = M^-1 r, rho = r.z, p = z + beta p
 // point pass: t_p = sum_e Y_e^T v_cam(e) -> t[NP][4]; lane = point over its SELL slots
 // (coalesced planar records of both extrinsic slots)
 template <class YT>
@@ -395,10 +400,12 @@ __global__ __launch_bounds__(kOneWG) void k_pcg_update(int NC, int mode, const d
                                                        const int* __restrict__ xptr, const int* __restrict__ xlist,
                                                        const int2* __restrict__ xcam, const double* __restrict__ X,
                                                        const double* __restrict__ scc, const double* __restrict__ bvec,
-                                                       const double* __restrict__ p, double* __restrict__ q,
+                                                       double* __restrict__ p, double* __restrict__ q,
                                                        double* __restrict__ x, double* __restrict__ r,
-                                                       PcgState* st) {
+                                                       PcgState* st, const double* __restrict__ Minv,
+                                                       double* __restrict__ z) {
   __shared__ double sh[kOneWG / 64];
+  __shared__ int s_status;
   if (st->status != kPcgRunning) return;
   int status = kPcgRunning;
   if (mode != 2) {
@@ -449,14 +456,18 @@ __global__ __launch_bounds__(kOneWG) void k_pcg_update(int NC, int mode, const d
     }
   }
   const double Q1 = -wg_sum(acc, sh);
+  const int iter = st->iter;
   if (threadIdx.x == 0) {
-    const int iter = st->iter;
     const double zeta = iter * (Q1 - st->Q0) / Q1;
     if (zeta < st->eta && iter >= st->min_iter) status = kPcgSuccess;
     else if (iter >= st->max_iter) status = kPcgNoConvergence;
     st->Q0 = Q1;
     st->status = status;
+    s_status = status;
   }
+  __syncthreads();
+  // still running: the next iteration's direction, in the same launch
+  if (s_status == kPcgRunning) pcg_direction(NC, Minv, r, z, p, st, iter + 1, sh);
 }
 
 // ---- launchers -------------------------------------------------------------------------
@@ -478,15 +489,11 @@ void launch_pcg_setup(hipStream_t s, int NC, const double* ug, const double* sca
   k_pcg_setup<<<grid_for(NC, 256, 1 << 20), 256, 0, s>>>(NC, ug, scale_c, sc, red, Ad, Minv, bvec, x, r, fail);
 }
 
-void launch_pcg_init(hipStream_t s, int n, const double* bvec, const int* fail, PcgState* st, double eta,
-                     int min_iter, int max_iter) {
-  k_pcg_init<<<1, kOneWG, 0, s>>>(n, bvec, fail, st, eta, min_iter, max_iter);
+void launch_pcg_init(hipStream_t s, int NC, const double* bvec, const int* fail, PcgState* st, double eta,
+                     int min_iter, int max_iter, const double* Minv, const double* r, double* z, double* p) {
+  k_pcg_init<<<1, kOneWG, 0, s>>>(NC, bvec, fail, st, eta, min_iter, max_iter, Minv, r, z, p);
 }
 
-void launch_pcg_direction(hipStream_t s, int NC, const double* Minv, const double* r, double* z, double* p,
-                          PcgState* st) {
-  k_pcg_direction<<<1, kOneWG, 0, s>>>(NC, Minv, r, z, p, st);
-}
 
 void launch_pcg_matvec_passes(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, YBufs Y,
                               const double* vec, double* t, double* partial, const PcgState* st) {
@@ -504,8 +511,9 @@ void launch_pcg_matvec_passes(hipStream_t s, const DevView& v, int nchunk, const
 
 void launch_pcg_update(hipStream_t s, int NC, int mode, const double* Ad, const double* w, const int* xptr,
                        const int* xlist, const int2* xcam, const double* X, const double* scale_c,
-                       const double* bvec, const double* p, double* q, double* x, double* r, PcgState* st) {
-  k_pcg_update<<<1, kOneWG, 0, s>>>(NC, mode, Ad, w, xptr, xlist, xcam, X, scale_c, bvec, p, q, x, r, st);
+                       const double* bvec, double* p, double* q, double* x, double* r, PcgState* st,
+                       const double* Minv, double* z) {
+  k_pcg_update<<<1, kOneWG, 0, s>>>(NC, mode, Ad, w, xptr, xlist, xcam, X, scale_c, bvec, p, q, x, r, st, Minv, z);
 }
 
 }  // namespace dab

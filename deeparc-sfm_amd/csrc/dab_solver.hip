@@ -706,12 +706,14 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
     // point-side kernel: LDS-staged camera tables when they fit (persistent grid, one
     // 1024-thread work-group per CU), else global tables (one block per slice).
     const char* env = getenv("DAB_EVAL_WPS");
-    h->eval_wps = env ? atoi(env) : (eval_points_lds_fits(h->E) ? 0 : 4);
+    h->eval_wps = env ? atoi(env) : (eval_points_lds_fits(h->E) ? -2 : 4);
     int ncu = 256;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, h->device) == hipSuccess && prop.multiProcessorCount > 0)
       ncu = prop.multiProcessorCount;
-    h->eval_grid = h->eval_wps == 0 ? std::max(1, std::min(ncu, (h->nslice + 3) / 4)) : std::max(1, h->nslice);
+    const int in_flight = h->eval_wps == 0 ? 4 : (h->eval_wps == -1 ? 16 : 8);  // slices per work-group
+    h->eval_grid = h->eval_wps <= 0 ? std::max(1, std::min(ncu, (h->nslice + in_flight - 1) / in_flight))
+                                    : std::max(1, h->nslice);
   }
   CHECK_RC(d.alloc(&h->d_gpart, (size_t)std::max(h->red_grid, h->eval_grid) * 4));
   CHECK_RC(d.alloc(&h->d_scal, S_NSLOTS));
@@ -897,22 +899,23 @@ static int pcg_solve(dab_handle* h, const dab_options& opt, StepScalars sc, YBuf
   launch_pcg_setup(s, NC, h->ug(), h->d_scale_c, sc, h->d_pcg_red, h->d_pcg_Ad, h->d_pcg_Minv, h->d_pcg_b,
                    h->d_yc, h->d_pcg_r, h->d_flags + 1);
   const int max_it = std::max(0, opt.max_linear_solver_iterations);
-  launch_pcg_init(s, 6 * NC, h->d_pcg_b, h->d_flags + 1, h->d_pcg_state, opt.eta,
-                  opt.min_linear_solver_iterations, max_it);
+  launch_pcg_init(s, NC, h->d_pcg_b, h->d_flags + 1, h->d_pcg_state, opt.eta, opt.min_linear_solver_iterations,
+                  max_it, h->d_pcg_Minv, h->d_pcg_r, h->d_pcg_z, h->d_pcg_p);
   const int* xptr = h->nxlist > 0 ? h->d_xptr : nullptr;
   int done = 0, batch = 4;
   for (;;) {
     for (int j = 0; j < batch && done < max_it; ++j) {
       ++done;
-      launch_pcg_direction(s, NC, h->d_pcg_Minv, h->d_pcg_r, h->d_pcg_z, h->d_pcg_p, h->d_pcg_state);
       CHECK_RC(pcg_matvec(h, yb, h->d_pcg_p));
       const bool reset = done % 10 == 0;  // r = b - S x every 10th iteration
       launch_pcg_update(s, NC, reset ? 1 : 0, h->d_pcg_Ad, h->d_pcg_w, xptr, h->d_xlist, h->d_cross_cam, h->Ux(),
-                        h->d_scale_c, h->d_pcg_b, h->d_pcg_p, h->d_pcg_q, h->d_yc, h->d_pcg_r, h->d_pcg_state);
+                        h->d_scale_c, h->d_pcg_b, h->d_pcg_p, h->d_pcg_q, h->d_yc, h->d_pcg_r, h->d_pcg_state,
+                        h->d_pcg_Minv, h->d_pcg_z);
       if (reset) {
         CHECK_RC(pcg_matvec(h, yb, h->d_yc));
         launch_pcg_update(s, NC, 2, h->d_pcg_Ad, h->d_pcg_w, xptr, h->d_xlist, h->d_cross_cam, h->Ux(),
-                          h->d_scale_c, h->d_pcg_b, h->d_pcg_p, h->d_pcg_q, h->d_yc, h->d_pcg_r, h->d_pcg_state);
+                          h->d_scale_c, h->d_pcg_b, h->d_pcg_p, h->d_pcg_q, h->d_yc, h->d_pcg_r, h->d_pcg_state,
+                          h->d_pcg_Minv, h->d_pcg_z);
       }
     }
     HIP_OK(hipMemcpyAsync(h->h_pcg_state, h->d_pcg_state, sizeof(PcgState), hipMemcpyDeviceToHost, s));
