@@ -48,6 +48,14 @@ struct DevView {
   const int* cm_pt;         // [NE] point of the entry at camera-major position
   const int* ext_col;       // [E] free camera index or -1
   const double* intr;       // [NI][kIntr]
+  const int2* chunk_uni;    // [nchunk] (ext, intr) shared by every entry of the chunk, or (-1, -1)
+};
+
+// camera-side chunks split by whether one camera/intrinsic serves the whole chunk
+struct ChunkLists {
+  int nchunk = 0, nuni = 0, ngen = 0;
+  const int* uni = nullptr;  // [nuni] chunk ids with chunk_uni >= 0
+  const int* gen = nullptr;  // [ngen] the others
 };
 
 // camera tables for all extrinsics from ext[E][6]
@@ -70,8 +78,8 @@ void launch_filter(hipStream_t s, const DevView& v, const double* points, const 
                    const double c[3], double radius, unsigned char* slot_keep, unsigned char* pt_keep);
 // camera side of the evaluation pass (matrix-free, camera-major inputs):
 //  U/g: per entry 21 (Jc^T Jc upper) + 6 (Jc^T r) -> partial[chunk][27]
-void launch_eval_cams(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const double* points,
-                      const double* camtab, double* partial);
+void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, const int* chunk_beg,
+                      const double* points, const double* camtab, double* partial);
 //  arc∘ring cross blocks Jc0^T Jc1 over composed observations (pair-major copy) -> partial[chunk][36]
 void launch_eval_cross(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
                        const double2* x_xy, const double* points, const double* camtab, double* partial);

@@ -248,8 +248,11 @@ struct Proj {
 __device__ __forceinline__ void project(const double P[3], const double* __restrict__ K, double ox,
                                         double oy, Proj& o, bool want_jac) {
   const double cx = K[0], cy = K[1], fx = K[2], fy = K[3], k0 = K[4], k1 = K[5];
-  const double xp = P[0] / P[2];
-  const double yp = P[1] / P[2];
+  // one reciprocal for the perspective divide and its derivative (within 1 ulp of the
+  // two divisions of the functor)
+  const double iz = 1.0 / P[2];
+  const double xp = P[0] * iz;
+  const double yp = P[1] * iz;
   const double r2 = xp * xp + yp * yp;
   // |k| = 0, 1, 2 are all this expression with unused coefficients zeroed (exact)
   const double d = 1.0 + r2 * (k0 + k1 * r2);
@@ -259,7 +262,6 @@ __device__ __forceinline__ void project(const double P[3], const double* __restr
   const double dd = k0 + 2.0 * k1 * r2;
   const double du_dx = fx * (d + 2.0 * xp * xp * dd), du_dy = fx * (2.0 * xp * yp * dd);
   const double dv_dx = fy * (2.0 * xp * yp * dd), dv_dy = fy * (d + 2.0 * yp * yp * dd);
-  const double iz = 1.0 / P[2];
   o.A0[0] = du_dx * iz;
   o.A0[1] = du_dy * iz;
   o.A0[2] = -(du_dx * xp + du_dy * yp) * iz;
@@ -342,6 +344,33 @@ struct GlobalTabs {
   __device__ __forceinline__ void rt(int e, double (&T)[12]) const { load_tab_at<0, 12>(camtab, e, T); }
   __device__ __forceinline__ void dj(int e, double (&T)[18]) const { load_tab_at<12, 18>(camtab, e, T); }
   __device__ __forceinline__ void k(int i, double (&K)[6]) const { load_intr(intr, i, K); }
+};
+// One camera and intrinsic for the whole work-group (chunk_uni): the tables are read once
+// with uniform (scalar) loads and the per-entry index is ignored.
+struct UniTabs {
+  double T[30];  // R t Rd Jd
+  double K[6];
+  __device__ __forceinline__ UniTabs(const double* __restrict__ camtab, const double* __restrict__ intr, int e,
+                                     int i) {
+    const double* t = camtab + (size_t)kCamTab * e;
+#pragma unroll
+    for (int q = 0; q < 30; ++q) T[q] = t[q];
+    const double* k = intr + (size_t)kIntr * i;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) K[q] = k[q];
+  }
+  __device__ __forceinline__ void rt(int, double (&o)[12]) const {
+#pragma unroll
+    for (int q = 0; q < 12; ++q) o[q] = T[q];
+  }
+  __device__ __forceinline__ void dj(int, double (&o)[18]) const {
+#pragma unroll
+    for (int q = 0; q < 18; ++q) o[q] = T[12 + q];
+  }
+  __device__ __forceinline__ void k(int, double (&o)[6]) const {
+#pragma unroll
+    for (int q = 0; q < 6; ++q) o[q] = K[q];
+  }
 };
 template <bool K_IN_LDS>
 struct LdsTabs {
@@ -803,16 +832,9 @@ void launch_filter(hipStream_t s, const DevView& v, const double* points, const 
 // One block per chunk of camera-major entry positions (one camera per chunk): the
 // entry's observation is re-evaluated from its camera-major input copy (cm_idx, cm_xy,
 // 32 B, contiguous) and its camera rows reduced into U (21 upper) | g_c (6).
-__global__ __launch_bounds__(256) void k_eval_cams(DevView v, const int* __restrict__ chunk_beg,
-                                                   const double* __restrict__ points,
-                                                   const double* __restrict__ camtab,
-                                                   double* __restrict__ partial) {
-  const int c = blockIdx.x;
-  const int b = chunk_beg[c], e = chunk_beg[c + 1];
-  const GlobalTabs tabs{camtab, v.intr};
-  double acc[27];
-#pragma unroll
-  for (int i = 0; i < 27; ++i) acc[i] = 0.0;
+template <class Tabs>
+__device__ __forceinline__ void eval_cams_chunk(const DevView& v, int b, int e, const double* __restrict__ points,
+                                                const Tabs& tabs, double (&acc)[27]) {
   // software-pipelined: the next entry's inputs (and its point) load while this one computes
   int i = b + threadIdx.x;
   int4 id_n = make_int4(0, 0, -1, 0);
@@ -853,13 +875,37 @@ __global__ __launch_bounds__(256) void k_eval_cams(DevView v, const int* __restr
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[21 + a] = fma(jb[a], rv, fma(ja[a], ru, acc[21 + a]));
   }
+}
+
+// UNI: the chunks of `list` are uniform (chunk_uni), tables read once per block
+template <bool UNI>
+__global__ __launch_bounds__(256) void k_eval_cams(DevView v, const int* __restrict__ chunk_beg,
+                                                   const int* __restrict__ list,
+                                                   const double* __restrict__ points,
+                                                   const double* __restrict__ camtab,
+                                                   double* __restrict__ partial) {
+  const int c = list ? list[blockIdx.x] : blockIdx.x;
+  const int b = chunk_beg[c], e = chunk_beg[c + 1];
+  double acc[27];
+#pragma unroll
+  for (int i = 0; i < 27; ++i) acc[i] = 0.0;
+  if constexpr (UNI) {
+    const int2 u = v.chunk_uni[c];
+    eval_cams_chunk(v, b, e, points, UniTabs(camtab, v.intr, u.x, u.y), acc);
+  } else {
+    eval_cams_chunk(v, b, e, points, GlobalTabs{camtab, v.intr}, acc);
+  }
   block_reduce_store<27>(acc, partial + 27 * (size_t)c);
 }
 
-void launch_eval_cams(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const double* points,
-                      const double* camtab, double* partial) {
-  if (nchunk <= 0) return;
-  k_eval_cams<<<nchunk, 256, 0, s>>>(v, chunk_beg, points, camtab, partial);
+void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, const int* chunk_beg,
+                      const double* points, const double* camtab, double* partial) {
+  if (cl.nuni > 0)
+    k_eval_cams<true><<<cl.nuni, 256, 0, s>>>(v, chunk_beg, cl.nuni == cl.nchunk ? nullptr : cl.uni, points,
+                                              camtab, partial);
+  if (cl.ngen > 0)
+    k_eval_cams<false><<<cl.ngen, 256, 0, s>>>(v, chunk_beg, cl.ngen == cl.nchunk ? nullptr : cl.gen, points,
+                                               camtab, partial);
 }
 
 // arc∘ring cross blocks Jc0^T Jc1, one block per chunk of composed observations sorted

@@ -149,6 +149,9 @@ struct dab_handle {
   int *d_slice_off = nullptr, *d_pt_ent_ptr = nullptr, *d_ent_os = nullptr, *d_ent_cam = nullptr,
       *d_ent_pt = nullptr, *d_ent_pos = nullptr, *d_cm_pt = nullptr, *d_ext_col = nullptr;
   int *d_chunk_beg = nullptr, *d_seg_chunk = nullptr;
+  int2* d_chunk_uni = nullptr;
+  int* d_chunk_lists = nullptr;  // uniform chunk ids, then the others
+  ChunkLists chunks;
   int *d_xchunk_beg = nullptr, *d_xseg_chunk = nullptr;
   int2* d_cross_cam = nullptr;
   int2 *d_pairs = nullptr, *d_blk_cam = nullptr;
@@ -553,6 +556,16 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
     cm_idx[i] = id;
     cm_xy[i] = obs_xy[s2];
   }
+  // chunks whose entries all see one camera through one intrinsic (single-extrinsic
+  // observations): the camera passes read that camera's tables once per block
+  std::vector<int2> chunk_uni(h->nchunk, make_int2(-1, -1));
+  for (int q = 0; q < h->nchunk; ++q) {
+    const int4 first = cm_idx[chunk_beg[q]];
+    bool uni = first.z < 0 && !(first.w & kSlotBit);
+    for (int i = chunk_beg[q]; uni && i < chunk_beg[q + 1]; ++i)
+      uni = cm_idx[i].z < 0 && cm_idx[i].y == first.y && cm_idx[i].w == first.w;
+    if (uni) chunk_uni[q] = make_int2(first.y, first.w);
+  }
   // arc∘ring cross blocks: composed observations whose two cameras are both free.
   // The pair table is the union over ranks so the all-reduced layout matches.
   std::vector<long long> xkeys;
@@ -666,6 +679,21 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   CHECK_RC(upload(&h->d_cm_idx, d, cm_idx, s));
   CHECK_RC(upload(&h->d_cm_xy, d, cm_xy, s));
   CHECK_RC(upload(&h->d_chunk_beg, d, chunk_beg, s));
+  CHECK_RC(upload(&h->d_chunk_uni, d, chunk_uni, s));
+  {
+    std::vector<int> lists;
+    for (int q = 0; q < h->nchunk; ++q)
+      if (chunk_uni[q].x >= 0) lists.push_back(q);
+    const int nuni = (int)lists.size();
+    for (int q = 0; q < h->nchunk; ++q)
+      if (chunk_uni[q].x < 0) lists.push_back(q);
+    CHECK_RC(upload(&h->d_chunk_lists, d, lists, s));
+    h->chunks.nchunk = h->nchunk;
+    h->chunks.nuni = nuni;
+    h->chunks.ngen = h->nchunk - nuni;
+    h->chunks.uni = h->d_chunk_lists;
+    h->chunks.gen = h->d_chunk_lists + nuni;
+  }
   CHECK_RC(upload(&h->d_seg_chunk, d, seg_chunk, s));
   CHECK_RC(upload(&h->d_x_idx, d, x_idx, s));
   CHECK_RC(upload(&h->d_x_xy, d, x_xy, s));
@@ -733,6 +761,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   v.obs_xy = h->d_obs_xy;
   v.cm_idx = h->d_cm_idx;
   v.cm_xy = h->d_cm_xy;
+  v.chunk_uni = h->d_chunk_uni;
   v.slice_off = h->d_slice_off;
   v.pt_ent_ptr = h->d_pt_ent_ptr;
   v.ent_os = h->d_ent_os;
@@ -979,7 +1008,7 @@ static int eval_pass(dab_handle* h, hipEvent_t ev_mid = nullptr, hipEvent_t ev_e
   if (h->NC > 0) {
     // one chunk per camera: the chunk kernels write the camera rows directly
     const bool direct = h->nchunk == h->NC;
-    launch_eval_cams(s, v, h->nchunk, h->d_chunk_beg, h->d_points, h->d_camtab, direct ? h->ug() : h->d_partial);
+    launch_eval_cams(s, v, h->chunks, h->d_chunk_beg, h->d_points, h->d_camtab, direct ? h->ug() : h->d_partial);
     if (!direct) launch_seg_final(s, h->NC, 27, h->d_seg_chunk, h->d_partial, h->ug(), h->max_seg_chunks);
     if (h->ncross > 0) {
       if (h->nxchunk > 0) {

@@ -10,7 +10,7 @@ import _pkgload  # noqa: E402
 pkg = _pkgload.load()
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3_1kcam"
 prob = pkg.synth(**pkg.CONFIGS[cfg])
-for wps, chunk in ((0, 4096), (-1, 4096), (-2, 4096)):
+for wps, chunk in ((-2, 4096), (0, 4096)):
     os.environ["DAB_CHUNK"] = str(chunk)
     os.environ["DAB_EVAL_WPS"] = str(wps)
     s = pkg.Solver(0)
