@@ -4,30 +4,44 @@
 // S is stored row-major, lower triangle, with the right-hand side appended as row n
 // (the augmented matrix [[S, b], [b^T, *]]). Factoring the first n pivots of the
 // augmented matrix leaves L in rows 0..n-1 and z = L^-1 b in row n, so the forward
-// substitution rides along with the factorisation. Blocked right-looking, NB = 64:
-//   k_potrf_inv  factor + invert the 64x64 diagonal block (one workgroup, LDS-resident,
-//                one barrier per pivot; inverse by 4 lanes per column, no barriers)
-//   k_trsm_inv   panel rows <- rows L_kk^-T (product with the stored inverse; every row
-//                independent, 16 rows per workgroup to fill the chip)
+// substitution rides along with the factorisation. Blocked right-looking, NB = 64, with a
+// one-block-column lookahead:
+//   k_panel      one launch per block column: every work-group factors the 64x64 diagonal
+//                block (16x16 sub-blocks in registers, rank-16 updates and the panel
+//                solve on fp64 MFMA) and solves its own 64 rows below it with the 16x16
+//                inverses; work-group 0 stores L_kk and the inverses
 //   k_syrk_mfma  trailing update C -= P P^T on lower 64x64 tiles with fp64 MFMA
-//                (v_mfma_f64_16x16x4_f64, 4 waves x 32x32 quadrants, P tiles in LDS)
+//                (v_mfma_f64_16x16x4_f64, 4 waves x 32x32 quadrants, P tiles in LDS), split
+//                into the next block column (on the panel chain) and the bulk (on a second
+//                stream, overlapping the next panel step)
 // Back substitution L^T y = z: one launch per block, y_k = L_kk^-T z_k from the stored
-// inverse followed by the block-column update of z[0:k].
+// 16x16 inverses followed by the block-column update of z[0:k].
+// The whole sequence is captured once into a hipGraph (two streams) and replayed.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
 #include "dab_kernels.h"
+#include "dab_wave.h"
 
 namespace dab {
 
 constexpr int NB = 64;
 constexpr int kThreads = 256;
 constexpr int LDP = 66;  // padded LDS row stride (doubles): conflict-free fragment reads
+constexpr int kBlk = 1024 + NB * NB;
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 struct CholCtx {
-  double* linv = nullptr;  // [nblk][NB][NB] inverses of the diagonal blocks
-  size_t linv_blocks = 0;
+  double* blk = nullptr;  // per block column: D [4][16][16] (inverses of the 16x16 diagonal
+                          // blocks), then L_kk [64][64]; stride kBlk
+
+  hipStream_t side = nullptr;                     // bulk trailing updates (captured into the graph)
+  std::vector<hipEvent_t> ev_panel, ev_bulk;      // per block column
+  size_t nblk_alloc = 0;
   // the ~5 x n/64 dependent launches are captured once per (n, buffers) and replayed
   hipGraphExec_t exec = nullptr;
   int g_n = -1, g_lda = -1;
@@ -38,185 +52,234 @@ CholCtx* chol_create() { return new CholCtx(); }
 void chol_destroy(CholCtx* c) {
   if (!c) return;
   if (c->exec) (void)hipGraphExecDestroy(c->exec);
-  if (c->linv) (void)hipFree(c->linv);
+  if (c->blk) (void)hipFree(c->blk);
+  for (hipEvent_t e : c->ev_panel) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->ev_bulk) (void)hipEventDestroy(e);
+  if (c->side) (void)hipStreamDestroy(c->side);
   delete c;
 }
 
-__device__ __forceinline__ double bcast(double v, int lane) {  // lane: compile-time constant
-  const int2 p = *reinterpret_cast<int2*>(&v);
-  int2 r;
-  r.x = __builtin_amdgcn_readlane(p.x, lane);
-  r.y = __builtin_amdgcn_readlane(p.y, lane);
-  return *reinterpret_cast<double*>(&r);
+// ---- panel step in one launch --------------------------------------------------------
+// Every work-group factors the 64x64 diagonal block itself (blocked by 16: wave 0 factors
+// and inverts each 16x16 diagonal block in registers, lane = row, broadcasts by
+// v_readlane; the work-group solves the rows below it with that inverse and applies the
+// rank-16 update in LDS), then solves its own 64 panel rows P <- P L_kk^-T block column by
+// block column with the four 16x16 inverses. Work-group 0 also stores L_kk and the
+// inverses (for the back substitution). The redundant factorisations run side by side,
+// so the dependent chain per step is one launch instead of potrf -> inverse -> trsm.
+constexpr int LS = NB + 1;
+constexpr int DS = 17;
+#ifdef DAB_CHOL_PROFILE  // phase timestamps of work-group 0 (scripts/potrf_micro.hip only)
+__device__ long long g_prof[16];
+#define PROF_MARK(i) \
+  if (blockIdx.x == 0 && threadIdx.x == 0) g_prof[i] = wall_clock64();
+#else
+#define PROF_MARK(i)
+#endif
+
+// 1/sqrt(d): v_rsq_f64 and two Newton steps
+__device__ __forceinline__ double rsqrt_nr(double d) {
+  double y = __builtin_amdgcn_rsq(d);
+  y = y * fma(-0.5 * d * y, y, 1.5);
+  y = y * fma(-0.5 * d * y, y, 1.5);
+  return y;
 }
 
-// Factor A[k:k+kb, k:k+kb] (lower) in place (identity padding beyond kb). One wave, lane =
-// row held in registers, fully unrolled. VAR 0: the pivot column is broadcast with
-// v_readlane; VAR 1: through LDS (one ds_write per lane, then ds_read_b128 broadcasts).
-template <int VAR>
-__global__ __launch_bounds__(64) void k_potrf(double* __restrict__ A, int lda, int k, int kb,
-                                              int* __restrict__ flag) {
-  __shared__ double col[NB];
-  const int m = threadIdx.x;
-  double a[NB];
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    double v = (m == j) ? 1.0 : 0.0;
-    if (m < kb && j < kb && j <= m) v = A[(size_t)(k + m) * lda + k + j];
-    a[j] = v;
+// lane j of each 16-lane row to the whole row (DPP row_newbcast): a VGPR broadcast, no
+// SGPR round trip
+template <int J>
+__device__ __forceinline__ double rowb(double v) {
+  return dpp_full_f64<0x150 + J>(v);
+}
+template <int J, int I = 0>
+struct RowB {
+  static __device__ __forceinline__ double get(double v, int j) {
+    if constexpr (I >= 16) return v;
+    else return j == I ? rowb<I>(v) : RowB<J, I + 1>::get(v, j);
   }
-  bool bad = false;
+};
+#define ROWB(v, j) RowB<0>::get((v), (j))
+
+// wave 0: factor L[o:o+16, o:o+16] in place, its inverse into D[16][DS]
+__device__ __noinline__ void factor16(double (*L)[LS], double (*D)[DS], int o, bool& bad) {
+  const int lane = threadIdx.x & 63, r = lane & 15;
+  double a[16], rd[16];
 #pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    double d;
-    if constexpr (VAR == 0) {
-      d = bcast(a[j], j);  // pivot a_jj (updated)
-    } else {
-      if (m == j) col[0] = a[j];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      d = col[0];
-      __builtin_amdgcn_wave_barrier();
-    }
+  for (int j = 0; j < 16; ++j) a[j] = (j <= r) ? L[o + r][o + j] : 0.0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const double d = ROWB(a[j], j);
     bad |= !(d > 0.0) || !isfinite(d);
-    const double sd = sqrt(d);
-    const double lmj = (m == j) ? sd : a[j] / sd;  // L[m][j] (meaningful for m >= j)
+    const double y = rsqrt_nr(d);
+    rd[j] = y;  // 1 / L[j][j]
+    const double lmj = (r == j) ? d * y : a[j] * y;
     a[j] = lmj;
-    if constexpr (VAR == 0) {
 #pragma unroll
-      for (int l = j + 1; l < NB; ++l) {
-        const double llj = bcast(lmj, l);
-        if (m >= l) a[l] -= lmj * llj;
-      }
-    } else {
-      col[m] = lmj;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int l = j + 1; l < NB; ++l) {
-        const double llj = col[l];
-        if (m >= l) a[l] -= lmj * llj;
-      }
-      __builtin_amdgcn_wave_barrier();
+    for (int l = j + 1; l < 16; ++l) {
+      const double llj = ROWB(lmj, l);
+      if (r >= l) a[l] -= lmj * llj;
     }
   }
-  if (m == 0 && bad) atomicOr(flag, 1);
-  if (m < kb) {
+  // lane c: column c of the inverse, x[i] = (delta_ic - sum_{c<=m<i} L[i][m] x[m]) / L[i][i]
+  const int cc = r;
+  double x[16];
 #pragma unroll
-    for (int j = 0; j < NB; ++j)
-      if (j <= m && j < kb) A[(size_t)(k + m) * lda + k + j] = a[j];
+  for (int i = 0; i < 16; ++i) {
+    double s = (i == cc) ? 1.0 : 0.0;
+#pragma unroll
+    for (int m = 0; m < i; ++m) s -= ROWB(a[m], i) * x[m];
+    x[i] = (i >= cc) ? s * rd[i] : 0.0;
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (j <= r) L[o + r][o + j] = a[j];
+      D[j][cc] = x[j];
+    }
   }
 }
 
-// Inverse of the factored diagonal block L_kk (lower, identity-padded beyond kb) by
-// recursive doubling: the eight 8x8 diagonal blocks by substitution (one lane per
-// column), then three levels X21 = -X22 (L21 X11) of small parallel products. The
-// dependent chain is 8 substitution steps + 6 barriers instead of 64 pivot steps.
-__global__ __launch_bounds__(kThreads) void k_trinv(const double* __restrict__ A, int lda, int k, int kb,
-                                                    double* __restrict__ linv) {
-  __shared__ double L[NB][NB + 1];
-  __shared__ double X[NB][NB + 1];
-  __shared__ double T[NB][NB + 1];
-  const int tid = threadIdx.x;
+// 16x16 tiles on fp64 MFMA (v_mfma_f64_16x16x4f64; A: lane l holds A[l&15][l>>4], B:
+// B[l>>4][l&15], C/D: C[(l>>4) + 4r][l&15]). acc += sign * A B with A(i,k) = As[i0+i][ka+k]
+// and B(k,j) = Bt[j0+j][kb+k] (B given transposed, as the row-major factor blocks are).
+template <int SA, int SB>
+__device__ __forceinline__ void mma_nt(int K, dbl4& acc, const double* As, int i0, int ka, const double* Bt, int j0,
+                                       int kb, double sign) {
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int ks = 0; ks < K / 4; ++ks) {
+    const double a = sign * As[(i0 + li) * SA + ka + 4 * ks + lk];
+    const double b = Bt[(j0 + li) * SB + kb + 4 * ks + lk];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+}
+template <int S>
+__device__ __forceinline__ dbl4 tile_load(const double* M, int i0, int j0) {
+  const int lane = threadIdx.x & 63;
+  dbl4 t;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t[r] = M[(i0 + (lane >> 4) + 4 * r) * S + j0 + (lane & 15)];
+  return t;
+}
+template <int S>
+__device__ __forceinline__ void tile_store(double* M, int i0, int j0, const dbl4& t) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) M[(i0 + (lane >> 4) + 4 * r) * S + j0 + (lane & 15)] = t[r];
+}
+
+// the 64x64 diagonal block (in LDS) -> L in place, D[p] = inverse of its p-th 16x16 block
+__device__ __forceinline__ void factor64(double (*L)[LS], double (*D)[16][DS], bool& bad) {
+  const int tid = threadIdx.x, w = tid >> 6;
+  double* Lf = &L[0][0];
+#pragma unroll 1
+  for (int p = 0; p < 4; ++p) {
+    const int o = 16 * p;
+    if (w == 0) factor16(L, D[p], o, bad);
+    __syncthreads();
+    PROF_MARK(2 + 2 * p);
+    if (p == 3) break;
+    const int nrc = 3 - p;  // 16-row chunks below the diagonal block
+    // block column p below the diagonal: L_R = A_R D_p^T (wave w: chunk w)
+    if (w < nrc) {
+      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+      mma_nt<LS, DS>(16, acc, Lf, o + 16 + 16 * w, o, &D[p][0][0], 0, 0, 1.0);
+      __builtin_amdgcn_wave_barrier();
+      tile_store<LS>(Lf, o + 16 + 16 * w, o, acc);
+    }
+    __syncthreads();
+    // rank-16 update of the trailing lower tiles (ti >= tj), round robin over the waves
+    for (int t = w; t < nrc * (nrc + 1) / 2; t += kThreads / 64) {
+      int ti = 0;
+      while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+      const int tj = t - ti * (ti + 1) / 2;
+      const int ri = o + 16 + 16 * ti, rj = o + 16 + 16 * tj;
+      dbl4 acc = tile_load<LS>(Lf, ri, rj);
+      mma_nt<LS, LS>(16, acc, Lf, ri, o, Lf, rj, o, -1.0);
+      tile_store<LS>(Lf, ri, rj, acc);
+    }
+    __syncthreads();
+    PROF_MARK(3 + 2 * p);
+  }
+}
+
+// panel rows [r0, r1) (64 per work-group): P <- P L_kk^-T ; work-group 0 stores D and L_kk
+// to the block scratch
+__global__ __launch_bounds__(kThreads) void k_panel(double* __restrict__ A, int lda, int k, int kb, int r0,
+                                                    int r1, double* __restrict__ blk, int* __restrict__ flag) {
+  __shared__ double L[NB][LS];
+  __shared__ double P[NB][LS];
+  __shared__ double D[4][16][DS];
+  const int tid = threadIdx.x, w = tid >> 6;
+  const int row0 = r0 + NB * blockIdx.x;
 #pragma unroll
   for (int q = 0; q < NB * NB / kThreads; ++q) {
     const int idx = tid + q * kThreads, i = idx >> 6, j = idx & 63;
     double v = (i == j) ? 1.0 : 0.0;
     if (i < kb && j <= i) v = A[(size_t)(k + i) * lda + k + j];
     L[i][j] = v;
-    X[i][j] = 0.0;
-  }
-  __syncthreads();
-  if (tid < NB) {  // level 0: block b = tid / 8, column c = tid % 8
-    const int b = tid >> 3, c = tid & 7, o = 8 * b;
-    double x[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      double s = (r == c) ? 1.0 : 0.0;
-#pragma unroll
-      for (int mm = 0; mm < r; ++mm) s -= L[o + r][o + mm] * x[mm];
-      x[r] = (r >= c) ? s / L[o + r][o + r] : 0.0;
-    }
-#pragma unroll
-    for (int r = 0; r < 8; ++r) X[o + r][o + c] = x[r];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int h = 8; h < NB; h *= 2) {
-    // pairs of h-blocks at offsets o = 2h q: T = L21 X11, then X21 = -X22 T
-    const int nout = NB / (2 * h) * h * h;  // outputs per phase over all pairs
-    for (int e = tid; e < nout; e += kThreads) {
-      const int pq = e / (h * h), rem = e - pq * h * h, i = rem / h, j = rem - (rem / h) * h;
-      const int o = 2 * h * pq;
-      double s = 0.0;
-      for (int mm = j; mm < h; ++mm) s += L[o + h + i][o + mm] * X[o + mm][o + j];
-      T[o + h + i][o + j] = s;
-    }
-    __syncthreads();
-    for (int e = tid; e < nout; e += kThreads) {
-      const int pq = e / (h * h), rem = e - pq * h * h, i = rem / h, j = rem - (rem / h) * h;
-      const int o = 2 * h * pq;
-      double s = 0.0;
-      for (int mm = 0; mm <= i; ++mm) s += X[o + h + i][o + h + mm] * T[o + h + mm][o + j];
-      X[o + h + i][o + j] = -s;
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int q = 0; q < NB * NB / kThreads; ++q) {
-    const int idx = tid + q * kThreads;
-    linv[idx] = X[idx >> 6][idx & 63];
-  }
-}
-
-// rows [r0, r1): A[i, k:k+kb] <- A[i, k:k+kb] Linv^T ; 16 rows per workgroup
-constexpr int TR = 16;
-__global__ __launch_bounds__(kThreads) void k_trsm_inv(double* __restrict__ A, int lda, int k, int kb, int r0,
-                                                       int r1, const double* __restrict__ linv) {
-  __shared__ double P[TR][NB + 1];
-  __shared__ double Li[NB][NB + 1];
-  const int tid = threadIdx.x;
-  const int row0 = r0 + blockIdx.x * TR;
-#pragma unroll
-  for (int q = 0; q < NB * NB / kThreads; ++q) {
-    const int idx = tid + q * kThreads;
-    Li[idx >> 6][idx & 63] = linv[idx];
-  }
-#pragma unroll
-  for (int q = 0; q < TR * NB / kThreads; ++q) {
-    const int idx = tid + q * kThreads, i = idx >> 6, j = idx & 63;
     P[i][j] = (row0 + i < r1 && j < kb) ? A[(size_t)(row0 + i) * lda + k + j] : 0.0;
   }
+  PROF_MARK(0);
   __syncthreads();
-  const int rr = tid >> 4;  // 16 rows x 16 threads, 4 outputs each
-  double out[4];
+  PROF_MARK(1);
+  bool bad = false;
+  factor64(L, D, bad);
+  if (blockIdx.x == 0) {
+    // L_kk goes to the scratch, not back into A: the other work-groups of this launch
+    // may not have read the original diagonal block yet
+    if (tid == 0 && bad) atomicOr(flag, 1);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int j = (tid & 15) + 16 * q;
-    double s = 0.0;
-    for (int mm = 0; mm <= j; ++mm) s += P[rr][mm] * Li[j][mm];
-    out[q] = s;
-  }
-  if (row0 + rr < r1) {
+    for (int q = 0; q < NB * NB / kThreads; ++q) {
+      const int idx = tid + q * kThreads, i = idx >> 6, j = idx & 63;
+      blk[1024 + idx] = (j <= i) ? L[i][j] : 0.0;
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int j = (tid & 15) + 16 * q;
-      if (j < kb) A[(size_t)(row0 + rr) * lda + k + j] = out[q];
+      const int idx = tid + q * kThreads;  // [4][16][16]
+      blk[idx] = D[idx >> 8][(idx >> 4) & 15][idx & 15];
     }
+  }
+  if (row0 >= r1) return;
+  // wave w solves rows [16w, 16w+16) of P, block column by block column (no barriers:
+  // the rows are its own): T = P_q - X_{<q} L_{q,<q}^T, X_q = T D_q^T
+  double* Pf = &P[0][0];
+  const double* Lf = &L[0][0];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    dbl4 acc = tile_load<LS>(Pf, 16 * w, 16 * q);
+    if (q > 0) mma_nt<LS, LS>(16 * q, acc, Pf, 16 * w, 0, Lf, 16 * q, 0, -1.0);
+    __builtin_amdgcn_wave_barrier();
+    tile_store<LS>(Pf, 16 * w, 16 * q, acc);
+    __builtin_amdgcn_wave_barrier();
+    dbl4 x = {0.0, 0.0, 0.0, 0.0};
+    mma_nt<LS, DS>(16, x, Pf, 16 * w, 16 * q, &D[q][0][0], 0, 0, 1.0);
+    __builtin_amdgcn_wave_barrier();
+    tile_store<LS>(Pf, 16 * w, 16 * q, x);
+  }
+  __syncthreads();
+  PROF_MARK(10);
+#pragma unroll
+  for (int q = 0; q < NB * NB / kThreads; ++q) {
+    const int idx = tid + q * kThreads, i = idx >> 6, j = idx & 63;
+    if (row0 + i < r1 && j < kb) A[(size_t)(row0 + i) * lda + k + j] = P[i][j];
   }
 }
 
-// trailing update on lower 64x64 tiles of the m x m matrix at (r0, r0):
-//   C[i][j] -= sum_kk P[i][kk] P[j][kk], P = A[r0.., k..k+kb)
+// col_only: just the first tile column of the trailing matrix (tile (t, 0)), the block
+// column the next panel step factors; otherwise the whole lower triangle of tiles.
 __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, int lda, int r0, int m, int k,
-                                                        int kb) {
+                                                        int kb, int col_only) {
   __shared__ double Pa[NB * LDP];
   __shared__ double Pb[NB * LDP];
   const int t = blockIdx.x;
-  int bi = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
-  while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
-  while (bi * (bi + 1) / 2 > t) --bi;
-  const int bj = t - bi * (bi + 1) / 2;
+  int bi = t, bj = 0;
+  if (!col_only) {
+    bi = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
+    while (bi * (bi + 1) / 2 > t) --bi;
+    bj = t - bi * (bi + 1) / 2;
+  }
   const int tid = threadIdx.x;
   const bool diag = bi == bj;
   const int w = tid >> 6, lane = tid & 63;
@@ -284,27 +347,48 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
       }
 }
 
-// back substitution step for block [k, k+kb): y_k = Linv^T z_k (a 64x64 matvec with the
-// stored inverse), then z[0:k] -= L[k:k+kb, 0:k]^T y_k
+// back substitution step for block [k, k+kb): y_k = L_kk^-T z_k by 16-blocks with the
+// stored inverses D_q (y_q = D_q^T (z_q - sum_{r>q} L_rq^T y_r)), then
+// z[0:k] -= L[k:k+kb, 0:k]^T y_k
 __global__ __launch_bounds__(kThreads) void k_trsv_back(const double* __restrict__ A, int lda, int k, int kb,
-                                                        const double* __restrict__ linv,
+                                                        const double* __restrict__ blk,
                                                         double* __restrict__ z, double* __restrict__ y) {
-  __shared__ double Li[NB][NB + 1];
-  __shared__ double zz[NB];
+  __shared__ double Lk[NB][LS];
+  __shared__ double Dq[4][16][DS];
   __shared__ double yy[NB];
+  __shared__ double tt[16];
   const int tid = threadIdx.x;
 #pragma unroll
   for (int q = 0; q < NB * NB / kThreads; ++q) {
-    const int idx = tid + q * kThreads;
-    Li[idx >> 6][idx & 63] = linv[idx];
+    const int idx = tid + q * kThreads, i = idx >> 6, j = idx & 63;
+    Lk[i][j] = blk[1024 + idx];
   }
-  if (tid < NB) zz[tid] = tid < kb ? z[k + tid] : 0.0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int idx = tid + q * kThreads;
+    Dq[idx >> 8][(idx >> 4) & 15][idx & 15] = blk[idx];
+  }
+  if (tid < NB) yy[tid] = tid < kb ? z[k + tid] : 0.0;
   __syncthreads();
-  if (tid < NB) {
-    double s = 0.0;
-#pragma unroll 8
-    for (int mm = 0; mm < NB; ++mm) s += (mm >= tid ? Li[mm][tid] : 0.0) * zz[mm];
-    yy[tid] = s;
+  if (tid < 64) {  // one wave, lanes 0..15 carry the 16-vectors
+    const int c = tid & 15;
+#pragma unroll
+    for (int q = 3; q >= 0; --q) {
+      double t = yy[16 * q + c];
+#pragma unroll
+      for (int r = q + 1; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) t = fma(-Lk[16 * r + i][16 * q + c], yy[16 * r + i], t);
+      if (tid < 16) tt[c] = t;
+      __builtin_amdgcn_wave_barrier();
+      double s = 0.0;
+#pragma unroll
+      for (int m = 0; m < 16; ++m)
+        if (m >= c) s = fma(Dq[q][m][c], tt[m], s);
+      __builtin_amdgcn_wave_barrier();
+      if (tid < 16) yy[16 * q + c] = s;
+      __builtin_amdgcn_wave_barrier();
+    }
   }
   __syncthreads();
   if (blockIdx.x == 0 && tid < kb) y[k + tid] = yy[tid];
@@ -331,13 +415,25 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
 int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag) {
   if (n <= 0) return 0;
   const int nblk = (n + NB - 1) / NB;
-  if ((size_t)nblk > c->linv_blocks) {
+  if ((size_t)nblk > c->nblk_alloc) {
     if (c->exec) (void)hipGraphExecDestroy(c->exec);
     c->exec = nullptr;
-    if (c->linv) (void)hipFree(c->linv);
-    c->linv = nullptr;
-    if (hipMalloc(&c->linv, sizeof(double) * NB * NB * (size_t)nblk) != hipSuccess) return -2;
-    c->linv_blocks = nblk;
+    if (c->blk) (void)hipFree(c->blk);
+    c->blk = nullptr;
+    if (hipMalloc(&c->blk, sizeof(double) * kBlk * (size_t)nblk) != hipSuccess) return -2;
+    c->nblk_alloc = nblk;
+  }
+  if (!c->side && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) return -3;
+  while ((int)c->ev_panel.size() < nblk) {
+    hipEvent_t a, b;
+    if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess) return -3;
+    if (hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) return -3;
+    c->ev_panel.push_back(a);
+    c->ev_bulk.push_back(b);
+  }
+  if (getenv("DAB_CHOL_NOGRAPH")) {  // debugging aid: launch directly on the two streams
+    enqueue_factor_solve(c, s, n, A, lda, y, d_flag);
+    return 0;
   }
   const bool same = c->exec && c->g_n == n && c->g_lda == lda && c->g_A == A && c->g_y == y && c->g_flag == d_flag;
   if (!same) {
@@ -364,25 +460,52 @@ int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
 
 static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y,
                                  int* d_flag) {
+  // Lookahead by one block column. Chain stream s: P(0), then per step b
+  // [wait bulk(b-1)] col-update(b) -> P(b+1); bulk stream s2: bulk(b) after P(b). The
+  // bulk trailing update of step b overlaps the next panel step.
   const int nblk = (n + NB - 1) / NB;
+  hipStream_t s2 = getenv("DAB_CHOL_SERIAL") ? s : c->side;  // serial: debugging aid
+  auto panel = [&](int b) {
+    const int k = b * NB, kb = (n - k < NB) ? n - k : NB;
+    const int r0 = k + kb, r1 = n + 1;  // includes the rhs row n
+    const int grid = std::max(1, (r1 - r0 + NB - 1) / NB);
+    k_panel<<<grid, kThreads, 0, s>>>(A, lda, k, kb, r0, r1, c->blk + (size_t)b * kBlk, d_flag);
+  };
+  panel(0);
+  bool bulk_prev = false;
   for (int b = 0; b < nblk; ++b) {
     const int k = b * NB, kb = (n - k < NB) ? n - k : NB;
-    double* li = c->linv + (size_t)b * NB * NB;
-    k_potrf<0><<<1, 64, 0, s>>>(A, lda, k, kb, d_flag);
-    k_trinv<<<1, kThreads, 0, s>>>(A, lda, k, kb, li);
-    const int r0 = k + kb, r1 = n + 1;  // includes the rhs row n
-    k_trsm_inv<<<(r1 - r0 + TR - 1) / TR, kThreads, 0, s>>>(A, lda, k, kb, r0, r1, li);
-    const int m = r1 - r0;
-    if (m > 1) {
-      const int nt = (m + NB - 1) / NB;
-      k_syrk_mfma<<<nt * (nt + 1) / 2, kThreads, 0, s>>>(A, lda, r0, m, k, kb);
+    const int r0 = k + kb, m = n + 1 - r0;
+    if (m <= 1 && b + 1 >= nblk) break;
+    const int nt = (m + NB - 1) / NB;
+    bool bulk = false;
+    if (nt > 1) {  // tile columns 1.. of the trailing matrix
+      (void)hipEventRecord(c->ev_panel[b], s);
+      (void)hipStreamWaitEvent(s2, c->ev_panel[b], 0);
+      const int m2 = m - NB, nt2 = (m2 + NB - 1) / NB;
+      k_syrk_mfma<<<nt2 * (nt2 + 1) / 2, kThreads, 0, s2>>>(A, lda, r0 + NB, m2, k, kb, 0);
+      (void)hipEventRecord(c->ev_bulk[b], s2);
+      bulk = true;
+    }
+    if (bulk_prev) (void)hipStreamWaitEvent(s, c->ev_bulk[b - 1], 0);
+    if (m > 1) k_syrk_mfma<<<nt, kThreads, 0, s>>>(A, lda, r0, m, k, kb, 1);
+    if (b + 1 < nblk) panel(b + 1);
+    bulk_prev = bulk;
+  }
+  // join the bulk stream (its last event) before the back substitution
+  for (int b = nblk - 1; b >= 0; --b) {
+    const int k = b * NB, kb = (n - k < NB) ? n - k : NB;
+    const int m = n + 1 - (k + kb), nt = (m + NB - 1) / NB;
+    if (nt > 1) {
+      (void)hipStreamWaitEvent(s, c->ev_bulk[b], 0);
+      break;
     }
   }
   double* z = A + (size_t)n * lda;
   for (int b = nblk - 1; b >= 0; --b) {
     const int k = b * NB, kb = (n - k < NB) ? n - k : NB;
     const int grid = k > 0 ? (k + 63) / 64 : 1;
-    k_trsv_back<<<grid, kThreads, 0, s>>>(A, lda, k, kb, c->linv + (size_t)b * NB * NB, z, y);
+    k_trsv_back<<<grid, kThreads, 0, s>>>(A, lda, k, kb, c->blk + (size_t)b * kBlk, z, y);
   }
 }
 
