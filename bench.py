@@ -34,8 +34,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c3_1kcam")
     ap.add_argument("--lm-iters", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
@@ -106,15 +106,13 @@ def main():
         return float(t.item())
 
     # ---- evaluation passes (the headline metric) ----
-    for _ in range(args.warmup):
-        solver.bench_eval_pass(True)
+    solver.bench_eval_pass(True, args.warmup)
     solver.sync()
     solver.bench_kernel_ms()  # reset event accumulators
     barrier()
     solver.sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        solver.bench_eval_pass(True)
+    solver.bench_eval_pass(True, args.steps)  # K passes enqueued back to back
     solver.sync()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)

@@ -109,7 +109,7 @@ SIGNATURES = {
     "dab_eval_jacobians": (C.c_int, [C.c_void_p, _dp, _dp]),
     "dab_filter": (C.c_int, [C.c_void_p, C.c_double, _dp, C.c_double, _u8p, _u8p, _ip, _ip]),
     "dab_dense_spd_solve": (C.c_int, [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp]),
-    "dab_bench_eval_pass": (C.c_int, [C.c_void_p, C.c_int]),
+    "dab_bench_eval_pass": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "dab_sync": (C.c_int, [C.c_void_p]),
     "dab_bench_kernel_ms": (C.c_int, [C.c_void_p, _dp, _dp]),
     "dab_jacobian_bytes": (C.c_int, [C.c_void_p, _dp]),

@@ -271,8 +271,9 @@ class Solver:
         return x, ms.value, rc == 0
 
     # --- benchmark hooks ---
-    def bench_eval_pass(self, with_assembly=True):
-        check(self.lib.dab_bench_eval_pass(self.h, int(with_assembly)), self.lib)
+    def bench_eval_pass(self, with_assembly=True, count=1):
+        """Enqueue `count` evaluation passes (asynchronous; sync() waits)."""
+        check(self.lib.dab_bench_eval_pass(self.h, int(with_assembly), int(count)), self.lib)
 
     def sync(self):
         check(self.lib.dab_sync(self.h), self.lib)

@@ -61,11 +61,15 @@ struct ChunkLists {
 // camera tables for all extrinsics from ext[E][6]
 void launch_cam_tables(hipStream_t s, int E, const double* ext, double* camtab);
 // Point side of the evaluation pass (rows a1-a4, matrix-free): residual + d r / d X per
-// observation reduced into V[6][NP], g[3][NP] (one SELL slice per block, lane = point,
-// wps = 4 | 8 | 16 waves per slice with global tables, 0 = LDS-staged tables with a
-// persistent grid), partial[grid][2] = {sum r^2, non-finite}.
-void launch_eval_points(hipStream_t s, const DevView& v, const double* points, const double* camtab, double* V,
-                        double* g, double* partial, int grid, int wps);
+// observation reduced into V[6][NP], g[3][NP] (one SELL slice per block, lane = point;
+// wps = 4 | 8 | 16 waves per slice reading camtab; 0 / -2 = 4 / 2 waves per slice with R,t
+// built from ext into LDS on a persistent grid), cost[2] = {sum r^2, non-finite count}
+// (partial[grid][2] is scratch; arrivals is a zeroed counter the kernel leaves zeroed).
+void launch_eval_points(hipStream_t s, const DevView& v, const double* points, const double* ext,
+                        const double* camtab, double* V, double* g, double* partial, unsigned* arrivals,
+                        double* cost, int grid, int wps);
+// whether the chosen variant reads camtab (the LDS variants build R,t from ext themselves)
+bool eval_points_needs_camtab(int wps);
 bool eval_points_lds_fits(int E);
 // Full Jacobian planes (parity API): Jfull[30][N], r[N]
 void launch_jacobian_full(hipStream_t s, const DevView& v, const double* points,
@@ -79,7 +83,7 @@ void launch_filter(hipStream_t s, const DevView& v, const double* points, const 
 // camera side of the evaluation pass (matrix-free, camera-major inputs):
 //  U/g: per entry 21 (Jc^T Jc upper) + 6 (Jc^T r) -> partial[chunk][27]
 void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, const int* chunk_beg,
-                      const double* points, const double* camtab, double* partial);
+                      const double* points, const double* ext, const double* camtab, double* partial);
 //  arc∘ring cross blocks Jc0^T Jc1 over composed observations (pair-major copy) -> partial[chunk][36]
 void launch_eval_cross(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
                        const double2* x_xy, const double* points, const double* camtab, double* partial);

@@ -178,12 +178,12 @@ void launch_final_sum(hipStream_t s, int grid, int K, const double* partial, dou
 // ------------------------------------------------------------------------------------
 // per-extrinsic tables (R, t, Rd, Jd)
 // ------------------------------------------------------------------------------------
-__global__ void k_cam_tables(int E, const double* __restrict__ ext, double* __restrict__ tab) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= E) return;
-  const double w0 = ext[6 * e], w1 = ext[6 * e + 1], w2 = ext[6 * e + 2];
-  double* T = tab + (size_t)kCamTab * e;
-  double R[9], Rd[9], Jd[9];
+// R (row-major), t, Rd, Jd of one extrinsic (w, t): the table every pass reads
+__device__ __forceinline__ void cam_table(const double* __restrict__ ext6, double (&T)[30]) {
+  const double w0 = ext6[0], w1 = ext6[1], w2 = ext6[2];
+  double* R = T;
+  double* Rd = T + 12;
+  double* Jd = T + 21;
   const double th2 = w0 * w0 + w1 * w1 + w2 * w2;
   if (th2 > DBL_EPSILON) {
     const double th = sqrt(th2);
@@ -219,17 +219,21 @@ __global__ void k_cam_tables(int E, const double* __restrict__ ext, double* __re
 #pragma unroll
     for (int i = 0; i < 9; ++i) Jd[i] = (i % 4 == 0) ? 1.0 : 0.0;
   }
+  T[9] = ext6[3];
+  T[10] = ext6[4];
+  T[11] = ext6[5];
+}
+
+__global__ void k_cam_tables(int E, const double* __restrict__ ext, double* __restrict__ tab) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  double T[30];
+  cam_table(ext + 6 * (size_t)e, T);
+  double* o = tab + (size_t)kCamTab * e;
 #pragma unroll
-  for (int i = 0; i < 9; ++i) T[i] = R[i];
-  T[9] = ext[6 * e + 3];
-  T[10] = ext[6 * e + 4];
-  T[11] = ext[6 * e + 5];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) T[12 + i] = Rd[i];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) T[21 + i] = Jd[i];
-  T[30] = 0.0;
-  T[31] = 0.0;
+  for (int i = 0; i < 30; ++i) o[i] = T[i];
+  o[30] = 0.0;
+  o[31] = 0.0;
 }
 
 void launch_cam_tables(hipStream_t s, int E, const double* ext, double* camtab) {
@@ -345,19 +349,27 @@ struct GlobalTabs {
   __device__ __forceinline__ void dj(int e, double (&T)[18]) const { load_tab_at<12, 18>(camtab, e, T); }
   __device__ __forceinline__ void k(int i, double (&K)[6]) const { load_intr(intr, i, K); }
 };
-// One camera and intrinsic for the whole work-group (chunk_uni): the tables are read once
-// with uniform (scalar) loads and the per-entry index is ignored.
+// One camera and intrinsic for the whole work-group (chunk_uni): the table is computed once
+// from the extrinsic (uniform values) and the per-entry index is ignored.
 struct UniTabs {
   double T[30];  // R t Rd Jd
   double K[6];
-  __device__ __forceinline__ UniTabs(const double* __restrict__ camtab, const double* __restrict__ intr, int e,
+  __device__ __forceinline__ UniTabs(const double* __restrict__ ext, const double* __restrict__ intr, int e,
                                      int i) {
-    const double* t = camtab + (size_t)kCamTab * e;
-#pragma unroll
-    for (int q = 0; q < 30; ++q) T[q] = t[q];
+    cam_table(ext + 6 * (size_t)e, T);  // built in place: no table pass needed before this one
     const double* k = intr + (size_t)kIntr * i;
 #pragma unroll
     for (int q = 0; q < 6; ++q) K[q] = k[q];
+    // the values are wave-uniform: keep them in SGPRs, not 72 VGPRs
+#pragma unroll
+    for (int q = 0; q < 30; ++q) T[q] = uniform(T[q]);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) K[q] = uniform(K[q]);
+  }
+  static __device__ __forceinline__ double uniform(double x) {
+    const int lo = __builtin_amdgcn_readfirstlane(__double2loint(x));
+    const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(x));
+    return __hiloint2double(hi, lo);
   }
   __device__ __forceinline__ void rt(int, double (&o)[12]) const {
 #pragma unroll
@@ -620,6 +632,57 @@ __device__ __forceinline__ void store_cost_partial(double (&acc)[2], double* __r
   }
 }
 
+// As store_cost_partial, and the last work-group to arrive sums all partials (fixed
+// order) into cost[2]. The partials are stored write-through (agent-scope atomic stores)
+// and drained before the arrival count, and read back with agent-scope atomic loads: no
+// release/acquire fences (the hand-off recipe of the CDNA4 guide, Guideline 16).
+template <int NW>
+__device__ __forceinline__ void store_cost_partial_last(double (&acc)[2], double* __restrict__ partial,
+                                                        unsigned* __restrict__ arrivals, double* __restrict__ cost) {
+  __shared__ double shp[NW][2];
+  __shared__ int last;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double t = wave_sum_lane63(acc[i]);
+    if (lane == 63) shp[w][i] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    if (threadIdx.x < 2) {
+      double t = shp[0][threadIdx.x];
+#pragma unroll
+      for (int q = 1; q < NW; ++q) t += shp[q][threadIdx.x];
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(partial) + 2 * (size_t)blockIdx.x + threadIdx.x,
+                         (unsigned long long)__double_as_longlong(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0)
+      last = __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __shared__ double red[2][NW];
+  const unsigned long long* pp = reinterpret_cast<const unsigned long long*>(partial);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    double v = 0.0;
+    for (int c = threadIdx.x; c < (int)gridDim.x; c += blockDim.x)
+      v += __longlong_as_double((long long)__hip_atomic_load(pp + 2 * (size_t)c + i, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT));
+    const double t = wave_sum_lane63(v);
+    if (lane == 63) red[i][w] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    double t = red[threadIdx.x][0];
+#pragma unroll
+    for (int q = 1; q < NW; ++q) t += red[threadIdx.x][q];
+    cost[threadIdx.x] = t;
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(arrivals, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // tables from global memory: one block per slice, grid-strided
 template <int WPS, int VAR = 0>
 __global__ __launch_bounds__(64 * WPS) void k_eval_points(DevView v, const double* __restrict__ points,
@@ -643,16 +706,22 @@ __global__ __launch_bounds__(64 * WPS) void k_eval_points(DevView v, const doubl
 constexpr int kLdsCams = 1024;
 template <int KI, int WPS>
 __global__ __launch_bounds__(1024) void k_eval_points_lds(DevView v, const double* __restrict__ points,
+                                                          const double* __restrict__ ext,
                                                           const double* __restrict__ camtab,
                                                           double* __restrict__ V, double* __restrict__ g,
-                                                          double* __restrict__ partial) {
+                                                          double* __restrict__ partial,
+                                                          unsigned* __restrict__ arrivals,
+                                                          double* __restrict__ cost) {
   constexpr int G = 16 / WPS;  // slices in flight per work-group
   __shared__ double rt_s[kLdsCams * 12];
   __shared__ double k_s[KI > 0 ? KI * 6 : 2];
   __shared__ double sh[G][WPS > 1 ? WPS - 1 : 1][9][64];
-  for (int i = threadIdx.x; i < v.E * 6; i += blockDim.x) {
-    const int e = i / 6, q = i - 6 * (i / 6);
-    reinterpret_cast<double2*>(rt_s)[i] = reinterpret_cast<const double2*>(camtab + (size_t)kCamTab * e)[q];
+  // R,t of every extrinsic, computed here from the parameters (no table pass in front)
+  for (int e = threadIdx.x; e < v.E; e += blockDim.x) {
+    double T[30];
+    cam_table(ext + 6 * (size_t)e, T);
+#pragma unroll
+    for (int q = 0; q < 12; ++q) rt_s[12 * e + q] = T[q];
   }
   if constexpr (KI > 0) {
     for (int i = threadIdx.x; i < v.NI * 3; i += blockDim.x) {
@@ -668,23 +737,25 @@ __global__ __launch_bounds__(1024) void k_eval_points_lds(DevView v, const doubl
   const int rounds = (v.nslice + per_round - 1) / per_round;
   for (int r = 0; r < rounds; ++r)
     eval_slice<WPS, 0>(v, points, tabs, V, g, (r * gridDim.x + blockIdx.x) * G + grp, w, sh[grp], acc);
-  store_cost_partial<16>(acc, partial);
+  store_cost_partial_last<16>(acc, partial, arrivals, cost);
 }
 
 // LDS variants (all <= 160 KiB): wps 0 = 4 waves/slice, K staged when NI <= 128;
 // wps -1 = 1 wave/slice with every intrinsic staged (NI <= 1024); wps -2 = 2 waves/slice
-void launch_eval_points(hipStream_t s, const DevView& v, const double* points, const double* camtab, double* V,
-                        double* g, double* partial, int grid, int wps) {
-  if (wps == 0) {  // LDS-staged tables; grid = persistent work-groups
-    if (v.NI <= 128) k_eval_points_lds<128, 4><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
-    else k_eval_points_lds<0, 4><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
-  } else if (wps == -1) {
-    if (v.NI <= 1024) k_eval_points_lds<1024, 1><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
-    else k_eval_points_lds<0, 1><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
-  } else if (wps == -2) {
-    if (v.NI <= 128) k_eval_points_lds<128, 2><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
-    else k_eval_points_lds<0, 2><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
-  } else if (wps == 41) {  // ablations
+void launch_eval_points(hipStream_t s, const DevView& v, const double* points, const double* ext,
+                        const double* camtab, double* V, double* g, double* partial, unsigned* arrivals,
+                        double* cost, int grid, int wps) {
+  if (wps == 0 || wps == -2) {  // LDS tables built in-kernel; grid = persistent work-groups
+    if (wps == 0) {
+      if (v.NI <= 128) k_eval_points_lds<128, 4><<<grid, 1024, 0, s>>>(v, points, ext, camtab, V, g, partial, arrivals, cost);
+      else k_eval_points_lds<0, 4><<<grid, 1024, 0, s>>>(v, points, ext, camtab, V, g, partial, arrivals, cost);
+    } else {
+      if (v.NI <= 128) k_eval_points_lds<128, 2><<<grid, 1024, 0, s>>>(v, points, ext, camtab, V, g, partial, arrivals, cost);
+      else k_eval_points_lds<0, 2><<<grid, 1024, 0, s>>>(v, points, ext, camtab, V, g, partial, arrivals, cost);
+    }
+    return;
+  }
+  if (wps == 41) {  // ablations
     k_eval_points<4, 1><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);
   } else if (wps == 42) {
     k_eval_points<4, 2><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);
@@ -695,7 +766,9 @@ void launch_eval_points(hipStream_t s, const DevView& v, const double* points, c
   } else {
     k_eval_points<4><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);
   }
+  launch_final_sum(s, grid, 2, partial, cost);
 }
+bool eval_points_needs_camtab(int wps) { return wps > 0; }
 
 bool eval_points_lds_fits(int E) { return E <= kLdsCams; }
 
@@ -882,6 +955,7 @@ template <bool UNI>
 __global__ __launch_bounds__(256) void k_eval_cams(DevView v, const int* __restrict__ chunk_beg,
                                                    const int* __restrict__ list,
                                                    const double* __restrict__ points,
+                                                   const double* __restrict__ ext,
                                                    const double* __restrict__ camtab,
                                                    double* __restrict__ partial) {
   const int c = list ? list[blockIdx.x] : blockIdx.x;
@@ -891,7 +965,7 @@ __global__ __launch_bounds__(256) void k_eval_cams(DevView v, const int* __restr
   for (int i = 0; i < 27; ++i) acc[i] = 0.0;
   if constexpr (UNI) {
     const int2 u = v.chunk_uni[c];
-    eval_cams_chunk(v, b, e, points, UniTabs(camtab, v.intr, u.x, u.y), acc);
+    eval_cams_chunk(v, b, e, points, UniTabs(ext, v.intr, u.x, u.y), acc);
   } else {
     eval_cams_chunk(v, b, e, points, GlobalTabs{camtab, v.intr}, acc);
   }
@@ -899,12 +973,12 @@ __global__ __launch_bounds__(256) void k_eval_cams(DevView v, const int* __restr
 }
 
 void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, const int* chunk_beg,
-                      const double* points, const double* camtab, double* partial) {
+                      const double* points, const double* ext, const double* camtab, double* partial) {
   if (cl.nuni > 0)
-    k_eval_cams<true><<<cl.nuni, 256, 0, s>>>(v, chunk_beg, cl.nuni == cl.nchunk ? nullptr : cl.uni, points,
+    k_eval_cams<true><<<cl.nuni, 256, 0, s>>>(v, chunk_beg, cl.nuni == cl.nchunk ? nullptr : cl.uni, points, ext,
                                               camtab, partial);
   if (cl.ngen > 0)
-    k_eval_cams<false><<<cl.ngen, 256, 0, s>>>(v, chunk_beg, cl.ngen == cl.nchunk ? nullptr : cl.gen, points,
+    k_eval_cams<false><<<cl.ngen, 256, 0, s>>>(v, chunk_beg, cl.ngen == cl.nchunk ? nullptr : cl.gen, points, ext,
                                                camtab, partial);
 }
 

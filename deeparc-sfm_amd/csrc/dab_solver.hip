@@ -150,6 +150,7 @@ struct dab_handle {
       *d_ent_pt = nullptr, *d_ent_pos = nullptr, *d_cm_pt = nullptr, *d_ext_col = nullptr;
   int *d_chunk_beg = nullptr, *d_seg_chunk = nullptr;
   int2* d_chunk_uni = nullptr;
+  unsigned* d_arrivals = nullptr;  // last-arriver counter of the point kernel (kept zeroed)
   int* d_chunk_lists = nullptr;  // uniform chunk ids, then the others
   ChunkLists chunks;
   int *d_xchunk_beg = nullptr, *d_xseg_chunk = nullptr;
@@ -680,6 +681,8 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   CHECK_RC(upload(&h->d_cm_xy, d, cm_xy, s));
   CHECK_RC(upload(&h->d_chunk_beg, d, chunk_beg, s));
   CHECK_RC(upload(&h->d_chunk_uni, d, chunk_uni, s));
+  CHECK_RC(d.alloc(&h->d_arrivals, 1));
+  HIP_OK(hipMemsetAsync(h->d_arrivals, 0, sizeof(unsigned), s));
   {
     std::vector<int> lists;
     for (int q = 0; q < h->nchunk; ++q)
@@ -1001,14 +1004,19 @@ extern "C" int dab_get_parameters(dab_handle* h, double* points, double* ext) {
 // GPUs, its RCCL all-reduce runs on comm_stream while the point-side kernel
 // (k_eval_points -> V, g, cost) runs on the main stream. Expects the camera tables of
 // the current x in d_camtab. ev_mid / ev_end (nullable) bracket the point kernel.
-static int eval_pass(dab_handle* h, hipEvent_t ev_mid = nullptr, hipEvent_t ev_end = nullptr) {
+// camtab_ready: the caller has just built the camera tables (the LM step needs them for
+// later passes); otherwise they are built here only if a pass of this problem reads them.
+static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullptr, hipEvent_t ev_end = nullptr) {
   hipStream_t s = h->stream;
   const DevView& v = h->view;
   bool overlapped = false;
+  const bool need_tab = (h->NC > 0 && (h->chunks.ngen > 0 || h->ncross > 0)) || eval_points_needs_camtab(h->eval_wps);
+  if (!camtab_ready && need_tab) launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
   if (h->NC > 0) {
     // one chunk per camera: the chunk kernels write the camera rows directly
     const bool direct = h->nchunk == h->NC;
-    launch_eval_cams(s, v, h->chunks, h->d_chunk_beg, h->d_points, h->d_camtab, direct ? h->ug() : h->d_partial);
+    launch_eval_cams(s, v, h->chunks, h->d_chunk_beg, h->d_points, h->d_ext, h->d_camtab,
+                     direct ? h->ug() : h->d_partial);
     if (!direct) launch_seg_final(s, h->NC, 27, h->d_seg_chunk, h->d_partial, h->ug(), h->max_seg_chunks);
     if (h->ncross > 0) {
       if (h->nxchunk > 0) {
@@ -1031,9 +1039,9 @@ static int eval_pass(dab_handle* h, hipEvent_t ev_mid = nullptr, hipEvent_t ev_e
     }
   }
   if (ev_mid) HIP_OK(hipEventRecord(ev_mid, s));
-  launch_eval_points(s, h->view, h->d_points, h->d_camtab, h->d_V, h->d_g, h->d_gpart, h->eval_grid, h->eval_wps);
+  launch_eval_points(s, h->view, h->d_points, h->d_ext, h->d_camtab, h->d_V, h->d_g, h->d_gpart, h->d_arrivals,
+                     h->d_scal + S_COST, h->eval_grid, h->eval_wps);
   if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
-  launch_final_sum(s, h->eval_grid, 2, h->d_gpart, h->d_scal + S_COST);
   if (overlapped) HIP_OK(hipStreamWaitEvent(s, h->ev_comm, 0));
   return 0;
 }
@@ -1043,7 +1051,7 @@ static int eval_pass(dab_handle* h, hipEvent_t ev_mid = nullptr, hipEvent_t ev_e
 static int eval_jacobian_and_blocks(dab_handle* h, bool with_norms) {
   hipStream_t s = h->stream;
   launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
-  CHECK_RC(eval_pass(h));
+  CHECK_RC(eval_pass(h, true));
   if (with_norms) {
     launch_grad_points(s, h->NP, h->d_points, h->d_g, h->d_gpart, h->red_grid);
     launch_final_sum(s, h->red_grid, 3, h->d_gpart, h->d_scal + S_GMAX_P, 1u);
@@ -1491,6 +1499,8 @@ extern "C" int dab_dense_spd_solve(dab_handle* h, int n, const double* A, const 
 // benchmark hooks
 // ------------------------------------------------------------------------------------
 // accumulate the timings of the recorded bench steps (waits for the last one)
+constexpr int kBenchSample = 8;
+
 static int collect_bench_events(dab_handle* h) {
   if (h->bench_pending == 0) return 0;
   HIP_OK(hipEventSynchronize(h->bench_ev[h->bench_pending - 1][3]));
@@ -1508,34 +1518,48 @@ static int collect_bench_events(dab_handle* h) {
   return 0;
 }
 
-extern "C" int dab_bench_eval_pass(dab_handle* h, int with_assembly) {
+extern "C" int dab_bench_eval_pass(dab_handle* h, int with_assembly, int count) {
   clear_error();
   if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
+  if (count < 0) return set_error(DAB_E_INVALID, "negative pass count");
   HIP_OK(hipSetDevice(h->device));
   hipStream_t s = h->stream;
-  // per-step events from a pool: nothing here waits for the device, so back-to-back
-  // steps queue like the solver's own passes; dab_bench_kernel_ms reads them afterwards
-  if (h->bench_pending >= (int)h->bench_ev.size()) {
-    if (h->bench_pending >= 4096) CHECK_RC(collect_bench_events(h));
-    while ((int)h->bench_ev.size() <= h->bench_pending) {
-      std::array<hipEvent_t, 4> e{};
-      for (auto& x : e) HIP_OK(hipEventCreate(&x));
-      h->bench_ev.push_back(e);
+  // Timing events bracket every kBenchSample-th pass of the batch (the first one always):
+  // even fence-free, four event records add ~10 us to a ~40 us pass, so timing every pass
+  // would distort the throughput it measures. DAB_BENCH_SAMPLE overrides (0 = no events).
+  const char* env = getenv("DAB_BENCH_SAMPLE");
+  const int sample = env ? atoi(env) : kBenchSample;
+  for (int step = 0; step < count; ++step) {
+    if (sample <= 0 || step % sample != 0) {
+      CHECK_RC(eval_pass(h, false));
+      CHECK_RC(h->allreduce(h->d_scal + S_COST, 2, ncclSum));
+      continue;
     }
+    // per-step events from a pool: nothing here waits for the device, so back-to-back
+    // steps queue like the solver's own passes; dab_bench_kernel_ms reads them afterwards
+    if (h->bench_pending >= (int)h->bench_ev.size()) {
+      if (h->bench_pending >= 4096) CHECK_RC(collect_bench_events(h));
+      while ((int)h->bench_ev.size() <= h->bench_pending) {
+        std::array<hipEvent_t, 4> e{};
+        // timing-only events: no system-scope fence (it costs several us per record)
+        for (auto& x : e) HIP_OK(hipEventCreateWithFlags(&x, hipEventDisableSystemFence));
+        h->bench_ev.push_back(e);
+      }
+    }
+    const auto& ev = h->bench_ev[h->bench_pending++];
+    HIP_OK(hipEventRecord(ev[0], s));
+    if (with_assembly) {
+      CHECK_RC(eval_pass(h, false, ev[1], ev[2]));
+      CHECK_RC(h->allreduce(h->d_scal + S_COST, 2, ncclSum));
+    } else {
+      if (eval_points_needs_camtab(h->eval_wps)) launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
+      HIP_OK(hipEventRecord(ev[1], s));
+      launch_eval_points(s, h->view, h->d_points, h->d_ext, h->d_camtab, h->d_V, h->d_g, h->d_gpart, h->d_arrivals,
+                         h->d_scal + S_COST, h->eval_grid, h->eval_wps);
+      HIP_OK(hipEventRecord(ev[2], s));
+    }
+    HIP_OK(hipEventRecord(ev[3], s));
   }
-  const auto& ev = h->bench_ev[h->bench_pending++];
-  launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
-  HIP_OK(hipEventRecord(ev[0], s));
-  if (with_assembly) {
-    CHECK_RC(eval_pass(h, ev[1], ev[2]));
-    CHECK_RC(h->allreduce(h->d_scal + S_COST, 2, ncclSum));
-  } else {
-    HIP_OK(hipEventRecord(ev[1], s));
-    launch_eval_points(s, h->view, h->d_points, h->d_camtab, h->d_V, h->d_g, h->d_gpart, h->eval_grid,
-                       h->eval_wps);
-    HIP_OK(hipEventRecord(ev[2], s));
-  }
-  HIP_OK(hipEventRecord(ev[3], s));
   return 0;
 }
 

@@ -223,13 +223,16 @@ int dab_dense_spd_solve(dab_handle* h, int n, const double* A, const double* b, 
                         double* factor_ms);
 
 /* ---- benchmark hooks -------------------------------------------------------------------
- * One evaluation pass on device-resident data: residual+Jacobian kernel followed by the
- * JtJ / Jtr block assembly (per-point V,g and per-camera U,g; all-reduced across ranks).
- * Asynchronous on the handle's stream. dab_sync waits for it. */
-int dab_bench_eval_pass(dab_handle* h, int with_assembly);
+ * `count` evaluation passes on device-resident data, enqueued back to back: residual +
+ * Jacobian with the JtJ / Jtr block assembly (per-point V,g and per-camera U,g, all-reduced
+ * across ranks). Asynchronous on the handle's stream; dab_sync waits for them. One call per
+ * batch keeps the host's launch cost off the device's critical path. */
+int dab_bench_eval_pass(dab_handle* h, int with_assembly, int count);
 int dab_sync(dab_handle* h);
-/* Kernel timing: average device time (ms) of the residual+Jacobian kernel over the last
- * `n` dab_bench_eval_pass calls, measured with HIP events on the handle's stream. */
+/* Kernel timing: average device time (ms) of the point-side residual+Jacobian kernel and
+ * of the rest of the pass, over the passes since the last call, measured with HIP events on
+ * the handle's stream (every 8th pass of a dab_bench_eval_pass batch and its first one;
+ * environment DAB_BENCH_SAMPLE sets the stride). */
 int dab_bench_kernel_ms(dab_handle* h, double* jac_ms, double* assembly_ms);
 /* Algorithmic HBM bytes of one residual+Jacobian launch on the resident problem. */
 int dab_jacobian_bytes(dab_handle* h, double* bytes);

@@ -20,13 +20,11 @@ s = pkg.Solver(0)
 s.set_problem(prob)
 t2 = time.perf_counter()
 print(f"{cfg}: {prob.num_obs} obs, synth {t1 - t0:.1f} s, set_problem {t2 - t1:.1f} s", flush=True)
-for _ in range(3):
-    s.bench_eval_pass(True)
+s.bench_eval_pass(True, 3)
 s.sync()
 s.bench_kernel_ms()
 t3 = time.perf_counter()
-for _ in range(10):
-    s.bench_eval_pass(True)
+s.bench_eval_pass(True, 10)
 s.sync()
 dt = (time.perf_counter() - t3) / 10
 j, a = s.bench_kernel_ms()
