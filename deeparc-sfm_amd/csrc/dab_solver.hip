@@ -1589,11 +1589,12 @@ extern "C" int dab_jacobian_bytes(dab_handle* h, double* bytes) {
   // Algorithmic bytes of one launch of the point-side evaluation kernel (k_eval_points,
   // matrix-free residual + Jacobian reduced into V, g): the SURVEY §8d input terms
   // (16 xy + 4 n_idx per observation, n_idx = 2 single / 3 arc∘ring; 24 per point,
-  // 48 per intrinsic) plus what the kernel must read and write instead of the stored
-  // Jacobian: the R, t part of each camera table (96 B) and V, g per point (72 B).
-  // The Jacobian itself never reaches HBM, so its 16 k bytes per observation are not
-  // counted (they are not moved).
-  double b = (24.0 + 72.0) * h->NP + 96.0 * h->E + 48.0 * h->NI;
+  // 48 per intrinsic, 48 per extrinsic) plus the outputs V, g per point (72 B). The
+  // LDS variants build R, t from the 48-B extrinsics; the global-table variants read the
+  // 96-B R, t part of the camera tables instead. The Jacobian itself never reaches HBM, so
+  // its 16 k bytes per observation are not counted (they are not moved).
+  const double ext_b = eval_points_needs_camtab(h->eval_wps) ? 96.0 : 48.0;
+  double b = (24.0 + 72.0) * h->NP + ext_b * h->E + 48.0 * h->NI;
   for (int o = 0; o < h->N; ++o) b += 16.0 + 4.0 * (h->prob.obs_ext1[o] >= 0 ? 3 : 2);
   *bytes = b;
   return 0;
