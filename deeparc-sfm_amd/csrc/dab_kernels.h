@@ -163,6 +163,12 @@ void launch_pcg_setup(hipStream_t s, int NC, const double* ug, const double* sca
 void launch_pcg_init(hipStream_t s, int NC, const double* bvec, const int* fail, PcgState* st, double eta,
                      int min_iter, int max_iter, const double* Minv, const double* r, double* z, double* p);
 // the two Y passes of S vec: t[NP][4], partial[chunk][6] (= -sum Y t per chunk)
+// fused single-pass matvec for NC <= 160 cameras: w = -sum_e Y_e t_p(e) with the point-major
+// records only; partial[grid][6 NC] scratch
+bool pcg_fused_fits(int NC);
+int pcg_fused_grid(int NP, int ncu);
+void launch_pcg_fused(hipStream_t s, const DevView& v, YBufs Y, const double* vec, double* partial, double* w,
+                      int grid, const PcgState* st);
 void launch_pcg_matvec_passes(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, YBufs Y,
                               const double* vec, double* t, double* partial, const PcgState* st);
 // mode 0: q = S p, alpha, x, r, Q-test; 1: q = S p, alpha, x; 2: r = b - S x, Q-test.

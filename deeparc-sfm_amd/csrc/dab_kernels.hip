@@ -384,7 +384,7 @@ struct UniTabs {
     for (int q = 0; q < 6; ++q) o[q] = K[q];
   }
 };
-template <bool K_IN_LDS>
+template <bool K_IN_LDS, bool KMASK = false>
 struct LdsTabs {
   const double* rt_s;  // LDS [E][12]: R t
   const double* k_s;   // LDS [NI][6] when K_IN_LDS
@@ -402,7 +402,7 @@ struct LdsTabs {
   __device__ __forceinline__ void dj(int e, double (&T)[18]) const { load_tab_at<12, 18>(camtab, e, T); }
   __device__ __forceinline__ void k(int i, double (&K)[6]) const {
     if constexpr (K_IN_LDS) {
-      const double2* p = reinterpret_cast<const double2*>(k_s + 6 * i);
+      const double2* p = reinterpret_cast<const double2*>(k_s + 6 * (KMASK ? (i & 127) : i));
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         const double2 v = p[q];
@@ -704,7 +704,7 @@ __global__ __launch_bounds__(64 * WPS) void k_eval_points(DevView v, const doubl
 // ds_read_b128 instead of 64-line L2 gathers. Persistent: one 1024-thread work-group per
 // CU, 16 / WPS slices in flight (WPS waves each, rows split, LDS-combined).
 constexpr int kLdsCams = 1024;
-template <int KI, int WPS>
+template <int KI, int WPS, bool KMASK = false>  // KMASK: ablation (wrong K, all from LDS)
 __global__ __launch_bounds__(1024) void k_eval_points_lds(DevView v, const double* __restrict__ points,
                                                           const double* __restrict__ ext,
                                                           const double* __restrict__ camtab,
@@ -724,19 +724,22 @@ __global__ __launch_bounds__(1024) void k_eval_points_lds(DevView v, const doubl
     for (int q = 0; q < 12; ++q) rt_s[12 * e + q] = T[q];
   }
   if constexpr (KI > 0) {
-    for (int i = threadIdx.x; i < v.NI * 3; i += blockDim.x) {
+    for (int i = threadIdx.x; i < (KMASK ? min(v.NI, KI) : v.NI) * 3; i += blockDim.x) {
       const int n = i / 3, q = i - 3 * (i / 3);
       reinterpret_cast<double2*>(k_s)[i] = reinterpret_cast<const double2*>(v.intr + (size_t)kIntr * n)[q];
     }
   }
   __syncthreads();
-  const LdsTabs<(KI > 0)> tabs{rt_s, k_s, camtab, v.intr};
+  const LdsTabs<(KI > 0), KMASK> tabs{rt_s, k_s, camtab, v.intr};
   const int wave = threadIdx.x >> 6, grp = wave / WPS, w = wave % WPS;
   double acc[2] = {0.0, 0.0};
-  const int per_round = G * gridDim.x;
-  const int rounds = (v.nslice + per_round - 1) / per_round;
+  // slices dealt round robin over the work-groups (slot q of work-group b takes slice
+  // q * grid + b): every CU gets a share even when the slices are few (C3: 1,563 slices
+  // for 256 CUs), and the long slices (sorted first) spread over all of them
+  const int per_wg = (v.nslice + gridDim.x - 1) / gridDim.x;
+  const int rounds = (per_wg + G - 1) / G;
   for (int r = 0; r < rounds; ++r)
-    eval_slice<WPS, 0>(v, points, tabs, V, g, (r * gridDim.x + blockIdx.x) * G + grp, w, sh[grp], acc);
+    eval_slice<WPS, 0>(v, points, tabs, V, g, (r * G + grp) * gridDim.x + blockIdx.x, w, sh[grp], acc);
   store_cost_partial_last<16>(acc, partial, arrivals, cost);
 }
 
@@ -753,6 +756,10 @@ void launch_eval_points(hipStream_t s, const DevView& v, const double* points, c
       if (v.NI <= 128) k_eval_points_lds<128, 2><<<grid, 1024, 0, s>>>(v, points, ext, camtab, V, g, partial, arrivals, cost);
       else k_eval_points_lds<0, 2><<<grid, 1024, 0, s>>>(v, points, ext, camtab, V, g, partial, arrivals, cost);
     }
+    return;
+  }
+  if (wps == -5) {  // ablation: intrinsic index masked to the 128 staged in LDS (timing only)
+    k_eval_points_lds<128, 2, true><<<grid, 1024, 0, s>>>(v, points, ext, camtab, V, g, partial, arrivals, cost);
     return;
   }
   if (wps == 41) {  // ablations

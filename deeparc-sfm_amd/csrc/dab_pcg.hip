@@ -23,6 +23,9 @@
 // every rank.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include <cfloat>
 
 #include "dab_kernels.h"
@@ -313,6 +316,99 @@ __global__ __launch_bounds__(256) void k_pcg_point_pass(DevView v, const YT* __r
   reinterpret_cast<double2*>(t)[2 * (size_t)p + 1] = make_double2(t2, 0.0);
 }
 
+// Fused matvec for small camera systems (NC <= kFuseCams, e.g. the rig's 79 cameras): one
+// pass over the point-major Y records computes t_p = sum_e Y_e^T v_c(e) and then, re-reading
+// the point's records (L2-resident by then), adds -Y_e t_p into per-wave camera
+// accumulators in LDS. The camera-major copy of Y is not read, so the records cross HBM once
+// per product instead of twice (the re-read of a point's records mostly misses L2: 443 us
+// per product at C5 fp32 against 240 us for the first half alone and 706 us for the two
+// camera/point passes). Each wave owns its accumulator (LDS atomics only between
+// the lanes of one instruction, which the LDS resolves in a fixed order), the waves and
+// then the work-groups are summed in a fixed order: bitwise reproducible.
+constexpr int kFuseCams = 160;
+constexpr int kFuseBlock = 256;
+template <class YT>
+__global__ __launch_bounds__(kFuseBlock) void k_pcg_fused(DevView v, const YT* __restrict__ Ypm,
+                                                          const double* __restrict__ vec,
+                                                          double* __restrict__ partial, const PcgState* st) {
+  extern __shared__ double accs[];  // [kFuseBlock / 64][6 NC]
+  if (st->status != kPcgRunning) return;
+  const int NC6 = 6 * v.NC, w = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < (kFuseBlock / 64) * NC6; i += blockDim.x) accs[i] = 0.0;
+  __syncthreads();
+  double* acc = accs + w * NC6;
+  const size_t NS = (size_t)v.N;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < v.NP; p += gridDim.x * blockDim.x) {
+    const int sl = p >> 6, lane = p & 63;
+    const int off = v.slice_off[sl], len = (v.slice_off[sl + 1] - off) >> 6;
+    double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+    for (int k = 0; k < len; ++k) {
+      const int s = off + 64 * k + lane;
+      const int4 id = v.obs_idx[s];
+      if (id.x < 0) continue;
+#pragma unroll
+      for (int slot = 0; slot < 2; ++slot) {
+        const int e = slot ? id.z : id.y;
+        const int c = e >= 0 ? v.ext_col[e] : -1;
+        if (c < 0) continue;
+        double y[18];
+        load_yplane(Ypm + slot * 18 * NS, NS, (size_t)s, y);
+        const double2* v2 = reinterpret_cast<const double2*>(vec + 6 * (size_t)c);
+        double vc[6];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const double2 u = v2[q];
+          vc[2 * q] = u.x;
+          vc[2 * q + 1] = u.y;
+        }
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          t0 += y[3 * a] * vc[a];
+          t1 += y[3 * a + 1] * vc[a];
+          t2 += y[3 * a + 2] * vc[a];
+        }
+      }
+    }
+    for (int k = 0; k < len; ++k) {
+      const int s = off + 64 * k + lane;
+      const int4 id = v.obs_idx[s];
+      if (id.x < 0) continue;
+#pragma unroll
+      for (int slot = 0; slot < 2; ++slot) {
+        const int e = slot ? id.z : id.y;
+        const int c = e >= 0 ? v.ext_col[e] : -1;
+        if (c < 0) continue;
+        double y[18];
+        load_yplane(Ypm + slot * 18 * NS, NS, (size_t)s, y);
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+          atomicAdd(acc + 6 * c + a, -(y[3 * a] * t0 + y[3 * a + 1] * t1 + y[3 * a + 2] * t2));
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NC6; i += blockDim.x) {
+    double x = accs[i];
+#pragma unroll
+    for (int q = 1; q < kFuseBlock / 64; ++q) x += accs[q * NC6 + i];
+    partial[(size_t)blockIdx.x * NC6 + i] = x;
+  }
+}
+
+// w[i] = sum over the G work-group partials, fixed order (one block per output)
+__global__ __launch_bounds__(256) void k_pcg_fused_final(int G, int NC6, const double* __restrict__ partial,
+                                                         double* __restrict__ w, const PcgState* st) {
+  if (st->status != kPcgRunning) return;
+  const int i = blockIdx.x;
+  double x = 0.0;
+  for (int b = threadIdx.x; b < G; b += blockDim.x) x += partial[(size_t)b * NC6 + i];
+  __shared__ double sh[4];
+  const double t = wave_sum_lane63(x);
+  if ((threadIdx.x & 63) == 63) sh[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) w[i] = ((sh[0] + sh[1]) + sh[2]) + sh[3];
+}
+
 // camera pass: per chunk of positions -sum Y_pos t_pt(pos) -> partial[chunk][6]
 template <class YT>
 __global__ __launch_bounds__(256) void k_pcg_cam_pass(DevView v, const int* __restrict__ chunk_beg,
@@ -348,48 +444,58 @@ __global__ __launch_bounds__(256) void k_pcg_cam_pass(DevView v, const int* __re
 }
 
 // (A_cc + cross) vec + w for camera c, component-wise into out[6]
-__device__ __forceinline__ void apply_cam(int c, const double* __restrict__ Ad, const double* __restrict__ vec,
-                                          const double* __restrict__ w, const int* __restrict__ xptr,
-                                          const int* __restrict__ xlist, const int2* __restrict__ xcam,
-                                          const double* __restrict__ X, const double* __restrict__ scc,
-                                          double (&out)[6]) {
-  const double* ad = Ad + 36 * (size_t)c;
-  double vc[6];
+// S_cc v_c + w_c + sum of the cross terms of camera c, by the L consecutive lanes s of a
+// group (L = 16 with cross blocks, else 1): lane s takes every L-th cross block of c, the
+// diagonal goes to lane 0, and the L partials are combined by a fixed xor tree (every lane
+// of the group ends with the same sum). Cameras with ~60 cross blocks (rig arc cameras) no
+// longer serialise one lane.
+__device__ __forceinline__ void apply_cam8(int c, int s, int L, const double* __restrict__ Ad,
+                                           const double* __restrict__ vec, const double* __restrict__ w,
+                                           const int* __restrict__ xptr, const int* __restrict__ xlist,
+                                           const int2* __restrict__ xcam, const double* __restrict__ X,
+                                           const double* __restrict__ scc, double (&out)[6]) {
 #pragma unroll
-  for (int b = 0; b < 6; ++b) vc[b] = vec[6 * c + b];
+  for (int a = 0; a < 6; ++a) out[a] = 0.0;
+  if (c >= 0) {
+    if (s == 0) {
+      const double* ad = Ad + 36 * (size_t)c;
+      double vc[6];
 #pragma unroll
-  for (int a = 0; a < 6; ++a) {
-    double t = w[6 * c + a];
+      for (int b = 0; b < 6; ++b) vc[b] = vec[6 * c + b];
 #pragma unroll
-    for (int b = 0; b < 6; ++b) t += ad[6 * a + b] * vc[b];
-    out[a] = t;
-  }
-  if (xptr) {
-    for (int j = xptr[c]; j < xptr[c + 1]; ++j) {
-      const int code = xlist[j], k = code >> 1;
-      const int2 cc = xcam[k];  // X_k = Jc0^T Jc1, block (c0, c1)
-      const double* xk = X + 36 * (size_t)k;
-      if ((code & 1) == 0) {  // c == c0: out += (s0 X s1) v_c1
-        const int o = cc.y;
+      for (int a = 0; a < 6; ++a) {
+        double t = w[6 * c + a];
 #pragma unroll
-        for (int a = 0; a < 6; ++a) {
-          double t = 0.0;
-#pragma unroll
-          for (int b = 0; b < 6; ++b) t += xk[6 * a + b] * scc[6 * o + b] * vec[6 * o + b];
-          out[a] += scc[6 * c + a] * t;
-        }
-      } else {  // c == c1: out += (s0 X s1)^T v_c0
-        const int o = cc.x;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-          double t = 0.0;
-#pragma unroll
-          for (int b = 0; b < 6; ++b) t += xk[6 * b + a] * scc[6 * o + b] * vec[6 * o + b];
-          out[a] += scc[6 * c + a] * t;
-        }
+        for (int b = 0; b < 6; ++b) t += ad[6 * a + b] * vc[b];
+        out[a] = t;
       }
     }
+    if (xptr) {
+      double cr[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      for (int j = xptr[c] + s; j < xptr[c + 1]; j += L) {
+        const int code = xlist[j], k = code >> 1;
+        const int2 cc = xcam[k];  // X_k = Jc0^T Jc1, block (c0, c1)
+        const double* xk = X + 36 * (size_t)k;
+        const bool first = (code & 1) == 0;  // c == c0: (s0 X s1) v_c1, else (s0 X s1)^T v_c0
+        const int o = first ? cc.y : cc.x;
+        double sv[6];
+#pragma unroll
+        for (int b = 0; b < 6; ++b) sv[b] = scc[6 * o + b] * vec[6 * o + b];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          double t = 0.0;
+#pragma unroll
+          for (int b = 0; b < 6; ++b) t += (first ? xk[6 * a + b] : xk[6 * b + a]) * sv[b];
+          cr[a] += t;
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < 6; ++a) out[a] += scc[6 * c + a] * cr[a];
+    }
   }
+  for (int m = 1; m < L; m <<= 1)
+#pragma unroll
+    for (int a = 0; a < 6; ++a) out[a] += __shfl_xor(out[a], m, L);
 }
 
 // one work-group. mode 0: q = S p, alpha, x += alpha p, r -= alpha q, Q-test
@@ -408,15 +514,21 @@ __global__ __launch_bounds__(kOneWG) void k_pcg_update(int NC, int mode, const d
   __shared__ int s_status;
   if (st->status != kPcgRunning) return;
   int status = kPcgRunning;
+  const int L = xptr ? 16 : 1;  // lanes per camera
+  const int s8 = threadIdx.x & (L - 1), cpp = blockDim.x / L;
+  const int cam_rounds = (NC + cpp - 1) / cpp;
   if (mode != 2) {
     double acc = 0.0;
-    for (int c = threadIdx.x; c < NC; c += blockDim.x) {
+    for (int rr = 0; rr < cam_rounds; ++rr) {
+      const int c = rr * cpp + threadIdx.x / L;
       double o[6];
-      apply_cam(c, Ad, p, w, xptr, xlist, xcam, X, scc, o);
+      apply_cam8(c < NC ? c : -1, s8, L, Ad, p, w, xptr, xlist, xcam, X, scc, o);
+      if (c < NC && s8 == 0) {
 #pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        q[6 * c + a] = o[a];
-        acc += p[6 * c + a] * o[a];
+        for (int a = 0; a < 6; ++a) {
+          q[6 * c + a] = o[a];
+          acc += p[6 * c + a] * o[a];
+        }
       }
     }
     const double pq = wg_sum(acc, sh);
@@ -440,11 +552,14 @@ __global__ __launch_bounds__(kOneWG) void k_pcg_update(int NC, int mode, const d
     }
     if (mode == 1) return;
   } else {
-    for (int c = threadIdx.x; c < NC; c += blockDim.x) {
+    for (int rr = 0; rr < cam_rounds; ++rr) {
+      const int c = rr * cpp + threadIdx.x / L;
       double o[6];
-      apply_cam(c, Ad, x, w, xptr, xlist, xcam, X, scc, o);
+      apply_cam8(c < NC ? c : -1, s8, L, Ad, x, w, xptr, xlist, xcam, X, scc, o);
+      if (c < NC && s8 == 0) {
 #pragma unroll
-      for (int a = 0; a < 6; ++a) r[6 * c + a] = bvec[6 * c + a] - o[a];
+        for (int a = 0; a < 6; ++a) r[6 * c + a] = bvec[6 * c + a] - o[a];
+      }
     }
   }
   double acc = 0.0;
@@ -494,6 +609,18 @@ void launch_pcg_init(hipStream_t s, int NC, const double* bvec, const int* fail,
   k_pcg_init<<<1, kOneWG, 0, s>>>(NC, bvec, fail, st, eta, min_iter, max_iter, Minv, r, z, p);
 }
 
+
+bool pcg_fused_fits(int NC) { return NC > 0 && NC <= kFuseCams; }
+int pcg_fused_grid(int NP, int ncu) { return std::max(1, std::min((NP + kFuseBlock - 1) / kFuseBlock, 4 * ncu)); }
+
+void launch_pcg_fused(hipStream_t s, const DevView& v, YBufs Y, const double* vec, double* partial, double* w,
+                      int grid, const PcgState* st) {
+  const int NC6 = 6 * v.NC;
+  const size_t lds = sizeof(double) * (kFuseBlock / 64) * NC6;
+  if (Y.f32) k_pcg_fused<float><<<grid, kFuseBlock, lds, s>>>(v, (const float*)Y.pm, vec, partial, st);
+  else k_pcg_fused<double><<<grid, kFuseBlock, lds, s>>>(v, (const double*)Y.pm, vec, partial, st);
+  k_pcg_fused_final<<<NC6, 256, 0, s>>>(grid, NC6, partial, w, st);
+}
 
 void launch_pcg_matvec_passes(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, YBufs Y,
                               const double* vec, double* t, double* partial, const PcgState* st) {

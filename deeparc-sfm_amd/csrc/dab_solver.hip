@@ -185,6 +185,9 @@ struct dab_handle {
   int* h_flags = nullptr;      // pinned
   int red_grid = 1;
   int eval_grid = 1;  // k_eval_points blocks (one SELL slice per block)
+  int ncu = 256;      // compute units of the device
+  int fused_grid = 0;  // > 0: single-pass PCG matvec (small camera systems)
+  double* d_fused_partial = nullptr;
   int eval_wps = 0;   // 0: LDS tables; else waves per slice (DAB_EVAL_WPS tuning knob)
 
   ~dab_handle() {
@@ -742,9 +745,9 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, h->device) == hipSuccess && prop.multiProcessorCount > 0)
       ncu = prop.multiProcessorCount;
-    const int in_flight = h->eval_wps == 0 ? 4 : (h->eval_wps == -1 ? 16 : 8);  // slices per work-group
-    h->eval_grid = h->eval_wps <= 0 ? std::max(1, std::min(ncu, (h->nslice + in_flight - 1) / in_flight))
-                                    : std::max(1, h->nslice);
+    h->ncu = ncu;
+    // LDS variants: one persistent work-group per CU (at most one per slice)
+    h->eval_grid = h->eval_wps <= 0 ? std::max(1, std::min(ncu, h->nslice)) : std::max(1, h->nslice);
   }
   CHECK_RC(d.alloc(&h->d_gpart, (size_t)std::max(h->red_grid, h->eval_grid) * 4));
   CHECK_RC(d.alloc(&h->d_scal, S_NSLOTS));
@@ -898,6 +901,12 @@ static int build_pcg_buffers(dab_handle* h) {
   CHECK_RC(d.alloc(&h->d_pcg_red, (size_t)27 * h->NC));
   CHECK_RC(d.alloc(&h->d_pcg_t, (size_t)4 * h->NP));
   CHECK_RC(d.alloc(&h->d_pcg_state, 1));
+  // the single-pass matvec when the camera system is small (DAB_PCG_FUSED=0 disables it)
+  const char* fz = getenv("DAB_PCG_FUSED");
+  if (pcg_fused_fits(h->NC) && h->NP > 0 && !(fz && atoi(fz) == 0)) {
+    h->fused_grid = pcg_fused_grid(h->NP, h->ncu);
+    CHECK_RC(d.alloc(&h->d_fused_partial, (size_t)h->fused_grid * 6 * h->NC));
+  }
   if (!h->h_pcg_state &&
       hipHostMalloc(reinterpret_cast<void**>(&h->h_pcg_state), sizeof(PcgState)) != hipSuccess)
     return set_error(DAB_E_NOMEM, "pinned PCG state allocation failed");
@@ -908,6 +917,11 @@ static int build_pcg_buffers(dab_handle* h) {
 // S vec (Y part) -> d_pcg_w, all-reduced across ranks
 static int pcg_matvec(dab_handle* h, YBufs yb, const double* vec) {
   hipStream_t s = h->stream;
+  if (h->fused_grid > 0) {
+    launch_pcg_fused(s, h->view, yb, vec, h->d_fused_partial, h->d_pcg_w, h->fused_grid, h->d_pcg_state);
+    CHECK_RC(h->allreduce(h->d_pcg_w, (size_t)6 * h->NC, ncclSum));
+    return 0;
+  }
   const bool direct = h->nchunk == h->NC;
   launch_pcg_matvec_passes(s, h->view, h->nchunk, h->d_chunk_beg, yb, vec, h->d_pcg_t,
                            direct ? h->d_pcg_w : h->d_partial, h->d_pcg_state);

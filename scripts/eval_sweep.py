@@ -10,7 +10,7 @@ import _pkgload  # noqa: E402
 pkg = _pkgload.load()
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3_1kcam"
 prob = pkg.synth(**pkg.CONFIGS[cfg])
-for wps, chunk, noev in ((-2, 4096, 0), (-2, 4096, 1)):
+for wps, chunk, noev in ((-2, 4096, 0), (-5, 4096, 0), (42, 4096, 0), (41, 4096, 0)):
     os.environ["DAB_CHUNK"] = str(chunk)
     os.environ["DAB_EVAL_WPS"] = str(wps)
     os.environ["DAB_BENCH_SAMPLE"] = "0" if noev else "8"

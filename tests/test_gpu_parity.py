@@ -153,6 +153,34 @@ def test_lm_pcg_fp32_reaches_same_minimum(pkg, gpu, kind):
     assert res[1]["termination"] == "CONVERGENCE"
 
 
+@pytest.mark.parametrize("kind", ["bal", "rig"])
+def test_pcg_fused_matvec_matches_two_pass(pkg, gpu, kind, monkeypatch):
+    """Small camera systems use the single-pass S*p (per-wave LDS camera accumulators);
+    DAB_PCG_FUSED=0 forces the camera-major + point-major passes. Both must give the same
+    LM trajectory: per-iteration cost 1e-9 relative and the same CG iteration counts
+    (only the summation order of S*p differs). The fused one must be bitwise repeatable."""
+    if kind == "bal":
+        prob = pkg.synth(kind=0, num_cameras=60, num_points=4000, obs_per_point=7, seed=41)
+    else:
+        prob = pkg.synth(kind=1, num_arcs=6, num_rings=16, num_points=3000, obs_per_point=8, seed=42)
+    opts = dict(max_num_iterations=15, linear_solver_type=pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)
+    res, pts = [], []
+    for fused in ("1", "0", "1"):
+        monkeypatch.setenv("DAB_PCG_FUSED", fused)
+        p = prob.copy()
+        s = pkg.Solver(0)
+        s.set_problem(p)
+        res.append(s.solve(pkg.options(**opts)))
+        s.close()
+        pts.append(p.points.copy())
+    a, b = res[0], res[1]
+    assert [it["linear_solver_iterations"] for it in a["iterations"]] == \
+        [it["linear_solver_iterations"] for it in b["iterations"]]
+    np.testing.assert_allclose([it["cost"] for it in a["iterations"]], [it["cost"] for it in b["iterations"]],
+                               rtol=1e-9)
+    np.testing.assert_array_equal(pts[0], pts[2])  # fused path: bitwise repeatable
+
+
 def test_lm_freeze_camera_matches_oracle(pkg, orc, gpu):
     prob = pkg.synth(kind=1, num_arcs=4, num_rings=10, num_points=2000, obs_per_point=6, seed=23)
     prob.freeze_camera = True  # solve(..., freeze_camera=true), sfm.cc:111
