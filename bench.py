@@ -14,7 +14,9 @@ metric (BASELINE.json): "M observations/sec residual+Jacobian; wall-clock/LM-ite
           (the reference's DENSE_SCHUR), lm_pcg_* with implicit-Schur PCG, lm_pcg32_* with
           the mixed-precision PCG (fp32 Schur factors).
   rig_*:  BASELINE config 5 (rig 16 x 64, 1M points, 10M observations) point-sharded over
-          the N ranks (strong scaling), mixed-precision PCG, wall-clock per LM iteration.
+          the N ranks (strong scaling): the evaluation pass (step time, M obs/s, the point
+          kernel's time and HBM roofline fraction on rank 0's shard) and the mixed-precision
+          PCG LM iteration (wall-clock, median).
   roofline: k_eval_points (point side of the pass), algorithmic bytes / HIP-event time.
   cpu_baseline: the C oracle (Ceres-semantics restatement, OpenMP) on the box's host
           cores, rank 0 at N=1 only, bounded sample.
@@ -168,6 +170,24 @@ def main():
         rsolver.set_problem(rprob)
         t_set = time.perf_counter() - t_set
         barrier()
+        # the rig's evaluation pass (same contract as the headline step, strong scaling)
+        rsolver.bench_eval_pass(True, 5)
+        rsolver.sync()
+        rsolver.bench_kernel_ms()
+        barrier()
+        rsolver.sync()
+        t_ev = time.perf_counter()
+        rsolver.bench_eval_pass(True, 40)
+        rsolver.sync()
+        barrier()
+        ev_dt = max_over_ranks(time.perf_counter() - t_ev) / 40
+        r_jac_ms, _ = rsolver.bench_kernel_ms()
+        r_jac_ms = max_over_ranks(r_jac_ms)
+        r_bytes = rsolver.jacobian_bytes()
+        r_gbs = r_bytes / (r_jac_ms * 1e-3) / 1e9
+        rig_eval = {"rig_eval_ms_per_step": 1e3 * ev_dt, "rig_eval_mobs_per_s": gprob.num_obs / ev_dt / 1e6,
+                    "rig_point_kernel_ms": r_jac_ms, "rig_point_kernel_bytes_per_launch_rank0": r_bytes,
+                    "rig_point_kernel_roofline_frac": r_gbs / HBM_PEAK_GBS}
         opts = pkg.options(max_num_iterations=args.lm_iters, function_tolerance=0.0, gradient_tolerance=0.0,
                            parameter_tolerance=0.0, linear_solver_type=pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG,
                            pcg_fp32=1)
@@ -178,7 +198,7 @@ def main():
                "rig_lm_iterations": summ["num_iterations"],
                "rig_lm_linear_iterations": [it["linear_solver_iterations"] for it in summ["iterations"][1:]],
                "rig_initial_cost": summ["initial_cost"], "rig_final_cost": summ["final_cost"],
-               "rig_set_problem_s": max_over_ranks(t_set)}
+               "rig_set_problem_s": max_over_ranks(t_set), **rig_eval}
         rsolver.close()
         del gprob, rprob
 
