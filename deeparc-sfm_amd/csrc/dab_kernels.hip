@@ -384,6 +384,55 @@ struct UniTabs {
     for (int q = 0; q < 6; ++q) o[q] = K[q];
   }
 };
+
+// Every extrinsic's R t Rd Jd and every intrinsic staged in LDS once per block (small
+// camera sets: the rig's 79 extrinsics and 16 intrinsics take 20 KB); per-entry table
+// reads then come from LDS instead of L2 gathers.
+constexpr int kSmallTabs = 128;   // E and NI limit
+constexpr int kSmallGrid = 2048;  // grid-stride blocks of the staged-table variants
+__host__ __device__ inline bool small_tabs_fit(int E, int NI) { return E <= kSmallTabs && NI <= kSmallTabs; }
+__host__ __device__ inline size_t small_tabs_bytes(int E, int NI) { return sizeof(double) * (30 * (size_t)E + 6 * (size_t)NI); }
+struct SmallTabs {
+  const double* t_s;  // LDS [E][30]
+  const double* k_s;  // LDS [NI][6]
+  __device__ __forceinline__ void rt(int e, double (&o)[12]) const {
+    const double2* p = reinterpret_cast<const double2*>(t_s + 30 * e);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const double2 u = p[q];
+      o[2 * q] = u.x;
+      o[2 * q + 1] = u.y;
+    }
+  }
+  __device__ __forceinline__ void dj(int e, double (&o)[18]) const {
+    const double2* p = reinterpret_cast<const double2*>(t_s + 30 * e + 12);
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      const double2 u = p[q];
+      o[2 * q] = u.x;
+      o[2 * q + 1] = u.y;
+    }
+  }
+  __device__ __forceinline__ void k(int i, double (&o)[6]) const {
+    const double2* p = reinterpret_cast<const double2*>(k_s + 6 * i);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const double2 u = p[q];
+      o[2 * q] = u.x;
+      o[2 * q + 1] = u.y;
+    }
+  }
+};
+// block-cooperative staging into dynamic LDS; returns the table view (barrier inside)
+__device__ __forceinline__ SmallTabs stage_small_tabs(double* lds, int E, int NI, const double* __restrict__ camtab,
+                                                      const double* __restrict__ intr) {
+  double* t_s = lds;
+  double* k_s = lds + 30 * (size_t)E;
+  for (int i = threadIdx.x; i < 30 * E; i += blockDim.x) t_s[i] = camtab[(size_t)kCamTab * (i / 30) + i % 30];
+  for (int i = threadIdx.x; i < 6 * NI; i += blockDim.x) k_s[i] = intr[(size_t)kIntr * (i / 6) + i % 6];
+  __syncthreads();
+  return SmallTabs{t_s, k_s};
+}
 template <bool K_IN_LDS, bool KMASK = false>
 struct LdsTabs {
   const double* rt_s;  // LDS [E][12]: R t
@@ -502,11 +551,11 @@ __device__ __forceinline__ void obs_rows(const int4 id, const double2 xy, const 
 }
 
 // Every row of one observation (parity API, cross blocks, candidate pass).
-__device__ __forceinline__ void obs_jacobian(const int4 id, const double2 xy, const double X[3],
-                                             const double* __restrict__ camtab,
-                                             const double* __restrict__ intr, ObsJac& o) {
+template <class Tabs>
+__device__ __forceinline__ void obs_jacobian_t(const int4 id, const double2 xy, const double X[3], const Tabs& tb,
+                                               ObsJac& o) {
   double c0[6], c1[6], d0[6], d1[6];
-  obs_rows<true, 2>(id, xy, X, GlobalTabs{camtab, intr}, o.pr.ru, o.pr.rv, o.jx0, o.jx1, c0, c1, d0, d1);
+  obs_rows<true, 2>(id, xy, X, tb, o.pr.ru, o.pr.rv, o.jx0, o.jx1, c0, c1, d0, d1);
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     o.jw0a[i] = c0[i];
@@ -518,6 +567,11 @@ __device__ __forceinline__ void obs_jacobian(const int4 id, const double2 xy, co
     o.jt1a[i] = d0[3 + i];
     o.jt1b[i] = d1[3 + i];
   }
+}
+__device__ __forceinline__ void obs_jacobian(const int4 id, const double2 xy, const double X[3],
+                                             const double* __restrict__ camtab,
+                                             const double* __restrict__ intr, ObsJac& o) {
+  obs_jacobian_t(id, xy, X, GlobalTabs{camtab, intr}, o);
 }
 
 // Point side of the evaluation pass (rows a1-a4 + the point half of a7), matrix-free:
@@ -973,6 +1027,9 @@ __global__ __launch_bounds__(256) void k_eval_cams(DevView v, const int* __restr
   if constexpr (UNI) {
     const int2 u = v.chunk_uni[c];
     eval_cams_chunk(v, b, e, points, UniTabs(ext, v.intr, u.x, u.y), acc);
+  } else if (small_tabs_fit(v.E, v.NI)) {
+    extern __shared__ double tabs_lds[];
+    eval_cams_chunk(v, b, e, points, stage_small_tabs(tabs_lds, v.E, v.NI, camtab, v.intr), acc);
   } else {
     eval_cams_chunk(v, b, e, points, GlobalTabs{camtab, v.intr}, acc);
   }
@@ -984,9 +1041,11 @@ void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, con
   if (cl.nuni > 0)
     k_eval_cams<true><<<cl.nuni, 256, 0, s>>>(v, chunk_beg, cl.nuni == cl.nchunk ? nullptr : cl.uni, points, ext,
                                               camtab, partial);
-  if (cl.ngen > 0)
-    k_eval_cams<false><<<cl.ngen, 256, 0, s>>>(v, chunk_beg, cl.ngen == cl.nchunk ? nullptr : cl.gen, points, ext,
-                                               camtab, partial);
+  if (cl.ngen > 0) {
+    const size_t lds = small_tabs_fit(v.E, v.NI) ? small_tabs_bytes(v.E, v.NI) : 0;
+    k_eval_cams<false><<<cl.ngen, 256, lds, s>>>(v, chunk_beg, cl.ngen == cl.nchunk ? nullptr : cl.gen, points,
+                                                 ext, camtab, partial);
+  }
 }
 
 // arc∘ring cross blocks Jc0^T Jc1, one block per chunk of composed observations sorted
@@ -1002,11 +1061,16 @@ __global__ __launch_bounds__(256) void k_eval_cross(DevView v, const int* __rest
   double acc[36];
 #pragma unroll
   for (int i = 0; i < 36; ++i) acc[i] = 0.0;
+  extern __shared__ double tabs_lds[];
+  const bool small = small_tabs_fit(v.E, v.NI);
+  SmallTabs st{nullptr, nullptr};
+  if (small) st = stage_small_tabs(tabs_lds, v.E, v.NI, camtab, v.intr);
   for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
     const int4 id = x_idx[i];
     const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
     ObsJac o;
-    obs_jacobian(id, x_xy[i], X, camtab, v.intr, o);
+    if (small) obs_jacobian_t(id, x_xy[i], X, st, o);
+    else obs_jacobian(id, x_xy[i], X, camtab, v.intr, o);
     const double qa[12] = {o.jw0a[0], o.jw0a[1], o.jw0a[2], o.pr.A0[0], o.pr.A0[1], o.pr.A0[2],
                            o.jw0b[0], o.jw0b[1], o.jw0b[2], o.pr.A1[0], o.pr.A1[1], o.pr.A1[2]};
     const double qb[12] = {o.jw1a[0], o.jw1a[1], o.jw1a[2], o.jt1a[0], o.jt1a[1], o.jt1a[2],
@@ -1022,7 +1086,8 @@ __global__ __launch_bounds__(256) void k_eval_cross(DevView v, const int* __rest
 void launch_eval_cross(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
                        const double2* x_xy, const double* points, const double* camtab, double* partial) {
   if (nchunk <= 0) return;
-  k_eval_cross<<<nchunk, 256, 0, s>>>(v, chunk_beg, x_idx, x_xy, points, camtab, partial);
+  const size_t lds = small_tabs_fit(v.E, v.NI) ? small_tabs_bytes(v.E, v.NI) : 0;
+  k_eval_cross<<<nchunk, 256, lds, s>>>(v, chunk_beg, x_idx, x_xy, points, camtab, partial);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1104,65 +1169,86 @@ __device__ __forceinline__ void make_y(const double (&ja)[6], const double (&jb)
   }
 }
 
-template <class YT>
+// SMALL: the camera tables are staged in LDS (small_tabs_fit) and the grid strides
+template <class YT, bool SMALL>
 __global__ __launch_bounds__(256) void k_entry_y(DevView v, const double* __restrict__ points,
                                                  const double* __restrict__ camtab,
                                                  const double* __restrict__ scc,
                                                  const double* __restrict__ PU, YT* __restrict__ Ycm) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= v.NE) return;
-  int4 id = v.cm_idx[i];
-  const bool slot1 = (id.w & kSlotBit) != 0;
-  id.w &= ~kSlotBit;
-  const int c = v.ext_col[slot1 ? id.z : id.y];
-  const double2 xy = v.cm_xy[i];
-  const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
-  double ru, rv, jx0[3], jx1[3], ja[6], jb[6];
-  if (slot1) obs_rows<true, 1>(id, xy, X, GlobalTabs{camtab, v.intr}, ru, rv, jx0, jx1, ja, jb);
-  else obs_rows<true, 0>(id, xy, X, GlobalTabs{camtab, v.intr}, ru, rv, jx0, jx1, ja, jb);
-  double y[18];
-  make_y(ja, jb, jx0, jx1, scc + 6 * c, PU + 6 * (size_t)id.x, y);
-  store_yplane(Ycm, (size_t)v.NE, (size_t)i, y);
+  extern __shared__ double tabs_lds[];
+  SmallTabs st{nullptr, nullptr};
+  if constexpr (SMALL) st = stage_small_tabs(tabs_lds, v.E, v.NI, camtab, v.intr);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < v.NE; i += gridDim.x * blockDim.x) {
+    int4 id = v.cm_idx[i];
+    const bool slot1 = (id.w & kSlotBit) != 0;
+    id.w &= ~kSlotBit;
+    const int c = v.ext_col[slot1 ? id.z : id.y];
+    const double2 xy = v.cm_xy[i];
+    const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
+    double ru, rv, jx0[3], jx1[3], ja[6], jb[6];
+    if constexpr (SMALL) {
+      if (slot1) obs_rows<true, 1>(id, xy, X, st, ru, rv, jx0, jx1, ja, jb);
+      else obs_rows<true, 0>(id, xy, X, st, ru, rv, jx0, jx1, ja, jb);
+    } else {
+      if (slot1) obs_rows<true, 1>(id, xy, X, GlobalTabs{camtab, v.intr}, ru, rv, jx0, jx1, ja, jb);
+      else obs_rows<true, 0>(id, xy, X, GlobalTabs{camtab, v.intr}, ru, rv, jx0, jx1, ja, jb);
+    }
+    double y[18];
+    make_y(ja, jb, jx0, jx1, scc + 6 * c, PU + 6 * (size_t)id.x, y);
+    store_yplane(Ycm, (size_t)v.NE, (size_t)i, y);
+  }
 }
 
-template <class YT>
+template <class YT, bool SMALL>
 __global__ __launch_bounds__(256) void k_entry_y_slots(DevView v, const double* __restrict__ points,
                                                        const double* __restrict__ camtab,
                                                        const double* __restrict__ scc,
                                                        const double* __restrict__ PU, YT* __restrict__ Ypm) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= v.N) return;
-  const int4 id = v.obs_idx[s];
-  if (id.x < 0) return;  // padding slot
-  const int c0 = v.ext_col[id.y], c1 = id.z >= 0 ? v.ext_col[id.z] : -1;
-  if (c0 < 0 && c1 < 0) return;
-  const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
-  double ru, rv, jx0[3], jx1[3], ja[6], jb[6], da[6], db[6];
-  obs_rows<true, 2>(id, v.obs_xy[s], X, GlobalTabs{camtab, v.intr}, ru, rv, jx0, jx1, ja, jb, da, db);
-  const double* pu = PU + 6 * (size_t)id.x;
+  extern __shared__ double tabs_lds[];
+  SmallTabs st{nullptr, nullptr};
+  if constexpr (SMALL) st = stage_small_tabs(tabs_lds, v.E, v.NI, camtab, v.intr);
   const size_t NS = (size_t)v.N;
-  double y[18];
-  if (c0 >= 0) {
-    make_y(ja, jb, jx0, jx1, scc + 6 * c0, pu, y);
-    store_yplane(Ypm, NS, (size_t)s, y);
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < v.N; s += gridDim.x * blockDim.x) {
+    const int4 id = v.obs_idx[s];
+    if (id.x < 0) continue;  // padding slot
+    const int c0 = v.ext_col[id.y], c1 = id.z >= 0 ? v.ext_col[id.z] : -1;
+    if (c0 < 0 && c1 < 0) continue;
+    const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
+    double ru, rv, jx0[3], jx1[3], ja[6], jb[6], da[6], db[6];
+    if constexpr (SMALL) obs_rows<true, 2>(id, v.obs_xy[s], X, st, ru, rv, jx0, jx1, ja, jb, da, db);
+    else obs_rows<true, 2>(id, v.obs_xy[s], X, GlobalTabs{camtab, v.intr}, ru, rv, jx0, jx1, ja, jb, da, db);
+    const double* pu = PU + 6 * (size_t)id.x;
+    double y[18];
+    if (c0 >= 0) {
+      make_y(ja, jb, jx0, jx1, scc + 6 * c0, pu, y);
+      store_yplane(Ypm, NS, (size_t)s, y);
+    }
+    if (c1 >= 0) {
+      make_y(da, db, jx0, jx1, scc + 6 * c1, pu, y);
+      store_yplane(Ypm + 18 * NS, NS, (size_t)s, y);
+    }
   }
-  if (c1 >= 0) {
-    make_y(da, db, jx0, jx1, scc + 6 * c1, pu, y);
-    store_yplane(Ypm + 18 * NS, NS, (size_t)s, y);
+}
+
+template <class YT>
+static void launch_entry_y_t(hipStream_t s, const DevView& v, const double* points, const double* camtab,
+                             const double* scale_c, const double* PU, YT* cm, YT* pm) {
+  const int g = grid_for(v.NE, 256, 1 << 20), gs = grid_for(v.N, 256, 1 << 20);
+  if (small_tabs_fit(v.E, v.NI)) {
+    const size_t lds = small_tabs_bytes(v.E, v.NI);
+    if (cm) k_entry_y<YT, true><<<std::min(g, kSmallGrid), 256, lds, s>>>(v, points, camtab, scale_c, PU, cm);
+    if (pm) k_entry_y_slots<YT, true><<<std::min(gs, kSmallGrid), 256, lds, s>>>(v, points, camtab, scale_c, PU, pm);
+  } else {
+    if (cm) k_entry_y<YT, false><<<g, 256, 0, s>>>(v, points, camtab, scale_c, PU, cm);
+    if (pm) k_entry_y_slots<YT, false><<<gs, 256, 0, s>>>(v, points, camtab, scale_c, PU, pm);
   }
 }
 
 void launch_entry_y(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                     const double* scale_c, const double* PU, YBufs Y, bool with_pm) {
   if (v.NE <= 0) return;
-  const int g = grid_for(v.NE, 256, 1 << 20), gs = grid_for(v.N, 256, 1 << 20);
-  if (Y.f32) {
-    k_entry_y<float><<<g, 256, 0, s>>>(v, points, camtab, scale_c, PU, (float*)Y.cm);
-    if (with_pm) k_entry_y_slots<float><<<gs, 256, 0, s>>>(v, points, camtab, scale_c, PU, (float*)Y.pm);
-  } else {
-    k_entry_y<double><<<g, 256, 0, s>>>(v, points, camtab, scale_c, PU, (double*)Y.cm);
-    if (with_pm) k_entry_y_slots<double><<<gs, 256, 0, s>>>(v, points, camtab, scale_c, PU, (double*)Y.pm);
-  }
+  if (Y.f32) launch_entry_y_t<float>(s, v, points, camtab, scale_c, PU, (float*)Y.cm, with_pm ? (float*)Y.pm : nullptr);
+  else launch_entry_y_t<double>(s, v, points, camtab, scale_c, PU, (double*)Y.cm, with_pm ? (double*)Y.pm : nullptr);
 }
 
 // one wave per S block; lane (a,b) < 36 accumulates -sum Y_row[a,:] . Y_col[b,:]
@@ -1361,12 +1447,23 @@ void launch_cam_candidate(hipStream_t s, int E, const int* ext_col, const double
 // Model cost change -(J delta).(r + J delta / 2) and the candidate residual at x + delta
 // in one observation pass; J and r at x are re-evaluated (bitwise what the evaluation
 // pass saw), the candidate point is formed as x + delta exactly as k_axpy_points does.
+template <bool SMALL>
 __global__ __launch_bounds__(256) void k_candidate(DevView v, const double* __restrict__ points,
                                                    const double* __restrict__ camtab,
                                                    const double* __restrict__ dp,
                                                    const double* __restrict__ dc,
                                                    const double* __restrict__ camtab_c,
                                                    double* __restrict__ partial) {
+  extern __shared__ double tabs_lds[];
+  SmallTabs st{nullptr, nullptr};
+  SmallTabs stc{nullptr, nullptr};  // R, t at x + delta (rt() only) in its own LDS region
+  if constexpr (SMALL) {
+    double* tc = tabs_lds + 30 * (size_t)v.E + 6 * (size_t)v.NI;
+    for (int i = threadIdx.x; i < 30 * v.E; i += blockDim.x)
+      tc[i] = camtab_c[(size_t)kCamTab * (i / 30) + i % 30];
+    st = stage_small_tabs(tabs_lds, v.E, v.NI, camtab, v.intr);  // barrier inside
+    stc = SmallTabs{tc, st.k_s};
+  }
   double acc[3] = {0.0, 0.0, 0.0};
   const size_t NPs = (size_t)v.NP;
   for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < v.N; s += gridDim.x * blockDim.x) {
@@ -1375,11 +1472,11 @@ __global__ __launch_bounds__(256) void k_candidate(DevView v, const double* __re
     const double2 xy = v.obs_xy[s];
     const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
     const double d3[3] = {dp[id.x], dp[NPs + id.x], dp[2 * NPs + id.x]};
-    const double* K = v.intr + (size_t)kIntr * id.w;
     double m0 = 0.0, m1 = 0.0, ru, rv;
     {
       ObsJac o;
-      obs_jacobian(id, xy, X, camtab, v.intr, o);
+      if constexpr (SMALL) obs_jacobian_t(id, xy, X, st, o);
+      else obs_jacobian(id, xy, X, camtab, v.intr, o);
       ru = o.pr.ru;
       rv = o.pr.rv;
 #pragma unroll
@@ -1419,19 +1516,26 @@ __global__ __launch_bounds__(256) void k_candidate(DevView v, const double* __re
     acc[0] += -(m0 * (ru + m0 / 2.0) + m1 * (rv + m1 / 2.0));
     // candidate residual at (x + delta)
     const double Xc[3] = {X[0] + d3[0], X[1] + d3[1], X[2] + d3[2]};
-    double T0[12];
-    load_tab<12>(camtab_c, id.y, T0);
+    double T0[12], Kc[6];
+    if constexpr (SMALL) {
+      stc.rt(id.y, T0);
+      stc.k(id.w, Kc);
+    } else {
+      load_tab<12>(camtab_c, id.y, T0);
+      load_intr(v.intr, id.w, Kc);
+    }
     double P[3];
     if (id.z >= 0) {
       double T1[12], P2[3];
-      load_tab<12>(camtab_c, id.z, T1);
+      if constexpr (SMALL) stc.rt(id.z, T1);
+      else load_tab<12>(camtab_c, id.z, T1);
       matvec_add(T1, Xc, T1 + 9, P2);
       matvec_add(T0, P2, T0 + 9, P);
     } else {
       matvec_add(T0, Xc, T0 + 9, P);
     }
     Proj pc;
-    project(P, K, xy.x, xy.y, pc, false);
+    project(P, Kc, xy.x, xy.y, pc, false);
     acc[1] += pc.ru * pc.ru + pc.rv * pc.rv;
     acc[2] += (isfinite(pc.ru) && isfinite(pc.rv)) ? 0.0 : 1.0;
   }
@@ -1441,7 +1545,12 @@ __global__ __launch_bounds__(256) void k_candidate(DevView v, const double* __re
 void launch_candidate(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                       const double* delta_p, const double* delta_c, const double* camtab_c, double* partial,
                       int grid) {
-  k_candidate<<<grid, 256, 0, s>>>(v, points, camtab, delta_p, delta_c, camtab_c, partial);
+  if (small_tabs_fit(v.E, v.NI)) {
+    const size_t lds = small_tabs_bytes(v.E, v.NI) + sizeof(double) * 30 * (size_t)v.E;
+    k_candidate<true><<<grid, 256, lds, s>>>(v, points, camtab, delta_p, delta_c, camtab_c, partial);
+  } else {
+    k_candidate<false><<<grid, 256, 0, s>>>(v, points, camtab, delta_p, delta_c, camtab_c, partial);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_grad_points(int NP, const double* __restrict__ x,
