@@ -14,7 +14,7 @@
 //                (v_mfma_f64_16x16x4_f64, 4 waves x 32x32 quadrants, P tiles in LDS), split
 //                into the next block column (on the panel chain) and the bulk (on a second
 //                stream, overlapping the next panel step)
-// Back substitution L^T y = z: one launch per 4 blocks, y_k = L_kk^-T z_k from the stored
+// Back substitution L^T y = z: one launch per block, y_k = L_kk^-T z_k from the stored
 // 16x16 inverses followed by the block-column update of z[0:k].
 // The whole sequence is captured once into a hipGraph (two streams) and replayed.
 #include <hip/hip_runtime.h>
@@ -347,87 +347,66 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
       }
 }
 
-// Back substitution for a group of up to kGrp consecutive blocks [b0, b0+nb): every
-// work-group solves the group's blocks top-down-reversed itself (L_kk^T y_k = z_k with the
-// 16x16 inverses, then the in-group updates z_j -= L_kj^T y_k), then updates its 64
-// columns of z[0:k0] with all of the group's rows. One launch per kGrp blocks.
-constexpr int kGrp = 4;
-__global__ __launch_bounds__(kThreads) void k_trsv_back_grp(const double* __restrict__ A, int lda, int n, int b0,
-                                                            int nb, const double* __restrict__ blk,
-                                                            double* __restrict__ z, double* __restrict__ y) {
+// back substitution step for block [k, k+kb): y_k = L_kk^-T z_k by 16-blocks with the
+// stored inverses D_q (y_q = D_q^T (z_q - sum_{r>q} L_rq^T y_r)), then
+// z[0:k] -= L[k:k+kb, 0:k]^T y_k
+__global__ __launch_bounds__(kThreads) void k_trsv_back(const double* __restrict__ A, int lda, int k, int kb,
+                                                        const double* __restrict__ blk,
+                                                        double* __restrict__ z, double* __restrict__ y) {
   __shared__ double Lk[NB][LS];
   __shared__ double Dq[4][16][DS];
-  __shared__ double yy[kGrp * NB];
+  __shared__ double yy[NB];
   __shared__ double tt[16];
-  __shared__ double red[4][64];
   const int tid = threadIdx.x;
-  const int k0 = NB * b0;
-  const int rows = min(n, NB * (b0 + nb)) - k0;
-  for (int i = tid; i < kGrp * NB; i += kThreads) yy[i] = i < rows ? z[k0 + i] : 0.0;
-  for (int bi = nb - 1; bi >= 0; --bi) {
-    const double* bk = blk + (size_t)(b0 + bi) * kBlk;
-    const int kb = min(NB, n - NB * (b0 + bi));
-    __syncthreads();  // previous block's readers of Lk/Dq are done, yy updates visible
 #pragma unroll
-    for (int q = 0; q < NB * NB / kThreads; ++q) {
-      const int idx = tid + q * kThreads;
-      Lk[idx >> 6][idx & 63] = bk[1024 + idx];
-    }
+  for (int q = 0; q < NB * NB / kThreads; ++q) {
+    const int idx = tid + q * kThreads, i = idx >> 6, j = idx & 63;
+    Lk[i][j] = blk[1024 + idx];
+  }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int idx = tid + q * kThreads;
-      Dq[idx >> 8][(idx >> 4) & 15][idx & 15] = bk[idx];
-    }
-    __syncthreads();
-    double* yb = yy + NB * bi;
-    if (tid < 64) {  // one wave, lanes 0..15 carry the 16-vectors
-      const int cc = tid & 15;
+  for (int q = 0; q < 4; ++q) {
+    const int idx = tid + q * kThreads;
+    Dq[idx >> 8][(idx >> 4) & 15][idx & 15] = blk[idx];
+  }
+  if (tid < NB) yy[tid] = tid < kb ? z[k + tid] : 0.0;
+  __syncthreads();
+  if (tid < 64) {  // one wave, lanes 0..15 carry the 16-vectors
+    const int c = tid & 15;
 #pragma unroll
-      for (int q = 3; q >= 0; --q) {
-        double t = yb[16 * q + cc];
+    for (int q = 3; q >= 0; --q) {
+      double t = yy[16 * q + c];
 #pragma unroll
-        for (int r = q + 1; r < 4; ++r)
+      for (int r = q + 1; r < 4; ++r)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) t = fma(-Lk[16 * r + i][16 * q + cc], yb[16 * r + i], t);
-        if (tid < 16) tt[cc] = t;
-        __builtin_amdgcn_wave_barrier();
-        double s = 0.0;
-#pragma unroll
-        for (int m = 0; m < 16; ++m)
-          if (m >= cc) s = fma(Dq[q][m][cc], tt[m], s);
-        __builtin_amdgcn_wave_barrier();
-        if (tid < 16) yb[16 * q + cc] = s;
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
-    __syncthreads();
-    // in-group update of the blocks below: z_j -= L[block bi rows, block j cols]^T y_bi
-    if (tid < NB * bi) {
-      const double* Lr = A + (size_t)(k0 + NB * bi) * lda + k0 + tid;
+        for (int i = 0; i < 16; ++i) t = fma(-Lk[16 * r + i][16 * q + c], yy[16 * r + i], t);
+      if (tid < 16) tt[c] = t;
+      __builtin_amdgcn_wave_barrier();
       double s = 0.0;
-#pragma unroll 16
-      for (int m = 0; m < NB; ++m)
-        if (m < kb) s = fma(Lr[(size_t)m * lda], yb[m], s);
-      yy[tid] -= s;
+#pragma unroll
+      for (int m = 0; m < 16; ++m)
+        if (m >= c) s = fma(Dq[q][m][c], tt[m], s);
+      __builtin_amdgcn_wave_barrier();
+      if (tid < 16) yy[16 * q + c] = s;
+      __builtin_amdgcn_wave_barrier();
     }
   }
   __syncthreads();
-  if (blockIdx.x == 0)
-    for (int i = tid; i < rows; i += kThreads) y[k0 + i] = yy[i];
-  // z[0:k0] -= L[k0:k0+rows, 0:k0]^T y: 64 columns per work-group, 4 lanes per column
+  if (blockIdx.x == 0 && tid < kb) y[k + tid] = yy[tid];
+  // 64 columns per workgroup, 4 lanes per column (16 rows of the block each)
   const int i = blockIdx.x * (kThreads / 4) + (tid & 63);
   const int part = tid >> 6;
   double s = 0.0;
-  if (i < k0) {  // part p takes rows [64p, 64p+64) of the group
-#pragma unroll 16
-    for (int q = 0; q < NB; ++q) {
-      const int m = part * NB + q;
-      if (m < rows) s = fma(A[(size_t)(k0 + m) * lda + i], yy[m], s);
+  if (i < k) {
+#pragma unroll
+    for (int q = 0; q < NB / 4; ++q) {
+      const int mm = part * (NB / 4) + q;
+      if (mm < kb) s += A[(size_t)(k + mm) * lda + i] * yy[mm];
     }
   }
+  __shared__ double red[4][64];
   red[part][tid & 63] = s;
   __syncthreads();
-  if (part == 0 && i < k0) z[i] -= ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+  if (part == 0 && i < k) z[i] -= ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
 }
 
 static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y,
@@ -523,12 +502,10 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
     }
   }
   double* z = A + (size_t)n * lda;
-  const char* ge = getenv("DAB_TRSV_GRP");  // blocks per back-substitution launch (1..4)
-  const int grp = ge ? std::min(kGrp, std::max(1, atoi(ge))) : kGrp;
-  for (int b1 = nblk; b1 > 0; b1 -= grp) {
-    const int b0 = std::max(0, b1 - grp), k0 = b0 * NB;
-    const int grid = k0 > 0 ? (k0 + 63) / 64 : 1;
-    k_trsv_back_grp<<<grid, kThreads, 0, s>>>(A, lda, n, b0, b1 - b0, c->blk, z, y);
+  for (int b = nblk - 1; b >= 0; --b) {
+    const int k = b * NB, kb = (n - k < NB) ? n - k : NB;
+    const int grid = k > 0 ? (k + 63) / 64 : 1;
+    k_trsv_back<<<grid, kThreads, 0, s>>>(A, lda, k, kb, c->blk + (size_t)b * kBlk, z, y);
   }
 }
 
