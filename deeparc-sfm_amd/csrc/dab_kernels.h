@@ -147,7 +147,7 @@ void launch_grad_points(hipStream_t s, int NP, const double* x, const double* g 
 // ---- implicit-Schur PCG (dab_pcg.hip) -------------------------------------------------------
 enum { kPcgRunning = 0, kPcgSuccess = 1, kPcgNoConvergence = 2, kPcgFailure = 3 };
 struct PcgState {
-  double rho, Q0, alpha, eta, norm_b, pad[3];
+  double rho, Q0, alpha, eta, norm_b, pad[3];  // pad[0]: beta of the multi-work-group update
   int iter, status, min_iter, max_iter;
 };
 // per chunk: 21 upper of sum_runs Z Z^T (Z = sum of the run's Y; run[i] = length of the
@@ -175,6 +175,13 @@ void launch_pcg_matvec_passes(hipStream_t s, const DevView& v, int nchunk, const
 // Modes 0 and 2 end with the next direction (z = M^-1 r, rho, beta, p) when still running.
 // w[NC][6] = all-reduced Y part of the product; xptr/xlist: per-camera CSR of cross blocks
 // (code = 2*k + (camera is c1)), nullable when there are none.
+// The same CG update spread over work-groups (three launches, last-arriver grid sums):
+// partial[cg_partial_size(NC)] scratch, cnt a zeroed counter (left zeroed).
+void launch_cg_update(hipStream_t s, int NC, int mode, const double* Ad, const double* w, const int* xptr,
+                      const int* xlist, const int2* xcam, const double* X, const double* scale_c,
+                      const double* bvec, double* p, double* q, double* x, double* r, PcgState* st,
+                      const double* Minv, double* z, double* partial, unsigned* cnt);
+int cg_partial_size(int NC);
 void launch_pcg_update(hipStream_t s, int NC, int mode, const double* Ad, const double* w, const int* xptr,
                        const int* xlist, const int2* xcam, const double* X, const double* scale_c,
                        const double* bvec, double* p, double* q, double* x, double* r, PcgState* st,

@@ -585,6 +585,163 @@ __global__ __launch_bounds__(kOneWG) void k_pcg_update(int NC, int mode, const d
   if (s_status == kPcgRunning) pcg_direction(NC, Minv, r, z, p, st, iter + 1, sh);
 }
 
+// ---- multi-work-group CG update ---------------------------------------------------------
+// The single-work-group update above pulls Ad, M^-1 and five vectors through one CU (~50
+// us at NC = 999). Here the camera-wise work is spread over 64-thread work-groups and each
+// global dot product is finished by the last work-group to arrive (partials stored
+// write-through and drained before one atomic count, read back with atomic loads, summed
+// in work-group order: deterministic, no fences), so the scalar recurrences stay on the
+// device. Three launches per CG iteration:
+//   k_cg_q      q = S p (Y part w + diagonal + cross terms), pq -> alpha (mode 0/1);
+//               mode 2: r = b - S x
+//   k_cg_xr     x += alpha p, r -= alpha q (mode 0), Q-test, z = M^-1 r, rho -> beta, iter
+//   k_cg_p      p = z + beta p
+constexpr int kCgBlock = 64;
+
+// sum of v over the grid, valid in the last-arriving work-group (returns true there)
+template <int K>
+__device__ __forceinline__ bool grid_sum_last(double (&v)[K], double* __restrict__ partial, unsigned* __restrict__ cnt,
+                                              double (&out)[K]) {
+  __shared__ int last;
+#pragma unroll
+  for (int i = 0; i < K; ++i) v[i] = wave_sum_lane63(v[i]);  // one wave per work-group
+  if (threadIdx.x == 63) {
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(partial) + K * (size_t)blockIdx.x + i,
+                         (unsigned long long)__double_as_longlong(v[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return false;
+  const unsigned long long* pp = reinterpret_cast<const unsigned long long*>(partial);
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    double s = 0.0;
+    for (int b = threadIdx.x; b < (int)gridDim.x; b += blockDim.x)
+      s += __longlong_as_double((long long)__hip_atomic_load(pp + K * (size_t)b + i, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT));
+    out[i] = wave_sum_lane63(s);  // lane 63 holds the total
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+__global__ __launch_bounds__(kCgBlock) void k_cg_q(int NC, int mode, int L, const double* __restrict__ Ad,
+                                                   const double* __restrict__ w, const int* __restrict__ xptr,
+                                                   const int* __restrict__ xlist, const int2* __restrict__ xcam,
+                                                   const double* __restrict__ X, const double* __restrict__ scc,
+                                                   const double* __restrict__ bvec, const double* __restrict__ p,
+                                                   double* __restrict__ q, const double* __restrict__ x,
+                                                   double* __restrict__ r, PcgState* st, double* __restrict__ partial,
+                                                   unsigned* __restrict__ cnt) {
+  if (st->status != kPcgRunning) return;
+  const int s8 = threadIdx.x & (L - 1);
+  const int c0 = blockIdx.x * (kCgBlock / L) + threadIdx.x / L;
+  const int c = c0 < NC ? c0 : -1;
+  double o[6];
+  apply_cam8(c, s8, L, Ad, mode == 2 ? x : p, w, xptr, xlist, xcam, X, scc, o);
+  double acc[1] = {0.0};
+  if (c >= 0 && s8 == 0) {
+    if (mode == 2) {
+#pragma unroll
+      for (int a = 0; a < 6; ++a) r[6 * c + a] = bvec[6 * c + a] - o[a];
+    } else {
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        q[6 * c + a] = o[a];
+        acc[0] += p[6 * c + a] * o[a];
+      }
+    }
+  }
+  if (mode == 2) return;
+  double pq[1];
+  if (!grid_sum_last<1>(acc, partial, cnt, pq)) return;
+  if (threadIdx.x == 63) {
+    if (pq[0] <= 0.0 || isinf(pq[0])) {
+      st->status = kPcgNoConvergence;  // Ceres: matrix indefinite, keep x
+    } else {
+      const double alpha = st->rho / pq[0];
+      if (isinf(alpha)) st->status = kPcgFailure;
+      st->alpha = alpha;
+    }
+  }
+}
+
+// mode 0: x, r update + Q-test + direction scalars; 1: x update only; 2: Q-test + direction
+__global__ __launch_bounds__(kCgBlock) void k_cg_xr(int NC, int mode, const double* __restrict__ bvec,
+                                                    const double* __restrict__ p, const double* __restrict__ q,
+                                                    double* __restrict__ x, double* __restrict__ r,
+                                                    const double* __restrict__ Minv, double* __restrict__ z,
+                                                    PcgState* st, double* __restrict__ partial,
+                                                    unsigned* __restrict__ cnt) {
+  if (st->status != kPcgRunning) return;
+  const int c = blockIdx.x * kCgBlock + threadIdx.x;
+  double acc[2] = {0.0, 0.0};  // x.(b + r), r.z
+  if (c < NC) {
+    double xc[6], rc[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      xc[a] = x[6 * c + a];
+      rc[a] = r[6 * c + a];
+    }
+    if (mode != 2) {
+      const double alpha = st->alpha;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        xc[a] += alpha * p[6 * c + a];
+        x[6 * c + a] = xc[a];
+        if (mode == 0) {
+          rc[a] -= alpha * q[6 * c + a];
+          r[6 * c + a] = rc[a];
+        }
+      }
+    }
+    if (mode != 1) {
+#pragma unroll
+      for (int a = 0; a < 6; ++a) acc[0] += xc[a] * (bvec[6 * c + a] + rc[a]);
+      const double* mi = Minv + 36 * (size_t)c;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        double t = 0.0;
+#pragma unroll
+        for (int b = 0; b < 6; ++b) t += mi[6 * a + b] * rc[b];
+        z[6 * c + a] = t;
+        acc[1] += rc[a] * t;
+      }
+    }
+  }
+  if (mode == 1) return;
+  double sums[2];
+  if (!grid_sum_last<2>(acc, partial, cnt, sums)) return;
+  if (threadIdx.x == 63) {
+    const double Q1 = -sums[0];
+    const int iter = st->iter;
+    int status = kPcgRunning;
+    const double zeta = iter * (Q1 - st->Q0) / Q1;
+    if (zeta < st->eta && iter >= st->min_iter) status = kPcgSuccess;
+    else if (iter >= st->max_iter) status = kPcgNoConvergence;
+    st->Q0 = Q1;
+    if (status == kPcgRunning) {  // the next iteration's direction scalars
+      const double rho = sums[1];
+      const double beta = rho / st->rho;
+      if (zero_or_inf(rho) || zero_or_inf(beta)) status = kPcgFailure;
+      st->pad[0] = beta;
+      st->rho = rho;
+      st->iter = iter + 1;
+    }
+    st->status = status;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_cg_p(int n, const double* __restrict__ z, double* __restrict__ p,
+                                              const PcgState* st) {
+  if (st->status != kPcgRunning) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = z[i] + st->pad[0] * p[i];
+}
+
 // ---- launchers -------------------------------------------------------------------------
 
 void launch_pcg_diag_rhs_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
@@ -635,6 +792,22 @@ void launch_pcg_matvec_passes(hipStream_t s, const DevView& v, int nchunk, const
       k_pcg_cam_pass<double><<<nchunk, kRedBlock, 0, s>>>(v, chunk_beg, (const double*)Y.cm, t, partial, st);
   }
 }
+
+void launch_cg_update(hipStream_t s, int NC, int mode, const double* Ad, const double* w, const int* xptr,
+                      const int* xlist, const int2* xcam, const double* X, const double* scale_c,
+                      const double* bvec, double* p, double* q, double* x, double* r, PcgState* st,
+                      const double* Minv, double* z, double* partial, unsigned* cnt) {
+  if (NC <= 0) return;
+  const int L = xptr ? 16 : 1;
+  const int gq = (NC + kCgBlock / L - 1) / (kCgBlock / L), gx = (NC + kCgBlock - 1) / kCgBlock;
+  if (mode != 2)
+    k_cg_q<<<gq, kCgBlock, 0, s>>>(NC, mode, L, Ad, w, xptr, xlist, xcam, X, scale_c, bvec, p, q, x, r, st, partial, cnt);
+  else
+    k_cg_q<<<gq, kCgBlock, 0, s>>>(NC, 2, L, Ad, w, xptr, xlist, xcam, X, scale_c, bvec, p, q, x, r, st, partial, cnt);
+  k_cg_xr<<<gx, kCgBlock, 0, s>>>(NC, mode, bvec, p, q, x, r, Minv, z, st, partial, cnt);
+  if (mode != 1) k_cg_p<<<(6 * NC + 255) / 256, 256, 0, s>>>(6 * NC, z, p, st);
+}
+int cg_partial_size(int NC) { return 2 * ((NC + 3) / 4) + 2 * ((NC + kCgBlock - 1) / kCgBlock); }
 
 void launch_pcg_update(hipStream_t s, int NC, int mode, const double* Ad, const double* w, const int* xptr,
                        const int* xlist, const int2* xcam, const double* X, const double* scale_c,

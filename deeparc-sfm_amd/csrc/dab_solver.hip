@@ -187,6 +187,9 @@ struct dab_handle {
   int eval_grid = 1;  // k_eval_points blocks (one SELL slice per block)
   int ncu = 256;      // compute units of the device
   int fused_grid = 0;  // > 0: single-pass PCG matvec (small camera systems)
+  int pcg_hint = 2;    // CG iterations of the previous solve (first batch size)
+  double* d_cg_partial = nullptr;  // multi-work-group CG update: grid partials + counter
+  unsigned* d_cg_cnt = nullptr;
   double* d_fused_partial = nullptr;
   int eval_wps = 0;   // 0: LDS tables; else waves per slice (DAB_EVAL_WPS tuning knob)
 
@@ -901,6 +904,9 @@ static int build_pcg_buffers(dab_handle* h) {
   CHECK_RC(d.alloc(&h->d_pcg_red, (size_t)27 * h->NC));
   CHECK_RC(d.alloc(&h->d_pcg_t, (size_t)4 * h->NP));
   CHECK_RC(d.alloc(&h->d_pcg_state, 1));
+  CHECK_RC(d.alloc(&h->d_cg_partial, (size_t)cg_partial_size(h->NC)));
+  CHECK_RC(d.alloc(&h->d_cg_cnt, 1));
+  HIP_OK(hipMemsetAsync(h->d_cg_cnt, 0, sizeof(unsigned), h->stream));
   // the single-pass matvec when the camera system is small (DAB_PCG_FUSED=0 disables it)
   const char* fz = getenv("DAB_PCG_FUSED");
   if (pcg_fused_fits(h->NC) && h->NP > 0 && !(fz && atoi(fz) == 0)) {
@@ -948,27 +954,41 @@ static int pcg_solve(dab_handle* h, const dab_options& opt, StepScalars sc, YBuf
   launch_pcg_init(s, NC, h->d_pcg_b, h->d_flags + 1, h->d_pcg_state, opt.eta, opt.min_linear_solver_iterations,
                   max_it, h->d_pcg_Minv, h->d_pcg_r, h->d_pcg_z, h->d_pcg_p);
   const int* xptr = h->nxlist > 0 ? h->d_xptr : nullptr;
-  int done = 0, batch = 4;
+  // the CG update: spread over work-groups (default) or one work-group (DAB_CG_ONEWG=1)
+  const char* one = getenv("DAB_CG_ONEWG");
+  const bool onewg = one && atoi(one) != 0;
+  auto update = [&](int mode) {
+    if (onewg)
+      launch_pcg_update(s, NC, mode, h->d_pcg_Ad, h->d_pcg_w, xptr, h->d_xlist, h->d_cross_cam, h->Ux(),
+                        h->d_scale_c, h->d_pcg_b, h->d_pcg_p, h->d_pcg_q, h->d_yc, h->d_pcg_r, h->d_pcg_state,
+                        h->d_pcg_Minv, h->d_pcg_z);
+    else
+      launch_cg_update(s, NC, mode, h->d_pcg_Ad, h->d_pcg_w, xptr, h->d_xlist, h->d_cross_cam, h->Ux(),
+                       h->d_scale_c, h->d_pcg_b, h->d_pcg_p, h->d_pcg_q, h->d_yc, h->d_pcg_r, h->d_pcg_state,
+                       h->d_pcg_Minv, h->d_pcg_z, h->d_cg_partial, h->d_cg_cnt);
+  };
+  // CG iterations are enqueued in batches between reads of the device-side state. The
+  // first batch is the previous solve's count + 2 (counts change slowly between LM
+  // iterations); a finished CG turns the rest of a batch into no-op launches (~4.5 us
+  // each), a read costs a host round trip (~25 us).
+  int done = 0, batch = std::min(32, std::max(2, h->pcg_hint + 2));
   for (;;) {
     for (int j = 0; j < batch && done < max_it; ++j) {
       ++done;
       CHECK_RC(pcg_matvec(h, yb, h->d_pcg_p));
       const bool reset = done % 10 == 0;  // r = b - S x every 10th iteration
-      launch_pcg_update(s, NC, reset ? 1 : 0, h->d_pcg_Ad, h->d_pcg_w, xptr, h->d_xlist, h->d_cross_cam, h->Ux(),
-                        h->d_scale_c, h->d_pcg_b, h->d_pcg_p, h->d_pcg_q, h->d_yc, h->d_pcg_r, h->d_pcg_state,
-                        h->d_pcg_Minv, h->d_pcg_z);
+      update(reset ? 1 : 0);
       if (reset) {
         CHECK_RC(pcg_matvec(h, yb, h->d_yc));
-        launch_pcg_update(s, NC, 2, h->d_pcg_Ad, h->d_pcg_w, xptr, h->d_xlist, h->d_cross_cam, h->Ux(),
-                          h->d_scale_c, h->d_pcg_b, h->d_pcg_p, h->d_pcg_q, h->d_yc, h->d_pcg_r, h->d_pcg_state,
-                          h->d_pcg_Minv, h->d_pcg_z);
+        update(2);
       }
     }
     HIP_OK(hipMemcpyAsync(h->h_pcg_state, h->d_pcg_state, sizeof(PcgState), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     if (h->h_pcg_state->status != kPcgRunning || done >= max_it) break;
-    batch = std::min(2 * batch, 32);
+    batch = batch < 4 ? 4 : std::min(2 * batch, 32);
   }
+  h->pcg_hint = h->h_pcg_state->iter;
   *iters = h->h_pcg_state->iter;
   *status = h->h_pcg_state->status;
   return 0;

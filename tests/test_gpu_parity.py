@@ -181,6 +181,30 @@ def test_pcg_fused_matvec_matches_two_pass(pkg, gpu, kind, monkeypatch):
     np.testing.assert_array_equal(pts[0], pts[2])  # fused path: bitwise repeatable
 
 
+@pytest.mark.parametrize("kind", ["bal", "rig"])
+def test_cg_update_work_groups_match_single(pkg, gpu, kind, monkeypatch):
+    """The CG update spread over work-groups (last-arriver grid sums) against the
+    single-work-group kernel (DAB_CG_ONEWG=1): same CG iteration counts, costs 1e-10."""
+    if kind == "bal":
+        prob = pkg.synth(kind=0, num_cameras=300, num_points=6000, obs_per_point=6, seed=43)
+    else:
+        prob = pkg.synth(kind=1, num_arcs=6, num_rings=16, num_points=3000, obs_per_point=8, seed=44)
+    res = []
+    for one in ("1", "0"):
+        monkeypatch.setenv("DAB_CG_ONEWG", one)
+        p = prob.copy()
+        s = pkg.Solver(0)
+        s.set_problem(p)
+        res.append(s.solve(pkg.options(max_num_iterations=12,
+                                       linear_solver_type=pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)))
+        s.close()
+    a, b = res
+    assert [it["linear_solver_iterations"] for it in a["iterations"]] == \
+        [it["linear_solver_iterations"] for it in b["iterations"]]
+    np.testing.assert_allclose([it["cost"] for it in a["iterations"]], [it["cost"] for it in b["iterations"]],
+                               rtol=1e-10)
+
+
 def test_lm_freeze_camera_matches_oracle(pkg, orc, gpu):
     prob = pkg.synth(kind=1, num_arcs=4, num_rings=10, num_points=2000, obs_per_point=6, seed=23)
     prob.freeze_camera = True  # solve(..., freeze_camera=true), sfm.cc:111
