@@ -20,6 +20,11 @@ struct YBufs {
   bool f32;
 };
 constexpr int kRedBlock = 256;
+// fixed-point cost accumulators (cost_fx_add): kFxCopies shards of 128 B, each holding
+// {sum r^2 integer part, fraction * 2^52, non-finite count} as uint64 in words 0..2
+constexpr int kFxStride = 16;   // 8-B words per shard
+constexpr int kFxCopies = 32;   // shards (work-group b adds into shard b % kFxCopies)
+constexpr int kFxWords = kFxStride * kFxCopies;
 constexpr int kChunk = 4096;  // max entries per reduction chunk (C3: one chunk per camera)
 constexpr int kSlotBit = 1 << 30;  // cm_idx.w flag: the entry is the ring (slot 1) camera
 
@@ -35,6 +40,7 @@ struct DevView {
   int NE;         // entries
   int NI;         // intrinsics
   int nslice;     // SELL-64 slices (64 points each)
+  int any_comp;   // some observation is arc∘ring (ext1 >= 0)
   const int4* obs_idx;      // (point, ext0, ext1, intr)
   const double2* obs_xy;
   const int4* cm_idx;       // [NE] obs_idx of the entry's observation, w |= kSlotBit for slot 1
@@ -65,9 +71,13 @@ void launch_cam_tables(hipStream_t s, int E, const double* ext, double* camtab);
 // wps = 4 | 8 | 16 waves per slice reading camtab; 0 / -2 = 4 / 2 waves per slice with R,t
 // built from ext into LDS on a persistent grid), cost[2] = {sum r^2, non-finite count}
 // (partial[grid][2] is scratch; arrivals is a zeroed counter the kernel leaves zeroed).
+// wps <= -100 (the prefetch kernels) add the cost into the fixed-point shards costfx
+// [kFxWords] (zeroed by the previous pass) and zero fx_next [kFxWords] for the next pass;
+// the other variants write cost[2].
 void launch_eval_points(hipStream_t s, const DevView& v, const double* points, const double* ext,
                         const double* camtab, double* V, double* g, double* partial, unsigned* arrivals,
-                        double* cost, int grid, int wps);
+                        double* cost, unsigned long long* costfx, unsigned long long* fx_next, int grid, int wps);
+inline bool eval_points_fx(int wps) { return wps <= -100 && (-wps - 100) / 1000 != 64; }
 // whether the chosen variant reads camtab (the LDS variants build R,t from ext themselves)
 bool eval_points_needs_camtab(int wps);
 bool eval_points_lds_fits(int E);
@@ -84,6 +94,13 @@ void launch_filter(hipStream_t s, const DevView& v, const double* points, const 
 //  U/g: per entry 21 (Jc^T Jc upper) + 6 (Jc^T r) -> partial[chunk][27]
 void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, const int* chunk_beg,
                       const double* points, const double* ext, const double* camtab, double* partial);
+// Fused evaluation pass for BAL-shaped problems (camera side -> ug[NC][27] directly,
+// point side -> V, g, cost in fixed point as launch_eval_points): one launch, camera and
+// point waves side by side. fused_eval_fits: whether the problem qualifies for `grid`.
+bool fused_eval_fits(const DevView& v, int nchunk, int ngen, int ncross, int grid);
+void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
+                       double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
+                       int grid);
 //  arc∘ring cross blocks Jc0^T Jc1 over composed observations (pair-major copy) -> partial[chunk][36]
 void launch_eval_cross(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
                        const double2* x_xy, const double* points, const double* camtab, double* partial);

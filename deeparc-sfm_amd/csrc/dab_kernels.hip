@@ -469,11 +469,13 @@ struct LdsTabs {
 // ring camera of an arc∘ring observation; SLOT 2: both (jc0/jc1 = slot 0 rows, jd0/jd1 =
 // slot 1 rows); SLOT -1: no camera rows. Q is the point the arc/single rotation acts on:
 // X (single) or P2 = R1 X + t1 (arc∘ring).
-template <bool JP, int SLOT, class Tabs>
+// MAYCOMP = false: the caller knows no observation is arc∘ring (ext1 < 0 everywhere), so
+// the second table is never read and its registers are never allocated.
+template <bool JP, int SLOT, class Tabs, bool MAYCOMP = true>
 __device__ __forceinline__ void obs_rows(const int4 id, const double2 xy, const double X[3], const Tabs& tb,
                                          double& ru, double& rv, double jx0[3], double jx1[3], double jc0[6],
                                          double jc1[6], double jd0[6] = nullptr, double jd1[6] = nullptr) {
-  const bool comp = id.z >= 0;
+  const bool comp = MAYCOMP && id.z >= 0;
   double A[12];  // R0 | t0
   tb.rt(id.y, A);
   double Kr[6];
@@ -797,11 +799,275 @@ __global__ __launch_bounds__(1024) void k_eval_points_lds(DevView v, const doubl
   store_cost_partial_last<16>(acc, partial, arrivals, cost);
 }
 
+// Cost sum as an exact fixed-point integer pair. Each work-group adds its (fixed-order)
+// partial sum of r^2 as hi = trunc(p) and lo = (p - hi) * 2^52 with no-return 64-bit
+// atomics, and its non-finite count; integer addition is associative, so the total is the
+// same bits whatever order the work-groups finish in (bitwise reproducible, identical on
+// every rank's copy after an integer all-reduce), and the kernel ends without the
+// store-wait-count-load chain of a last-arriver sum (~2.5 us at C3). Same-address atomics
+// serialize at the memory side (~12 ns each), so the adds are spread over kFxCopies
+// shards of their own lines (8 work-groups per shard at C3). Readers sum the shards and
+// convert: cost = hi + lo * 2^-52 (dab_solver.hip, read_scalars). Two shard sets alternate
+// between consecutive passes: block 0 of a pass zeroes the set the next pass adds into
+// (fx_next), so no memset or extra launch runs in front of the kernel; the set of a pass
+// stays valid until the pass after next.
+template <int NW>
+__device__ __forceinline__ void cost_fx_add(double (&acc)[2], unsigned long long* __restrict__ fx) {
+  __shared__ double shp[NW][2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double t = wave_sum_lane63(acc[i]);
+    if (lane == 63) shp[w][i] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double p = shp[0][0], b = shp[0][1];
+#pragma unroll
+    for (int q = 1; q < NW; ++q) {
+      p += shp[q][0];
+      b += shp[q][1];
+    }
+    long long hi = 0, lo = 0;
+    if (p >= 0.0 && p < 0x1p62) {
+      const double ip = trunc(p);
+      hi = (long long)ip;
+      lo = (long long)rint((p - ip) * 0x1p52);
+    } else {
+      b += 1.0;  // non-finite (or absurd) partial: the evaluation is flagged bad
+    }
+    unsigned long long* sh = fx + kFxStride * (blockIdx.x % kFxCopies);
+    if (hi) __hip_atomic_fetch_add(sh, (unsigned long long)hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lo) __hip_atomic_fetch_add(sh + 1, (unsigned long long)lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (b != 0.0) __hip_atomic_fetch_add(sh + 2, (unsigned long long)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Deep-prefetch variant. The SELL rows of a slice are independent loads, but the kernel
+// above keeps only one row per wave in flight, and the work-group's first loads wait
+// for the table build. Here every wave holds a queue of D rows (idx + xy, 8 VGPRs per
+// row) and issues its first D rows and its points before building the tables, so HBM
+// latency overlaps the prologue and ~D x more bytes are in flight per CU. R,t and (when
+// NI <= kLdsCams) every intrinsic sit in LDS; the two-wave combine goes through a small
+// buffer in three phases of three components, so all three fit in 160 KiB.
+template <int D>
+struct RowQueue {
+  int4 id[D];
+  double2 xy[D];
+};
+template <int WPS, int D>
+__device__ __forceinline__ void rowq_fill(const DevView& v, int off, int len, int w, int lane, RowQueue<D>& q) {
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const int k = w + d * WPS;
+    if (k < len) {
+      q.id[d] = v.obs_idx[off + 64 * k + lane];
+      q.xy[d] = v.obs_xy[off + 64 * k + lane];
+    } else {
+      q.id[d] = make_int4(-1, 0, -1, 0);
+      q.xy[d] = make_double2(0.0, 0.0);
+    }
+  }
+}
+// VAR (timing ablations, wrong results unless noted): bit 0 no trig in the table build,
+// bit 1 loads only (no row math), bit 2 no table staging at all, bit 3 plain partials (no
+// cost total), bit 4 no V/g stores, bit 5 no cross-wave combine, bit 6 last-arriver cost
+// sum into cost[] instead of the fixed-point atomics (correct results)
+template <bool KL, int WPS, int D, int VAR = 0, bool COMP = true>
+__global__ __launch_bounds__(1024) void k_eval_points_pf(DevView v, const double* __restrict__ points,
+                                                         const double* __restrict__ ext,
+                                                         double* __restrict__ V, double* __restrict__ g,
+                                                         double* __restrict__ partial,
+                                                         unsigned* __restrict__ arrivals,
+                                                         double* __restrict__ cost,
+                                                         unsigned long long* __restrict__ costfx,
+                                                         unsigned long long* __restrict__ fx_next) {
+  constexpr int G = 16 / WPS;  // slices in flight per work-group
+  if (blockIdx.x == 0 && fx_next)
+    for (int i = threadIdx.x; i < kFxWords; i += blockDim.x) fx_next[i] = 0ull;
+  constexpr int PH = WPS <= 2 ? 3 : 1;  // components per combine phase
+  __shared__ double rt_s[kLdsCams * 12];
+  __shared__ double k_s[KL ? kLdsCams * 6 : 2];
+  __shared__ double sh[WPS > 1 ? G : 1][WPS > 1 ? WPS - 1 : 1][PH][64];
+  // wave-uniform indices in SGPRs: slice bounds and row loops become scalar branches
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = wave / WPS, w = wave % WPS;
+  const size_t NPs = (size_t)v.NP;
+  const int per_wg = (v.nslice + gridDim.x - 1) / gridDim.x;
+  const int rounds = (per_wg + G - 1) / G;
+  RowQueue<D> q;
+  double X[3] = {0.0, 0.0, 0.0};
+  int sl = grp * gridDim.x + blockIdx.x;  // round 0 (slot q of the work-group: slice q * grid + b)
+  int off = 0, len = 0;
+  // round 0's first rows and points go out before the table build
+  if (sl < v.nslice) {
+    off = v.slice_off[sl];
+    len = (v.slice_off[sl + 1] - off) >> 6;
+    const int p = 64 * sl + lane;
+    if (p < v.NP) {
+      X[0] = points[3 * (size_t)p];
+      X[1] = points[3 * (size_t)p + 1];
+      X[2] = points[3 * (size_t)p + 2];
+    }
+  }
+  rowq_fill<WPS, D>(v, off, len, w, lane, q);
+  // table staging: every load of this thread's share (its extrinsic: 3 x 16 B; up to three
+  // 16-B intrinsic pieces) is issued before any of them is used, so the prologue costs
+  // one L2/HBM round trip, not one per loop turn (E, NI <= kLdsCams = blockDim)
+  if constexpr (!(VAR & 4)) {
+    const int e = threadIdx.x;
+    double2 xw[3];
+    if (e < v.E) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) xw[i] = reinterpret_cast<const double2*>(ext + 6 * (size_t)e)[i];
+    }
+    double2 kq[3];
+    if constexpr (KL) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int i = threadIdx.x + j * 1024;
+        if (i < v.NI * 3) kq[j] = reinterpret_cast<const double2*>(v.intr + (size_t)kIntr * (i / 3))[i % 3];
+      }
+    }
+    if (e < v.E) {
+      const double x6[6] = {xw[0].x, xw[0].y, xw[1].x, xw[1].y, xw[2].x, xw[2].y};
+      double T[30];
+      if constexpr (VAR & 1) {
+#pragma unroll
+        for (int i = 0; i < 12; ++i) T[i] = (i % 4 == 0 ? 1.0 : 0.0) + (i >= 9 ? x6[i - 6] : 0.0);
+      } else {
+        cam_table(x6, T);
+      }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) reinterpret_cast<double2*>(rt_s + 12 * e)[i] = make_double2(T[2 * i], T[2 * i + 1]);
+    }
+    if constexpr (KL) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int i = threadIdx.x + j * 1024;
+        if (i < v.NI * 3) reinterpret_cast<double2*>(k_s)[i] = kq[j];
+      }
+    }
+  }
+  __syncthreads();
+  const LdsTabs<KL> tabs{rt_s, k_s, nullptr, v.intr};
+  double acc[2] = {0.0, 0.0};
+  for (int r = 0; r < rounds; ++r) {
+    if (r > 0) {
+      sl = (r * G + grp) * gridDim.x + blockIdx.x;
+      off = len = 0;
+      X[0] = X[1] = X[2] = 0.0;
+      if (sl < v.nslice) {
+        off = v.slice_off[sl];
+        len = (v.slice_off[sl + 1] - off) >> 6;
+        const int p = 64 * sl + lane;
+        if (p < v.NP) {
+          X[0] = points[3 * (size_t)p];
+          X[1] = points[3 * (size_t)p + 1];
+          X[2] = points[3 * (size_t)p + 2];
+        }
+      }
+      rowq_fill<WPS, D>(v, off, len, w, lane, q);
+    }
+    double c[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) c[k] = 0.0;
+    // the queue is walked in place (row k + d WPS sits in slot d of the current turn,
+    // and the slot is refilled with the row D turns later), so no register holding a
+    // load in flight is ever copied and each wait covers only the oldest row
+#pragma unroll 1
+    for (int k0 = w; k0 < len; k0 += D * WPS) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int k = k0 + d * WPS;
+        if (k >= len) break;
+        const int4 id = q.id[d];
+        const double2 xy = q.xy[d];
+        const int kn = k + D * WPS;
+        if (kn < len) {
+          q.id[d] = v.obs_idx[off + 64 * kn + lane];
+          q.xy[d] = v.obs_xy[off + 64 * kn + lane];
+        }
+        // branch-free: padding slots (point -1; ext0 = intr = 0, ext1 = -1) are evaluated
+        // and dropped by selects, so the row has no exec-mask branch around it
+        const bool live = id.x >= 0;
+        double ru, rv, jx0[3], jx1[3];
+        if constexpr (VAR & 2) {
+          ru = xy.x + id.y;
+          rv = xy.y + id.w;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) jx0[q] = jx1[q] = X[q];
+        } else {
+          obs_rows<true, -1, LdsTabs<KL>, COMP>(id, xy, X, tabs, ru, rv, jx0, jx1, nullptr, nullptr);
+        }
+        if (!live) ru = rv = jx0[0] = jx0[1] = jx0[2] = jx1[0] = jx1[1] = jx1[2] = 0.0;
+        c[0] = fma(jx1[0], jx1[0], fma(jx0[0], jx0[0], c[0]));
+        c[1] = fma(jx1[0], jx1[1], fma(jx0[0], jx0[1], c[1]));
+        c[2] = fma(jx1[0], jx1[2], fma(jx0[0], jx0[2], c[2]));
+        c[3] = fma(jx1[1], jx1[1], fma(jx0[1], jx0[1], c[3]));
+        c[4] = fma(jx1[1], jx1[2], fma(jx0[1], jx0[2], c[4]));
+        c[5] = fma(jx1[2], jx1[2], fma(jx0[2], jx0[2], c[5]));
+        c[6] = fma(jx1[0], rv, fma(jx0[0], ru, c[6]));
+        c[7] = fma(jx1[1], rv, fma(jx0[1], ru, c[7]));
+        c[8] = fma(jx1[2], rv, fma(jx0[2], ru, c[8]));
+        acc[0] = fma(rv, rv, fma(ru, ru, acc[0]));
+        acc[1] += (isfinite(ru) && isfinite(rv)) ? 0.0 : 1.0;
+      }
+    }
+    // waves 1.. of the group hand their sums to wave 0 (fixed order), PH components at a time
+    if constexpr (WPS > 1 && !(VAR & 32)) {
+#pragma unroll
+      for (int ph = 0; ph < 9; ph += PH) {
+        if (w > 0) {
+#pragma unroll
+          for (int k = 0; k < PH; ++k) sh[grp][w - 1][k][lane] = c[ph + k];
+        }
+        __syncthreads();
+        if (w == 0) {
+#pragma unroll
+          for (int k = 0; k < PH; ++k) {
+            double t = c[ph + k];
+#pragma unroll
+            for (int u = 0; u < WPS - 1; ++u) t += sh[grp][u][k][lane];
+            c[ph + k] = t;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    const int p = 64 * sl + lane;
+    if (!(VAR & 16) && w == 0 && sl < v.nslice && p < v.NP) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) V[k * NPs + p] = c[k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) g[k * NPs + p] = c[6 + k];
+    }
+  }
+  if constexpr (VAR & 8) store_cost_partial<16>(acc, partial);
+  else if constexpr (VAR & 64) store_cost_partial_last<16>(acc, partial, arrivals, cost);
+  else cost_fx_add<16>(acc, costfx);
+}
+
+template <int WPS, int D, int VAR = 0>
+static void launch_pf(hipStream_t s, const DevView& v, const double* points, const double* ext, double* V, double* g,
+                      double* partial, unsigned* arrivals, double* cost, unsigned long long* costfx,
+                      unsigned long long* fx_next, int grid) {
+  // single-extrinsic problems: no second table, so the row queue can be 2 deeper
+  if (!v.any_comp && v.NI <= kLdsCams)
+    k_eval_points_pf<true, WPS, D + 2, VAR, false>
+        <<<grid, 1024, 0, s>>>(v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next);
+  else if (v.NI <= kLdsCams)
+    k_eval_points_pf<true, WPS, D, VAR><<<grid, 1024, 0, s>>>(v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next);
+  else
+    k_eval_points_pf<false, WPS, D, VAR><<<grid, 1024, 0, s>>>(v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next);
+}
+
 // LDS variants (all <= 160 KiB): wps 0 = 4 waves/slice, K staged when NI <= 128;
 // wps -1 = 1 wave/slice with every intrinsic staged (NI <= 1024); wps -2 = 2 waves/slice
 void launch_eval_points(hipStream_t s, const DevView& v, const double* points, const double* ext,
                         const double* camtab, double* V, double* g, double* partial, unsigned* arrivals,
-                        double* cost, int grid, int wps) {
+                        double* cost, unsigned long long* costfx, unsigned long long* fx_next, int grid,
+                        int wps) {
   if (wps == 0 || wps == -2) {  // LDS tables built in-kernel; grid = persistent work-groups
     if (wps == 0) {
       if (v.NI <= 128) k_eval_points_lds<128, 4><<<grid, 1024, 0, s>>>(v, points, ext, camtab, V, g, partial, arrivals, cost);
@@ -809,6 +1075,20 @@ void launch_eval_points(hipStream_t s, const DevView& v, const double* points, c
     } else {
       if (v.NI <= 128) k_eval_points_lds<128, 2><<<grid, 1024, 0, s>>>(v, points, ext, camtab, V, g, partial, arrivals, cost);
       else k_eval_points_lds<0, 2><<<grid, 1024, 0, s>>>(v, points, ext, camtab, V, g, partial, arrivals, cost);
+    }
+    return;
+  }
+  if (wps <= -100) {  // deep-prefetch variants: -(100 + 10 WPS + D + 1000 VAR)
+    switch (-wps - 100) {
+      case 12: launch_pf<1, 2>(s, v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next, grid); break;
+      case 13: launch_pf<1, 3>(s, v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next, grid); break;
+      case 23: launch_pf<2, 3>(s, v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next, grid); break;
+      case 64012: launch_pf<1, 2, 64>(s, v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next, grid); break;
+      case 64022: launch_pf<2, 2, 64>(s, v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next, grid); break;
+      case 2012: launch_pf<1, 2, 2>(s, v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next, grid); break;
+      case 4012: launch_pf<1, 2, 4>(s, v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next, grid); break;
+      case 1012: launch_pf<1, 2, 1>(s, v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next, grid); break;
+      default: launch_pf<2, 2>(s, v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next, grid); break;
     }
     return;
   }
@@ -966,11 +1246,14 @@ void launch_filter(hipStream_t s, const DevView& v, const double* points, const 
 // One block per chunk of camera-major entry positions (one camera per chunk): the
 // entry's observation is re-evaluated from its camera-major input copy (cm_idx, cm_xy,
 // 32 B, contiguous) and its camera rows reduced into U (21 upper) | g_c (6).
+// entries i0, i0 + stride, ... < e of one chunk (a block: i0 = b + threadIdx.x, stride =
+// blockDim.x; one wave of the fused pass: i0 = b + lane, stride = 64)
 template <class Tabs>
-__device__ __forceinline__ void eval_cams_chunk(const DevView& v, int b, int e, const double* __restrict__ points,
-                                                const Tabs& tabs, double (&acc)[27]) {
+__device__ __forceinline__ void eval_cams_chunk(const DevView& v, int i0, int e, int stride,
+                                                const double* __restrict__ points, const Tabs& tabs,
+                                                double (&acc)[27]) {
   // software-pipelined: the next entry's inputs (and its point) load while this one computes
-  int i = b + threadIdx.x;
+  int i = i0;
   int4 id_n = make_int4(0, 0, -1, 0);
   double2 xy_n = make_double2(0.0, 0.0);
   double X_n[3] = {0.0, 0.0, 0.0};
@@ -981,11 +1264,11 @@ __device__ __forceinline__ void eval_cams_chunk(const DevView& v, int b, int e, 
     X_n[1] = points[3 * (size_t)id_n.x + 1];
     X_n[2] = points[3 * (size_t)id_n.x + 2];
   }
-  for (; i < e; i += blockDim.x) {
+  for (; i < e; i += stride) {
     int4 id = id_n;
     const double2 xy = xy_n;
     const double X[3] = {X_n[0], X_n[1], X_n[2]};
-    const int in = i + blockDim.x;
+    const int in = i + stride;
     if (in < e) {
       id_n = v.cm_idx[in];
       xy_n = v.cm_xy[in];
@@ -1026,12 +1309,13 @@ __global__ __launch_bounds__(256) void k_eval_cams(DevView v, const int* __restr
   for (int i = 0; i < 27; ++i) acc[i] = 0.0;
   if constexpr (UNI) {
     const int2 u = v.chunk_uni[c];
-    eval_cams_chunk(v, b, e, points, UniTabs(ext, v.intr, u.x, u.y), acc);
+    eval_cams_chunk(v, b + threadIdx.x, e, blockDim.x, points, UniTabs(ext, v.intr, u.x, u.y), acc);
   } else if (small_tabs_fit(v.E, v.NI)) {
     extern __shared__ double tabs_lds[];
-    eval_cams_chunk(v, b, e, points, stage_small_tabs(tabs_lds, v.E, v.NI, camtab, v.intr), acc);
+    eval_cams_chunk(v, b + threadIdx.x, e, blockDim.x, points, stage_small_tabs(tabs_lds, v.E, v.NI, camtab, v.intr),
+                    acc);
   } else {
-    eval_cams_chunk(v, b, e, points, GlobalTabs{camtab, v.intr}, acc);
+    eval_cams_chunk(v, b + threadIdx.x, e, blockDim.x, points, GlobalTabs{camtab, v.intr}, acc);
   }
   block_reduce_store<27>(acc, partial + 27 * (size_t)c);
 }
@@ -1046,6 +1330,232 @@ void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, con
     k_eval_cams<false><<<cl.ngen, 256, lds, s>>>(v, chunk_beg, cl.ngen == cl.nchunk ? nullptr : cl.gen, points,
                                                  ext, camtab, partial);
   }
+}
+
+// ------------------------------------------------------------------------------------
+// Fused evaluation pass (BAL-shaped problems): both halves of the pass in ONE launch,
+// with camera-side and point-side waves side by side on every CU.
+// ------------------------------------------------------------------------------------
+// Why: the camera side is fp64-VALU heavy (~55 % VALU-busy on its own) and the point
+// side is latency bound (~30 %), but as two kernels they cannot overlap: the point
+// kernel's 1024-thread work-group at 128 VGPRs fills a CU's register file. Here waves
+// 0..kFusedPW-1 of each work-group run the point side (SELL slices, lane = point, a
+// D-deep row queue, R,t and K staged in LDS) and the other waves run the camera side (a
+// pair of waves per free camera, each half of its uniform chunk, table in SGPRs), so the
+// VALU work of one hides the memory latency of the other. Only the point waves need the
+// LDS tables: they stage them and meet at an LDS-counter barrier of their own, while the
+// camera waves start at once. Every reduction keeps a fixed order: the camera pair's two
+// halves are combined (row sums in LDS) by whichever wave of the pair arrives second,
+// in half-then-row order; the point waves' cost partials are summed by the last point
+// wave in wave order and added as fixed-point integers (cost_fx_add). Bitwise identical
+// results to the two-kernel pass for V, g, U, g_c (same per-lane order for V, g; the
+// camera sums are regrouped, so U, g_c agree to rounding), deterministic run to run.
+// Requirements (checked by fused_eval_fits): every observation single-extrinsic, one
+// uniform chunk per free camera, E, NI <= kLdsCams, NC <= (camera waves / 2) x grid.
+constexpr int kFusedPW = 8;               // point waves per work-group
+constexpr int kFusedCW = 16 - kFusedPW;   // camera waves (kFusedCW / 2 cameras per round)
+template <int D, int ABL = 0>  // ABL (timing ablations): 1 camera waves exit at once, 2 point waves do
+__global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __restrict__ chunk_beg,
+                                                     const double* __restrict__ points,
+                                                     const double* __restrict__ ext, double* __restrict__ V,
+                                                     double* __restrict__ g, double* __restrict__ ug,
+                                                     unsigned long long* __restrict__ costfx,
+                                                     unsigned long long* __restrict__ fx_next) {
+  constexpr int NPAIR = kFusedCW / 2;
+  __shared__ double rt_s[kLdsCams * 12];
+  __shared__ double k_s[kLdsCams * 6];
+  __shared__ double csum[NPAIR][2][4][27];  // camera pair: [half][16-lane row][component]
+  __shared__ double shp[kFusedPW][2];       // point waves' cost partials
+  __shared__ unsigned ccount[NPAIR], pbar, pdone;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (threadIdx.x < NPAIR) ccount[threadIdx.x] = 0u;
+  if (threadIdx.x == 0) pbar = pdone = 0u;
+  if (blockIdx.x == 0 && fx_next)
+    for (int i = threadIdx.x; i < kFxWords; i += blockDim.x) fx_next[i] = 0ull;
+  __syncthreads();
+
+  if (wave >= kFusedPW) {
+    // ---------------- camera side: one half of one camera's chunk per wave ----------------
+    const int cw = wave - kFusedPW, pair = cw >> 1, half = cw & 1;
+    const int c = pair * gridDim.x + blockIdx.x;  // one round (fused_eval_fits)
+    if (c >= v.NC || ABL == 1) return;
+    const int b = chunk_beg[c], e = chunk_beg[c + 1], mid = b + ((e - b) >> 1);
+    const int2 u = v.chunk_uni[c];
+    double acc[27];
+#pragma unroll
+    for (int i = 0; i < 27; ++i) acc[i] = 0.0;
+    eval_cams_chunk(v, (half ? mid : b) + lane, half ? e : mid, 64, points, UniTabs(ext, v.intr, u.x, u.y), acc);
+#pragma unroll
+    for (int k = 0; k < 27; ++k) {
+      const double t = row_sum16(acc[k]);
+      if ((lane & 15) == 15) csum[pair][half][lane >> 4][k] = t;
+    }
+    unsigned old = 0;
+    if (lane == 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      old = __hip_atomic_fetch_add(&ccount[pair], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != 1u) return;  // the other half is still running: it writes the camera row
+    if (lane < 27) {
+      double t = 0.0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t += csum[pair][h][r][lane];
+      ug[27 * (size_t)c + lane] = t;
+    }
+    return;
+  }
+
+  // ---------------- point side ----------------
+  if constexpr (ABL == 2) return;
+  const size_t NPs = (size_t)v.NP;
+  const int pw = wave;
+  const int rounds = (v.nslice + kFusedPW * gridDim.x - 1) / (kFusedPW * gridDim.x);
+  RowQueue<D> q;
+  double X[3] = {0.0, 0.0, 0.0};
+  int sl = pw * gridDim.x + blockIdx.x, off = 0, len = 0;
+  if (sl < v.nslice) {
+    off = v.slice_off[sl];
+    len = (v.slice_off[sl + 1] - off) >> 6;
+    const int p = 64 * sl + lane;
+    if (p < v.NP) {
+      X[0] = points[3 * (size_t)p];
+      X[1] = points[3 * (size_t)p + 1];
+      X[2] = points[3 * (size_t)p + 2];
+    }
+  }
+  rowq_fill<1, D>(v, off, len, 0, lane, q);
+  // intrinsics: LDS-DMA straight into k_s (no registers), 16 B per lane, k_s is lane-linear
+  {
+    const int npiece = 3 * v.NI;
+    for (int base = pw * 64; base < npiece; base += kFusedPW * 64) {
+      const int i = min(base + lane, npiece - 1);  // tail lanes repeat the last piece (same bytes, same place)
+      const double* src = v.intr + (size_t)kIntr * (i / 3) + 2 * (i % 3);
+      __builtin_amdgcn_global_load_lds(src, k_s + 2 * (size_t)base, 16, 0, 0);
+    }
+  }
+  // R, t of every extrinsic from the parameters (point threads only)
+  for (int e0 = threadIdx.x; e0 < v.E; e0 += kFusedPW * 64) {
+    double2 xw[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) xw[i] = reinterpret_cast<const double2*>(ext + 6 * (size_t)e0)[i];
+    const double x6[6] = {xw[0].x, xw[0].y, xw[1].x, xw[1].y, xw[2].x, xw[2].y};
+    double T[30];
+    cam_table(x6, T);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) reinterpret_cast<double2*>(rt_s + 12 * e0)[i] = make_double2(T[2 * i], T[2 * i + 1]);
+  }
+  // barrier of the point waves only (LDS counter): own LDS writes and LDS-DMAs retired
+  // before the arrival, acquire before the first table read
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_add(&pbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (__hip_atomic_load(&pbar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)kFusedPW)
+    __builtin_amdgcn_s_sleep(1);
+  const LdsTabs<true> tabs{rt_s, k_s, nullptr, v.intr};
+  double acc[2] = {0.0, 0.0};
+  for (int r = 0; r < rounds; ++r) {
+    if (r > 0) {
+      sl = (r * kFusedPW + pw) * gridDim.x + blockIdx.x;
+      off = len = 0;
+      X[0] = X[1] = X[2] = 0.0;
+      if (sl < v.nslice) {
+        off = v.slice_off[sl];
+        len = (v.slice_off[sl + 1] - off) >> 6;
+        const int p = 64 * sl + lane;
+        if (p < v.NP) {
+          X[0] = points[3 * (size_t)p];
+          X[1] = points[3 * (size_t)p + 1];
+          X[2] = points[3 * (size_t)p + 2];
+        }
+      }
+      rowq_fill<1, D>(v, off, len, 0, lane, q);
+    }
+    double c[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) c[k] = 0.0;
+#pragma unroll 1
+    for (int k0 = 0; k0 < len; k0 += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int k = k0 + d;
+        if (k >= len) break;
+        const int4 id = q.id[d];
+        const double2 xy = q.xy[d];
+        if (k + D < len) {
+          q.id[d] = v.obs_idx[off + 64 * (k + D) + lane];
+          q.xy[d] = v.obs_xy[off + 64 * (k + D) + lane];
+        }
+        const bool live = id.x >= 0;
+        double ru, rv, jx0[3], jx1[3];
+        obs_rows<true, -1, LdsTabs<true>, false>(id, xy, X, tabs, ru, rv, jx0, jx1, nullptr, nullptr);
+        if (!live) ru = rv = jx0[0] = jx0[1] = jx0[2] = jx1[0] = jx1[1] = jx1[2] = 0.0;
+        c[0] = fma(jx1[0], jx1[0], fma(jx0[0], jx0[0], c[0]));
+        c[1] = fma(jx1[0], jx1[1], fma(jx0[0], jx0[1], c[1]));
+        c[2] = fma(jx1[0], jx1[2], fma(jx0[0], jx0[2], c[2]));
+        c[3] = fma(jx1[1], jx1[1], fma(jx0[1], jx0[1], c[3]));
+        c[4] = fma(jx1[1], jx1[2], fma(jx0[1], jx0[2], c[4]));
+        c[5] = fma(jx1[2], jx1[2], fma(jx0[2], jx0[2], c[5]));
+        c[6] = fma(jx1[0], rv, fma(jx0[0], ru, c[6]));
+        c[7] = fma(jx1[1], rv, fma(jx0[1], ru, c[7]));
+        c[8] = fma(jx1[2], rv, fma(jx0[2], ru, c[8]));
+        acc[0] = fma(rv, rv, fma(ru, ru, acc[0]));
+        acc[1] += (isfinite(ru) && isfinite(rv)) ? 0.0 : 1.0;
+      }
+    }
+    const int p = 64 * sl + lane;
+    if (sl < v.nslice && p < v.NP) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) V[k * NPs + p] = c[k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) g[k * NPs + p] = c[6 + k];
+    }
+  }
+  // cost: wave sums, summed in wave order by the last point wave, added in fixed point
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double t = wave_sum_lane63(acc[i]);
+    if (lane == 63) shp[pw][i] = t;
+  }
+  unsigned old = 0;
+  if (lane == 63) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    old = __hip_atomic_fetch_add(&pdone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  old = __builtin_amdgcn_readlane(old, 63);
+  if (old != (unsigned)kFusedPW - 1 || lane != 0) return;
+  double pc = shp[0][0], bc = shp[0][1];
+#pragma unroll
+  for (int w = 1; w < kFusedPW; ++w) {
+    pc += shp[w][0];
+    bc += shp[w][1];
+  }
+  long long hi = 0, lo = 0;
+  if (pc >= 0.0 && pc < 0x1p62) {
+    const double ip = trunc(pc);
+    hi = (long long)ip;
+    lo = (long long)rint((pc - ip) * 0x1p52);
+  } else {
+    bc += 1.0;
+  }
+  unsigned long long* shd = costfx + kFxStride * (blockIdx.x % kFxCopies);
+  if (hi) __hip_atomic_fetch_add(shd, (unsigned long long)hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lo) __hip_atomic_fetch_add(shd + 1, (unsigned long long)lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (bc != 0.0) __hip_atomic_fetch_add(shd + 2, (unsigned long long)bc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+bool fused_eval_fits(const DevView& v, int nchunk, int ngen, int ncross, int grid) {
+  return !v.any_comp && ncross == 0 && ngen == 0 && nchunk == v.NC && v.NC > 0 && v.E <= kLdsCams &&
+         v.NI <= kLdsCams && v.NC <= (kFusedCW / 2) * grid;
+}
+void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
+                       double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
+                       int grid) {
+  const int abl = getenv("DAB_FUSED_ABL") ? atoi(getenv("DAB_FUSED_ABL")) : 0;  // timing ablations
+  if (abl == 1) k_eval_fused<4, 1><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
+  else if (abl == 2) k_eval_fused<4, 2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
+  else k_eval_fused<4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
 }
 
 // arc∘ring cross blocks Jc0^T Jc1, one block per chunk of composed observations sorted

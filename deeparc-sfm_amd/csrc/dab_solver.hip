@@ -72,7 +72,10 @@ enum Slot {
   S_CAM0,          // 5 camera slots (launch_cam_norms)
   S_TIME = S_CAM0 + 5,  // solver wall-clock (max over ranks)
   S_END,
-  S_NSLOTS = 16
+  // fixed-point cost shards of the prefetch point kernel (uint64 bit patterns: sum r^2
+  // integer part, fraction * 2^52, non-finite count per shard; cost_fx_add)
+  S_CFX = 16,  // two sets of kFxWords, alternating between passes
+  S_NSLOTS = S_CFX + 2 * kFxWords
 };
 
 struct Dev {
@@ -182,6 +185,8 @@ struct dab_handle {
   double* d_scal = nullptr;    // S_NSLOTS
   int* d_flags = nullptr;      // [0] point factor fail, [1] chol fail
   double* h_scal = nullptr;    // pinned
+  bool cost_fx_pending = false;  // fixed-point set fx_last holds the last evaluation's cost (read_scalars converts)
+  int fx_last = 1;               // set of the last fixed-point pass (both sets start zeroed)
   int* h_flags = nullptr;      // pinned
   int red_grid = 1;
   int eval_grid = 1;  // k_eval_points blocks (one SELL slice per block)
@@ -192,6 +197,7 @@ struct dab_handle {
   unsigned* d_cg_cnt = nullptr;
   double* d_fused_partial = nullptr;
   int eval_wps = 0;   // 0: LDS tables; else waves per slice (DAB_EVAL_WPS tuning knob)
+  bool fused = false;  // evaluation pass as one launch (launch_eval_fused; DAB_EVAL_FUSED=0 disables)
 
   ~dab_handle() {
     dev.release();
@@ -245,6 +251,40 @@ struct dab_handle {
     HIP_OK(hipMemcpyAsync(buf, h_stage, n * sizeof(double), hipMemcpyHostToDevice, stream));
     HIP_OK(hipStreamSynchronize(stream));
     return 0;
+  }
+
+  // exact integer sum over ranks of n uint64 words (the fixed-point cost); the host path
+  // moves each word as three 22-bit pieces, which gloo's double sum adds exactly
+  int allreduce_u64(uint64_t* buf, size_t n) {
+    if (world <= 1 || n == 0) return 0;
+    if (!host_cb) {
+      NCCL_OK(ncclAllReduce(buf, buf, n, ncclUint64, ncclSum, comm, stream));
+      return 0;
+    }
+    std::vector<uint64_t> tmp(n);
+    CHECK_RC(stage(3 * n));
+    HIP_OK(hipMemcpyAsync(tmp.data(), buf, n * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    for (size_t i = 0; i < n; ++i)
+      for (int k = 0; k < 3; ++k) h_stage[3 * i + k] = (double)((tmp[i] >> (22 * k)) & 0x3fffffull);
+    if (host_cb(h_stage, (int64_t)(3 * n), 0, host_user) != 0)
+      return set_error(DAB_E_COMM, "host all-reduce callback failed");
+    for (size_t i = 0; i < n; ++i) {
+      uint64_t v = 0;
+      for (int k = 0; k < 3; ++k) v += (uint64_t)h_stage[3 * i + k] << (22 * k);
+      tmp[i] = v;
+    }
+    HIP_OK(hipMemcpyAsync(buf, tmp.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    return 0;
+  }
+  unsigned long long* cost_fx(int set) const {
+    return reinterpret_cast<unsigned long long*>(d_scal + S_CFX + (size_t)kFxWords * set);
+  }
+  // cost of the last evaluation pass summed over ranks (fixed point or double slots)
+  int allreduce_cost() {
+    if (cost_fx_pending) return allreduce_u64(reinterpret_cast<uint64_t*>(cost_fx(fx_last)), kFxWords);
+    return allreduce(d_scal + S_COST, 2, ncclSum);
   }
 
   int allreduce(double* buf, size_t n, ncclRedOp_t op) {
@@ -751,10 +791,15 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
     h->ncu = ncu;
     // LDS variants: one persistent work-group per CU (at most one per slice)
     h->eval_grid = h->eval_wps <= 0 ? std::max(1, std::min(ncu, h->nslice)) : std::max(1, h->nslice);
+    const char* fenv = getenv("DAB_EVAL_FUSED");
+    h->fused = (!fenv || atoi(fenv) != 0) && h->world == 1;
   }
   CHECK_RC(d.alloc(&h->d_gpart, (size_t)std::max(h->red_grid, h->eval_grid) * 4));
   CHECK_RC(d.alloc(&h->d_scal, S_NSLOTS));
   CHECK_RC(d.alloc(&h->d_flags, 4));
+  HIP_OK(hipMemsetAsync(h->d_scal, 0, sizeof(double) * S_NSLOTS, s));  // both fixed-point cost sets start zeroed
+  h->fx_last = 1;
+  h->cost_fx_pending = false;
   HIP_OK(hipMemsetAsync(h->d_dc, 0, sizeof(double) * std::max(1, 6 * NC), s));
   HIP_OK(hipStreamSynchronize(s));
 
@@ -766,6 +811,8 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   v.NI = h->NI;
   v.NE = NE;
   v.nslice = h->nslice;
+  v.any_comp = 0;
+  for (int o = 0; o < h->N && !v.any_comp; ++o) v.any_comp = h->prob.obs_ext1[o] >= 0;
   v.obs_idx = h->d_obs_idx;
   v.obs_xy = h->d_obs_xy;
   v.cm_idx = h->d_cm_idx;
@@ -780,6 +827,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   v.cm_pt = h->d_cm_pt;
   v.ext_col = h->d_ext_col;
   v.intr = h->d_intr;
+  h->fused = h->fused && fused_eval_fits(v, h->nchunk, h->chunks.ngen, h->ncross, h->ncu);
   h->have_problem = true;
   return 0;
 }
@@ -1046,6 +1094,17 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
   bool overlapped = false;
   const bool need_tab = (h->NC > 0 && (h->chunks.ngen > 0 || h->ncross > 0)) || eval_points_needs_camtab(h->eval_wps);
   if (!camtab_ready && need_tab) launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
+  const bool fx = h->fused || eval_points_fx(h->eval_wps);
+  if (fx) h->fx_last ^= 1;  // this pass adds into set fx_last and zeroes the other
+  h->cost_fx_pending = fx;
+  if (h->fused) {  // both halves of the pass in one launch (launch_eval_fused)
+    if (ev_mid) HIP_OK(hipEventRecord(ev_mid, s));
+    launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
+                      h->cost_fx(h->fx_last ^ 1), h->ncu);
+    if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
+    if (h->NC > 0) CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
+    return 0;
+  }
   if (h->NC > 0) {
     // one chunk per camera: the chunk kernels write the camera rows directly
     const bool direct = h->nchunk == h->NC;
@@ -1074,7 +1133,8 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
   }
   if (ev_mid) HIP_OK(hipEventRecord(ev_mid, s));
   launch_eval_points(s, h->view, h->d_points, h->d_ext, h->d_camtab, h->d_V, h->d_g, h->d_gpart, h->d_arrivals,
-                     h->d_scal + S_COST, h->eval_grid, h->eval_wps);
+                     h->d_scal + S_COST, h->cost_fx(h->fx_last), h->cost_fx(h->fx_last ^ 1), h->eval_grid,
+                     h->eval_wps);
   if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
   if (overlapped) HIP_OK(hipStreamWaitEvent(s, h->ev_comm, 0));
   return 0;
@@ -1093,7 +1153,7 @@ static int eval_jacobian_and_blocks(dab_handle* h, bool with_norms) {
                      h->d_scal + S_CAM0);
   }
   // cross-rank: sums of cost, bad, gnorm, xnorm; max of gmax
-  CHECK_RC(h->allreduce(h->d_scal + S_COST, 2, ncclSum));
+  CHECK_RC(h->allreduce_cost());
   if (with_norms) {
     CHECK_RC(h->allreduce(h->d_scal + S_GMAX_P, 1, ncclMax));
     CHECK_RC(h->allreduce(h->d_scal + S_GNORM_P, 2, ncclSum));
@@ -1105,6 +1165,20 @@ static int read_scalars(dab_handle* h) {
   HIP_OK(hipMemcpyAsync(h->h_scal, h->d_scal, sizeof(double) * S_NSLOTS, hipMemcpyDeviceToHost, h->stream));
   HIP_OK(hipMemcpyAsync(h->h_flags, h->d_flags, sizeof(int) * 4, hipMemcpyDeviceToHost, h->stream));
   HIP_OK(hipStreamSynchronize(h->stream));
+  if (h->cost_fx_pending) {
+    // the last evaluation pass left its cost in fixed point (cost_fx_add): exact integer
+    // sums, converted once here
+    uint64_t fx[3] = {0, 0, 0};
+    for (int c = 0; c < kFxCopies; ++c)
+      for (int i = 0; i < 3; ++i) {
+        uint64_t w;
+        std::memcpy(&w, h->h_scal + S_CFX + (size_t)kFxWords * h->fx_last + kFxStride * c + i, sizeof(uint64_t));
+        fx[i] += w;
+      }
+    h->h_scal[S_COST] = (double)(int64_t)fx[0] + (double)(int64_t)fx[1] * 0x1p-52;
+    h->h_scal[S_COST_BAD] = (double)fx[2];
+    h->cost_fx_pending = false;
+  }
   return 0;
 }
 
@@ -1410,6 +1484,7 @@ extern "C" int dab_eval_residuals(dab_handle* h, double* residuals, double* cost
   launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
   launch_residual(s, h->view, h->d_points, h->d_camtab, h->d_r, h->d_gpart, h->red_grid);
   launch_final_sum(s, h->red_grid, 2, h->d_gpart, h->d_scal + S_COST);
+  h->cost_fx_pending = false;
   CHECK_RC(read_scalars(h));
   if (cost) *cost = 0.5 * h->h_scal[S_COST];
   if (residuals) {
@@ -1566,7 +1641,7 @@ extern "C" int dab_bench_eval_pass(dab_handle* h, int with_assembly, int count) 
   for (int step = 0; step < count; ++step) {
     if (sample <= 0 || step % sample != 0) {
       CHECK_RC(eval_pass(h, false));
-      CHECK_RC(h->allreduce(h->d_scal + S_COST, 2, ncclSum));
+      CHECK_RC(h->allreduce_cost());
       continue;
     }
     // per-step events from a pool: nothing here waits for the device, so back-to-back
@@ -1584,12 +1659,15 @@ extern "C" int dab_bench_eval_pass(dab_handle* h, int with_assembly, int count) 
     HIP_OK(hipEventRecord(ev[0], s));
     if (with_assembly) {
       CHECK_RC(eval_pass(h, false, ev[1], ev[2]));
-      CHECK_RC(h->allreduce(h->d_scal + S_COST, 2, ncclSum));
+      CHECK_RC(h->allreduce_cost());
     } else {
       if (eval_points_needs_camtab(h->eval_wps)) launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
       HIP_OK(hipEventRecord(ev[1], s));
+      if (eval_points_fx(h->eval_wps)) h->fx_last ^= 1;
+      h->cost_fx_pending = eval_points_fx(h->eval_wps);
       launch_eval_points(s, h->view, h->d_points, h->d_ext, h->d_camtab, h->d_V, h->d_g, h->d_gpart, h->d_arrivals,
-                         h->d_scal + S_COST, h->eval_grid, h->eval_wps);
+                         h->d_scal + S_COST, h->cost_fx(h->fx_last), h->cost_fx(h->fx_last ^ 1), h->eval_grid,
+                         h->eval_wps);
       HIP_OK(hipEventRecord(ev[2], s));
     }
     HIP_OK(hipEventRecord(ev[3], s));
