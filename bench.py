@@ -3,7 +3,9 @@
 metric (BASELINE.json): "M observations/sec residual+Jacobian; wall-clock/LM-iter".
   step  = one evaluation pass over the rank's shard with inputs resident in HBM:
           residual + analytic Jacobian of every observation, reduced on chip into the
-          J^T J / J^T r blocks (matrix-free: point side k_eval_points -> V, g; camera
+          J^T J / J^T r blocks (matrix-free; BAL-shaped problems on one GPU: one fused
+          launch k_eval_fused with camera-side and point-side waves side by side; else point
+          side k_eval_points -> V, g; camera
           side k_eval_cams -> U, g_c, all-reduced over RCCL when N > 1).
   value = observations processed by all ranks / max-over-ranks wall time, in M obs/s.
   workload: BASELINE config 3 shape per GPU (1k cameras / 100k points / 1M obs, fp64);
@@ -17,7 +19,9 @@ metric (BASELINE.json): "M observations/sec residual+Jacobian; wall-clock/LM-ite
           the N ranks (strong scaling): the evaluation pass (step time, M obs/s, the point
           kernel's time and HBM roofline fraction on rank 0's shard) and the mixed-precision
           PCG LM iteration (wall-clock, median).
-  roofline: k_eval_points (point side of the pass), algorithmic bytes / HIP-event time.
+  roofline: the evaluation kernel (k_eval_fused, or k_eval_points for the two-kernel
+          pass), algorithmic bytes (observations read once, parameters, outputs) / HIP-event
+          time.
   cpu_baseline: the C oracle (Ceres-semantics restatement, OpenMP) on the box's host
           cores, rank 0 at N=1 only, bounded sample.
 """
@@ -124,6 +128,8 @@ def main():
     value = world * n_obs * args.steps / dt / 1e6
     jac_bytes = solver.jacobian_bytes()
     achieved = jac_bytes / (jac_ms * 1e-3) / 1e9
+    fused = solver.eval_fused()
+    eval_kernel = "k_eval_fused" if fused else "k_eval_points"
 
     # ---- LM iterations (wall-clock per iteration, same problem) ----
     # "lm_*": exact reduced-camera solve (dense Schur + device Cholesky, the reference's
@@ -231,7 +237,8 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             t = json.load(open(args.traffic_json))
-            if t.get("config") == args.config and t.get("n_obs") == n_obs:
+            if (t.get("config") == args.config and t.get("n_obs") == n_obs
+                    and str(t.get("kernel", "")).startswith(eval_kernel)):
                 traffic = t.get("bytes_per_launch")
         except Exception:
             traffic = None
@@ -249,10 +256,12 @@ def main():
                        "parallelism": f"point-sharded x{world}, RCCL all-reduce of camera blocks"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_eval_points", "kernel_ms": jac_ms,
+                         "kernel": eval_kernel, "kernel_ms": jac_ms,
                          "algorithmic_bytes_per_launch": jac_bytes},
-            "point_kernel_mobs_per_s": n_obs / (jac_ms * 1e-3) / 1e6,
-            "camera_side_ms": asm_ms,
+            "eval_kernel_mobs_per_s": n_obs / (jac_ms * 1e-3) / 1e6,
+            "eval_schedule": ("fused: camera and point side in one launch" if fused else
+                              "two kernels: k_eval_cams then k_eval_points"),
+            "outside_kernel_ms": asm_ms,
             "cpu_baseline": cpu,
         }
         if lm:

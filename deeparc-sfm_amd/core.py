@@ -288,6 +288,11 @@ class Solver:
         check(self.lib.dab_jacobian_bytes(self.h, C.byref(b)), self.lib)
         return b.value
 
+    def eval_fused(self):
+        f = C.c_int32()
+        check(self.lib.dab_eval_schedule(self.h, C.byref(f)), self.lib)
+        return bool(f.value)
+
 
 def solve(problem, max_iteration=1000, max_second=3600, freeze_camera=False, device=0,
           verbose=False, **opt_kw):

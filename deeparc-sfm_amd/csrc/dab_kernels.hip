@@ -1248,10 +1248,12 @@ void launch_filter(hipStream_t s, const DevView& v, const double* points, const 
 // 32 B, contiguous) and its camera rows reduced into U (21 upper) | g_c (6).
 // entries i0, i0 + stride, ... < e of one chunk (a block: i0 = b + threadIdx.x, stride =
 // blockDim.x; one wave of the fused pass: i0 = b + lane, stride = 64)
-template <class Tabs>
-__device__ __forceinline__ void eval_cams_chunk(const DevView& v, int i0, int e, int stride,
-                                                const double* __restrict__ points, const Tabs& tabs,
-                                                double (&acc)[27]) {
+// MakeTabs: a callable returning the table view, called after the first entry's loads
+// are issued (the fused pass builds the camera table in SGPRs while they are in flight).
+template <class MakeTabs>
+__device__ __forceinline__ void eval_cams_chunk_lazy(const DevView& v, int i0, int e, int stride,
+                                                     const double* __restrict__ points, MakeTabs make_tabs,
+                                                     double (&acc)[27]) {
   // software-pipelined: the next entry's inputs (and its point) load while this one computes
   int i = i0;
   int4 id_n = make_int4(0, 0, -1, 0);
@@ -1264,6 +1266,7 @@ __device__ __forceinline__ void eval_cams_chunk(const DevView& v, int i0, int e,
     X_n[1] = points[3 * (size_t)id_n.x + 1];
     X_n[2] = points[3 * (size_t)id_n.x + 2];
   }
+  const auto tabs = make_tabs();
   for (; i < e; i += stride) {
     int4 id = id_n;
     const double2 xy = xy_n;
@@ -1291,6 +1294,79 @@ __device__ __forceinline__ void eval_cams_chunk(const DevView& v, int i0, int e,
       }
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[21 + a] = fma(jb[a], rv, fma(ja[a], ru, acc[21 + a]));
+  }
+}
+
+template <class Tabs>
+__device__ __forceinline__ void eval_cams_chunk(const DevView& v, int i0, int e, int stride,
+                                                const double* __restrict__ points, const Tabs& tabs,
+                                                double (&acc)[27]) {
+  eval_cams_chunk_lazy(v, i0, e, stride, points, [&]() -> const Tabs& { return tabs; }, acc);
+}
+
+// Uniform chunk, single-extrinsic observations (the fused pass's camera waves): entries
+// i0, i0 + stride, ... < e with a three-slot software pipeline in static registers: while
+// entry i computes, the point of entry i + stride is gathered (its index arrived one step
+// earlier) and the index and pixel of entry i + 2 stride are loaded. The simple one-ahead
+// pipeline waits for the next index right before every gather, i.e. one HBM latency per
+// entry; here a wait only ever covers loads issued a full step earlier. Only the point
+// index (4 B of the 16-B cm_idx record) is read: the table is the chunk's.
+template <class MakeTabs>
+__device__ __forceinline__ void eval_cams_uni_pipe(const DevView& v, int i0, int e, int stride,
+                                                   const double* __restrict__ points, MakeTabs make_tabs,
+                                                   double (&acc)[27]) {
+  const int* __restrict__ cm_pt = reinterpret_cast<const int*>(v.cm_idx);  // .x of record i at 4 i
+  int pt[3];
+  double2 xy[3];
+  double X[3][3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    pt[s] = -1;
+    xy[s] = make_double2(0.0, 0.0);
+    X[s][0] = X[s][1] = X[s][2] = 0.0;
+  }
+  if (i0 < e) {
+    pt[0] = cm_pt[4 * (size_t)i0];
+    xy[0] = v.cm_xy[i0];
+  }
+  if (i0 + stride < e) {
+    pt[1] = cm_pt[4 * (size_t)(i0 + stride)];
+    xy[1] = v.cm_xy[i0 + stride];
+  }
+  if (pt[0] >= 0) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) X[0][q] = points[3 * (size_t)pt[0] + q];
+  }
+  const auto tabs = make_tabs();
+  for (int i = i0; i < e; i += 3 * stride) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int ii = i + u * stride;
+      if (ii >= e) break;
+      constexpr int S1[3] = {1, 2, 0}, S2[3] = {2, 0, 1};
+      const int s1 = S1[u], s2 = S2[u];
+      if (pt[s1] >= 0 && ii + stride < e) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) X[s1][q] = points[3 * (size_t)pt[s1] + q];
+      }
+      if (ii + 2 * stride < e) {
+        pt[s2] = cm_pt[4 * (size_t)(ii + 2 * stride)];
+        xy[s2] = v.cm_xy[ii + 2 * stride];
+      }
+      double ru, rv, ja[6], jb[6];
+      obs_rows<false, 0, UniTabs, false>(make_int4(pt[u], 0, -1, 0), xy[u], X[u], tabs, ru, rv, nullptr, nullptr,
+                                          ja, jb);
+      int k = 0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int bb = a; bb < 6; ++bb) {
+          acc[k] = fma(jb[a], jb[bb], fma(ja[a], ja[bb], acc[k]));
+          ++k;
+        }
+#pragma unroll
+      for (int a = 0; a < 6; ++a) acc[21 + a] = fma(jb[a], rv, fma(ja[a], ru, acc[21 + a]));
+    }
   }
 }
 
@@ -1364,7 +1440,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
   constexpr int NPAIR = kFusedCW / 2;
   __shared__ double rt_s[kLdsCams * 12];
   __shared__ double k_s[kLdsCams * 6];
-  __shared__ double csum[NPAIR][2][4][27];  // camera pair: [half][16-lane row][component]
+  __shared__ double csum[NPAIR][2][27];     // camera pair: [half][component]
   __shared__ double shp[kFusedPW][2];       // point waves' cost partials
   __shared__ unsigned ccount[NPAIR], pbar, pdone;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1384,12 +1460,9 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
     double acc[27];
 #pragma unroll
     for (int i = 0; i < 27; ++i) acc[i] = 0.0;
-    eval_cams_chunk(v, (half ? mid : b) + lane, half ? e : mid, 64, points, UniTabs(ext, v.intr, u.x, u.y), acc);
-#pragma unroll
-    for (int k = 0; k < 27; ++k) {
-      const double t = row_sum16(acc[k]);
-      if ((lane & 15) == 15) csum[pair][half][lane >> 4][k] = t;
-    }
+    eval_cams_uni_pipe(v, (half ? mid : b) + lane, half ? e : mid, 64, points,
+                       [&]() { return UniTabs(ext, v.intr, u.x, u.y); }, acc);
+    wave_sums_transposed<27>(acc, csum[pair][half]);
     unsigned old = 0;
     if (lane == 0) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1397,14 +1470,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
     }
     old = __builtin_amdgcn_readfirstlane(old);
     if (old != 1u) return;  // the other half is still running: it writes the camera row
-    if (lane < 27) {
-      double t = 0.0;
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) t += csum[pair][h][r][lane];
-      ug[27 * (size_t)c + lane] = t;
-    }
+    if (lane < 27) ug[27 * (size_t)c + lane] = csum[pair][0][lane] + csum[pair][1][lane];
     return;
   }
 
@@ -1553,9 +1619,10 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
                        double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
                        int grid) {
   const int abl = getenv("DAB_FUSED_ABL") ? atoi(getenv("DAB_FUSED_ABL")) : 0;  // timing ablations
-  if (abl == 1) k_eval_fused<4, 1><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
-  else if (abl == 2) k_eval_fused<4, 2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
-  else k_eval_fused<4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
+  if (abl == 1) k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
+  else if (abl == 2) k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
+  else if (abl == 14) k_eval_fused<4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
+  else k_eval_fused<2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
 }
 
 // arc∘ring cross blocks Jc0^T Jc1, one block per chunk of composed observations sorted

@@ -1705,9 +1705,21 @@ extern "C" int dab_jacobian_bytes(dab_handle* h, double* bytes) {
   // LDS variants build R, t from the 48-B extrinsics; the global-table variants read the
   // 96-B R, t part of the camera tables instead. The Jacobian itself never reaches HBM, so
   // its 16 k bytes per observation are not counted (they are not moved).
+  // The fused pass (k_eval_fused) also writes U | g_c (216 B per free camera); its
+  // camera-side waves read the observations a second time from the camera-major copy, but
+  // that re-read is a property of the schedule, not of the work, so it is not counted
+  // (it shows up in the PMC traffic instead).
   const double ext_b = eval_points_needs_camtab(h->eval_wps) ? 96.0 : 48.0;
   double b = (24.0 + 72.0) * h->NP + ext_b * h->E + 48.0 * h->NI;
+  if (h->fused) b += 216.0 * h->NC;
   for (int o = 0; o < h->N; ++o) b += 16.0 + 4.0 * (h->prob.obs_ext1[o] >= 0 ? 3 : 2);
   *bytes = b;
+  return 0;
+}
+
+extern "C" int dab_eval_schedule(dab_handle* h, int32_t* fused) {
+  clear_error();
+  if (!h || !h->have_problem || !fused) return set_error(DAB_E_STATE, "no problem set");
+  *fused = h->fused ? 1 : 0;
   return 0;
 }

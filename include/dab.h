@@ -236,6 +236,10 @@ int dab_sync(dab_handle* h);
 int dab_bench_kernel_ms(dab_handle* h, double* jac_ms, double* assembly_ms);
 /* Algorithmic HBM bytes of one residual+Jacobian launch on the resident problem. */
 int dab_jacobian_bytes(dab_handle* h, double* bytes);
+/* Which evaluation schedule the resident problem uses: *fused = 1 when the pass is the
+ * single fused launch (k_eval_fused: camera and point side together), 0 for the
+ * two-kernel pass (k_eval_cams + k_eval_points). */
+int dab_eval_schedule(dab_handle* h, int32_t* fused);
 
 /* ---- host utilities (no device needed) ----------------------------------------------- */
 /* Deterministic synthetic problems. kind 0: BAL-shaped (non-shared, one

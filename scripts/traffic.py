@@ -38,7 +38,8 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--config", default="c3_1kcam")
     ap.add_argument("--n-obs", type=int, default=1000000)
-    ap.add_argument("--kernel", default="k_eval_points")
+    ap.add_argument("--kernel", default="auto", help="kernel name prefix (auto: k_eval_fused if it ran, "
+                    "else k_eval_points)")
     a = ap.parse_args()
     fetch, write = load(a.fetch_dir, "FETCH_SIZE"), load(a.write_dir, "WRITE_SIZE")
     table = {}
@@ -49,7 +50,9 @@ def main():
         wb = 1024.0 * sum(w) / len(w) if w else None
         table[short(k)] = dict(launches=max(len(f), len(w)), fetch_bytes_x2=fb, write_bytes=wb,
                                bytes_per_launch=(fb or 0.0) + (wb or 0.0))
-    # the point-kernel variant the bench ran (most launches among the matching names)
+    if a.kernel == "auto":
+        a.kernel = "k_eval_fused" if any(k.startswith("k_eval_fused") for k in table) else "k_eval_points"
+    # the evaluation-kernel variant the bench ran (most launches among the matching names)
     main_k = sorted((k for k in table if k.startswith(a.kernel)), key=lambda k: -table[k]["launches"])
     out = dict(config=a.config, n_obs=a.n_obs, kernel=main_k[0] if main_k else None,
                bytes_per_launch=table[main_k[0]]["bytes_per_launch"] if main_k else None,
