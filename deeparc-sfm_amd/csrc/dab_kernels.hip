@@ -1310,12 +1310,12 @@ __device__ __forceinline__ void eval_cams_chunk(const DevView& v, int i0, int e,
 // earlier) and the index and pixel of entry i + 2 stride are loaded. The simple one-ahead
 // pipeline waits for the next index right before every gather, i.e. one HBM latency per
 // entry; here a wait only ever covers loads issued a full step earlier. Only the point
-// index (4 B of the 16-B cm_idx record) is read: the table is the chunk's.
+// index is read (cm_pt, 4 B, not the 16-B cm_idx record): the table is the chunk's.
 template <class MakeTabs>
 __device__ __forceinline__ void eval_cams_uni_pipe(const DevView& v, int i0, int e, int stride,
                                                    const double* __restrict__ points, MakeTabs make_tabs,
                                                    double (&acc)[27]) {
-  const int* __restrict__ cm_pt = reinterpret_cast<const int*>(v.cm_idx);  // .x of record i at 4 i
+  const int* __restrict__ cm_pt = v.cm_pt;
   int pt[3];
   double2 xy[3];
   double X[3][3];
@@ -1326,11 +1326,11 @@ __device__ __forceinline__ void eval_cams_uni_pipe(const DevView& v, int i0, int
     X[s][0] = X[s][1] = X[s][2] = 0.0;
   }
   if (i0 < e) {
-    pt[0] = cm_pt[4 * (size_t)i0];
+    pt[0] = cm_pt[i0];
     xy[0] = v.cm_xy[i0];
   }
   if (i0 + stride < e) {
-    pt[1] = cm_pt[4 * (size_t)(i0 + stride)];
+    pt[1] = cm_pt[i0 + stride];
     xy[1] = v.cm_xy[i0 + stride];
   }
   if (pt[0] >= 0) {
@@ -1350,7 +1350,7 @@ __device__ __forceinline__ void eval_cams_uni_pipe(const DevView& v, int i0, int
         for (int q = 0; q < 3; ++q) X[s1][q] = points[3 * (size_t)pt[s1] + q];
       }
       if (ii + 2 * stride < e) {
-        pt[s2] = cm_pt[4 * (size_t)(ii + 2 * stride)];
+        pt[s2] = cm_pt[ii + 2 * stride];
         xy[s2] = v.cm_xy[ii + 2 * stride];
       }
       double ru, rv, ja[6], jb[6];
@@ -1385,7 +1385,8 @@ __global__ __launch_bounds__(256) void k_eval_cams(DevView v, const int* __restr
   for (int i = 0; i < 27; ++i) acc[i] = 0.0;
   if constexpr (UNI) {
     const int2 u = v.chunk_uni[c];
-    eval_cams_chunk(v, b + threadIdx.x, e, blockDim.x, points, UniTabs(ext, v.intr, u.x, u.y), acc);
+    eval_cams_uni_pipe(v, b + threadIdx.x, e, blockDim.x, points, [&]() { return UniTabs(ext, v.intr, u.x, u.y); },
+                       acc);
   } else if (small_tabs_fit(v.E, v.NI)) {
     extern __shared__ double tabs_lds[];
     eval_cams_chunk(v, b + threadIdx.x, e, blockDim.x, points, stage_small_tabs(tabs_lds, v.E, v.NI, camtab, v.intr),
@@ -1393,7 +1394,16 @@ __global__ __launch_bounds__(256) void k_eval_cams(DevView v, const int* __restr
   } else {
     eval_cams_chunk(v, b + threadIdx.x, e, blockDim.x, points, GlobalTabs{camtab, v.intr}, acc);
   }
-  block_reduce_store<27>(acc, partial + 27 * (size_t)c);
+  // per-wave transposed sums (wave_sums_transposed), then the waves in order
+  __shared__ double wsum[kRedBlock / 64][27];
+  wave_sums_transposed<27>(acc, wsum[threadIdx.x >> 6]);
+  __syncthreads();
+  if (threadIdx.x < 27) {
+    double t = wsum[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < kRedBlock / 64; ++w) t += wsum[w][threadIdx.x];
+    partial[27 * (size_t)c + threadIdx.x] = t;
+  }
 }
 
 void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, const int* chunk_beg,
@@ -1430,7 +1440,8 @@ void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, con
 // uniform chunk per free camera, E, NI <= kLdsCams, NC <= (camera waves / 2) x grid.
 constexpr int kFusedPW = 8;               // point waves per work-group
 constexpr int kFusedCW = 16 - kFusedPW;   // camera waves (kFusedCW / 2 cameras per round)
-template <int D, int ABL = 0>  // ABL (timing ablations): 1 camera waves exit at once, 2 point waves do
+template <int D, int ABL = 0>  // ABL (timing ablations): 1 camera waves exit at once, 2 point waves do;
+                                // 21 / 22: point / camera waves at raised issue priority
 __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __restrict__ chunk_beg,
                                                      const double* __restrict__ points,
                                                      const double* __restrict__ ext, double* __restrict__ V,
@@ -1452,6 +1463,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
 
   if (wave >= kFusedPW) {
     // ---------------- camera side: one half of one camera's chunk per wave ----------------
+    if constexpr (ABL == 22) __builtin_amdgcn_s_setprio(2);
     const int cw = wave - kFusedPW, pair = cw >> 1, half = cw & 1;
     const int c = pair * gridDim.x + blockIdx.x;  // one round (fused_eval_fits)
     if (c >= v.NC || ABL == 1) return;
@@ -1476,6 +1488,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
 
   // ---------------- point side ----------------
   if constexpr (ABL == 2) return;
+  if constexpr (ABL == 21) __builtin_amdgcn_s_setprio(2);
   const size_t NPs = (size_t)v.NP;
   const int pw = wave;
   const int rounds = (v.nslice + kFusedPW * gridDim.x - 1) / (kFusedPW * gridDim.x);
@@ -1621,6 +1634,8 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
   const int abl = getenv("DAB_FUSED_ABL") ? atoi(getenv("DAB_FUSED_ABL")) : 0;  // timing ablations
   if (abl == 1) k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
   else if (abl == 2) k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
+  else if (abl == 21) k_eval_fused<2, 21><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
+  else if (abl == 22) k_eval_fused<2, 22><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
   else if (abl == 14) k_eval_fused<4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
   else k_eval_fused<2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
 }

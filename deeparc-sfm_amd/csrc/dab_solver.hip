@@ -1705,13 +1705,14 @@ extern "C" int dab_jacobian_bytes(dab_handle* h, double* bytes) {
   // LDS variants build R, t from the 48-B extrinsics; the global-table variants read the
   // 96-B R, t part of the camera tables instead. The Jacobian itself never reaches HBM, so
   // its 16 k bytes per observation are not counted (they are not moved).
-  // The fused pass (k_eval_fused) also writes U | g_c (216 B per free camera); its
-  // camera-side waves read the observations a second time from the camera-major copy, but
-  // that re-read is a property of the schedule, not of the work, so it is not counted
-  // (it shows up in the PMC traffic instead).
+  // The fused pass (k_eval_fused) also produces the camera side: it writes U | g_c (216 B
+  // per free camera) and reads every entry a second time in camera-major order (20 B:
+  // point index + pixel; the chunk's camera and intrinsic are per block). A deterministic
+  // matrix-free pass needs both traversal orders (point-major for V, g; camera-major for
+  // U, g_c: no atomics, no per-observation partials), so both reads are algorithmic.
   const double ext_b = eval_points_needs_camtab(h->eval_wps) ? 96.0 : 48.0;
   double b = (24.0 + 72.0) * h->NP + ext_b * h->E + 48.0 * h->NI;
-  if (h->fused) b += 216.0 * h->NC;
+  if (h->fused) b += 216.0 * h->NC + 20.0 * h->NE;
   for (int o = 0; o < h->N; ++o) b += 16.0 + 4.0 * (h->prob.obs_ext1[o] >= 0 ? 3 : 2);
   *bytes = b;
   return 0;

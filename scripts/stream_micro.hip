@@ -106,5 +106,30 @@ int main(int argc, char** argv) {
   for (auto e : eg)
     printf("empty %4d x %4d: 1 KB LDS %.2f us, 150 KB LDS %.2f us\n", e[0], e[1], run_empty<1>(part, e[0], e[1], reps),
            run_empty<150>(part, e[0], e[1], reps));
+  // the same launches captured once into a graph and replayed
+  for (auto e : eg) {
+    hipStream_t st;
+    CK(hipStreamCreate(&st));
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+    for (int r = 0; r < reps; ++r) k_stream<1><<<e[0], e[1], 0, st>>>(n, idx, xy, part);
+    CK(hipStreamEndCapture(st, &g));
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    CK(hipGraphLaunch(ge, st));
+    CK(hipStreamSynchronize(st));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    CK(hipEventRecord(a, st));
+    CK(hipGraphLaunch(ge, st));
+    CK(hipEventRecord(b, st));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    const float us_stream = run<1>(n, idx, xy, part, e[0], e[1], reps);
+    printf("stream kernel %4d x %4d: graph %.2f us/launch, stream %.2f us/launch\n", e[0], e[1], ms / reps * 1e3f,
+           us_stream);
+  }
   return 0;
 }
