@@ -205,6 +205,59 @@ def test_cg_update_work_groups_match_single(pkg, gpu, kind, monkeypatch):
                                rtol=1e-10)
 
 
+@pytest.mark.parametrize("solver", ["explicit", "pcg"])
+def test_fused_eval_matches_two_kernel_pass(pkg, gpu, solver, monkeypatch):
+    """BAL-shaped problems evaluate in one fused launch (camera and point waves side by
+    side, fixed-point cost); DAB_EVAL_FUSED=0 forces the two-kernel pass. The LM
+    trajectories must agree (cost 1e-10 relative, same iteration and CG counts; V, g and
+    the cost are summed in the same order, U, g_c regrouped), and the fused pass must be
+    bitwise repeatable."""
+    prob = pkg.synth(kind=0, num_cameras=120, num_points=9000, obs_per_point=8, seed=51)
+    lst = (pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR if solver == "explicit"
+           else pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)
+    res, pts = [], []
+    for fused in ("1", "0", "1"):
+        monkeypatch.setenv("DAB_EVAL_FUSED", fused)
+        p = prob.copy()
+        s = pkg.Solver(0)
+        s.set_problem(p)
+        res.append(s.solve(pkg.options(max_num_iterations=12, linear_solver_type=lst)))
+        s.close()
+        pts.append(p.points.copy())
+    a, b = res[0], res[1]
+    assert len(a["iterations"]) == len(b["iterations"]) and a["termination"] == b["termination"]
+    assert [it["linear_solver_iterations"] for it in a["iterations"]] == \
+        [it["linear_solver_iterations"] for it in b["iterations"]]
+    np.testing.assert_allclose([it["cost"] for it in a["iterations"]], [it["cost"] for it in b["iterations"]],
+                               rtol=1e-10)
+    np.testing.assert_array_equal(pts[0], pts[2])
+
+
+@pytest.mark.parametrize("wps", ["-112", "-122", "-113"])
+@pytest.mark.parametrize("kind", ["bal", "rig"])
+def test_prefetch_point_kernels_match(pkg, gpu, kind, wps, monkeypatch):
+    """The prefetch-queue point kernels (DAB_EVAL_WPS <= -100: fixed-point cost, LDS
+    intrinsics, single-extrinsic fast path for BAL) against the default LDS kernel in the
+    two-kernel pass: same LM trajectory (cost 1e-10 relative)."""
+    if kind == "bal":
+        prob = pkg.synth(kind=0, num_cameras=50, num_points=5000, obs_per_point=7, seed=52)
+    else:
+        prob = pkg.synth(kind=1, num_arcs=5, num_rings=12, num_points=4000, obs_per_point=7, seed=53)
+    monkeypatch.setenv("DAB_EVAL_FUSED", "0")
+    res = []
+    for w in ("-2", wps):
+        monkeypatch.setenv("DAB_EVAL_WPS", w)
+        p = prob.copy()
+        s = pkg.Solver(0)
+        s.set_problem(p)
+        res.append(s.solve(pkg.options(max_num_iterations=10)))
+        s.close()
+    a, b = res
+    assert len(a["iterations"]) == len(b["iterations"])
+    np.testing.assert_allclose([it["cost"] for it in a["iterations"]], [it["cost"] for it in b["iterations"]],
+                               rtol=1e-10)
+
+
 def test_lm_freeze_camera_matches_oracle(pkg, orc, gpu):
     prob = pkg.synth(kind=1, num_arcs=4, num_rings=10, num_points=2000, obs_per_point=6, seed=23)
     prob.freeze_camera = True  # solve(..., freeze_camera=true), sfm.cc:111
