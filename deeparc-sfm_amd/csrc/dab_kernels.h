@@ -204,6 +204,25 @@ void launch_pcg_update(hipStream_t s, int NC, int mode, const double* Ad, const 
                        const double* bvec, double* p, double* q, double* x, double* r, PcgState* st,
                        const double* Minv, double* z);
 
+// ---- matrix-free implicit Schur (small camera sets; dab_kernels.hip) -------------------
+// Y_e is never stored: rows are re-evaluated per pass (tables and s_c staged in LDS).
+bool mf_schur_fits(int NC, int E, int NI);
+int mf_grid(int NP, int ncu);
+// Y part of S vec: partial[grid][6 NC] scratch -> w[NC][6] (fixed order)
+void launch_mf_product(hipStream_t s, const DevView& v, const double* points, const double* camtab,
+                       const double* scale_c, const double* PU, const double* vec, double* partial, double* w,
+                       int grid, const PcgState* st);
+// dp[3][NP] = -PU (q - sum_e Y_e^T y_c)
+void launch_mf_backsub(hipStream_t s, const DevView& v, const double* points, const double* camtab,
+                       const double* scale_c, const double* PU, const double* q, const double* yc, double* dp,
+                       int grid);
+// per chunk: 21 of sum Z Z^T over same-point runs | 6 of -sum Y q -> partial[chunk][27]
+void launch_mf_diag_rhs(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int* run,
+                        const double* points, const double* camtab, const double* scale_c, const double* PU,
+                        const double* q, double* partial);
+// fixed-order sum of the per-work-group product partials (dab_pcg.hip)
+void launch_pcg_fused_final(hipStream_t s, int grid, int NC6, const double* partial, double* w, const PcgState* st);
+
 // ---- dense Cholesky (dab_chol.hip) -------------------------------------------------------
 // Factor the (n+1)x(n+1) augmented lower matrix [S b; b^T *] in place (row-major, ld = lda):
 // the first n rows end as L and row n as z = L^-1 b; then solve L^T y = z into y.

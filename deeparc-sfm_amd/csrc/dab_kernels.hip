@@ -19,6 +19,7 @@
 // Every reduction has a fixed shape and order: results are bitwise reproducible.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cstdlib>
 
@@ -1982,6 +1983,211 @@ __global__ __launch_bounds__(256) void k_backsub(DevView v, const double* __rest
   dp[p] = -(pu[0] * r[0] + pu[1] * r[1] + pu[2] * r[2]);
   dp[NPs + p] = -(pu[3] * r[1] + pu[4] * r[2]);
   dp[2 * NPs + p] = -(pu[5] * r[2]);
+}
+
+// ------------------------------------------------------------------------------------
+// Matrix-free implicit Schur (small camera sets: NC <= kMfCams and the tables fit in LDS,
+// i.e. the rig and BAL problems of up to ~100 cameras).
+// ------------------------------------------------------------------------------------
+// The stored-Y PCG writes Y_e = diag(s_c) (J_c^T J_p) PU_p (144 B fp64 / 72 B fp32 per
+// entry) once per LM step and streams it twice per CG product: at C5 that is 1.38 GB
+// per pass (fp32), 430 us per product and 1.2 ms per step to build. Here nothing is
+// stored: every pass re-evaluates the observation's rows from its 32-B inputs (tables
+// and s_c in LDS) and applies the factors directly,
+//   t_p  = PU_p^T sum_e J_p^T (J_c (s_c o v_c))          (Y_e^T v, summed over the point)
+//   w_c -= s_c o J_c^T (J_p (PU_p t_p))                   (Y_e t_p, per entry)
+// with J_p shared by both extrinsic slots of an arc∘ring observation. One product = two
+// sweeps over a point's SELL rows (lane = point); the camera sums go to per-wave LDS
+// accumulators (LDS atomics only between the lanes of one instruction; waves, then
+// work-groups, summed in fixed order: bitwise repeatable). All arithmetic fp64.
+constexpr int kMfCams = 160;
+constexpr int kMfBlock = 256;
+bool mf_schur_fits(int NC, int E, int NI) { return NC > 0 && NC <= kMfCams && small_tabs_fit(E, NI); }
+static size_t mf_lds_doubles(int E, int NI, int NC, bool product) {
+  return 30 * (size_t)E + 6 * (size_t)NI + 12 * (size_t)NC + (product ? (kMfBlock / 64) * 6 * (size_t)NC : 0);
+}
+
+// MODE 0: product (vec = p) -> partial[block][6 NC]; MODE 1: back substitution (vec = y_c)
+// -> dp[3][NP] = -PU_p (q_p - t_p), the Y-free form of k_backsub
+template <int MODE>
+__global__ __launch_bounds__(kMfBlock) void k_mf_points(DevView v, const double* __restrict__ points,
+                                                        const double* __restrict__ camtab,
+                                                        const double* __restrict__ scc,
+                                                        const double* __restrict__ PU,
+                                                        const double* __restrict__ vec,
+                                                        const double* __restrict__ q, double* __restrict__ out,
+                                                        const PcgState* st) {
+  extern __shared__ double mf_lds[];
+  if (MODE == 0 && st->status != kPcgRunning) return;
+  const int NC6 = 6 * v.NC;
+  const SmallTabs tabs = stage_small_tabs(mf_lds, v.E, v.NI, camtab, v.intr);
+  double* s_c = mf_lds + 30 * (size_t)v.E + 6 * (size_t)v.NI;  // [NC][6]
+  double* sv = s_c + NC6;                                         // s_c o vec
+  double* accs = sv + NC6;                                        // [waves][NC][6] (MODE 0)
+  for (int i = threadIdx.x; i < NC6; i += blockDim.x) {
+    s_c[i] = scc[i];
+    sv[i] = scc[i] * vec[i];
+  }
+  if constexpr (MODE == 0)
+    for (int i = threadIdx.x; i < (kMfBlock / 64) * NC6; i += blockDim.x) accs[i] = 0.0;
+  __syncthreads();
+  double* acc = accs + (threadIdx.x >> 6) * NC6;
+  const size_t NPs = (size_t)v.NP;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < v.NP; p += gridDim.x * blockDim.x) {
+    const int sl = p >> 6, lane = p & 63;
+    const int off = v.slice_off[sl], len = (v.slice_off[sl + 1] - off) >> 6;
+    const double X[3] = {points[3 * (size_t)p], points[3 * (size_t)p + 1], points[3 * (size_t)p + 2]};
+    double pu[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) pu[k] = PU[6 * (size_t)p + k];
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    for (int k = 0; k < len; ++k) {
+      const int s = off + 64 * k + lane;
+      const int4 id = v.obs_idx[s];
+      if (id.x < 0) continue;
+      const int c0 = v.ext_col[id.y], c1 = id.z >= 0 ? v.ext_col[id.z] : -1;
+      if (c0 < 0 && c1 < 0) continue;
+      double ru, rv, jx0[3], jx1[3], ja[6], jb[6], da[6], db[6];
+      obs_rows<true, 2>(id, v.obs_xy[s], X, tabs, ru, rv, jx0, jx1, ja, jb, da, db);
+      double u0 = 0.0, u1 = 0.0;
+      if (c0 >= 0)
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          u0 += ja[a] * sv[6 * c0 + a];
+          u1 += jb[a] * sv[6 * c0 + a];
+        }
+      if (c1 >= 0)
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          u0 += da[a] * sv[6 * c1 + a];
+          u1 += db[a] * sv[6 * c1 + a];
+        }
+      a0 += jx0[0] * u0 + jx1[0] * u1;
+      a1 += jx0[1] * u0 + jx1[1] * u1;
+      a2 += jx0[2] * u0 + jx1[2] * u1;
+    }
+    // t = PU^T a (PU upper triangular: 00 01 02 11 12 22)
+    const double t0 = pu[0] * a0, t1 = pu[1] * a0 + pu[3] * a1, t2 = pu[2] * a0 + pu[4] * a1 + pu[5] * a2;
+    if constexpr (MODE == 1) {
+      const double r0 = q[4 * (size_t)p] - t0, r1 = q[4 * (size_t)p + 1] - t1, r2 = q[4 * (size_t)p + 2] - t2;
+      out[p] = -(pu[0] * r0 + pu[1] * r1 + pu[2] * r2);
+      out[NPs + p] = -(pu[3] * r1 + pu[4] * r2);
+      out[2 * NPs + p] = -(pu[5] * r2);
+      continue;
+    }
+    const double up0 = pu[0] * t0 + pu[1] * t1 + pu[2] * t2, up1 = pu[3] * t1 + pu[4] * t2, up2 = pu[5] * t2;
+    for (int k = 0; k < len; ++k) {
+      const int s = off + 64 * k + lane;
+      const int4 id = v.obs_idx[s];
+      if (id.x < 0) continue;
+      const int c0 = v.ext_col[id.y], c1 = id.z >= 0 ? v.ext_col[id.z] : -1;
+      if (c0 < 0 && c1 < 0) continue;
+      double ru, rv, jx0[3], jx1[3], ja[6], jb[6], da[6], db[6];
+      obs_rows<true, 2>(id, v.obs_xy[s], X, tabs, ru, rv, jx0, jx1, ja, jb, da, db);
+      const double z0 = jx0[0] * up0 + jx0[1] * up1 + jx0[2] * up2;
+      const double z1 = jx1[0] * up0 + jx1[1] * up1 + jx1[2] * up2;
+      if (c0 >= 0)
+#pragma unroll
+        for (int a = 0; a < 6; ++a) atomicAdd(acc + 6 * c0 + a, -s_c[6 * c0 + a] * (ja[a] * z0 + jb[a] * z1));
+      if (c1 >= 0)
+#pragma unroll
+        for (int a = 0; a < 6; ++a) atomicAdd(acc + 6 * c1 + a, -s_c[6 * c1 + a] * (da[a] * z0 + db[a] * z1));
+    }
+  }
+  if constexpr (MODE == 0) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < NC6; i += blockDim.x) {
+      double x = accs[i];
+#pragma unroll
+      for (int w = 1; w < kMfBlock / 64; ++w) x += accs[w * NC6 + i];
+      out[(size_t)blockIdx.x * NC6 + i] = x;
+    }
+  }
+}
+
+// Per chunk of camera-major positions, Y re-evaluated: 21 upper of sum Z Z^T over
+// same-point runs (Z = sum of the run's Y_e; the diagonal block of the Schur term) | 6 of
+// -sum Y_e q_p -> partial[chunk][27]. Replaces k_entry_y + k_pcg_diag_rhs_partial.
+__global__ __launch_bounds__(256) void k_mf_diag_rhs(DevView v, const int* __restrict__ chunk_beg,
+                                                     const int* __restrict__ run,
+                                                     const double* __restrict__ points,
+                                                     const double* __restrict__ camtab,
+                                                     const double* __restrict__ scc,
+                                                     const double* __restrict__ PU, const double* __restrict__ q,
+                                                     double* __restrict__ partial) {
+  extern __shared__ double mf_lds[];
+  const SmallTabs tabs = stage_small_tabs(mf_lds, v.E, v.NI, camtab, v.intr);
+  const int c = blockIdx.x;
+  const int b = chunk_beg[c], e = chunk_beg[c + 1];
+  auto entry_y = [&](int i, int& pt, double (&y)[18]) {
+    int4 id = v.cm_idx[i];
+    const bool slot1 = (id.w & kSlotBit) != 0;
+    id.w &= ~kSlotBit;
+    const int cam = v.ext_col[slot1 ? id.z : id.y];
+    pt = id.x;
+    const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
+    double ru, rv, jx0[3], jx1[3], ja[6], jb[6];
+    if (slot1) obs_rows<true, 1>(id, v.cm_xy[i], X, tabs, ru, rv, jx0, jx1, ja, jb);
+    else obs_rows<true, 0>(id, v.cm_xy[i], X, tabs, ru, rv, jx0, jx1, ja, jb);
+    make_y(ja, jb, jx0, jx1, scc + 6 * cam, PU + 6 * (size_t)id.x, y);
+  };
+  double acc[27];
+#pragma unroll
+  for (int i = 0; i < 27; ++i) acc[i] = 0.0;
+  for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
+    int p;
+    double y[18];
+    entry_y(i, p, y);
+    const double q0 = q[4 * (size_t)p], q1 = q[4 * (size_t)p + 1], q2 = q[4 * (size_t)p + 2];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[21 + a] -= y[3 * a] * q0 + y[3 * a + 1] * q1 + y[3 * a + 2] * q2;
+    const int len = run[i];
+    if (len == 0) continue;
+    for (int j = 1; j < len; ++j) {  // rare (rig): fold the run into Z
+      int pj;
+      double w[18];
+      entry_y(i + j, pj, w);
+#pragma unroll
+      for (int k = 0; k < 18; ++k) y[k] += w[k];
+    }
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int bb = a; bb < 6; ++bb)
+        acc[k++] += y[3 * a] * y[3 * bb] + y[3 * a + 1] * y[3 * bb + 1] + y[3 * a + 2] * y[3 * bb + 2];
+  }
+  __shared__ double wsum[kRedBlock / 64][27];
+  wave_sums_transposed<27>(acc, wsum[threadIdx.x >> 6]);
+  __syncthreads();
+  if (threadIdx.x < 27) {
+    double t = wsum[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < kRedBlock / 64; ++w) t += wsum[w][threadIdx.x];
+    partial[27 * (size_t)c + threadIdx.x] = t;
+  }
+}
+
+int mf_grid(int NP, int ncu) { return std::max(1, std::min((NP + kMfBlock - 1) / kMfBlock, 4 * ncu)); }
+void launch_mf_product(hipStream_t s, const DevView& v, const double* points, const double* camtab,
+                       const double* scale_c, const double* PU, const double* vec, double* partial, double* w,
+                       int grid, const PcgState* st) {
+  const size_t lds = sizeof(double) * mf_lds_doubles(v.E, v.NI, v.NC, true);
+  k_mf_points<0><<<grid, kMfBlock, lds, s>>>(v, points, camtab, scale_c, PU, vec, nullptr, partial, st);
+  launch_pcg_fused_final(s, grid, 6 * v.NC, partial, w, st);
+}
+void launch_mf_backsub(hipStream_t s, const DevView& v, const double* points, const double* camtab,
+                       const double* scale_c, const double* PU, const double* q, const double* yc, double* dp,
+                       int grid) {
+  const size_t lds = sizeof(double) * mf_lds_doubles(v.E, v.NI, v.NC, false);
+  k_mf_points<1><<<grid, kMfBlock, lds, s>>>(v, points, camtab, scale_c, PU, yc, q, dp, nullptr);
+}
+void launch_mf_diag_rhs(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int* run,
+                        const double* points, const double* camtab, const double* scale_c, const double* PU,
+                        const double* q, double* partial) {
+  if (nchunk <= 0) return;
+  const size_t lds = small_tabs_bytes(v.E, v.NI);
+  k_mf_diag_rhs<<<nchunk, 256, lds, s>>>(v, chunk_beg, run, points, camtab, scale_c, PU, q, partial);
 }
 
 void launch_backsub(hipStream_t s, const DevView& v, const double* PU, const double* q, YBufs Y,

@@ -779,6 +779,10 @@ void launch_pcg_fused(hipStream_t s, const DevView& v, YBufs Y, const double* ve
   k_pcg_fused_final<<<NC6, 256, 0, s>>>(grid, NC6, partial, w, st);
 }
 
+void launch_pcg_fused_final(hipStream_t s, int grid, int NC6, const double* partial, double* w, const PcgState* st) {
+  k_pcg_fused_final<<<NC6, 256, 0, s>>>(grid, NC6, partial, w, st);
+}
+
 void launch_pcg_matvec_passes(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, YBufs Y,
                               const double* vec, double* t, double* partial, const PcgState* st) {
   const int g = grid_for(v.NP, 256, 1 << 20);

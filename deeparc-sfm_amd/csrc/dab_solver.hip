@@ -192,6 +192,9 @@ struct dab_handle {
   int eval_grid = 1;  // k_eval_points blocks (one SELL slice per block)
   int ncu = 256;      // compute units of the device
   int fused_grid = 0;  // > 0: single-pass PCG matvec (small camera systems)
+  bool mf = false;     // matrix-free implicit Schur (no Y records; DAB_PCG_MF=0 disables)
+  int mf_grid_n = 0;
+  double* d_mf_partial = nullptr;
   int pcg_hint = 2;    // CG iterations of the previous solve (first batch size)
   double* d_cg_partial = nullptr;  // multi-work-group CG update: grid partials + counter
   unsigned* d_cg_cnt = nullptr;
@@ -957,6 +960,12 @@ static int build_pcg_buffers(dab_handle* h) {
   HIP_OK(hipMemsetAsync(h->d_cg_cnt, 0, sizeof(unsigned), h->stream));
   // the single-pass matvec when the camera system is small (DAB_PCG_FUSED=0 disables it)
   const char* fz = getenv("DAB_PCG_FUSED");
+  const char* mfe = getenv("DAB_PCG_MF");
+  h->mf = mf_schur_fits(h->NC, h->E, h->NI) && h->NP > 0 && !(mfe && atoi(mfe) == 0);
+  if (h->mf) {
+    h->mf_grid_n = mf_grid(h->NP, h->ncu);
+    CHECK_RC(d.alloc(&h->d_mf_partial, (size_t)h->mf_grid_n * 6 * h->NC));
+  }
   if (pcg_fused_fits(h->NC) && h->NP > 0 && !(fz && atoi(fz) == 0)) {
     h->fused_grid = pcg_fused_grid(h->NP, h->ncu);
     CHECK_RC(d.alloc(&h->d_fused_partial, (size_t)h->fused_grid * 6 * h->NC));
@@ -971,6 +980,12 @@ static int build_pcg_buffers(dab_handle* h) {
 // S vec (Y part) -> d_pcg_w, all-reduced across ranks
 static int pcg_matvec(dab_handle* h, YBufs yb, const double* vec) {
   hipStream_t s = h->stream;
+  if (h->mf) {
+    launch_mf_product(s, h->view, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, vec, h->d_mf_partial, h->d_pcg_w,
+                      h->mf_grid_n, h->d_pcg_state);
+    CHECK_RC(h->allreduce(h->d_pcg_w, (size_t)6 * h->NC, ncclSum));
+    return 0;
+  }
   if (h->fused_grid > 0) {
     launch_pcg_fused(s, h->view, yb, vec, h->d_fused_partial, h->d_pcg_w, h->fused_grid, h->d_pcg_state);
     CHECK_RC(h->allreduce(h->d_pcg_w, (size_t)6 * h->NC, ncclSum));
@@ -992,8 +1007,12 @@ static int pcg_solve(dab_handle* h, const dab_options& opt, StepScalars sc, YBuf
   const DevView& v = h->view;
   const int NC = h->NC;
   const bool direct = h->nchunk == h->NC;
-  launch_pcg_diag_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_run, yb, h->d_q,
-                              direct ? h->d_pcg_red : h->d_partial);
+  if (h->mf)
+    launch_mf_diag_rhs(s, v, h->nchunk, h->d_chunk_beg, h->d_run, h->d_points, h->d_camtab, h->d_scale_c, h->d_L,
+                       h->d_q, direct ? h->d_pcg_red : h->d_partial);
+  else
+    launch_pcg_diag_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_run, yb, h->d_q,
+                                direct ? h->d_pcg_red : h->d_partial);
   if (!direct) launch_seg_final(s, NC, 27, h->d_seg_chunk, h->d_partial, h->d_pcg_red, h->max_seg_chunks);
   CHECK_RC(h->allreduce(h->d_pcg_red, (size_t)27 * NC, ncclSum));
   launch_pcg_setup(s, NC, h->ug(), h->d_scale_c, sc, h->d_pcg_red, h->d_pcg_Ad, h->d_pcg_Minv, h->d_pcg_b,
@@ -1241,7 +1260,8 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
   CHECK_RC(use_pcg ? build_pcg_buffers(h) : build_schur_tables(h));
   // Y records of each step: fp64 (both layouts), or fp32 for the mixed-precision PCG
   // (Jacobians, residuals, V/U/g, the CG vectors and scalars stay fp64)
-  const bool y32 = use_pcg && opt.pcg_fp32 != 0;
+  // (the matrix-free PCG of small camera sets stores no Y and is all fp64)
+  const bool y32 = use_pcg && opt.pcg_fp32 != 0 && !h->mf;
   if (y32 && !h->d_Y32c) {
     CHECK_RC(h->dev.alloc(&h->d_Y32c, (size_t)kYRec * std::max(1, h->NE)));
     CHECK_RC(h->dev.alloc(&h->d_Y32p, (size_t)kYRec * std::max(1, h->NS) * (h->any_compose ? 2 : 1)));
@@ -1358,7 +1378,7 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
     launch_point_factor(s, v, h->d_V, h->d_g, h->d_scale_p, sc, h->d_L, h->d_q, h->d_flags);
     bool pcg_fail = false;
     if (NC > 0 && use_pcg) {
-      launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, yb, true);
+      if (!h->mf) launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, yb, true);
       int cg_iters = 0, cg_status = 0;
       CHECK_RC(pcg_solve(h, opt, sc, yb, &cg_iters, &cg_status));
       it.linear_solver_iterations = cg_iters;
@@ -1374,7 +1394,10 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
       if (chol_factor_solve(h->chol, s, n, h->d_S, h->lds, h->d_yc, h->d_flags + 1) != 0)
         return set_error(DAB_E_DEVICE, "dense Cholesky launch failed");
     }
-    launch_backsub(s, v, h->d_L, h->d_q, yb, NC > 0 ? h->d_yc : nullptr, h->d_dp);
+    if (use_pcg && h->mf)
+      launch_mf_backsub(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, h->d_q, h->d_yc, h->d_dp, h->mf_grid_n);
+    else
+      launch_backsub(s, v, h->d_L, h->d_q, yb, NC > 0 ? h->d_yc : nullptr, h->d_dp);
     // candidate x + delta and the model / candidate cost in one observation pass
     launch_axpy_points(s, NP, h->d_points, h->d_dp, h->d_points_c, h->d_gpart, h->red_grid);
     launch_final_sum(s, h->red_grid, 2, h->d_gpart, h->d_scal + S_STEP_P);

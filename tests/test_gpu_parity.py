@@ -133,10 +133,12 @@ def test_lm_pcg_reaches_dense_schur_minimum(pkg, gpu):
 
 
 @pytest.mark.parametrize("kind", ["bal", "rig"])
-def test_lm_pcg_fp32_reaches_same_minimum(pkg, gpu, kind):
+def test_lm_pcg_fp32_reaches_same_minimum(pkg, gpu, kind, monkeypatch):
     """Mixed-precision PCG (fp32 Schur factors Y, fp64 everything else): the same LM
     reaches the fp64 minimum (final cost 1e-6 relative); its CG iteration counts may
-    differ, so only the endpoint is compared."""
+    differ, so only the endpoint is compared. (Small camera sets default to the
+    matrix-free PCG, which stores no Y; DAB_PCG_MF=0 keeps the stored-Y path here.)"""
+    monkeypatch.setenv("DAB_PCG_MF", "0")
     if kind == "bal":
         prob = pkg.synth(kind=0, num_cameras=50, num_points=3000, obs_per_point=6, seed=34)
     else:
@@ -163,6 +165,7 @@ def test_pcg_fused_matvec_matches_two_pass(pkg, gpu, kind, monkeypatch):
         prob = pkg.synth(kind=0, num_cameras=60, num_points=4000, obs_per_point=7, seed=41)
     else:
         prob = pkg.synth(kind=1, num_arcs=6, num_rings=16, num_points=3000, obs_per_point=8, seed=42)
+    monkeypatch.setenv("DAB_PCG_MF", "0")  # the stored-Y products (the matrix-free PCG has its own test)
     opts = dict(max_num_iterations=15, linear_solver_type=pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)
     res, pts = [], []
     for fused in ("1", "0", "1"):
@@ -179,6 +182,35 @@ def test_pcg_fused_matvec_matches_two_pass(pkg, gpu, kind, monkeypatch):
     np.testing.assert_allclose([it["cost"] for it in a["iterations"]], [it["cost"] for it in b["iterations"]],
                                rtol=1e-9)
     np.testing.assert_array_equal(pts[0], pts[2])  # fused path: bitwise repeatable
+
+
+@pytest.mark.parametrize("kind", ["bal", "rig"])
+def test_matrix_free_pcg_matches_stored_y(pkg, gpu, kind, monkeypatch):
+    """Small camera sets run the PCG matrix-free (Y_e re-evaluated in every pass: diagonal
+    blocks and rhs, products, back substitution). DAB_PCG_MF=0 stores the fp64 Y records
+    instead. Same LM trajectory: cost 1e-9 relative, same CG iteration counts (only the
+    association of the Schur products differs); the matrix-free path is bitwise
+    repeatable."""
+    if kind == "bal":
+        prob = pkg.synth(kind=0, num_cameras=60, num_points=4000, obs_per_point=7, seed=45)
+    else:
+        prob = pkg.synth(kind=1, num_arcs=6, num_rings=16, num_points=3000, obs_per_point=8, seed=46)
+    opts = dict(max_num_iterations=15, linear_solver_type=pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)
+    res, pts = [], []
+    for mf in ("1", "0", "1"):
+        monkeypatch.setenv("DAB_PCG_MF", mf)
+        p = prob.copy()
+        s = pkg.Solver(0)
+        s.set_problem(p)
+        res.append(s.solve(pkg.options(**opts)))
+        s.close()
+        pts.append(p.points.copy())
+    a, b = res[0], res[1]
+    assert [it["linear_solver_iterations"] for it in a["iterations"]] == \
+        [it["linear_solver_iterations"] for it in b["iterations"]]
+    np.testing.assert_allclose([it["cost"] for it in a["iterations"]], [it["cost"] for it in b["iterations"]],
+                               rtol=1e-9)
+    np.testing.assert_array_equal(pts[0], pts[2])
 
 
 @pytest.mark.parametrize("kind", ["bal", "rig"])
