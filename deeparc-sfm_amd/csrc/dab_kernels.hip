@@ -2003,14 +2003,102 @@ __global__ __launch_bounds__(256) void k_backsub(DevView v, const double* __rest
 constexpr int kMfCams = 160;
 constexpr int kMfBlock = 256;
 bool mf_schur_fits(int NC, int E, int NI) { return NC > 0 && NC <= kMfCams && small_tabs_fit(E, NI); }
+// LDS: tables | s_c o vec [NC][6] | per-wave camera sums [4][NC][6] (products): <= 40 KB for
+// the rig (79 extrinsics, 16 intrinsics), so 4 blocks of 256 fit a CU
 static size_t mf_lds_doubles(int E, int NI, int NC, bool product) {
-  return 30 * (size_t)E + 6 * (size_t)NI + 12 * (size_t)NC + (product ? (kMfBlock / 64) * 6 * (size_t)NC : 0);
+  return 30 * (size_t)E + 6 * (size_t)NI + 6 * (size_t)NC + (product ? (kMfBlock / 64) * 6 * (size_t)NC : 0);
+}
+
+// The products never materialise a Jacobian row. With A = d r / d P (2x3) of the
+// projection, Q = P2 (arc∘ring) or X, and the tables' R, Rd, Jd of the arc (a) and ring (r)
+// extrinsics, the directional forms (rows of obs_rows contracted analytically) are
+//   J_c0 d = A (-Rd_a (Q x (Jd_a dw_a)) + dt_a)            J_c1 d = A R_a (-Rd_r (X x (Jd_r dw_r)) + dt_r)
+//   J_c0^T z = [Jd_a^T (Q x (Rd_a^T g)); g], g = A^T z      J_c1^T z = [Jd_r^T (X x (Rd_r^T h)); h], h = R_a^T g
+//   J_p^T u = R_r^T R_a^T A^T u                            J_p u_p = A R_a R_r u_p     (R_r: arc∘ring only)
+// ~80 fp64 operations per observation and sweep after the projection, against ~200 to
+// build the rows (and ~70 fewer live registers).
+struct MfGeo {
+  double A0[3], A1[3];  // d (ru, rv) / d P
+  double Q[3];          // the point the arc / single rotation acts on
+  double R[9];          // R of ext0 (arc / single)
+  bool comp;
+};
+__device__ __forceinline__ void mf_geo(const int4 id, const double2 xy, const double (&X)[3], const SmallTabs& tb,
+                                       MfGeo& g) {
+  g.comp = id.z >= 0;
+  double A[12];
+  tb.rt(id.y, A);
+  double Kr[6];
+  tb.k(id.w, Kr);
+  if (g.comp) {
+    double B[12];
+    tb.rt(id.z, B);
+    matvec_add(B, X, B + 9, g.Q);
+  } else {
+    g.Q[0] = X[0];
+    g.Q[1] = X[1];
+    g.Q[2] = X[2];
+  }
+  double P[3];
+  matvec_add(A, g.Q, A + 9, P);
+  Proj pr;
+  project(P, Kr, xy.x, xy.y, pr, true);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    g.A0[i] = pr.A0[i];
+    g.A1[i] = pr.A1[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) g.R[i] = A[i];
+}
+__device__ __forceinline__ void mv3(const double* __restrict__ M, const double (&x)[3], double (&o)[3]) {
+  o[0] = M[0] * x[0] + M[1] * x[1] + M[2] * x[2];
+  o[1] = M[3] * x[0] + M[4] * x[1] + M[5] * x[2];
+  o[2] = M[6] * x[0] + M[7] * x[1] + M[8] * x[2];
+}
+__device__ __forceinline__ void mtv3(const double* __restrict__ M, const double (&x)[3], double (&o)[3]) {
+  o[0] = M[0] * x[0] + M[3] * x[1] + M[6] * x[2];
+  o[1] = M[1] * x[0] + M[4] * x[1] + M[7] * x[2];
+  o[2] = M[2] * x[0] + M[5] * x[1] + M[8] * x[2];
+}
+__device__ __forceinline__ void cross3(const double (&a)[3], const double (&b)[3], double (&o)[3]) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+// dP of one camera slot along d = (dw, dt): -Rd (Y x (Jd dw)) + dt, tables D = Rd | Jd
+__device__ __forceinline__ void mf_dp(const double* __restrict__ D, const double (&Y)[3], const double* __restrict__ d,
+                                      double (&o)[3]) {
+  const double dw[3] = {d[0], d[1], d[2]};
+  double y[3], c[3], r[3];
+  mv3(D + 9, dw, y);
+  cross3(Y, y, c);
+  mv3(D, c, r);
+  o[0] = d[3] - r[0];
+  o[1] = d[4] - r[1];
+  o[2] = d[5] - r[2];
+}
+// J_c^T of one slot applied to the 3-vector g (= A^T z, or R_a^T A^T z for the ring):
+// out[0..2] = Jd^T (Y x (Rd^T g)), out[3..5] = g
+__device__ __forceinline__ void mf_jct(const double* __restrict__ D, const double (&Y)[3], const double (&g)[3],
+                                       double (&out)[6]) {
+  double d[3], c[3], w[3];
+  mtv3(D, g, d);
+  cross3(Y, d, c);
+  mtv3(D + 9, c, w);
+  out[0] = w[0];
+  out[1] = w[1];
+  out[2] = w[2];
+  out[3] = g[0];
+  out[4] = g[1];
+  out[5] = g[2];
 }
 
 // MODE 0: product (vec = p) -> partial[block][6 NC]; MODE 1: back substitution (vec = y_c)
-// -> dp[3][NP] = -PU_p (q_p - t_p), the Y-free form of k_backsub
+// -> dp[3][NP] = -PU_p (q_p - t_p), the Y-free form of k_backsub; MODE 2: the Schur rhs
+// part -sum_e Y_e q_p (sweep 2 with u_p = PU_p q_p) -> partial[block][6 NC]
 template <int MODE>
-__global__ __launch_bounds__(kMfBlock) void k_mf_points(DevView v, const double* __restrict__ points,
+__global__ __launch_bounds__(kMfBlock, 4) void k_mf_points(DevView v, const double* __restrict__ points,
                                                         const double* __restrict__ camtab,
                                                         const double* __restrict__ scc,
                                                         const double* __restrict__ PU,
@@ -2021,14 +2109,12 @@ __global__ __launch_bounds__(kMfBlock) void k_mf_points(DevView v, const double*
   if (MODE == 0 && st->status != kPcgRunning) return;
   const int NC6 = 6 * v.NC;
   const SmallTabs tabs = stage_small_tabs(mf_lds, v.E, v.NI, camtab, v.intr);
-  double* s_c = mf_lds + 30 * (size_t)v.E + 6 * (size_t)v.NI;  // [NC][6]
-  double* sv = s_c + NC6;                                         // s_c o vec
-  double* accs = sv + NC6;                                        // [waves][NC][6] (MODE 0)
-  for (int i = threadIdx.x; i < NC6; i += blockDim.x) {
-    s_c[i] = scc[i];
-    sv[i] = scc[i] * vec[i];
-  }
-  if constexpr (MODE == 0)
+  double* sv = mf_lds + 30 * (size_t)v.E + 6 * (size_t)v.NI;  // s_c o vec [NC][6]
+  double* accs = sv + NC6;                                       // [waves][NC][6] (MODE 0, 2)
+  const double* __restrict__ s_c = scc;                          // L1-resident
+  if constexpr (MODE != 2)
+    for (int i = threadIdx.x; i < NC6; i += blockDim.x) sv[i] = scc[i] * vec[i];
+  if constexpr (MODE != 1)
     for (int i = threadIdx.x; i < (kMfBlock / 64) * NC6; i += blockDim.x) accs[i] = 0.0;
   __syncthreads();
   double* acc = accs + (threadIdx.x >> 6) * NC6;
@@ -2040,61 +2126,112 @@ __global__ __launch_bounds__(kMfBlock) void k_mf_points(DevView v, const double*
     double pu[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) pu[k] = PU[6 * (size_t)p + k];
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-    for (int k = 0; k < len; ++k) {
-      const int s = off + 64 * k + lane;
-      const int4 id = v.obs_idx[s];
-      if (id.x < 0) continue;
-      const int c0 = v.ext_col[id.y], c1 = id.z >= 0 ? v.ext_col[id.z] : -1;
-      if (c0 < 0 && c1 < 0) continue;
-      double ru, rv, jx0[3], jx1[3], ja[6], jb[6], da[6], db[6];
-      obs_rows<true, 2>(id, v.obs_xy[s], X, tabs, ru, rv, jx0, jx1, ja, jb, da, db);
-      double u0 = 0.0, u1 = 0.0;
-      if (c0 >= 0)
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-          u0 += ja[a] * sv[6 * c0 + a];
-          u1 += jb[a] * sv[6 * c0 + a];
+    double up[3];
+    if constexpr (MODE == 2) {
+      const double q0 = q[4 * (size_t)p], q1 = q[4 * (size_t)p + 1], q2 = q[4 * (size_t)p + 2];
+      up[0] = pu[0] * q0 + pu[1] * q1 + pu[2] * q2;
+      up[1] = pu[3] * q1 + pu[4] * q2;
+      up[2] = pu[5] * q2;
+    } else {
+      // sweep 1: a = sum_e J_p^T (J_c (s_c o v_c))
+      double a[3] = {0.0, 0.0, 0.0};
+      for (int k = 0; k < len; ++k) {
+        const int s = off + 64 * k + lane;
+        const int4 id = v.obs_idx[s];
+        if (id.x < 0) continue;
+        const int c0 = v.ext_col[id.y], c1 = id.z >= 0 ? v.ext_col[id.z] : -1;
+        if (c0 < 0 && c1 < 0) continue;
+        MfGeo g;
+        mf_geo(id, v.obs_xy[s], X, tabs, g);
+        double dP[3] = {0.0, 0.0, 0.0};
+        if (c0 >= 0) {
+          double D[18];
+          tabs.dj(id.y, D);
+          mf_dp(D, g.Q, sv + 6 * c0, dP);
         }
-      if (c1 >= 0)
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-          u0 += da[a] * sv[6 * c1 + a];
-          u1 += db[a] * sv[6 * c1 + a];
+        if (c1 >= 0) {
+          double D[18], d2[3], r2[3];
+          tabs.dj(id.z, D);
+          mf_dp(D, X, sv + 6 * c1, d2);
+          mv3(g.R, d2, r2);
+          dP[0] += r2[0];
+          dP[1] += r2[1];
+          dP[2] += r2[2];
         }
-      a0 += jx0[0] * u0 + jx1[0] * u1;
-      a1 += jx0[1] * u0 + jx1[1] * u1;
-      a2 += jx0[2] * u0 + jx1[2] * u1;
+        const double u0 = g.A0[0] * dP[0] + g.A0[1] * dP[1] + g.A0[2] * dP[2];
+        const double u1 = g.A1[0] * dP[0] + g.A1[1] * dP[1] + g.A1[2] * dP[2];
+        const double au[3] = {u0 * g.A0[0] + u1 * g.A1[0], u0 * g.A0[1] + u1 * g.A1[1], u0 * g.A0[2] + u1 * g.A1[2]};
+        double h[3];
+        mtv3(g.R, au, h);
+        if (g.comp) {
+          double B[12], h2[3];
+          tabs.rt(id.z, B);
+          mtv3(B, h, h2);
+          h[0] = h2[0];
+          h[1] = h2[1];
+          h[2] = h2[2];
+        }
+        a[0] += h[0];
+        a[1] += h[1];
+        a[2] += h[2];
+      }
+      // t = PU^T a (PU upper triangular: 00 01 02 11 12 22)
+      const double t0 = pu[0] * a[0], t1 = pu[1] * a[0] + pu[3] * a[1];
+      const double t2 = pu[2] * a[0] + pu[4] * a[1] + pu[5] * a[2];
+      if constexpr (MODE == 1) {
+        const double r0 = q[4 * (size_t)p] - t0, r1 = q[4 * (size_t)p + 1] - t1, r2 = q[4 * (size_t)p + 2] - t2;
+        out[p] = -(pu[0] * r0 + pu[1] * r1 + pu[2] * r2);
+        out[NPs + p] = -(pu[3] * r1 + pu[4] * r2);
+        out[2 * NPs + p] = -(pu[5] * r2);
+        continue;
+      }
+      up[0] = pu[0] * t0 + pu[1] * t1 + pu[2] * t2;
+      up[1] = pu[3] * t1 + pu[4] * t2;
+      up[2] = pu[5] * t2;
     }
-    // t = PU^T a (PU upper triangular: 00 01 02 11 12 22)
-    const double t0 = pu[0] * a0, t1 = pu[1] * a0 + pu[3] * a1, t2 = pu[2] * a0 + pu[4] * a1 + pu[5] * a2;
-    if constexpr (MODE == 1) {
-      const double r0 = q[4 * (size_t)p] - t0, r1 = q[4 * (size_t)p + 1] - t1, r2 = q[4 * (size_t)p + 2] - t2;
-      out[p] = -(pu[0] * r0 + pu[1] * r1 + pu[2] * r2);
-      out[NPs + p] = -(pu[3] * r1 + pu[4] * r2);
-      out[2 * NPs + p] = -(pu[5] * r2);
-      continue;
-    }
-    const double up0 = pu[0] * t0 + pu[1] * t1 + pu[2] * t2, up1 = pu[3] * t1 + pu[4] * t2, up2 = pu[5] * t2;
-    for (int k = 0; k < len; ++k) {
-      const int s = off + 64 * k + lane;
-      const int4 id = v.obs_idx[s];
-      if (id.x < 0) continue;
-      const int c0 = v.ext_col[id.y], c1 = id.z >= 0 ? v.ext_col[id.z] : -1;
-      if (c0 < 0 && c1 < 0) continue;
-      double ru, rv, jx0[3], jx1[3], ja[6], jb[6], da[6], db[6];
-      obs_rows<true, 2>(id, v.obs_xy[s], X, tabs, ru, rv, jx0, jx1, ja, jb, da, db);
-      const double z0 = jx0[0] * up0 + jx0[1] * up1 + jx0[2] * up2;
-      const double z1 = jx1[0] * up0 + jx1[1] * up1 + jx1[2] * up2;
-      if (c0 >= 0)
+    if constexpr (MODE != 1) {
+      // sweep 2: w_c -= s_c o J_c^T (J_p u_p)
+      for (int k = 0; k < len; ++k) {
+        const int s = off + 64 * k + lane;
+        const int4 id = v.obs_idx[s];
+        if (id.x < 0) continue;
+        const int c0 = v.ext_col[id.y], c1 = id.z >= 0 ? v.ext_col[id.z] : -1;
+        if (c0 < 0 && c1 < 0) continue;
+        MfGeo g;
+        mf_geo(id, v.obs_xy[s], X, tabs, g);
+        double m[3], kk[3];
+        if (g.comp) {
+          double B[12];
+          tabs.rt(id.z, B);
+          mv3(B, up, kk);
+        } else {
+          kk[0] = up[0];
+          kk[1] = up[1];
+          kk[2] = up[2];
+        }
+        mv3(g.R, kk, m);
+        const double z0 = g.A0[0] * m[0] + g.A0[1] * m[1] + g.A0[2] * m[2];
+        const double z1 = g.A1[0] * m[0] + g.A1[1] * m[1] + g.A1[2] * m[2];
+        const double gz[3] = {z0 * g.A0[0] + z1 * g.A1[0], z0 * g.A0[1] + z1 * g.A1[1], z0 * g.A0[2] + z1 * g.A1[2]};
+        if (c0 >= 0) {
+          double D[18], o[6];
+          tabs.dj(id.y, D);
+          mf_jct(D, g.Q, gz, o);
 #pragma unroll
-        for (int a = 0; a < 6; ++a) atomicAdd(acc + 6 * c0 + a, -s_c[6 * c0 + a] * (ja[a] * z0 + jb[a] * z1));
-      if (c1 >= 0)
+          for (int a = 0; a < 6; ++a) atomicAdd(acc + 6 * c0 + a, -s_c[6 * c0 + a] * o[a]);
+        }
+        if (c1 >= 0) {
+          double D[18], hz[3], o[6];
+          tabs.dj(id.z, D);
+          mtv3(g.R, gz, hz);
+          mf_jct(D, X, hz, o);
 #pragma unroll
-        for (int a = 0; a < 6; ++a) atomicAdd(acc + 6 * c1 + a, -s_c[6 * c1 + a] * (da[a] * z0 + db[a] * z1));
+          for (int a = 0; a < 6; ++a) atomicAdd(acc + 6 * c1 + a, -s_c[6 * c1 + a] * o[a]);
+        }
+      }
     }
   }
-  if constexpr (MODE == 0) {
+  if constexpr (MODE != 1) {
     __syncthreads();
     for (int i = threadIdx.x; i < NC6; i += blockDim.x) {
       double x = accs[i];
