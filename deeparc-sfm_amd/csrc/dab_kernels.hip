@@ -2245,7 +2245,7 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_points(DevView v, const doub
 // Per chunk of camera-major positions, Y re-evaluated: 21 upper of sum Z Z^T over
 // same-point runs (Z = sum of the run's Y_e; the diagonal block of the Schur term) | 6 of
 // -sum Y_e q_p -> partial[chunk][27]. Replaces k_entry_y + k_pcg_diag_rhs_partial.
-__global__ __launch_bounds__(256) void k_mf_diag_rhs(DevView v, const int* __restrict__ chunk_beg,
+__global__ __launch_bounds__(256) void k_mf_diag_rhs(DevView v, int nchunk, const int* __restrict__ chunk_beg,
                                                      const int* __restrict__ run,
                                                      const double* __restrict__ points,
                                                      const double* __restrict__ camtab,
@@ -2253,8 +2253,9 @@ __global__ __launch_bounds__(256) void k_mf_diag_rhs(DevView v, const int* __res
                                                      const double* __restrict__ PU, const double* __restrict__ q,
                                                      double* __restrict__ partial) {
   extern __shared__ double mf_lds[];
-  const SmallTabs tabs = stage_small_tabs(mf_lds, v.E, v.NI, camtab, v.intr);
-  const int c = blockIdx.x;
+  const SmallTabs tabs = stage_small_tabs(mf_lds, v.E, v.NI, camtab, v.intr);  // once per block
+  __shared__ double wsum[kRedBlock / 64][27];
+  for (int c = blockIdx.x; c < nchunk; c += gridDim.x) {
   const int b = chunk_beg[c], e = chunk_beg[c + 1];
   auto entry_y = [&](int i, int& pt, double (&y)[18]) {
     int4 id = v.cm_idx[i];
@@ -2294,7 +2295,6 @@ __global__ __launch_bounds__(256) void k_mf_diag_rhs(DevView v, const int* __res
       for (int bb = a; bb < 6; ++bb)
         acc[k++] += y[3 * a] * y[3 * bb] + y[3 * a + 1] * y[3 * bb + 1] + y[3 * a + 2] * y[3 * bb + 2];
   }
-  __shared__ double wsum[kRedBlock / 64][27];
   wave_sums_transposed<27>(acc, wsum[threadIdx.x >> 6]);
   __syncthreads();
   if (threadIdx.x < 27) {
@@ -2302,6 +2302,8 @@ __global__ __launch_bounds__(256) void k_mf_diag_rhs(DevView v, const int* __res
 #pragma unroll
     for (int w = 1; w < kRedBlock / 64; ++w) t += wsum[w][threadIdx.x];
     partial[27 * (size_t)c + threadIdx.x] = t;
+  }
+  __syncthreads();  // wsum is reused by the next chunk
   }
 }
 
@@ -2324,7 +2326,9 @@ void launch_mf_diag_rhs(hipStream_t s, const DevView& v, int nchunk, const int* 
                         const double* q, double* partial) {
   if (nchunk <= 0) return;
   const size_t lds = small_tabs_bytes(v.E, v.NI);
-  k_mf_diag_rhs<<<nchunk, 256, lds, s>>>(v, chunk_beg, run, points, camtab, scale_c, PU, q, partial);
+  // persistent blocks: the 20-KB tables are staged once per block, not once per chunk
+  k_mf_diag_rhs<<<std::min(nchunk, kSmallGrid), 256, lds, s>>>(v, nchunk, chunk_beg, run, points, camtab, scale_c,
+                                                                PU, q, partial);
 }
 
 void launch_backsub(hipStream_t s, const DevView& v, const double* PU, const double* q, YBufs Y,
