@@ -288,6 +288,11 @@ class Solver:
         check(self.lib.dab_jacobian_bytes(self.h, C.byref(b)), self.lib)
         return b.value
 
+    def pcg_matrix_free(self):
+        f = C.c_int32()
+        check(self.lib.dab_pcg_schedule(self.h, C.byref(f)), self.lib)
+        return bool(f.value)
+
     def eval_fused(self):
         f = C.c_int32()
         check(self.lib.dab_eval_schedule(self.h, C.byref(f)), self.lib)

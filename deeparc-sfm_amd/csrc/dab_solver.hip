@@ -1741,6 +1741,13 @@ extern "C" int dab_jacobian_bytes(dab_handle* h, double* bytes) {
   return 0;
 }
 
+extern "C" int dab_pcg_schedule(dab_handle* h, int32_t* matrix_free) {
+  clear_error();
+  if (!h || !h->have_problem || !matrix_free) return set_error(DAB_E_STATE, "no problem set");
+  *matrix_free = h->pcg_built && h->mf ? 1 : 0;
+  return 0;
+}
+
 extern "C" int dab_eval_schedule(dab_handle* h, int32_t* fused) {
   clear_error();
   if (!h || !h->have_problem || !fused) return set_error(DAB_E_STATE, "no problem set");

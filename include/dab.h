@@ -240,6 +240,10 @@ int dab_jacobian_bytes(dab_handle* h, double* bytes);
  * single fused launch (k_eval_fused: camera and point side together), 0 for the
  * two-kernel pass (k_eval_cams + k_eval_points). */
 int dab_eval_schedule(dab_handle* h, int32_t* fused);
+/* After an IMPLICIT_SCHUR_PCG solve: *matrix_free = 1 when the Schur products re-evaluate
+ * the observation rows in every pass (small camera sets: all fp64, no Y records, so
+ * pcg_fp32 has nothing to store in fp32), 0 for the stored-Y products. */
+int dab_pcg_schedule(dab_handle* h, int32_t* matrix_free);
 
 /* ---- host utilities (no device needed) ----------------------------------------------- */
 /* Deterministic synthetic problems. kind 0: BAL-shaped (non-shared, one
