@@ -94,6 +94,29 @@ def test_lm_bal_matches_oracle(pkg, orc, gpu):
     assert g["final_cost"] < 0.02 * g["initial_cost"]
 
 
+@pytest.mark.parametrize("solver", ["explicit", "pcg"])
+def test_lm_bal_ragged_matches_oracle(pkg, orc, gpu, solver):
+    """Ragged tracks (2..12 observations per point, so SELL slices carry padding slots and
+    the camera chunks differ in length) through the fused evaluation pass and both
+    linear solvers, against the oracle's trajectory. Two points of one observation are
+    kept (their V block is rank deficient until damped)."""
+    base = pkg.synth(kind=0, num_cameras=80, num_points=5000, obs_per_point=12, seed=61)
+    rng = np.random.default_rng(61)
+    keep_n = rng.integers(2, 13, size=base.points.shape[0])
+    keep_n[:2] = 1
+    rank_in_track = np.zeros(base.num_obs, np.int64)
+    order = np.argsort(base.obs_point, kind="stable")
+    pts = base.obs_point[order]
+    first = np.r_[0, np.flatnonzero(np.diff(pts)) + 1]
+    start = np.repeat(first, np.diff(np.r_[first, len(pts)]))
+    rank_in_track[order] = np.arange(len(pts)) - start
+    prob = base.subset(rank_in_track < keep_n[base.obs_point]).copy()
+    lst = (pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR if solver == "explicit"
+           else pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)
+    g, o, ref = run_both(pkg, orc, prob, max_num_iterations=20, linear_solver_type=lst)
+    assert_same_trajectory(g, o, prob, ref, tol_cost=1e-9 if solver == "explicit" else 1e-8)
+
+
 def test_lm_rig_matches_oracle(pkg, orc, gpu):
     prob = pkg.synth(kind=1, num_arcs=6, num_rings=16, num_points=3000, obs_per_point=8, seed=22)
     assert (prob.obs_ext1 >= 0).any() and (prob.obs_ext1 < 0).any()
