@@ -1315,47 +1315,49 @@ __device__ __forceinline__ void eval_cams_chunk(const DevView& v, int i0, int e,
 // pipeline waits for the next index right before every gather, i.e. one HBM latency per
 // entry; here a wait only ever covers loads issued a full step earlier. Only the point
 // index is read (cm_pt, 4 B, not the 16-B cm_idx record): the table is the chunk's.
-template <class MakeTabs>
+template <int NS = 3, class MakeTabs>
 __device__ __forceinline__ void eval_cams_uni_pipe(const DevView& v, int i0, int e, int stride,
                                                    const double* __restrict__ points, MakeTabs make_tabs,
                                                    double (&acc)[27]) {
+  // NS register slots: the index and pixel of entry i + (NS-1) stride are loaded and the
+  // point of entry i + (NS-2) stride is gathered while entry i computes
+  static_assert(NS >= 3, "at least three slots");
   const int* __restrict__ cm_pt = v.cm_pt;
-  int pt[3];
-  double2 xy[3];
-  double X[3][3];
+  int pt[NS];
+  double2 xy[NS];
+  double X[NS][3];
 #pragma unroll
-  for (int s = 0; s < 3; ++s) {
+  for (int s = 0; s < NS; ++s) {
     pt[s] = -1;
     xy[s] = make_double2(0.0, 0.0);
     X[s][0] = X[s][1] = X[s][2] = 0.0;
   }
-  if (i0 < e) {
-    pt[0] = cm_pt[i0];
-    xy[0] = v.cm_xy[i0];
-  }
-  if (i0 + stride < e) {
-    pt[1] = cm_pt[i0 + stride];
-    xy[1] = v.cm_xy[i0 + stride];
-  }
-  if (pt[0] >= 0) {
 #pragma unroll
-    for (int q = 0; q < 3; ++q) X[0][q] = points[3 * (size_t)pt[0] + q];
-  }
+  for (int s = 0; s < NS - 1; ++s)
+    if (i0 + s * stride < e) {
+      pt[s] = cm_pt[i0 + s * stride];
+      xy[s] = v.cm_xy[i0 + s * stride];
+    }
+#pragma unroll
+  for (int s = 0; s < NS - 2; ++s)
+    if (pt[s] >= 0) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) X[s][q] = points[3 * (size_t)pt[s] + q];
+    }
   const auto tabs = make_tabs();
-  for (int i = i0; i < e; i += 3 * stride) {
+  for (int i = i0; i < e; i += NS * stride) {
 #pragma unroll
-    for (int u = 0; u < 3; ++u) {
+    for (int u = 0; u < NS; ++u) {
       const int ii = i + u * stride;
       if (ii >= e) break;
-      constexpr int S1[3] = {1, 2, 0}, S2[3] = {2, 0, 1};
-      const int s1 = S1[u], s2 = S2[u];
-      if (pt[s1] >= 0 && ii + stride < e) {
+      const int sg = (u + NS - 2) % NS, sl = (u + NS - 1) % NS;
+      if (pt[sg] >= 0 && ii + (NS - 2) * stride < e) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) X[s1][q] = points[3 * (size_t)pt[s1] + q];
+        for (int q = 0; q < 3; ++q) X[sg][q] = points[3 * (size_t)pt[sg] + q];
       }
-      if (ii + 2 * stride < e) {
-        pt[s2] = cm_pt[ii + 2 * stride];
-        xy[s2] = v.cm_xy[ii + 2 * stride];
+      if (ii + (NS - 1) * stride < e) {
+        pt[sl] = cm_pt[ii + (NS - 1) * stride];
+        xy[sl] = v.cm_xy[ii + (NS - 1) * stride];
       }
       double ru, rv, ja[6], jb[6];
       obs_rows<false, 0, UniTabs, false>(make_int4(pt[u], 0, -1, 0), xy[u], X[u], tabs, ru, rv, nullptr, nullptr,
@@ -1444,8 +1446,9 @@ void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, con
 // uniform chunk per free camera, E, NI <= kLdsCams, NC <= (camera waves / 2) x grid.
 constexpr int kFusedPW = 8;               // point waves per work-group
 constexpr int kFusedCW = 16 - kFusedPW;   // camera waves (kFusedCW / 2 cameras per round)
-template <int D, int ABL = 0>  // ABL (timing ablations): 1 camera waves exit at once, 2 point waves do;
-                                // 21 / 22: point / camera waves at raised issue priority
+template <int D, int ABL = 0, int NS = 3>  // ABL (timing ablations): 1 camera waves exit at once, 2 point
+                                          // waves do; 21 / 22: point / camera waves at raised priority;
+                                          // NS: camera-entry pipeline slots
 __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __restrict__ chunk_beg,
                                                      const double* __restrict__ points,
                                                      const double* __restrict__ ext, double* __restrict__ V,
@@ -1476,8 +1479,8 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
     double acc[27];
 #pragma unroll
     for (int i = 0; i < 27; ++i) acc[i] = 0.0;
-    eval_cams_uni_pipe(v, (half ? mid : b) + lane, half ? e : mid, 64, points,
-                       [&]() { return UniTabs(ext, v.intr, u.x, u.y); }, acc);
+    eval_cams_uni_pipe<NS>(v, (half ? mid : b) + lane, half ? e : mid, 64, points,
+                           [&]() { return UniTabs(ext, v.intr, u.x, u.y); }, acc);
     wave_sums_transposed<27>(acc, csum[pair][half]);
     unsigned old = 0;
     if (lane == 0) {
@@ -1641,6 +1644,9 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
   else if (abl == 2) k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
   else if (abl == 21) k_eval_fused<2, 21><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
   else if (abl == 22) k_eval_fused<2, 22><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
+  else if (abl == 34) k_eval_fused<2, 0, 4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
+  else if (abl == 35) k_eval_fused<2, 0, 5><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
+  else if (abl == 234) k_eval_fused<2, 2, 4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
   else if (abl == 14) k_eval_fused<4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
   else k_eval_fused<2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
 }
