@@ -1376,6 +1376,51 @@ __device__ __forceinline__ void eval_cams_uni_pipe(const DevView& v, int i0, int
   }
 }
 
+// General entries (int4 index records, the rig's camera-major and pair-major copies): the
+// same three-slot register pipeline as eval_cams_uni_pipe — while entry i computes, the
+// point of entry i + stride is gathered and the record of entry i + 2 stride loaded —
+// around a per-entry body(id, xy, X).
+template <class Body>
+__device__ __forceinline__ void pipe_entries(const int4* __restrict__ idx, const double2* __restrict__ xyv, int i0,
+                                             int e, int stride, const double* __restrict__ points, Body body) {
+  int4 id[3];
+  double2 xy[3];
+  double X[3][3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    id[s] = make_int4(-1, 0, -1, 0);
+    xy[s] = make_double2(0.0, 0.0);
+    X[s][0] = X[s][1] = X[s][2] = 0.0;
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+    if (i0 + s * stride < e) {
+      id[s] = idx[i0 + s * stride];
+      xy[s] = xyv[i0 + s * stride];
+    }
+  if (id[0].x >= 0) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) X[0][q] = points[3 * (size_t)id[0].x + q];
+  }
+  for (int i = i0; i < e; i += 3 * stride) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int ii = i + u * stride;
+      if (ii >= e) break;
+      const int sg = (u + 1) % 3, sl = (u + 2) % 3;
+      if (id[sg].x >= 0 && ii + stride < e) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) X[sg][q] = points[3 * (size_t)id[sg].x + q];
+      }
+      if (ii + 2 * stride < e) {
+        id[sl] = idx[ii + 2 * stride];
+        xy[sl] = xyv[ii + 2 * stride];
+      }
+      body(id[u], xy[u], X[u]);
+    }
+  }
+}
+
 // UNI: the chunks of `list` are uniform (chunk_uni), tables read once per block
 template <bool UNI>
 __global__ __launch_bounds__(256) void k_eval_cams(DevView v, const int* __restrict__ chunk_beg,
@@ -1668,21 +1713,23 @@ __global__ __launch_bounds__(256) void k_eval_cross(DevView v, const int* __rest
   const bool small = small_tabs_fit(v.E, v.NI);
   SmallTabs st{nullptr, nullptr};
   if (small) st = stage_small_tabs(tabs_lds, v.E, v.NI, camtab, v.intr);
-  for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
-    const int4 id = x_idx[i];
-    const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
-    ObsJac o;
-    if (small) obs_jacobian_t(id, x_xy[i], X, st, o);
-    else obs_jacobian(id, x_xy[i], X, camtab, v.intr, o);
-    const double qa[12] = {o.jw0a[0], o.jw0a[1], o.jw0a[2], o.pr.A0[0], o.pr.A0[1], o.pr.A0[2],
-                           o.jw0b[0], o.jw0b[1], o.jw0b[2], o.pr.A1[0], o.pr.A1[1], o.pr.A1[2]};
-    const double qb[12] = {o.jw1a[0], o.jw1a[1], o.jw1a[2], o.jt1a[0], o.jt1a[1], o.jt1a[2],
-                           o.jw1b[0], o.jw1b[1], o.jw1b[2], o.jt1b[0], o.jt1b[1], o.jt1b[2]};
+  // both slots' camera rows (no d r / d X), Jc0^T Jc1 accumulated
+  auto body = [&](const int4 id, const double2 xy, const double (&X)[3], const auto& tabs) {
+    double ru, rv, ja[6], jb[6], da[6], db[6];
+    obs_rows<false, 2>(id, xy, X, tabs, ru, rv, nullptr, nullptr, ja, jb, da, db);
 #pragma unroll
     for (int a = 0; a < 6; ++a)
 #pragma unroll
-      for (int bb = 0; bb < 6; ++bb) acc[6 * a + bb] += qa[a] * qb[bb] + qa[6 + a] * qb[6 + bb];
-  }
+      for (int bb = 0; bb < 6; ++bb) acc[6 * a + bb] += ja[a] * da[bb] + jb[a] * db[bb];
+  };
+  if (small)
+    pipe_entries(x_idx, x_xy, b + threadIdx.x, e, blockDim.x, points,
+                 [&](const int4 id, const double2 xy, const double (&X)[3]) { body(id, xy, X, st); });
+  else
+    pipe_entries(x_idx, x_xy, b + threadIdx.x, e, blockDim.x, points,
+                 [&](const int4 id, const double2 xy, const double (&X)[3]) {
+                   body(id, xy, X, GlobalTabs{camtab, v.intr});
+                 });
   block_reduce_store<36>(acc, partial + 36 * (size_t)c);
 }
 
