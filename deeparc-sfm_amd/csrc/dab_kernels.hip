@@ -102,43 +102,64 @@ __global__ __launch_bounds__(256) void k_final_sum(int grid, int K, const double
   }
 }
 
-__global__ __launch_bounds__(256) void k_cam_norms(int E, const int* __restrict__ ext_col,
-                                                   const double* __restrict__ ext,
-                                                   const double* __restrict__ ext_c,
-                                                   const double* __restrict__ ug, double* __restrict__ out) {
-  __shared__ double sh[256][5];
+// One 1024-thread block; each thread's (at most a few) elements have all their loads in
+// flight together (the 256-thread loop form waited on ~24 dependent load pairs per thread:
+// 18.7 us at C3, twice per LM iteration). Sums: wave DPP sums, then the 16 waves in order;
+// the max is order-free.
+__global__ __launch_bounds__(1024) void k_cam_norms(int E, const int* __restrict__ ext_col,
+                                                    const double* __restrict__ ext,
+                                                    const double* __restrict__ ext_c,
+                                                    const double* __restrict__ ug, double* __restrict__ out) {
+  constexpr int U = 8;  // elements per thread per round (6 E <= 8192 in one round)
   double a[5] = {0, 0, 0, 0, 0};
-  for (int t = threadIdx.x; t < 6 * E; t += blockDim.x) {
-    const int e = t / 6, k = t - 6 * (t / 6);
-    const int c = ext_col[e];
-    if (c < 0) continue;
-    const double x = ext[t], xc = ext_c ? ext_c[t] : x;
-    const double dd = x - xc;
-    a[0] += dd * dd;
-    a[1] += xc * xc;
-    const double gg = ug ? x - (x + (-ug[27 * (size_t)c + 21 + k])) : 0.0;
-    a[2] = fmax(a[2], fabs(gg));
-    a[3] += gg * gg;
-    a[4] += x * x;
-  }
+  const int n = 6 * E;
+  for (int t0 = 0; t0 < n; t0 += U * 1024) {
+    int c[U];
+    double x[U], xc[U];
 #pragma unroll
-  for (int i = 0; i < 5; ++i) sh[threadIdx.x][i] = a[i];
-  __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (threadIdx.x < off) {
-#pragma unroll
-      for (int i = 0; i < 5; ++i)
-        sh[threadIdx.x][i] = (i == 2) ? fmax(sh[threadIdx.x][i], sh[threadIdx.x + off][i])
-                                      : sh[threadIdx.x][i] + sh[threadIdx.x + off][i];
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + u * 1024 + (int)threadIdx.x;
+      c[u] = t < n ? ext_col[t / 6] : -1;
+      x[u] = t < n ? ext[t] : 0.0;
+      xc[u] = (t < n && ext_c) ? ext_c[t] : x[u];
     }
-    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (c[u] < 0) continue;
+      const int k = (t0 + u * 1024 + (int)threadIdx.x) % 6;
+      const double dd = x[u] - xc[u];
+      a[0] += dd * dd;
+      a[1] += xc[u] * xc[u];
+      const double gg = ug ? x[u] - (x[u] + (-ug[27 * (size_t)c[u] + 21 + k])) : 0.0;
+      a[2] = fmax(a[2], fabs(gg));
+      a[3] += gg * gg;
+      a[4] += x[u] * x[u];
+    }
   }
-  if (threadIdx.x < 5) out[threadIdx.x] = sh[0][threadIdx.x];
+  __shared__ double sh[16][5];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    double v = a[i];
+    if (i == 2) {
+      for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+      if (lane == 63) sh[w][i] = v;
+    } else {
+      v = wave_sum_lane63(v);
+      if (lane == 63) sh[w][i] = v;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 5) {
+    double t = sh[0][threadIdx.x];
+    for (int q = 1; q < 16; ++q) t = threadIdx.x == 2 ? fmax(t, sh[q][threadIdx.x]) : t + sh[q][threadIdx.x];
+    out[threadIdx.x] = t;
+  }
 }
 
 void launch_cam_norms(hipStream_t s, int E, const int* ext_col, const double* ext, const double* ext_c,
                       const double* ug, double* out) {
-  k_cam_norms<<<1, 256, 0, s>>>(E, ext_col, ext, ext_c, ug, out);
+  k_cam_norms<<<1, 1024, 0, s>>>(E, ext_col, ext, ext_c, ug, out);
 }
 // segments with many chunks: one 256-thread block per segment, thread (k, stripe) sums the
 // stripe's chunks of component k, the stripes are added in order
