@@ -793,7 +793,17 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
       ncu = prop.multiProcessorCount;
     h->ncu = ncu;
     // LDS variants: one persistent work-group per CU (at most one per slice)
-    h->eval_grid = h->eval_wps <= 0 ? std::max(1, std::min(ncu, h->nslice)) : std::max(1, h->nslice);
+    // On several ranks the camera blocks' RCCL all-reduce runs during the point kernel. The
+    // persistent point kernel (one 1024-thread, ~147-KB-LDS work-group per CU) would fill
+    // every CU and hold the RCCL kernels off until it ends, so it leaves one CU per XCD
+    // free for them (DAB_EVAL_FREE_CUS overrides; its slices are dealt round robin over
+    // whatever grid it gets).
+    int pcus = ncu;
+    if (h->world > 1 && h->eval_wps <= 0) {
+      const char* fc = getenv("DAB_EVAL_FREE_CUS");
+      pcus = std::max(1, ncu - (fc ? atoi(fc) : 8));
+    }
+    h->eval_grid = h->eval_wps <= 0 ? std::max(1, std::min(pcus, h->nslice)) : std::max(1, h->nslice);
     const char* fenv = getenv("DAB_EVAL_FUSED");
     h->fused = (!fenv || atoi(fenv) != 0) && h->world == 1;
   }
