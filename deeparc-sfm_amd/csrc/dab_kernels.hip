@@ -1595,7 +1595,12 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
     for (int i = 0; i < 3; ++i) xw[i] = reinterpret_cast<const double2*>(ext + 6 * (size_t)e0)[i];
     const double x6[6] = {xw[0].x, xw[0].y, xw[1].x, xw[1].y, xw[2].x, xw[2].y};
     double T[30];
-    cam_table(x6, T);
+    if constexpr (ABL == 3) {  // timing ablation: no trig (wrong tables)
+#pragma unroll
+      for (int i = 0; i < 12; ++i) T[i] = (i % 4 == 0 ? 1.0 : 0.0) + (i >= 9 ? x6[i - 6] : 0.0);
+    } else {
+      cam_table(x6, T);
+    }
 #pragma unroll
     for (int i = 0; i < 6; ++i) reinterpret_cast<double2*>(rt_s + 12 * e0)[i] = make_double2(T[2 * i], T[2 * i + 1]);
   }
@@ -1708,6 +1713,7 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
   const int abl = getenv("DAB_FUSED_ABL") ? atoi(getenv("DAB_FUSED_ABL")) : 0;  // timing ablations
   if (abl == 1) k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
   else if (abl == 2) k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
+  else if (abl == 3) k_eval_fused<2, 3><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
   else if (abl == 21) k_eval_fused<2, 21><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
   else if (abl == 22) k_eval_fused<2, 22><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
   else if (abl == 34) k_eval_fused<2, 0, 4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
