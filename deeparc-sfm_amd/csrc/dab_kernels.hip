@@ -1520,42 +1520,46 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
                                                      const double* __restrict__ ext, double* __restrict__ V,
                                                      double* __restrict__ g, double* __restrict__ ug,
                                                      unsigned long long* __restrict__ costfx,
-                                                     unsigned long long* __restrict__ fx_next) {
-  constexpr int NPAIR = kFusedCW / 2;
+                                                     unsigned long long* __restrict__ fx_next, int wpc, int wps) {
   __shared__ double rt_s[kLdsCams * 12];
   __shared__ double k_s[kLdsCams * 6];
-  __shared__ double csum[NPAIR][2][27];     // camera pair: [half][component]
+  __shared__ double csum[kFusedCW][27];     // camera waves' sums: [camera slot * wpc + part][component]
   __shared__ double shp[kFusedPW][2];       // point waves' cost partials
-  __shared__ unsigned ccount[NPAIR], pbar, pdone;
+  __shared__ unsigned ccount[kFusedCW + kFusedPW], pbar, pdone;  // camera slots | point slots
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (threadIdx.x < NPAIR) ccount[threadIdx.x] = 0u;
+  if (threadIdx.x < kFusedCW + kFusedPW) ccount[threadIdx.x] = 0u;
   if (threadIdx.x == 0) pbar = pdone = 0u;
   if (blockIdx.x == 0 && fx_next)
     for (int i = threadIdx.x; i < kFxWords; i += blockDim.x) fx_next[i] = 0ull;
   __syncthreads();
 
   if (wave >= kFusedPW) {
-    // ---------------- camera side: one half of one camera's chunk per wave ----------------
+    // ------- camera side: wpc waves per camera (2 at C3; up to 8 for small camera sets),
+    // each one contiguous part of the camera's uniform chunk -------
     if constexpr (ABL == 22) __builtin_amdgcn_s_setprio(2);
-    const int cw = wave - kFusedPW, pair = cw >> 1, half = cw & 1;
-    const int c = pair * gridDim.x + blockIdx.x;  // one round (fused_eval_fits)
+    const int cw = wave - kFusedPW, slot = cw / wpc, part = cw - slot * wpc;
+    const int c = slot * gridDim.x + blockIdx.x;  // one round (fused_eval_fits / fused_wpc)
     if (c >= v.NC || ABL == 1) return;
-    const int b = chunk_beg[c], e = chunk_beg[c + 1], mid = b + ((e - b) >> 1);
+    const int b = chunk_beg[c], e = chunk_beg[c + 1];
+    const int lo = b + (int)(((long long)(e - b) * part) / wpc), hi = b + (int)(((long long)(e - b) * (part + 1)) / wpc);
     const int2 u = v.chunk_uni[c];
     double acc[27];
 #pragma unroll
     for (int i = 0; i < 27; ++i) acc[i] = 0.0;
-    eval_cams_uni_pipe<NS>(v, (half ? mid : b) + lane, half ? e : mid, 64, points,
-                           [&]() { return UniTabs(ext, v.intr, u.x, u.y); }, acc);
-    wave_sums_transposed<27>(acc, csum[pair][half]);
+    eval_cams_uni_pipe<NS>(v, lo + lane, hi, 64, points, [&]() { return UniTabs(ext, v.intr, u.x, u.y); }, acc);
+    wave_sums_transposed<27>(acc, csum[cw]);
     unsigned old = 0;
     if (lane == 0) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      old = __hip_atomic_fetch_add(&ccount[pair], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+      old = __hip_atomic_fetch_add(&ccount[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     old = __builtin_amdgcn_readfirstlane(old);
-    if (old != 1u) return;  // the other half is still running: it writes the camera row
-    if (lane < 27) ug[27 * (size_t)c + lane] = csum[pair][0][lane] + csum[pair][1][lane];
+    if (old != (unsigned)wpc - 1) return;  // another part is still running: the last one writes the row
+    if (lane < 27) {
+      double t = csum[slot * wpc][lane];
+      for (int q = 1; q < wpc; ++q) t += csum[slot * wpc + q][lane];  // parts in order
+      ug[27 * (size_t)c + lane] = t;
+    }
     return;
   }
 
@@ -1563,11 +1567,27 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
   if constexpr (ABL == 2) return;
   if constexpr (ABL == 21) __builtin_amdgcn_s_setprio(2);
   const size_t NPs = (size_t)v.NP;
-  const int pw = wave;
-  const int rounds = (v.nslice + kFusedPW * gridDim.x - 1) / (kFusedPW * gridDim.x);
+  // wps point waves per slice (1 at C3; more for small problems, whose slices would
+  // otherwise leave most point waves idle): part `part` of the slot's waves takes rows
+  // part, part + wps, ...; the parts are combined in LDS by the last one to finish
+  const int pw = wave, pslots = kFusedPW / wps, slot = pw / wps, part = pw - slot * wps;
+  const int rounds = (v.nslice + pslots * gridDim.x - 1) / (pslots * gridDim.x);
   RowQueue<D> q;
   double X[3] = {0.0, 0.0, 0.0};
-  int sl = pw * gridDim.x + blockIdx.x, off = 0, len = 0;
+  int sl = slot * gridDim.x + blockIdx.x, off = 0, len = 0;
+  auto fill_q = [&]() {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int k = part + d * wps;
+      if (k < len) {
+        q.id[d] = v.obs_idx[off + 64 * k + lane];
+        q.xy[d] = v.obs_xy[off + 64 * k + lane];
+      } else {
+        q.id[d] = make_int4(-1, 0, -1, 0);
+        q.xy[d] = make_double2(0.0, 0.0);
+      }
+    }
+  };
   if (sl < v.nslice) {
     off = v.slice_off[sl];
     len = (v.slice_off[sl + 1] - off) >> 6;
@@ -1578,7 +1598,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
       X[2] = points[3 * (size_t)p + 2];
     }
   }
-  rowq_fill<1, D>(v, off, len, 0, lane, q);
+  fill_q();
   // intrinsics: LDS-DMA straight into k_s (no registers), 16 B per lane, k_s is lane-linear
   {
     const int npiece = 3 * v.NI;
@@ -1614,7 +1634,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
   double acc[2] = {0.0, 0.0};
   for (int r = 0; r < rounds; ++r) {
     if (r > 0) {
-      sl = (r * kFusedPW + pw) * gridDim.x + blockIdx.x;
+      sl = (r * pslots + slot) * gridDim.x + blockIdx.x;
       off = len = 0;
       X[0] = X[1] = X[2] = 0.0;
       if (sl < v.nslice) {
@@ -1627,22 +1647,22 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
           X[2] = points[3 * (size_t)p + 2];
         }
       }
-      rowq_fill<1, D>(v, off, len, 0, lane, q);
+      fill_q();
     }
     double c[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) c[k] = 0.0;
 #pragma unroll 1
-    for (int k0 = 0; k0 < len; k0 += D) {
+    for (int k0 = part; k0 < len; k0 += D * wps) {
 #pragma unroll
       for (int d = 0; d < D; ++d) {
-        const int k = k0 + d;
+        const int k = k0 + d * wps;
         if (k >= len) break;
         const int4 id = q.id[d];
         const double2 xy = q.xy[d];
-        if (k + D < len) {
-          q.id[d] = v.obs_idx[off + 64 * (k + D) + lane];
-          q.xy[d] = v.obs_xy[off + 64 * (k + D) + lane];
+        if (k + D * wps < len) {
+          q.id[d] = v.obs_idx[off + 64 * (k + D * wps) + lane];
+          q.xy[d] = v.obs_xy[off + 64 * (k + D * wps) + lane];
         }
         const bool live = id.x >= 0;
         double ru, rv, jx0[3], jx1[3];
@@ -1663,6 +1683,26 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
       }
     }
     const int p = 64 * sl + lane;
+    if (wps > 1) {
+      // (one round by construction) parts -> LDS after the tables (fused_wps keeps
+      // 12 E + kFusedPW * 9 * 64 doubles inside rt_s); the last part sums them in order
+      double* cbuf = rt_s + ((12 * v.E + 1) & ~1);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) cbuf[(pw * 9 + k) * 64 + lane] = c[k];
+      unsigned old = 0;
+      if (lane == 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        old = __hip_atomic_fetch_add(&ccount[kFusedCW + slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      old = __builtin_amdgcn_readfirstlane(old);
+      if (old != (unsigned)wps - 1) continue;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        double t = cbuf[((slot * wps) * 9 + k) * 64 + lane];
+        for (int q2 = 1; q2 < wps; ++q2) t += cbuf[((slot * wps + q2) * 9 + k) * 64 + lane];
+        c[k] = t;
+      }
+    }
     if (sl < v.nslice && p < v.NP) {
 #pragma unroll
       for (int k = 0; k < 6; ++k) V[k * NPs + p] = c[k];
@@ -1707,20 +1747,37 @@ bool fused_eval_fits(const DevView& v, int nchunk, int ngen, int ncross, int gri
   return !v.any_comp && ncross == 0 && ngen == 0 && nchunk == v.NC && v.NC > 0 && v.E <= kLdsCams &&
          v.NI <= kLdsCams && v.NC <= (kFusedCW / 2) * grid;
 }
+// waves per camera: as many as still give every camera a slot in one round (small camera
+// sets split each chunk finer: C2's 99 cameras take 8 waves each, C3's 999 take 2)
+static int fused_wpc(int NC, int grid) {
+  int w = kFusedCW;
+  while (w > 2 && (long long)NC * w > (long long)kFusedCW * grid) w >>= 1;
+  return w;
+}
+// point waves per slice: more when the slices are few (every slice in one round), if the
+// per-part sums fit in rt_s beside the tables
+static int fused_wps(int nslice, int E, int grid) {
+  int w = kFusedPW;
+  while (w > 1 && ((long long)nslice * w > (long long)kFusedPW * grid ||
+                   ((12 * E + 1) & ~1) + kFusedPW * 9 * 64 > kLdsCams * 12))
+    w >>= 1;
+  return w;
+}
 void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
                        double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
                        int grid) {
   const int abl = getenv("DAB_FUSED_ABL") ? atoi(getenv("DAB_FUSED_ABL")) : 0;  // timing ablations
-  if (abl == 1) k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
-  else if (abl == 2) k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
-  else if (abl == 3) k_eval_fused<2, 3><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
-  else if (abl == 21) k_eval_fused<2, 21><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
-  else if (abl == 22) k_eval_fused<2, 22><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
-  else if (abl == 34) k_eval_fused<2, 0, 4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
-  else if (abl == 35) k_eval_fused<2, 0, 5><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
-  else if (abl == 234) k_eval_fused<2, 2, 4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
-  else if (abl == 14) k_eval_fused<4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
-  else k_eval_fused<2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next);
+  const int wpc = fused_wpc(v.NC, grid), wps = fused_wps(v.nslice, v.E, grid);
+  if (abl == 1) k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+  else if (abl == 2) k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+  else if (abl == 3) k_eval_fused<2, 3><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+  else if (abl == 21) k_eval_fused<2, 21><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+  else if (abl == 22) k_eval_fused<2, 22><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+  else if (abl == 34) k_eval_fused<2, 0, 4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+  else if (abl == 35) k_eval_fused<2, 0, 5><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+  else if (abl == 234) k_eval_fused<2, 2, 4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+  else if (abl == 14) k_eval_fused<4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+  else k_eval_fused<2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
 }
 
 // arc∘ring cross blocks Jc0^T Jc1, one block per chunk of composed observations sorted
