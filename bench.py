@@ -285,8 +285,9 @@ def main():
                          "kernel": eval_kernel, "kernel_ms": jac_ms,
                          "algorithmic_bytes_per_launch": jac_bytes},
             "eval_kernel_mobs_per_s": n_obs / (jac_ms * 1e-3) / 1e6,
-            "eval_schedule": ("fused: camera and point side in one launch" if fused else
-                              "two kernels: k_eval_cams then k_eval_points"),
+            "eval_schedule": {1: "fused: camera and point side in one launch",
+                              2: "fused kernel split: camera side, then point side beside the all-reduce",
+                              0: "two kernels: k_eval_cams then k_eval_points"}[fused],
             "outside_kernel_ms": asm_ms,
             "cpu_baseline": cpu,
         }

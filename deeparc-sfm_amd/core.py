@@ -296,7 +296,7 @@ class Solver:
     def eval_fused(self):
         f = C.c_int32()
         check(self.lib.dab_eval_schedule(self.h, C.byref(f)), self.lib)
-        return bool(f.value)
+        return f.value  # 0 two kernels, 1 one fused launch, 2 fused kernel split per side
 
 
 def solve(problem, max_iteration=1000, max_second=3600, freeze_camera=False, device=0,

@@ -98,9 +98,10 @@ void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, con
 // point side -> V, g, cost in fixed point as launch_eval_points): one launch, camera and
 // point waves side by side. fused_eval_fits: whether the problem qualifies for `grid`.
 bool fused_eval_fits(const DevView& v, int nchunk, int ngen, int ncross, int grid);
+// side: 0 both halves; 1 the point side only (V, g, cost); 2 the camera side only (ug)
 void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
                        double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
-                       int grid);
+                       int grid, int side);
 //  arc∘ring cross blocks Jc0^T Jc1 over composed observations (pair-major copy) -> partial[chunk][36]
 void launch_eval_cross(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
                        const double2* x_xy, const double* points, const double* camtab, double* partial);

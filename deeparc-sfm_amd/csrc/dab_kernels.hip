@@ -1512,9 +1512,10 @@ void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, con
 // uniform chunk per free camera, E, NI <= kLdsCams, NC <= (camera waves / 2) x grid.
 constexpr int kFusedPW = 8;               // point waves per work-group
 constexpr int kFusedCW = 16 - kFusedPW;   // camera waves (kFusedCW / 2 cameras per round)
-template <int D, int ABL = 0, int NS = 3>  // ABL (timing ablations): 1 camera waves exit at once, 2 point
-                                          // waves do; 21 / 22: point / camera waves at raised priority;
-                                          // NS: camera-entry pipeline slots
+template <int D, int ABL = 0, int NS = 3>  // ABL: 1 camera waves exit at once (point side only), 2 point
+                                          // waves do (camera side only) — the multi-rank split schedule;
+                                          // timing ablations: 3 no trig in the staging, 21 / 22 point /
+                                          // camera waves at raised priority; NS: camera-entry pipeline slots
 __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __restrict__ chunk_beg,
                                                      const double* __restrict__ points,
                                                      const double* __restrict__ ext, double* __restrict__ V,
@@ -1765,9 +1766,19 @@ static int fused_wps(int nslice, int E, int grid) {
 }
 void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
                        double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
-                       int grid) {
-  const int abl = getenv("DAB_FUSED_ABL") ? atoi(getenv("DAB_FUSED_ABL")) : 0;  // timing ablations
+                       int grid, int side) {
   const int wpc = fused_wpc(v.NC, grid), wps = fused_wps(v.nslice, v.E, grid);
+  // one side only (the multi-rank split schedule): the same kernel with the other side's
+  // waves leaving at once
+  if (side == 1) {
+    k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+    return;
+  }
+  if (side == 2) {
+    k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+    return;
+  }
+  const int abl = getenv("DAB_FUSED_ABL") ? atoi(getenv("DAB_FUSED_ABL")) : 0;  // timing ablations
   if (abl == 1) k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
   else if (abl == 2) k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
   else if (abl == 3) k_eval_fused<2, 3><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);

@@ -189,6 +189,7 @@ struct dab_handle {
   int fx_last = 1;               // set of the last fixed-point pass (both sets start zeroed)
   int* h_flags = nullptr;      // pinned
   int red_grid = 1;
+  bool fused_split = false;  // fused kernel as camera-side then point-side launches (world > 1)
   int eval_grid = 1;  // k_eval_points blocks (one SELL slice per block)
   int ncu = 256;      // compute units of the device
   int fused_grid = 0;  // > 0: single-pass PCG matvec (small camera systems)
@@ -805,7 +806,9 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
     }
     h->eval_grid = h->eval_wps <= 0 ? std::max(1, std::min(pcus, h->nslice)) : std::max(1, h->nslice);
     const char* fenv = getenv("DAB_EVAL_FUSED");
-    h->fused = (!fenv || atoi(fenv) != 0) && h->world == 1;
+    h->fused = !fenv || atoi(fenv) != 0;
+    const char* senv = getenv("DAB_EVAL_SPLIT");  // the split schedule on one rank too (tests)
+    h->fused_split = h->world > 1 || (senv && atoi(senv) != 0);
   }
   CHECK_RC(d.alloc(&h->d_gpart, (size_t)std::max(h->red_grid, h->eval_grid) * 4));
   CHECK_RC(d.alloc(&h->d_scal, S_NSLOTS));
@@ -1126,12 +1129,36 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
   const bool fx = h->fused || eval_points_fx(h->eval_wps);
   if (fx) h->fx_last ^= 1;  // this pass adds into set fx_last and zeroes the other
   h->cost_fx_pending = fx;
-  if (h->fused) {  // both halves of the pass in one launch (launch_eval_fused)
+  if (h->fused && !h->fused_split) {  // both halves of the pass in one launch (launch_eval_fused)
     if (ev_mid) HIP_OK(hipEventRecord(ev_mid, s));
     launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
-                      h->cost_fx(h->fx_last ^ 1), h->ncu);
+                      h->cost_fx(h->fx_last ^ 1), h->ncu, 0);
     if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
     if (h->NC > 0) CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
+    return 0;
+  }
+  if (h->fused) {
+    // several ranks: the same kernel as two launches, the camera side first so that its
+    // RCCL all-reduce runs on the communication stream during the point side (which
+    // leaves one CU per XCD free for it: eval_grid)
+    if (ev_mid) HIP_OK(hipEventRecord(ev_mid, s));
+    launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
+                      h->cost_fx(h->fx_last ^ 1), h->ncu, 2);
+    bool ovl = false;
+    if (h->comm && !h->host_cb) {
+      HIP_OK(hipEventRecord(h->ev_cam, s));
+      HIP_OK(hipStreamWaitEvent(h->comm_stream, h->ev_cam, 0));
+      NCCL_OK(ncclAllReduce(h->d_camred, h->d_camred, h->camred_count(), ncclDouble, ncclSum, h->comm,
+                            h->comm_stream));
+      HIP_OK(hipEventRecord(h->ev_comm, h->comm_stream));
+      ovl = true;
+    } else {
+      CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
+    }
+    launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
+                      h->cost_fx(h->fx_last ^ 1), h->eval_grid, 1);
+    if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
+    if (ovl) HIP_OK(hipStreamWaitEvent(s, h->ev_comm, 0));
     return 0;
   }
   if (h->NC > 0) {
@@ -1761,6 +1788,6 @@ extern "C" int dab_pcg_schedule(dab_handle* h, int32_t* matrix_free) {
 extern "C" int dab_eval_schedule(dab_handle* h, int32_t* fused) {
   clear_error();
   if (!h || !h->have_problem || !fused) return set_error(DAB_E_STATE, "no problem set");
-  *fused = h->fused ? 1 : 0;
+  *fused = h->fused ? (h->fused_split ? 2 : 1) : 0;
   return 0;
 }

@@ -237,8 +237,10 @@ int dab_bench_kernel_ms(dab_handle* h, double* jac_ms, double* assembly_ms);
 /* Algorithmic HBM bytes of one residual+Jacobian launch on the resident problem. */
 int dab_jacobian_bytes(dab_handle* h, double* bytes);
 /* Which evaluation schedule the resident problem uses: *fused = 1 when the pass is the
- * single fused launch (k_eval_fused: camera and point side together), 0 for the
- * two-kernel pass (k_eval_cams + k_eval_points). */
+ * single fused launch (k_eval_fused: camera and point side together), 2 when it is the
+ * same kernel as a camera-side then a point-side launch (several ranks: the camera blocks'
+ * all-reduce overlaps the point side), 0 for the two-kernel pass (k_eval_cams +
+ * k_eval_points). */
 int dab_eval_schedule(dab_handle* h, int32_t* fused);
 /* After an IMPLICIT_SCHUR_PCG solve: *matrix_free = 1 when the Schur products re-evaluate
  * the observation rows in every pass (small camera sets: all fp64, no Y records, so

@@ -15,11 +15,17 @@ import _pkgload  # noqa: E402
 
 pkg = _pkgload.load()
 cfg = sys.argv[1]
-variants = sys.argv[2:]  # DAB_EVAL_WPS values (two-kernel pass), or "fused"
+variants = sys.argv[2:]  # DAB_EVAL_WPS values (two-kernel pass), "fused[ABL]" or "split"
 base = pkg.synth(**pkg.CONFIGS[cfg])
 ref = None
 for wps in variants:
-    if wps.startswith("fused"):  # fused, fused1, fused2 (DAB_FUSED_ABL ablations)
+    os.environ.pop("DAB_EVAL_SPLIT", None)
+    if wps == "split":  # the multi-rank schedule (camera-side, then point-side launch)
+        os.environ["DAB_EVAL_FUSED"] = "1"
+        os.environ["DAB_EVAL_SPLIT"] = "1"
+        os.environ.pop("DAB_FUSED_ABL", None)
+        os.environ.pop("DAB_EVAL_WPS", None)
+    elif wps.startswith("fused"):  # fused, fused1, fused2 (DAB_FUSED_ABL ablations)
         os.environ["DAB_EVAL_FUSED"] = "1"
         os.environ["DAB_FUSED_ABL"] = wps[5:] or "0"
         os.environ.pop("DAB_EVAL_WPS", None)

@@ -288,6 +288,33 @@ def test_fused_eval_matches_two_kernel_pass(pkg, gpu, solver, monkeypatch):
     np.testing.assert_array_equal(pts[0], pts[2])
 
 
+@pytest.mark.parametrize("kind", ["bal", "c2"])
+def test_split_fused_schedule_matches_single_launch(pkg, gpu, kind, monkeypatch):
+    """The multi-rank schedule runs the fused kernel as a camera-side launch, then a
+    point-side launch (the camera blocks' all-reduce overlaps the second). DAB_EVAL_SPLIT=1
+    forces it on one rank, where both launches get the full grid: the LM trajectory must be
+    bitwise that of the single fused launch (same wave split, fixed-point cost)."""
+    if kind == "bal":
+        prob = pkg.synth(kind=0, num_cameras=120, num_points=9000, obs_per_point=8, seed=54)
+    else:
+        prob = pkg.synth(**pkg.CONFIGS["c2_100cam"])
+    monkeypatch.setenv("DAB_EVAL_FUSED", "1")
+    res, pts, sched = [], [], []
+    for split in ("0", "1"):
+        monkeypatch.setenv("DAB_EVAL_SPLIT", split)
+        p = prob.copy()
+        s = pkg.Solver(0)
+        s.set_problem(p)
+        sched.append(s.eval_fused())
+        res.append(s.solve(pkg.options(max_num_iterations=6,
+                                       linear_solver_type=pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)))
+        s.close()
+        pts.append(p.points.copy())
+    assert sched == [1, 2]
+    assert [it["cost"] for it in res[0]["iterations"]] == [it["cost"] for it in res[1]["iterations"]]
+    np.testing.assert_array_equal(pts[0], pts[1])
+
+
 @pytest.mark.parametrize("wps", ["-112", "-122", "-113"])
 @pytest.mark.parametrize("kind", ["bal", "rig"])
 def test_prefetch_point_kernels_match(pkg, gpu, kind, wps, monkeypatch):
