@@ -28,6 +28,28 @@
 
 namespace dab {
 
+#ifdef DAB_TRACE
+// timing build only (scripts/trace_fused.sh): per-wave s_memrealtime stamps (100 MHz)
+__device__ unsigned long long g_trace[256 * 16 * 4];
+#define DAB_STAMP(k)                                                                        \
+  do {                                                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                          \
+    if (lane == 0 && blockIdx.x < 256) g_trace[(blockIdx.x * 16 + wave) * 4 + (k)] = t_;     \
+  } while (0)
+#define DAB_STAMP_ANY(k)                                                                                     \
+  do {                                                                                                       \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                           \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 256) g_trace[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 4 + (k)] = t_; \
+  } while (0)
+#else
+#define DAB_STAMP_ANY(k) \
+  do {                   \
+  } while (0)
+#define DAB_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 int grid_for(int n, int block, int cap) {
   int g = (n + block - 1) / block;
   if (g < 1) g = 1;
@@ -1366,6 +1388,7 @@ __device__ __forceinline__ void eval_cams_uni_pipe(const DevView& v, int i0, int
       for (int q = 0; q < 3; ++q) X[s][q] = points[3 * (size_t)pt[s] + q];
     }
   const auto tabs = make_tabs();
+  DAB_STAMP_ANY(1);
   for (int i = i0; i < e; i += NS * stride) {
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
@@ -1395,6 +1418,178 @@ __device__ __forceinline__ void eval_cams_uni_pipe(const DevView& v, int i0, int
       for (int a = 0; a < 6; ++a) acc[21 + a] = fma(jb[a], rv, fma(ja[a], ru, acc[21 + a]));
     }
   }
+}
+
+
+
+// Camera blocks accumulated in the point frame (the fused pass's camera waves). With
+// Y = R X and J_l = R J_r (the left Jacobian), the rotation part of a row a (= dr/dP) is
+//   -((a R) x X)^T J_r = (Y x a)^T J_l          (R (u x v) = R u x R v),
+// so every row is w = [Y x a | a] times the per-camera constant blockdiag(J_l, I): the
+// loop accumulates the 6 x 6 block and the 6-vector in w's basis (no J_r product per row:
+// 118 fp64 instructions per entry instead of 154) and cam_frame_entry applies J_l once
+// per camera, after the sums. The small-angle tables (R = I + [w]x, Rd = J_r = I) take
+// Z = X in place of Y and J_l = I: the same rows as obs_rows, exactly.
+struct UniFrame {
+  double T[12];  // R | t
+  double K[6];
+  bool small;
+  // jl: J_l (row-major; I for the small-angle tables) goes to LDS for cam_frame_entry, so
+  // that it holds no registers through the entry loop
+  __device__ __forceinline__ UniFrame(const double* __restrict__ ext, const double* __restrict__ intr, int e,
+                                      int i, double* jl) {
+    double F[30];
+    cam_table(ext + 6 * (size_t)e, F);
+    // cam_table's branch (its small-angle Rd is exactly I, R never is otherwise)
+    small = F[12] == 1.0 && F[13] == 0.0 && F[14] == 0.0 && F[15] == 0.0 && F[16] == 1.0 && F[17] == 0.0 &&
+            F[18] == 0.0 && F[19] == 0.0 && F[20] == 1.0 && F[21] == 1.0 && F[25] == 1.0 && F[29] == 1.0;
+#pragma unroll
+    for (int q = 0; q < 12; ++q) T[q] = UniTabs::uniform(F[q]);
+    const double* k = intr + (size_t)kIntr * i;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) K[q] = UniTabs::uniform(k[q]);
+    // J_l = Rd Jd (Rd = R, or I with Jd = I for the small-angle tables), wave-uniform,
+    // stored by lane 0
+    double J[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        J[3 * r + c] = UniTabs::uniform(F[12 + 3 * r] * F[21 + c] + F[12 + 3 * r + 1] * F[24 + c] +
+                                        F[12 + 3 * r + 2] * F[27 + c]);
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+      for (int q = 0; q < 9; ++q) jl[q] = J[q];
+    }
+  }
+};
+
+__device__ __forceinline__ void frame_rows_acc(const double2 xy, const double (&X)[3], const UniFrame& f,
+                                               double (&acc)[27]) {
+  const double* R = f.T;
+  double Y[3], P[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    Y[r] = R[3 * r] * X[0] + R[3 * r + 1] * X[1] + R[3 * r + 2] * X[2];
+    P[r] = Y[r] + f.T[9 + r];
+  }
+  // a wave-uniform select (two loop copies, one per case, would spill)
+  double Z[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) Z[r] = f.small ? X[r] : Y[r];
+  Proj pr;
+  project(P, f.K, xy.x, xy.y, pr, true);
+  double ja[6], jb[6];
+  ja[0] = Z[1] * pr.A0[2] - Z[2] * pr.A0[1];
+  ja[1] = Z[2] * pr.A0[0] - Z[0] * pr.A0[2];
+  ja[2] = Z[0] * pr.A0[1] - Z[1] * pr.A0[0];
+  jb[0] = Z[1] * pr.A1[2] - Z[2] * pr.A1[1];
+  jb[1] = Z[2] * pr.A1[0] - Z[0] * pr.A1[2];
+  jb[2] = Z[0] * pr.A1[1] - Z[1] * pr.A1[0];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    ja[3 + i] = pr.A0[i];
+    jb[3 + i] = pr.A1[i];
+  }
+  int k = 0;
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int bb = a; bb < 6; ++bb) {
+      acc[k] = fma(jb[a], jb[bb], fma(ja[a], ja[bb], acc[k]));
+      ++k;
+    }
+#pragma unroll
+  for (int a = 0; a < 6; ++a) acc[21 + a] = fma(jb[a], pr.rv, fma(ja[a], pr.ru, acc[21 + a]));
+}
+
+// eval_cams_uni_pipe's three-slot pipeline over the frame accumulation; jl (LDS, 9
+// doubles) receives the camera's J_l for cam_frame_entry
+template <int NS>
+__device__ __forceinline__ void frame_pipe(const DevView& v, int i0, int e, int stride,
+                                           const double* __restrict__ points, const UniFrame& f,
+                                           int (&pt)[NS], double2 (&xy)[NS], double (&X)[NS][3],
+                                           double (&acc)[27]) {
+  const int* __restrict__ cm_pt = v.cm_pt;
+  for (int i = i0; i < e; i += NS * stride) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int ii = i + u * stride;
+      if (ii >= e) break;
+      const int sg = (u + NS - 2) % NS, sl = (u + NS - 1) % NS;
+      if (pt[sg] >= 0 && ii + (NS - 2) * stride < e) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) X[sg][q] = points[3 * (size_t)pt[sg] + q];
+      }
+      if (ii + (NS - 1) * stride < e) {
+        pt[sl] = cm_pt[ii + (NS - 1) * stride];
+        xy[sl] = v.cm_xy[ii + (NS - 1) * stride];
+      }
+      frame_rows_acc(xy[u], X[u], f, acc);
+    }
+  }
+}
+template <int NS = 3>
+__device__ __forceinline__ void eval_cams_uni_frame(const DevView& v, int i0, int e, int stride,
+                                                    const double* __restrict__ points, int ext_i, int intr_i,
+                                                    const double* __restrict__ ext, double (&acc)[27],
+                                                    double* jl) {
+  static_assert(NS >= 3, "at least three slots");
+  const int* __restrict__ cm_pt = v.cm_pt;
+  int pt[NS];
+  double2 xy[NS];
+  double X[NS][3];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    pt[s] = -1;
+    xy[s] = make_double2(0.0, 0.0);
+    X[s][0] = X[s][1] = X[s][2] = 0.0;
+  }
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (i0 + s * stride < e) {
+      pt[s] = cm_pt[i0 + s * stride];
+      xy[s] = v.cm_xy[i0 + s * stride];
+    }
+#pragma unroll
+  for (int s = 0; s < NS - 2; ++s)
+    if (pt[s] >= 0) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) X[s][q] = points[3 * (size_t)pt[s] + q];
+    }
+  const UniFrame f(ext, v.intr, ext_i, intr_i, jl);  // built while the first loads fly
+  DAB_STAMP_ANY(1);
+  frame_pipe<NS>(v, i0, e, stride, points, f, pt, xy, X, acc);
+}
+
+// entry k (< 27) of the camera's [U upper-packed | g_c] from the point-frame sums s
+// (same packing): U_rr = J^T U~_rr J, U_rt = J^T U~_rt, U_tt = U~_tt, g_r = J^T g~_r
+__device__ __forceinline__ int upk6(int a, int b) {  // packed index of (a, b), a <= b
+  return a * 6 - a * (a - 1) / 2 + (b - a);
+}
+__device__ __forceinline__ double cam_frame_entry(const double* s, const double* J, int k) {
+  if (k >= 21) {
+    const int i = k - 21;
+    if (i >= 3) return s[k];
+    return J[i] * s[21] + J[3 + i] * s[22] + J[6 + i] * s[23];
+  }
+  int a = 0, r = k;
+  while (r >= 6 - a) {
+    r -= 6 - a;
+    ++a;
+  }
+  const int b = a + r;
+  if (a >= 3) return s[k];
+  if (b >= 3) return J[a] * s[upk6(0, b)] + J[3 + a] * s[upk6(1, b)] + J[6 + a] * s[upk6(2, b)];
+  double t = 0.0;
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    double u = 0.0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) u += s[upk6(min(p, q), max(p, q))] * J[3 * q + b];
+    t += J[3 * p + a] * u;
+  }
+  return t;
 }
 
 // General entries (int4 index records, the rig's camera-major and pair-major copies): the
@@ -1499,7 +1694,8 @@ void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, con
 // kernel's 1024-thread work-group at 128 VGPRs fills a CU's register file. Here waves
 // 0..kFusedPW-1 of each work-group run the point side (SELL slices, lane = point, a
 // D-deep row queue, R,t and K staged in LDS) and the other waves run the camera side (a
-// pair of waves per free camera, each half of its uniform chunk, table in SGPRs), so the
+// pair of waves per free camera, each half of its uniform chunk, table in SGPRs, blocks
+// accumulated in the point frame: eval_cams_uni_frame), so the
 // VALU work of one hides the memory latency of the other. Only the point waves need the
 // LDS tables: they stage them and meet at an LDS-counter barrier of their own, while the
 // camera waves start at once. Every reduction keeps a fixed order: the camera pair's two
@@ -1525,9 +1721,11 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
   __shared__ double rt_s[kLdsCams * 12];
   __shared__ double k_s[kLdsCams * 6];
   __shared__ double csum[kFusedCW][27];     // camera waves' sums: [camera slot * wpc + part][component]
+  __shared__ double cjl[kFusedCW][9];       // camera waves' J_l (eval_cams_uni_frame)
   __shared__ double shp[kFusedPW][2];       // point waves' cost partials
   __shared__ unsigned ccount[kFusedCW + kFusedPW], pbar, pdone;  // camera slots | point slots
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  DAB_STAMP(0);
   if (threadIdx.x < kFusedCW + kFusedPW) ccount[threadIdx.x] = 0u;
   if (threadIdx.x == 0) pbar = pdone = 0u;
   if (blockIdx.x == 0 && fx_next)
@@ -1540,14 +1738,21 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
     if constexpr (ABL == 22) __builtin_amdgcn_s_setprio(2);
     const int cw = wave - kFusedPW, slot = cw / wpc, part = cw - slot * wpc;
     const int c = slot * gridDim.x + blockIdx.x;  // one round (fused_eval_fits / fused_wpc)
-    if (c >= v.NC || ABL == 1) return;
+    if (c >= v.NC || ABL == 1 || ABL == 15) return;
     const int b = chunk_beg[c], e = chunk_beg[c + 1];
     const int lo = b + (int)(((long long)(e - b) * part) / wpc), hi = b + (int)(((long long)(e - b) * (part + 1)) / wpc);
     const int2 u = v.chunk_uni[c];
     double acc[27];
 #pragma unroll
     for (int i = 0; i < 27; ++i) acc[i] = 0.0;
-    eval_cams_uni_pipe<NS>(v, lo + lane, hi, 64, points, [&]() { return UniTabs(ext, v.intr, u.x, u.y); }, acc);
+    if constexpr (ABL == 5 || ABL == 25) {  // timing ablation: rows through obs_rows (J_r per row)
+      eval_cams_uni_pipe<NS>(v, lo + lane, hi, 64, points, [&]() { return UniTabs(ext, v.intr, u.x, u.y); },
+                             acc);
+      if (lane < 9) cjl[cw][lane] = (lane % 4 == 0) ? 1.0 : 0.0;
+    } else {
+      eval_cams_uni_frame<NS>(v, lo + lane, hi, 64, points, u.x, u.y, ext, acc, cjl[cw]);
+    }
+    DAB_STAMP(2);
     wave_sums_transposed<27>(acc, csum[cw]);
     unsigned old = 0;
     if (lane == 0) {
@@ -1555,17 +1760,27 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
       old = __hip_atomic_fetch_add(&ccount[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     old = __builtin_amdgcn_readfirstlane(old);
-    if (old != (unsigned)wpc - 1) return;  // another part is still running: the last one writes the row
-    if (lane < 27) {
-      double t = csum[slot * wpc][lane];
-      for (int q = 1; q < wpc; ++q) t += csum[slot * wpc + q][lane];  // parts in order
-      ug[27 * (size_t)c + lane] = t;
+    if (old != (unsigned)wpc - 1) {  // another part is still running: the last one writes the row
+      DAB_STAMP(3);
+      return;
     }
+    // parts summed in order, then out of the point frame (cam_frame_entry)
+    double* cs = csum[slot * wpc];
+    if (lane < 27) {
+      double t = cs[lane];
+      for (int q = 1; q < wpc; ++q) t += csum[slot * wpc + q][lane];
+      cs[lane] = t;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane < 27) ug[27 * (size_t)c + lane] = cam_frame_entry(cs, cjl[cw], lane);
+    DAB_STAMP(3);
     return;
   }
 
   // ---------------- point side ----------------
-  if constexpr (ABL == 2) return;
+  if constexpr (ABL == 2 || ABL == 25) return;
   if constexpr (ABL == 21) __builtin_amdgcn_s_setprio(2);
   const size_t NPs = (size_t)v.NP;
   // wps point waves per slice (1 at C3; more for small problems, whose slices would
@@ -1631,6 +1846,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
   if (lane == 0) __hip_atomic_fetch_add(&pbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   while (__hip_atomic_load(&pbar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)kFusedPW)
     __builtin_amdgcn_s_sleep(1);
+  DAB_STAMP(1);
   const LdsTabs<true> tabs{rt_s, k_s, nullptr, v.intr};
   double acc[2] = {0.0, 0.0};
   for (int r = 0; r < rounds; ++r) {
@@ -1711,6 +1927,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
       for (int k = 0; k < 3; ++k) g[k * NPs + p] = c[6 + k];
     }
   }
+  DAB_STAMP(2);
   // cost: wave sums, summed in wave order by the last point wave, added in fixed point
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -1723,6 +1940,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
     old = __hip_atomic_fetch_add(&pdone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   old = __builtin_amdgcn_readlane(old, 63);
+  DAB_STAMP(3);
   if (old != (unsigned)kFusedPW - 1 || lane != 0) return;
   double pc = shp[0][0], bc = shp[0][1];
 #pragma unroll
@@ -1779,7 +1997,11 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
     return;
   }
   const int abl = getenv("DAB_FUSED_ABL") ? atoi(getenv("DAB_FUSED_ABL")) : 0;  // timing ablations
-  if (abl == 1) k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+  if (abl == 5)
+    k_eval_fused<2, 5><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+  else if (abl == 25)
+    k_eval_fused<2, 25><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+  else if (abl == 1) k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
   else if (abl == 2) k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
   else if (abl == 3) k_eval_fused<2, 3><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
   else if (abl == 21) k_eval_fused<2, 21><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
@@ -2677,3 +2899,13 @@ void launch_grad_points(hipStream_t s, int NP, const double* x, const double* g,
 }
 
 }  // namespace dab
+
+#ifdef DAB_TRACE
+extern "C" int dab_trace_fetch(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dab::g_trace), sizeof(dab::g_trace)) == hipSuccess ? 0 : -1;
+}
+extern "C" int dab_trace_clear() {
+  static unsigned long long z[256 * 16 * 4];
+  return hipMemcpyToSymbol(HIP_SYMBOL(dab::g_trace), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -288,6 +288,34 @@ def test_fused_eval_matches_two_kernel_pass(pkg, gpu, solver, monkeypatch):
     np.testing.assert_array_equal(pts[0], pts[2])
 
 
+def test_fused_camera_frame_small_angles(pkg, gpu, monkeypatch):
+    """The fused pass accumulates the camera blocks in the point frame and applies J_l per
+    camera afterwards; cameras on the small-angle tables (|w|^2 <= DBL_EPSILON, exactly
+    zero or not) take X in place of R X there. Against the two-kernel pass (obs_rows, J_r
+    per row) the LM trajectory must agree to 1e-10 relative (a 1.5e-8 Jacobian slip on
+    those cameras would not)."""
+    prob = pkg.synth(kind=0, num_cameras=60, num_points=6000, obs_per_point=8, seed=57)
+    prob.ext[1, :3] = 0.0
+    prob.ext[2, :3] = [1e-9, -2e-9, 3e-9]
+    prob.ext[3, :3] = [0.0, 1.4e-8, 0.0]
+    prob.ext[4, :3] = [1e-7, 0.0, 0.0]  # just above the threshold: the general tables
+    res, sched = [], []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DAB_EVAL_FUSED", fused)
+        p = prob.copy()
+        s = pkg.Solver(0)
+        s.set_problem(p)
+        sched.append(s.eval_fused())
+        res.append(s.solve(pkg.options(max_num_iterations=5)))
+        s.close()
+    assert sched == [1, 0]
+    a, b = res
+    assert [it["linear_solver_iterations"] for it in a["iterations"]] == \
+        [it["linear_solver_iterations"] for it in b["iterations"]]
+    np.testing.assert_allclose([it["cost"] for it in a["iterations"]], [it["cost"] for it in b["iterations"]],
+                               rtol=1e-10)
+
+
 @pytest.mark.parametrize("kind", ["bal", "c2"])
 def test_split_fused_schedule_matches_single_launch(pkg, gpu, kind, monkeypatch):
     """The multi-rank schedule runs the fused kernel as a camera-side launch, then a
