@@ -1479,28 +1479,29 @@ __device__ __forceinline__ void frame_rows_acc(const double2 xy, const double (&
   for (int r = 0; r < 3; ++r) Z[r] = f.small ? X[r] : Y[r];
   Proj pr;
   project(P, f.K, xy.x, xy.y, pr, true);
-  double ja[6], jb[6];
-  ja[0] = Z[1] * pr.A0[2] - Z[2] * pr.A0[1];
-  ja[1] = Z[2] * pr.A0[0] - Z[0] * pr.A0[2];
-  ja[2] = Z[0] * pr.A0[1] - Z[1] * pr.A0[0];
-  jb[0] = Z[1] * pr.A1[2] - Z[2] * pr.A1[1];
-  jb[1] = Z[2] * pr.A1[0] - Z[0] * pr.A1[2];
-  jb[2] = Z[0] * pr.A1[1] - Z[1] * pr.A1[0];
+  // one row at a time (the row's 6 values are all that is live beside the sums); the
+  // per-element order is the two-row fma(b, b, fma(a, a, acc)) of obs_rows' callers
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    ja[3 + i] = pr.A0[i];
-    jb[3 + i] = pr.A1[i];
+  for (int row = 0; row < 2; ++row) {
+    const double* A = row == 0 ? pr.A0 : pr.A1;
+    const double r = row == 0 ? pr.ru : pr.rv;
+    double j[6];
+    j[0] = Z[1] * A[2] - Z[2] * A[1];
+    j[1] = Z[2] * A[0] - Z[0] * A[2];
+    j[2] = Z[0] * A[1] - Z[1] * A[0];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) j[3 + i] = A[i];
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int bb = a; bb < 6; ++bb) {
+        acc[k] = fma(j[a], j[bb], acc[k]);
+        ++k;
+      }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[21 + a] = fma(j[a], r, acc[21 + a]);
   }
-  int k = 0;
-#pragma unroll
-  for (int a = 0; a < 6; ++a)
-#pragma unroll
-    for (int bb = a; bb < 6; ++bb) {
-      acc[k] = fma(jb[a], jb[bb], fma(ja[a], ja[bb], acc[k]));
-      ++k;
-    }
-#pragma unroll
-  for (int a = 0; a < 6; ++a) acc[21 + a] = fma(jb[a], pr.rv, fma(ja[a], pr.ru, acc[21 + a]));
 }
 
 // eval_cams_uni_pipe's three-slot pipeline over the frame accumulation; jl (LDS, 9
@@ -2001,6 +2002,7 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
     k_eval_fused<2, 5><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
   else if (abl == 25)
     k_eval_fused<2, 25><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+
   else if (abl == 1) k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
   else if (abl == 2) k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
   else if (abl == 3) k_eval_fused<2, 3><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
