@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cstdlib>
+#include <type_traits>
 
 #include "dab_kernels.h"
 #include "dab_wave.h"
@@ -2618,6 +2619,268 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_points(DevView v, const doub
   }
 }
 
+// The same products in the rotated frame. With J_l = Rd Jd (the left Jacobian; Rd = R, or
+// I for the small-angle tables) and Z = Rd Y (= P - t, or Y itself for the small-angle
+// tables), Rd (Y x (Jd dw)) = Z x (J_l dw) and Jd^T (Y x (Rd^T g)) = J_l^T (Z x g), so
+//   J_c0 d = A (dt_a - Z_a x w~_a)      w~ = J_l dw: one 3-vector per camera and product
+//   J_c0^T z = [J_l^T (Z_a x g); g]     J_l^T applied once per camera to the summed [Z x g]
+// (ring slot: Z_r = Q - t_r or X, and R_a as before). Per observation and sweep the rows
+// need only R, t (and K) from LDS: the 18 Rd | Jd doubles per slot of k_mf_points, the
+// s_c reads and the 3 x 3 products with them drop out. LDS: rt [E][12] | small-angle
+// flags [E] | w~, dt per camera [NC][6] | J_l per camera [NC][9] | per-wave sums [4][NC][6].
+static size_t mf2_lds_bytes(int E, int NI, int NC, bool product) {
+  return sizeof(double) * (12 * (size_t)E + 6 * (size_t)NI + 6 * (size_t)NC + 9 * (size_t)NC +
+                           (product ? (kMfBlock / 64) * 6 * (size_t)NC : 0)) +
+         sizeof(int) * (size_t)E;
+}
+template <int MODE>
+__global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const double* __restrict__ points,
+                                                       const double* __restrict__ camtab,
+                                                       const double* __restrict__ scc,
+                                                       const double* __restrict__ PU,
+                                                       const double* __restrict__ vec,
+                                                       const double* __restrict__ q, double* __restrict__ out,
+                                                       const PcgState* st) {
+  extern __shared__ double mf_lds[];
+  if (MODE == 0 && st->status != kPcgRunning) return;
+  const int NC6 = 6 * v.NC;
+  double* rt_s = mf_lds;                               // [E][12]
+  double* k_s = rt_s + 12 * (size_t)v.E;               // [NI][6]
+  double* dv_s = k_s + 6 * (size_t)v.NI;               // [NC][6]: w~ | dt (MODE 0, 1)
+  double* jl_s = dv_s + NC6;                           // [NC][9]: J_l (MODE 0, 2)
+  double* accs = jl_s + 9 * (size_t)v.NC;              // [waves][NC][6] (MODE 0, 2)
+  int* sm_s = reinterpret_cast<int*>(accs + (MODE != 1 ? (kMfBlock / 64) * NC6 : 0));  // [E]
+  for (int i = threadIdx.x; i < 12 * v.E; i += blockDim.x) rt_s[i] = camtab[(size_t)kCamTab * (i / 12) + i % 12];
+  for (int i = threadIdx.x; i < 6 * v.NI; i += blockDim.x) k_s[i] = v.intr[(size_t)kIntr * (i / 6) + i % 6];
+  for (int e = threadIdx.x; e < v.E; e += blockDim.x) {
+    const double* T = camtab + (size_t)kCamTab * e;  // R t Rd Jd
+    sm_s[e] = (T[12] == 1.0 && T[13] == 0.0 && T[14] == 0.0 && T[15] == 0.0 && T[16] == 1.0 && T[17] == 0.0 &&
+               T[18] == 0.0 && T[19] == 0.0 && T[20] == 1.0)
+                  ? 1
+                  : 0;  // Rd = I: the small-angle tables
+    const int c = v.ext_col[e];
+    if (c < 0) continue;
+    double J[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc)
+        J[3 * r + cc] = T[12 + 3 * r] * T[21 + cc] + T[12 + 3 * r + 1] * T[24 + cc] + T[12 + 3 * r + 2] * T[27 + cc];
+    if constexpr (MODE != 2) {
+      double d[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) d[k] = scc[6 * c + k] * vec[6 * c + k];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) dv_s[6 * c + r] = J[3 * r] * d[0] + J[3 * r + 1] * d[1] + J[3 * r + 2] * d[2];
+#pragma unroll
+      for (int k = 3; k < 6; ++k) dv_s[6 * c + k] = d[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) jl_s[9 * c + k] = J[k];
+  }
+  if constexpr (MODE != 1)
+    for (int i = threadIdx.x; i < (kMfBlock / 64) * NC6; i += blockDim.x) accs[i] = 0.0;
+  __syncthreads();
+  const SmallTabs tabs{nullptr, k_s};
+  auto rt = [&](int e, double (&o)[12]) {
+    const double2* pp = reinterpret_cast<const double2*>(rt_s + 12 * e);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const double2 u = pp[k];
+      o[2 * k] = u.x;
+      o[2 * k + 1] = u.y;
+    }
+  };
+  double* acc = accs + (threadIdx.x >> 6) * NC6;
+  const size_t NPs = (size_t)v.NP;
+  auto rot9 = [&](int e, double (&o)[9]) {
+    const double2* pp = reinterpret_cast<const double2*>(rt_s + 12 * e);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double2 u = pp[k];
+      o[2 * k] = u.x;
+      o[2 * k + 1] = u.y;
+    }
+    o[8] = rt_s[12 * e + 8];
+  };
+  // one observation's geometry: A (2 x 3), R_a, and the rotated-frame points Z of both
+  // slots; with RB, vout = R_b vin (vin for single-extrinsic observations) while the ring
+  // table is in registers, so that R_b never outlives its read
+  auto geo = [&](auto rb_tag, const int4 id, const double2 xy, const double (&X)[3], double (&A0)[3],
+                 double (&A1)[3], double (&Ra)[9], double (&Z0)[3], double (&Z1)[3], bool& comp,
+                 const double (&vin)[3], double (&vout)[3]) {
+    constexpr bool RB = decltype(rb_tag)::value;
+    double Ta[12];
+    rt(id.y, Ta);
+    double Kr[6];
+    tabs.k(id.w, Kr);
+    comp = id.z >= 0;
+    double Q[3];
+    if constexpr (RB) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) vout[k] = vin[k];
+    }
+    if (comp) {
+      double Tb[12];
+      rt(id.z, Tb);
+      matvec_add(Tb, X, Tb + 9, Q);
+      if constexpr (RB) mv3(Tb, vin, vout);
+      const bool sb = sm_s[id.z] != 0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) Z1[k] = sb ? X[k] : Q[k] - Tb[9 + k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) Q[k] = X[k];
+    }
+    double P[3];
+    matvec_add(Ta, Q, Ta + 9, P);
+    const bool sa = sm_s[id.y] != 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) Z0[k] = sa ? Q[k] : P[k] - Ta[9 + k];
+    Proj pr;
+    project(P, Kr, xy.x, xy.y, pr, true);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      A0[k] = pr.A0[k];
+      A1[k] = pr.A1[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Ra[k] = Ta[k];
+  };
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < v.NP; p += gridDim.x * blockDim.x) {
+    const int sl = p >> 6, lane = p & 63;
+    const int off = v.slice_off[sl], len = (v.slice_off[sl + 1] - off) >> 6;
+    const double X[3] = {points[3 * (size_t)p], points[3 * (size_t)p + 1], points[3 * (size_t)p + 2]};
+    double pu[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) pu[k] = PU[6 * (size_t)p + k];
+    double up[3];
+    if constexpr (MODE == 2) {
+      const double q0 = q[4 * (size_t)p], q1 = q[4 * (size_t)p + 1], q2 = q[4 * (size_t)p + 2];
+      up[0] = pu[0] * q0 + pu[1] * q1 + pu[2] * q2;
+      up[1] = pu[3] * q1 + pu[4] * q2;
+      up[2] = pu[5] * q2;
+    } else {
+      // sweep 1: a = sum_e J_p^T (J_c (s_c o v_c))
+      double a[3] = {0.0, 0.0, 0.0};
+      for (int k = 0; k < len; ++k) {
+        const int s = off + 64 * k + lane;
+        const int4 id = v.obs_idx[s];
+        if (id.x < 0) continue;
+        const int c0 = v.ext_col[id.y], c1 = id.z >= 0 ? v.ext_col[id.z] : -1;
+        if (c0 < 0 && c1 < 0) continue;
+        double A0[3], A1[3], Ra[9], Z0[3], Z1[3], unused[3];
+        bool comp;
+        geo(std::false_type{}, id, v.obs_xy[s], X, A0, A1, Ra, Z0, Z1, comp, unused, unused);
+        double dP[3] = {0.0, 0.0, 0.0};
+        if (c0 >= 0) {
+          const double* d = dv_s + 6 * c0;
+          const double w[3] = {d[0], d[1], d[2]};
+          double cz[3];
+          cross3(Z0, w, cz);
+#pragma unroll
+          for (int k2 = 0; k2 < 3; ++k2) dP[k2] = d[3 + k2] - cz[k2];
+        }
+        if (c1 >= 0) {
+          const double* d = dv_s + 6 * c1;
+          const double w[3] = {d[0], d[1], d[2]};
+          double cz[3], r[3], r2[3];
+          cross3(Z1, w, cz);
+#pragma unroll
+          for (int k2 = 0; k2 < 3; ++k2) r[k2] = d[3 + k2] - cz[k2];
+          mv3(Ra, r, r2);
+#pragma unroll
+          for (int k2 = 0; k2 < 3; ++k2) dP[k2] += r2[k2];
+        }
+        const double u0 = A0[0] * dP[0] + A0[1] * dP[1] + A0[2] * dP[2];
+        const double u1 = A1[0] * dP[0] + A1[1] * dP[1] + A1[2] * dP[2];
+        const double au[3] = {u0 * A0[0] + u1 * A1[0], u0 * A0[1] + u1 * A1[1], u0 * A0[2] + u1 * A1[2]};
+        double h[3];
+        mtv3(Ra, au, h);
+        if (comp) {
+          double Rb[9], h2[3];
+          rot9(id.z, Rb);  // re-read: fewer live registers than carrying it from geo
+          mtv3(Rb, h, h2);
+#pragma unroll
+          for (int k2 = 0; k2 < 3; ++k2) h[k2] = h2[k2];
+        }
+        a[0] += h[0];
+        a[1] += h[1];
+        a[2] += h[2];
+      }
+      const double t0 = pu[0] * a[0], t1 = pu[1] * a[0] + pu[3] * a[1];
+      const double t2 = pu[2] * a[0] + pu[4] * a[1] + pu[5] * a[2];
+      if constexpr (MODE == 1) {
+        const double r0 = q[4 * (size_t)p] - t0, r1 = q[4 * (size_t)p + 1] - t1, r2 = q[4 * (size_t)p + 2] - t2;
+        out[p] = -(pu[0] * r0 + pu[1] * r1 + pu[2] * r2);
+        out[NPs + p] = -(pu[3] * r1 + pu[4] * r2);
+        out[2 * NPs + p] = -(pu[5] * r2);
+        continue;
+      }
+      up[0] = pu[0] * t0 + pu[1] * t1 + pu[2] * t2;
+      up[1] = pu[3] * t1 + pu[4] * t2;
+      up[2] = pu[5] * t2;
+    }
+    if constexpr (MODE != 1) {
+      // sweep 2: per camera, sum [Z x g | g] (J_l^T and -s_c applied after the sums)
+      for (int k = 0; k < len; ++k) {
+        const int s = off + 64 * k + lane;
+        const int4 id = v.obs_idx[s];
+        if (id.x < 0) continue;
+        const int c0 = v.ext_col[id.y], c1 = id.z >= 0 ? v.ext_col[id.z] : -1;
+        if (c0 < 0 && c1 < 0) continue;
+        double A0[3], A1[3], Ra[9], Z0[3], Z1[3], kk[3];
+        bool comp;
+        geo(std::true_type{}, id, v.obs_xy[s], X, A0, A1, Ra, Z0, Z1, comp, up, kk);
+        double m[3];
+        mv3(Ra, kk, m);
+        const double z0 = A0[0] * m[0] + A0[1] * m[1] + A0[2] * m[2];
+        const double z1 = A1[0] * m[0] + A1[1] * m[1] + A1[2] * m[2];
+        const double gz[3] = {z0 * A0[0] + z1 * A1[0], z0 * A0[1] + z1 * A1[1], z0 * A0[2] + z1 * A1[2]};
+        if (c0 >= 0) {
+          double cz[3];
+          cross3(Z0, gz, cz);
+#pragma unroll
+          for (int a = 0; a < 3; ++a) atomicAdd(acc + 6 * c0 + a, cz[a]);
+#pragma unroll
+          for (int a = 0; a < 3; ++a) atomicAdd(acc + 6 * c0 + 3 + a, gz[a]);
+        }
+        if (c1 >= 0) {
+          double hz[3], cz[3];
+          mtv3(Ra, gz, hz);
+          cross3(Z1, hz, cz);
+#pragma unroll
+          for (int a = 0; a < 3; ++a) atomicAdd(acc + 6 * c1 + a, cz[a]);
+#pragma unroll
+          for (int a = 0; a < 3; ++a) atomicAdd(acc + 6 * c1 + 3 + a, hz[a]);
+        }
+      }
+    }
+  }
+  if constexpr (MODE != 1) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < NC6; i += blockDim.x) {
+      const int c = i / 6, k = i - 6 * c;
+      double x;
+      if (k < 3) {  // J_l^T of the summed rotation parts
+        x = 0.0;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          double t = accs[6 * c + r];
+#pragma unroll
+          for (int w = 1; w < kMfBlock / 64; ++w) t += accs[w * NC6 + 6 * c + r];
+          x += jl_s[9 * c + 3 * r + k] * t;
+        }
+      } else {
+        x = accs[i];
+#pragma unroll
+        for (int w = 1; w < kMfBlock / 64; ++w) x += accs[w * NC6 + i];
+      }
+      out[(size_t)blockIdx.x * NC6 + i] = -scc[i] * x;
+    }
+  }
+}
+
 // Per chunk of camera-major positions, Y re-evaluated: 21 upper of sum Z Z^T over
 // same-point runs (Z = sum of the run's Y_e; the diagonal block of the Schur term) | 6 of
 // -sum Y_e q_p -> partial[chunk][27]. Replaces k_entry_y + k_pcg_diag_rhs_partial.
@@ -2684,18 +2947,32 @@ __global__ __launch_bounds__(256) void k_mf_diag_rhs(DevView v, int nchunk, cons
 }
 
 int mf_grid(int NP, int ncu) { return std::max(1, std::min((NP + kMfBlock - 1) / kMfBlock, 4 * ncu)); }
+static bool mf_rd_jd_form() {  // DAB_MF_RDJD=1: the Rd | Jd form (k_mf_points), for A/B timing
+  static const bool f = getenv("DAB_MF_RDJD") && atoi(getenv("DAB_MF_RDJD")) != 0;
+  return f;
+}
 void launch_mf_product(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                        const double* scale_c, const double* PU, const double* vec, double* partial, double* w,
                        int grid, const PcgState* st) {
-  const size_t lds = sizeof(double) * mf_lds_doubles(v.E, v.NI, v.NC, true);
-  k_mf_points<0><<<grid, kMfBlock, lds, s>>>(v, points, camtab, scale_c, PU, vec, nullptr, partial, st);
+  if (mf_rd_jd_form()) {
+    const size_t lds = sizeof(double) * mf_lds_doubles(v.E, v.NI, v.NC, true);
+    k_mf_points<0><<<grid, kMfBlock, lds, s>>>(v, points, camtab, scale_c, PU, vec, nullptr, partial, st);
+  } else {
+    k_mf_frame<0><<<grid, kMfBlock, mf2_lds_bytes(v.E, v.NI, v.NC, true), s>>>(v, points, camtab, scale_c, PU, vec,
+                                                                              nullptr, partial, st);
+  }
   launch_pcg_fused_final(s, grid, 6 * v.NC, partial, w, st);
 }
 void launch_mf_backsub(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                        const double* scale_c, const double* PU, const double* q, const double* yc, double* dp,
                        int grid) {
-  const size_t lds = sizeof(double) * mf_lds_doubles(v.E, v.NI, v.NC, false);
-  k_mf_points<1><<<grid, kMfBlock, lds, s>>>(v, points, camtab, scale_c, PU, yc, q, dp, nullptr);
+  if (mf_rd_jd_form()) {
+    const size_t lds = sizeof(double) * mf_lds_doubles(v.E, v.NI, v.NC, false);
+    k_mf_points<1><<<grid, kMfBlock, lds, s>>>(v, points, camtab, scale_c, PU, yc, q, dp, nullptr);
+  } else {
+    k_mf_frame<1><<<grid, kMfBlock, mf2_lds_bytes(v.E, v.NI, v.NC, false), s>>>(v, points, camtab, scale_c, PU, yc,
+                                                                               q, dp, nullptr);
+  }
 }
 void launch_mf_diag_rhs(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int* run,
                         const double* points, const double* camtab, const double* scale_c, const double* PU,
