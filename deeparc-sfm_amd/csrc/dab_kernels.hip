@@ -1639,6 +1639,17 @@ __device__ __forceinline__ void pipe_entries(const int4* __restrict__ idx, const
   }
 }
 
+// J_l (row-major) and the small-angle flag of extrinsic e from the global tables
+__device__ __forceinline__ void ext_frame(const double* __restrict__ camtab, int e, double* jl, int k, bool& small) {
+  const double* T = camtab + (size_t)kCamTab * e;
+  small = T[12] == 1.0 && T[13] == 0.0 && T[14] == 0.0 && T[15] == 0.0 && T[16] == 1.0 && T[17] == 0.0 &&
+          T[18] == 0.0 && T[19] == 0.0 && T[20] == 1.0;
+  if (k < 9) {
+    const int r = k / 3, c = k - 3 * r;
+    jl[k] = T[12 + 3 * r] * T[21 + c] + T[12 + 3 * r + 1] * T[24 + c] + T[12 + 3 * r + 2] * T[27 + c];
+  }
+}
+
 // UNI: the chunks of `list` are uniform (chunk_uni), tables read once per block
 template <bool UNI>
 __global__ __launch_bounds__(256) void k_eval_cams(DevView v, const int* __restrict__ chunk_beg,
@@ -2042,14 +2053,93 @@ __global__ __launch_bounds__(256) void k_eval_cross(DevView v, const int* __rest
 #pragma unroll
       for (int bb = 0; bb < 6; ++bb) acc[6 * a + bb] += ja[a] * da[bb] + jb[a] * db[bb];
   };
-  if (small)
-    pipe_entries(x_idx, x_xy, b + threadIdx.x, e, blockDim.x, points,
-                 [&](const int4 id, const double2 xy, const double (&X)[3]) { body(id, xy, X, st); });
-  else
+  if (small && b < e) {
+    // rotated frame: rows [Z_a x A_k | A_k] and [Z_r x A_k R_a | A_k R_a] of the chunk's
+    // (arc, ring) pair, the sums taken to B_a^T M B_r afterwards (only R, t, K per entry)
+    __shared__ double jl[2][9];
+    __shared__ double wsx[kRedBlock / 64][36];
+    const int4 id0 = x_idx[b];
+    bool sa, sr;
+    ext_frame(camtab, id0.y, jl[0], threadIdx.x, sa);
+    ext_frame(camtab, id0.z, jl[1], threadIdx.x, sr);
     pipe_entries(x_idx, x_xy, b + threadIdx.x, e, blockDim.x, points,
                  [&](const int4 id, const double2 xy, const double (&X)[3]) {
-                   body(id, xy, X, GlobalTabs{camtab, v.intr});
+                   double Ta[12], Tb[12], Kr[6];
+                   st.rt(id.y, Ta);
+                   st.rt(id.z, Tb);
+                   st.k(id.w, Kr);
+                   double Q[3], P[3], Z0[3], Z1[3];
+                   matvec_add(Tb, X, Tb + 9, Q);
+                   matvec_add(Ta, Q, Ta + 9, P);
+#pragma unroll
+                   for (int k = 0; k < 3; ++k) {
+                     Z0[k] = sa ? Q[k] : P[k] - Ta[9 + k];
+                     Z1[k] = sr ? X[k] : Q[k] - Tb[9 + k];
+                   }
+                   Proj pr;
+                   project(P, Kr, xy.x, xy.y, pr, true);
+#pragma unroll
+                   for (int row = 0; row < 2; ++row) {
+                     const double* A = row == 0 ? pr.A0 : pr.A1;
+                     double at[3], w0[6], w1[6];
+                     rowmat(A, Ta, at);
+                     w0[0] = Z0[1] * A[2] - Z0[2] * A[1];
+                     w0[1] = Z0[2] * A[0] - Z0[0] * A[2];
+                     w0[2] = Z0[0] * A[1] - Z0[1] * A[0];
+                     w1[0] = Z1[1] * at[2] - Z1[2] * at[1];
+                     w1[1] = Z1[2] * at[0] - Z1[0] * at[2];
+                     w1[2] = Z1[0] * at[1] - Z1[1] * at[0];
+#pragma unroll
+                     for (int k = 0; k < 3; ++k) {
+                       w0[3 + k] = A[k];
+                       w1[3 + k] = at[k];
+                     }
+#pragma unroll
+                     for (int a = 0; a < 6; ++a)
+#pragma unroll
+                       for (int bb = 0; bb < 6; ++bb) acc[6 * a + bb] = fma(w0[a], w1[bb], acc[6 * a + bb]);
+                   }
                  });
+    {
+      double h0[18], h1[18];
+#pragma unroll
+      for (int k = 0; k < 18; ++k) {
+        h0[k] = acc[k];
+        h1[k] = acc[18 + k];
+      }
+      wave_sums_transposed<18>(h0, wsx[threadIdx.x >> 6]);
+      wave_sums_transposed<18>(h1, wsx[threadIdx.x >> 6] + 18);
+    }
+    __syncthreads();
+    if (threadIdx.x < 36) {
+      double t = wsx[0][threadIdx.x];
+#pragma unroll
+      for (int w = 1; w < kRedBlock / 64; ++w) t += wsx[w][threadIdx.x];
+      wsx[0][threadIdx.x] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < 36) {  // (B_a^T M B_r)_ij, B = blockdiag(J_l, I)
+      const int i = threadIdx.x / 6, j = threadIdx.x - 6 * (threadIdx.x / 6);
+      const double* M = wsx[0];
+      double x = 0.0;
+      if (i < 3 && j < 3) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+          for (int q = 0; q < 3; ++q) x += jl[0][3 * p + i] * M[6 * p + q] * jl[1][3 * q + j];
+      } else if (i < 3) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p) x += jl[0][3 * p + i] * M[6 * p + j];
+      } else if (j < 3) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) x += M[6 * i + q] * jl[1][3 * q + j];
+      } else {
+        x = M[6 * i + j];
+      }
+      partial[36 * (size_t)c + threadIdx.x] = x;
+    }
+    return;
+  }
   block_reduce_store<36>(acc, partial + 36 * (size_t)c);
 }
 
