@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-lm", action="store_true")
     ap.add_argument("--no-rig", action="store_true", help="skip the config-5 rig LM measurement")
+    ap.add_argument("--no-c2", action="store_true", help="skip the config-2 evaluation pass (PMC passes: "
+                    "its launches share the kernel name)")
     ap.add_argument("--rig-config", default="c5_rig_16x64")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return ap.parse_args()
@@ -217,7 +219,7 @@ def main():
     # The headline stays C3, the 1M-observation problem the LM target is quoted on; at
     # 100k observations one pass is a few microseconds and launch cadence dominates.
     c2 = {}
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not args.no_c2:
         c2prob = pkg.synth(**pkg.CONFIGS["c2_100cam"])
         c2s = pkg.Solver(device)
         c2s.set_problem(c2prob)
