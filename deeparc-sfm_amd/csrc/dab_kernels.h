@@ -105,6 +105,18 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
 //  arc∘ring cross blocks Jc0^T Jc1 over composed observations (pair-major copy) -> partial[chunk][36]
 void launch_eval_cross(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
                        const double2* x_xy, const double* points, const double* camtab, double* partial);
+// The rig's composed observations with both cameras free, one pair-major pass: per chunk
+// the cross block -> xpart[chunk][36] and both cameras' [U | g] -> cpart[chunk][54]
+// (arc 27 | ring 27); k_cam_final adds those halves to the camera-major partials of the
+// other entries (launch_eval_cams_gen over their own chunks).
+bool pair_eval_fits(int E, int NI);  // the tables fit LDS (small_tabs_fit)
+void launch_eval_pair(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
+                      const double2* x_xy, const double* points, const double* camtab, double* xpart,
+                      double* cpart);
+void launch_cam_final(hipStream_t s, int NC, const int* seg_chunk, const double* partial, const int* xcam_ptr,
+                      const int* xcam_list, const double* cpart, double* ug);
+void launch_eval_cams_gen(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const double* points,
+                          const double* ext, const double* camtab, double* partial);
 //  final: seg_out[seg][K] = sum of partial chunks [seg_chunk[seg], seg_chunk[seg+1])
 //  (max_chunks = the largest number of chunks of one segment: > 8 uses a block per segment)
 void launch_seg_final(hipStream_t s, int nseg, int K, const int* seg_chunk, const double* partial,

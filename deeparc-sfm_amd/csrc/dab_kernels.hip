@@ -2140,7 +2140,202 @@ __global__ __launch_bounds__(256) void k_eval_cross(DevView v, const int* __rest
     }
     return;
   }
+  if (small)
+    pipe_entries(x_idx, x_xy, b + threadIdx.x, e, blockDim.x, points,
+                 [&](const int4 id, const double2 xy, const double (&X)[3]) { body(id, xy, X, st); });
+  else
+    pipe_entries(x_idx, x_xy, b + threadIdx.x, e, blockDim.x, points,
+                 [&](const int4 id, const double2 xy, const double (&X)[3]) {
+                   body(id, xy, X, GlobalTabs{camtab, v.intr});
+                 });
   block_reduce_store<36>(acc, partial + 36 * (size_t)c);
+}
+
+// The rig's composed observations in ONE pair-major pass (both cameras free): per chunk of
+// one (arc, ring) pair, the arc's and the ring's camera blocks (27 each) and the cross
+// block (36) from a single projection per observation, in the rotated frame (rows
+// [Z_a x A_k | A_k], [Z_r x A_k R_a | A_k R_a]; each camera's J_l applied after the
+// sums). It replaces, for these observations, both camera-major entries and the separate
+// cross pass: one 56-B input per observation instead of three. k_cam_final adds the
+// camera halves to the camera-major partials of the remaining entries.
+__global__ __launch_bounds__(256) void k_eval_pair(DevView v, const int* __restrict__ chunk_beg,
+                                                   const int4* __restrict__ x_idx,
+                                                   const double2* __restrict__ x_xy,
+                                                   const double* __restrict__ points,
+                                                   const double* __restrict__ camtab, double* __restrict__ xpart,
+                                                   double* __restrict__ cpart) {
+  const int c = blockIdx.x;
+  const int b = chunk_beg[c], e = chunk_beg[c + 1];
+  extern __shared__ double tabs_lds[];
+  const SmallTabs st = stage_small_tabs(tabs_lds, v.E, v.NI, camtab, v.intr);  // barrier inside
+  __shared__ double jl[2][9];
+  __shared__ double ws[kRedBlock / 64][90];
+  if (b >= e) {
+    if (threadIdx.x < 36) xpart[36 * (size_t)c + threadIdx.x] = 0.0;
+    if (threadIdx.x < 54) cpart[54 * (size_t)c + threadIdx.x] = 0.0;
+    return;
+  }
+  const int4 id0 = x_idx[b];
+  bool sa, sr;
+  ext_frame(camtab, id0.y, jl[0], threadIdx.x, sa);
+  ext_frame(camtab, id0.z, jl[1], threadIdx.x, sr);
+  // [0, 27) arc U | g, [27, 54) ring U | g, [54, 90) cross (arc row-major)
+  double acc[90];
+#pragma unroll
+  for (int i = 0; i < 90; ++i) acc[i] = 0.0;
+  pipe_entries(x_idx, x_xy, b + threadIdx.x, e, blockDim.x, points,
+               [&](const int4 id, const double2 xy, const double (&X)[3]) {
+                 double Ta[12], Tb[12], Kr[6];
+                 st.rt(id.y, Ta);
+                 st.rt(id.z, Tb);
+                 st.k(id.w, Kr);
+                 double Q[3], P[3], Z0[3], Z1[3];
+                 matvec_add(Tb, X, Tb + 9, Q);
+                 matvec_add(Ta, Q, Ta + 9, P);
+#pragma unroll
+                 for (int k = 0; k < 3; ++k) {
+                   Z0[k] = sa ? Q[k] : P[k] - Ta[9 + k];
+                   Z1[k] = sr ? X[k] : Q[k] - Tb[9 + k];
+                 }
+                 Proj pr;
+                 project(P, Kr, xy.x, xy.y, pr, true);
+#pragma unroll
+                 for (int row = 0; row < 2; ++row) {
+                   const double* A = row == 0 ? pr.A0 : pr.A1;
+                   const double r = row == 0 ? pr.ru : pr.rv;
+                   double at[3], w0[6], w1[6];
+                   rowmat(A, Ta, at);
+                   w0[0] = Z0[1] * A[2] - Z0[2] * A[1];
+                   w0[1] = Z0[2] * A[0] - Z0[0] * A[2];
+                   w0[2] = Z0[0] * A[1] - Z0[1] * A[0];
+                   w1[0] = Z1[1] * at[2] - Z1[2] * at[1];
+                   w1[1] = Z1[2] * at[0] - Z1[0] * at[2];
+                   w1[2] = Z1[0] * at[1] - Z1[1] * at[0];
+#pragma unroll
+                   for (int k = 0; k < 3; ++k) {
+                     w0[3 + k] = A[k];
+                     w1[3 + k] = at[k];
+                   }
+                   int k = 0;
+#pragma unroll
+                   for (int a = 0; a < 6; ++a)
+#pragma unroll
+                     for (int bb = a; bb < 6; ++bb) {
+                       acc[k] = fma(w0[a], w0[bb], acc[k]);
+                       acc[27 + k] = fma(w1[a], w1[bb], acc[27 + k]);
+                       ++k;
+                     }
+#pragma unroll
+                   for (int a = 0; a < 6; ++a) {
+                     acc[21 + a] = fma(w0[a], r, acc[21 + a]);
+                     acc[48 + a] = fma(w1[a], r, acc[48 + a]);
+                   }
+#pragma unroll
+                   for (int a = 0; a < 6; ++a)
+#pragma unroll
+                     for (int bb = 0; bb < 6; ++bb) acc[54 + 6 * a + bb] = fma(w0[a], w1[bb], acc[54 + 6 * a + bb]);
+                 }
+               });
+  {
+    double h0[30], h1[30], h2[30];
+#pragma unroll
+    for (int k = 0; k < 30; ++k) {
+      h0[k] = acc[k];
+      h1[k] = acc[30 + k];
+      h2[k] = acc[60 + k];
+    }
+    wave_sums_transposed<30>(h0, ws[threadIdx.x >> 6]);
+    wave_sums_transposed<30>(h1, ws[threadIdx.x >> 6] + 30);
+    wave_sums_transposed<30>(h2, ws[threadIdx.x >> 6] + 60);
+  }
+  __syncthreads();
+  if (threadIdx.x < 90) {
+    double t = ws[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < kRedBlock / 64; ++w) t += ws[w][threadIdx.x];
+    ws[0][threadIdx.x] = t;  // each thread rewrites only what it read
+  }
+  __syncthreads();
+  const double* M = ws[0];
+  if (threadIdx.x < 27) {
+    cpart[54 * (size_t)c + threadIdx.x] = cam_frame_entry(M, jl[0], threadIdx.x);
+  } else if (threadIdx.x < 54) {
+    cpart[54 * (size_t)c + threadIdx.x] = cam_frame_entry(M + 27, jl[1], threadIdx.x - 27);
+  } else if (threadIdx.x < 90) {  // (B_a^T X B_r)_ij, B = blockdiag(J_l, I)
+    const int q = threadIdx.x - 54, i = q / 6, j = q - 6 * (q / 6);
+    const double* X = M + 54;
+    double x = 0.0;
+    if (i < 3 && j < 3) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) x += jl[0][3 * p + i] * X[6 * p + r] * jl[1][3 * r + j];
+    } else if (i < 3) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) x += jl[0][3 * p + i] * X[6 * p + j];
+    } else if (j < 3) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) x += X[6 * i + r] * jl[1][3 * r + j];
+    } else {
+      x = X[6 * i + j];
+    }
+    xpart[36 * (size_t)c + q] = x;
+  }
+}
+
+bool pair_eval_fits(int E, int NI) { return small_tabs_fit(E, NI); }
+void launch_eval_pair(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
+                      const double2* x_xy, const double* points, const double* camtab, double* xpart,
+                      double* cpart) {
+  if (nchunk <= 0) return;
+  // 90 sums per lane: ~300 VGPRs, one wave per SIMD (a 256-VGPR cap spills hundreds)
+  k_eval_pair<<<nchunk, 256, small_tabs_bytes(v.E, v.NI), s>>>(v, chunk_beg, x_idx, x_xy, points, camtab, xpart,
+                                                               cpart);
+}
+
+// ug[c] = its camera-major chunk partials (seg_chunk) + its halves of the pair chunks
+// (xcam_list codes 2 q + half, increasing q): one block per camera, 9 stripes of 27
+// threads over the terms, the stripes summed in order (fixed order, as k_seg_final_block)
+__global__ __launch_bounds__(256) void k_cam_final(const int* __restrict__ seg_chunk,
+                                                   const double* __restrict__ partial,
+                                                   const int* __restrict__ xcam_ptr,
+                                                   const int* __restrict__ xcam_list,
+                                                   const double* __restrict__ cpart, double* __restrict__ ug) {
+  constexpr int kS = 256 / 27;
+  __shared__ double sh[kS * 27];
+  const int c = blockIdx.x, k = threadIdx.x % 27, stripe = threadIdx.x / 27;
+  if (stripe < kS) {
+    double t = 0.0;
+    const int n1 = seg_chunk[c + 1] - seg_chunk[c], n2 = xcam_ptr[c + 1] - xcam_ptr[c];
+    for (int j = stripe; j < n1 + n2; j += kS) {
+      if (j < n1) {
+        t += partial[27 * (size_t)(seg_chunk[c] + j) + k];
+      } else {
+        const int code = xcam_list[xcam_ptr[c] + j - n1];
+        t += cpart[54 * (size_t)(code >> 1) + 27 * (code & 1) + k];
+      }
+    }
+    sh[stripe * 27 + k] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < 27) {
+    double t = sh[threadIdx.x];
+#pragma unroll
+    for (int q = 1; q < kS; ++q) t += sh[q * 27 + threadIdx.x];
+    ug[27 * (size_t)c + threadIdx.x] = t;
+  }
+}
+void launch_cam_final(hipStream_t s, int NC, const int* seg_chunk, const double* partial, const int* xcam_ptr,
+                      const int* xcam_list, const double* cpart, double* ug) {
+  if (NC <= 0) return;
+  k_cam_final<<<NC, 256, 0, s>>>(seg_chunk, partial, xcam_ptr, xcam_list, cpart, ug);
+}
+// the general camera-major kernel over an arbitrary chunk set (no uniform-chunk lists)
+void launch_eval_cams_gen(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const double* points,
+                          const double* ext, const double* camtab, double* partial) {
+  if (nchunk <= 0) return;
+  const size_t lds = small_tabs_fit(v.E, v.NI) ? small_tabs_bytes(v.E, v.NI) : 0;
+  k_eval_cams<false><<<nchunk, 256, lds, s>>>(v, chunk_beg, nullptr, points, ext, camtab, partial);
 }
 
 void launch_eval_cross(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,

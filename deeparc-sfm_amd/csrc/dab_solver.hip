@@ -171,6 +171,14 @@ struct dab_handle {
   double* d_camred = nullptr;  // [Ucc NC*21 | gc NC*6 | Ux ncross*36] (all-reduced)
   double* d_partial = nullptr; // chunk partials (max of chunk counts * 36)
   double* d_xpartial = nullptr; // cross-block chunk partials
+  // pair-major evaluation of the composed observations (launch_eval_pair): the other
+  // entries' camera-major copy and chunks, and per camera its pair-chunk halves
+  bool pair_eval = false;
+  int nchunk2 = 0;
+  int4* d_cm2_idx = nullptr;
+  double2* d_cm2_xy = nullptr;
+  int *d_chunk2_beg = nullptr, *d_seg2_chunk = nullptr, *d_xcam_ptr = nullptr, *d_xcam_list = nullptr;
+  double *d_partial2 = nullptr, *d_xcpart = nullptr;
   double* d_spack = nullptr;   // [packed nblk*36 | ybc NC*6] (all-reduced)
   double* d_S = nullptr;
   // implicit-Schur PCG (lazily allocated)
@@ -690,6 +698,46 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
     h->nxlist = (int)xlist.size();
   }
 
+  // pair-major evaluation (rig): the composed observations with both cameras free are
+  // evaluated per (arc, ring) pair chunk; the remaining camera-major entries keep chunks
+  // of their own, and every camera lists its halves of the pair chunks (increasing chunk)
+  std::vector<int4> cm2_idx;
+  std::vector<double2> cm2_xy;
+  std::vector<int> chunk2_beg, seg2_chunk(NC + 1, 0), xcam_ptr(NC + 1, 0), xcam_list;
+  {
+    const char* pe = getenv("DAB_PAIR_EVAL");
+    h->pair_eval = h->nxchunk > 0 && pair_eval_fits(h->E, h->NI) && !(pe && atoi(pe) == 0);
+  }
+  if (h->pair_eval) {
+    for (int c = 0; c < NC; ++c) {
+      seg2_chunk[c] = (int)chunk2_beg.size();
+      const int b2 = (int)cm2_idx.size();
+      for (int i = cam_cnt[c]; i < cam_cnt[c + 1]; ++i) {
+        const int4 id = cm_idx[i];
+        const bool paired = id.z >= 0 && h->ext_col[id.y] >= 0 && h->ext_col[id.z] >= 0;
+        if (paired) continue;
+        cm2_idx.push_back(id);
+        cm2_xy.push_back(cm_xy[i]);
+      }
+      for (int q = b2; q < (int)cm2_idx.size(); q += chunk) chunk2_beg.push_back(q);
+    }
+    seg2_chunk[NC] = (int)chunk2_beg.size();
+    h->nchunk2 = (int)chunk2_beg.size();
+    chunk2_beg.push_back((int)cm2_idx.size());
+    std::vector<std::vector<int>> per(NC);
+    for (int k = 0; k < h->ncross; ++k)
+      for (int q = xseg_chunk[k]; q < xseg_chunk[k + 1]; ++q) {
+        per[cross_cam[k].x].push_back(2 * q);
+        per[cross_cam[k].y].push_back(2 * q + 1);
+      }
+    for (int c = 0; c < NC; ++c) {
+      std::sort(per[c].begin(), per[c].end());
+      xcam_ptr[c] = (int)xcam_list.size();
+      xcam_list.insert(xcam_list.end(), per[c].begin(), per[c].end());
+    }
+    xcam_ptr[NC] = (int)xcam_list.size();
+  }
+
   h->h_pt_ent_ptr = pt_ent_ptr;
   h->h_ent_cam = ent_cam;
   h->h_ent_pos = ent_pos;
@@ -756,6 +804,18 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   CHECK_RC(upload(&h->d_xptr, d, xptr, s));
   CHECK_RC(upload(&h->d_run, d, run, s));
   CHECK_RC(upload(&h->d_xlist, d, xlist, s));
+  if (h->pair_eval) {
+    if (!cm2_idx.empty()) {
+      CHECK_RC(upload(&h->d_cm2_idx, d, cm2_idx, s));
+      CHECK_RC(upload(&h->d_cm2_xy, d, cm2_xy, s));
+    }
+    CHECK_RC(upload(&h->d_chunk2_beg, d, chunk2_beg, s));
+    CHECK_RC(upload(&h->d_seg2_chunk, d, seg2_chunk, s));
+    CHECK_RC(upload(&h->d_xcam_ptr, d, xcam_ptr, s));
+    if (!xcam_list.empty()) CHECK_RC(upload(&h->d_xcam_list, d, xcam_list, s));
+    CHECK_RC(d.alloc(&h->d_partial2, (size_t)std::max(1, h->nchunk2) * 27));
+    CHECK_RC(d.alloc(&h->d_xcpart, (size_t)h->nxchunk * 54));
+  }
   CHECK_RC(upload(&h->d_intr, d, intr, s));
   CHECK_RC(upload(&h->d_points, d, points, s));
   CHECK_RC(upload(&h->d_ext, d, ext, s));
@@ -1161,13 +1221,26 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
     if (ovl) HIP_OK(hipStreamWaitEvent(s, h->ev_comm, 0));
     return 0;
   }
-  if (h->NC > 0) {
+  if (h->NC > 0 && h->pair_eval) {
+    // the composed observations pair-major (camera halves + cross blocks in one pass),
+    // the other entries camera-major, then one fixed-order sum per camera
+    DevView v2 = v;
+    v2.cm_idx = h->d_cm2_idx;
+    v2.cm_xy = h->d_cm2_xy;
+    launch_eval_cams_gen(s, v2, h->nchunk2, h->d_chunk2_beg, h->d_points, h->d_ext, h->d_camtab, h->d_partial2);
+    launch_eval_pair(s, v, h->nxchunk, h->d_xchunk_beg, h->d_x_idx, h->d_x_xy, h->d_points, h->d_camtab,
+                     h->d_xpartial, h->d_xcpart);
+    launch_cam_final(s, h->NC, h->d_seg2_chunk, h->d_partial2, h->d_xcam_ptr, h->d_xcam_list, h->d_xcpart, h->ug());
+    launch_seg_final(s, h->ncross, 36, h->d_xseg_chunk, h->d_xpartial, h->Ux(), h->max_xseg_chunks);
+  } else if (h->NC > 0) {
     // one chunk per camera: the chunk kernels write the camera rows directly
     const bool direct = h->nchunk == h->NC;
     launch_eval_cams(s, v, h->chunks, h->d_chunk_beg, h->d_points, h->d_ext, h->d_camtab,
                      direct ? h->ug() : h->d_partial);
     if (!direct) launch_seg_final(s, h->NC, 27, h->d_seg_chunk, h->d_partial, h->ug(), h->max_seg_chunks);
-    if (h->ncross > 0) {
+  }
+  if (h->NC > 0) {
+    if (h->ncross > 0 && !h->pair_eval) {
       if (h->nxchunk > 0) {
         launch_eval_cross(s, v, h->nxchunk, h->d_xchunk_beg, h->d_x_idx, h->d_x_xy, h->d_points, h->d_camtab,
                           h->d_xpartial);

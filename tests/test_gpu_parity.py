@@ -124,6 +124,42 @@ def test_lm_rig_matches_oracle(pkg, orc, gpu):
     assert_same_trajectory(g, o, prob, ref)
 
 
+def test_lm_rig_large_tables_matches_oracle(pkg, orc, gpu):
+    """A rig whose extrinsic / intrinsic tables exceed the LDS staging limit (E > 128): the
+    camera-side and cross-block passes read the tables from global memory and the
+    pair-major pass is off. Against the oracle's trajectory."""
+    prob = pkg.synth(kind=1, num_arcs=9, num_rings=122, num_points=2500, obs_per_point=6, seed=23)
+    assert prob.ext.shape[0] > 128 and (prob.obs_ext1 >= 0).any()
+    g, o, ref = run_both(pkg, orc, prob, max_num_iterations=12)
+    assert_same_trajectory(g, o, prob, ref)
+
+
+@pytest.mark.parametrize("solver", ["explicit", "pcg"])
+def test_rig_pair_eval_matches_camera_major(pkg, gpu, solver, monkeypatch):
+    """The rig's composed observations evaluated pair-major (k_eval_pair: both cameras'
+    blocks and the cross block from one projection, rotated frame) against the
+    camera-major + cross passes (DAB_PAIR_EVAL=0): same LM trajectory to 1e-10 relative,
+    same CG counts; the pair-major pass is bitwise repeatable."""
+    prob = pkg.synth(kind=1, num_arcs=6, num_rings=16, num_points=3000, obs_per_point=8, seed=24)
+    lst = (pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR if solver == "explicit"
+           else pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)
+    res, pts = [], []
+    for pe in ("1", "0", "1"):
+        monkeypatch.setenv("DAB_PAIR_EVAL", pe)
+        p = prob.copy()
+        s = pkg.Solver(0)
+        s.set_problem(p)
+        res.append(s.solve(pkg.options(max_num_iterations=10, linear_solver_type=lst)))
+        s.close()
+        pts.append(p.points.copy())
+    a, b = res[0], res[1]
+    assert [it["linear_solver_iterations"] for it in a["iterations"]] == \
+        [it["linear_solver_iterations"] for it in b["iterations"]]
+    np.testing.assert_allclose([it["cost"] for it in a["iterations"]], [it["cost"] for it in b["iterations"]],
+                               rtol=1e-10)
+    np.testing.assert_array_equal(pts[0], pts[2])
+
+
 @pytest.mark.parametrize("kind", ["bal", "rig"])
 def test_lm_pcg_matches_oracle(pkg, orc, gpu, kind):
     """IMPLICIT_SCHUR_PCG: the GPU implicit operator vs the oracle's CG on the explicit S.
