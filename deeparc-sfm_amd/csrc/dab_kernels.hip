@@ -3419,10 +3419,153 @@ __global__ __launch_bounds__(256) void k_candidate(DevView v, const double* __re
   block_reduce_store<3>(acc, partial + 3 * (size_t)blockIdx.x);
 }
 
+// k_candidate for staged tables in the rotated frame (as k_mf_frame sweep 1): the model
+// change m = A dP with dP = dt_a - Z_a x w~_a + R_a (R_b dp_X + dt_r - Z_r x w~_r) and
+// w~ = J_l dw once per camera, instead of building every row of the observation; the
+// candidate residual as k_candidate. LDS: R, t at x | R, t at x + delta | K | small-angle
+// flags | [w~ | dt] per camera.
+__global__ __launch_bounds__(256) void k_candidate_frame(DevView v, const double* __restrict__ points,
+                                                         const double* __restrict__ camtab,
+                                                         const double* __restrict__ dp,
+                                                         const double* __restrict__ dc,
+                                                         const double* __restrict__ camtab_c,
+                                                         double* __restrict__ partial) {
+  extern __shared__ double cf_lds[];
+  double* rt_s = cf_lds;
+  double* rtc_s = rt_s + 12 * (size_t)v.E;
+  double* k_s = rtc_s + 12 * (size_t)v.E;
+  double* dv_s = k_s + 6 * (size_t)v.NI;
+  int* sm_s = reinterpret_cast<int*>(dv_s + 6 * (size_t)v.NC);
+  for (int i = threadIdx.x; i < 12 * v.E; i += blockDim.x) {
+    rt_s[i] = camtab[(size_t)kCamTab * (i / 12) + i % 12];
+    rtc_s[i] = camtab_c[(size_t)kCamTab * (i / 12) + i % 12];
+  }
+  for (int i = threadIdx.x; i < 6 * v.NI; i += blockDim.x) k_s[i] = v.intr[(size_t)kIntr * (i / 6) + i % 6];
+  for (int e = threadIdx.x; e < v.E; e += blockDim.x) {
+    const double* T = camtab + (size_t)kCamTab * e;
+    sm_s[e] = (T[12] == 1.0 && T[13] == 0.0 && T[14] == 0.0 && T[15] == 0.0 && T[16] == 1.0 && T[17] == 0.0 &&
+               T[18] == 0.0 && T[19] == 0.0 && T[20] == 1.0)
+                  ? 1
+                  : 0;
+    const int c = v.ext_col[e];
+    if (c < 0) continue;
+    const double* d = dc + 6 * c;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      double w = 0.0;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const double jl = T[12 + 3 * r] * T[21 + q] + T[12 + 3 * r + 1] * T[24 + q] + T[12 + 3 * r + 2] * T[27 + q];
+        w += jl * d[q];
+      }
+      dv_s[6 * c + r] = w;
+      dv_s[6 * c + 3 + r] = d[3 + r];
+    }
+  }
+  __syncthreads();
+  const SmallTabs tk{nullptr, k_s};
+  auto rt = [&](const double* base, int e, double (&o)[12]) {
+    const double2* pp = reinterpret_cast<const double2*>(base + 12 * e);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const double2 u = pp[k];
+      o[2 * k] = u.x;
+      o[2 * k + 1] = u.y;
+    }
+  };
+  double acc[3] = {0.0, 0.0, 0.0};
+  const size_t NPs = (size_t)v.NP;
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < v.N; s += gridDim.x * blockDim.x) {
+    const int4 id = v.obs_idx[s];
+    if (id.x < 0) continue;  // padding slot
+    const double2 xy = v.obs_xy[s];
+    const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
+    const double d3[3] = {dp[id.x], dp[NPs + id.x], dp[2 * NPs + id.x]};
+    double Kr[6];
+    tk.k(id.w, Kr);
+    double m0, m1, ru, rv;
+    {
+      double Ta[12];
+      rt(rt_s, id.y, Ta);
+      const bool comp = id.z >= 0;
+      double Q[3], inner[3];  // inner: R_b dp_X (+ the ring term), rotated by R_a below
+      if (comp) {
+        double Tb[12];
+        rt(rt_s, id.z, Tb);
+        matvec_add(Tb, X, Tb + 9, Q);
+        mv3(Tb, d3, inner);
+        const int c1 = v.ext_col[id.z];
+        if (c1 >= 0) {
+          const bool sb = sm_s[id.z] != 0;
+          double Z1[3], cz[3];
+#pragma unroll
+          for (int k = 0; k < 3; ++k) Z1[k] = sb ? X[k] : Q[k] - Tb[9 + k];
+          const double* d = dv_s + 6 * c1;
+          const double w[3] = {d[0], d[1], d[2]};
+          cross3(Z1, w, cz);
+#pragma unroll
+          for (int k = 0; k < 3; ++k) inner[k] += d[3 + k] - cz[k];
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          Q[k] = X[k];
+          inner[k] = d3[k];
+        }
+      }
+      double P[3], dP[3];
+      matvec_add(Ta, Q, Ta + 9, P);
+      mv3(Ta, inner, dP);
+      const int c0 = v.ext_col[id.y];
+      if (c0 >= 0) {
+        const bool sa = sm_s[id.y] != 0;
+        double Z0[3], cz[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) Z0[k] = sa ? Q[k] : P[k] - Ta[9 + k];
+        const double* d = dv_s + 6 * c0;
+        const double w[3] = {d[0], d[1], d[2]};
+        cross3(Z0, w, cz);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dP[k] += d[3 + k] - cz[k];
+      }
+      Proj pr;
+      project(P, Kr, xy.x, xy.y, pr, true);
+      ru = pr.ru;
+      rv = pr.rv;
+      m0 = pr.A0[0] * dP[0] + pr.A0[1] * dP[1] + pr.A0[2] * dP[2];
+      m1 = pr.A1[0] * dP[0] + pr.A1[1] * dP[1] + pr.A1[2] * dP[2];
+    }
+    acc[0] += -(m0 * (ru + m0 / 2.0) + m1 * (rv + m1 / 2.0));
+    // candidate residual at (x + delta)
+    const double Xc[3] = {X[0] + d3[0], X[1] + d3[1], X[2] + d3[2]};
+    double T0[12];
+    rt(rtc_s, id.y, T0);
+    double P[3];
+    if (id.z >= 0) {
+      double T1[12], P2[3];
+      rt(rtc_s, id.z, T1);
+      matvec_add(T1, Xc, T1 + 9, P2);
+      matvec_add(T0, P2, T0 + 9, P);
+    } else {
+      matvec_add(T0, Xc, T0 + 9, P);
+    }
+    Proj pc;
+    project(P, Kr, xy.x, xy.y, pc, false);
+    acc[1] += pc.ru * pc.ru + pc.rv * pc.rv;
+    acc[2] += (isfinite(pc.ru) && isfinite(pc.rv)) ? 0.0 : 1.0;
+  }
+  block_reduce_store<3>(acc, partial + 3 * (size_t)blockIdx.x);
+}
+
 void launch_candidate(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                       const double* delta_p, const double* delta_c, const double* camtab_c, double* partial,
                       int grid) {
-  if (small_tabs_fit(v.E, v.NI)) {
+  static const bool rows = getenv("DAB_CAND_ROWS") && atoi(getenv("DAB_CAND_ROWS")) != 0;  // A/B: row form
+  if (small_tabs_fit(v.E, v.NI) && !rows) {
+    const size_t lds = sizeof(double) * (24 * (size_t)v.E + 6 * (size_t)v.NI + 6 * (size_t)v.NC) +
+                       sizeof(int) * (size_t)v.E;
+    k_candidate_frame<<<grid, 256, lds, s>>>(v, points, camtab, delta_p, delta_c, camtab_c, partial);
+  } else if (small_tabs_fit(v.E, v.NI)) {
     const size_t lds = small_tabs_bytes(v.E, v.NI) + sizeof(double) * 30 * (size_t)v.E;
     k_candidate<true><<<grid, 256, lds, s>>>(v, points, camtab, delta_p, delta_c, camtab_c, partial);
   } else {
