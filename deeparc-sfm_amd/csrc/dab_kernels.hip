@@ -2294,14 +2294,14 @@ void launch_eval_pair(hipStream_t s, const DevView& v, int nchunk, const int* ch
 }
 
 // ug[c] = its camera-major chunk partials (seg_chunk) + its halves of the pair chunks
-// (xcam_list codes 2 q + half, increasing q): one block per camera, 9 stripes of 27
+// (xcam_list codes 2 q + half, increasing q): one block per camera, 37 stripes of 27
 // threads over the terms, the stripes summed in order (fixed order, as k_seg_final_block)
-__global__ __launch_bounds__(256) void k_cam_final(const int* __restrict__ seg_chunk,
+__global__ __launch_bounds__(1024) void k_cam_final(const int* __restrict__ seg_chunk,
                                                    const double* __restrict__ partial,
                                                    const int* __restrict__ xcam_ptr,
                                                    const int* __restrict__ xcam_list,
                                                    const double* __restrict__ cpart, double* __restrict__ ug) {
-  constexpr int kS = 256 / 27;
+  constexpr int kS = 1024 / 27;
   __shared__ double sh[kS * 27];
   const int c = blockIdx.x, k = threadIdx.x % 27, stripe = threadIdx.x / 27;
   if (stripe < kS) {
@@ -2328,7 +2328,7 @@ __global__ __launch_bounds__(256) void k_cam_final(const int* __restrict__ seg_c
 void launch_cam_final(hipStream_t s, int NC, const int* seg_chunk, const double* partial, const int* xcam_ptr,
                       const int* xcam_list, const double* cpart, double* ug) {
   if (NC <= 0) return;
-  k_cam_final<<<NC, 256, 0, s>>>(seg_chunk, partial, xcam_ptr, xcam_list, cpart, ug);
+  k_cam_final<<<NC, 1024, 0, s>>>(seg_chunk, partial, xcam_ptr, xcam_list, cpart, ug);
 }
 // the general camera-major kernel over an arbitrary chunk set (no uniform-chunk lists)
 void launch_eval_cams_gen(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const double* points,
