@@ -1650,6 +1650,54 @@ __device__ __forceinline__ void ext_frame(const double* __restrict__ camtab, int
   }
 }
 
+// pipe_entries with NS register slots: the record of entry i + (NS-1) stride is loaded and
+// the point of entry i + (NS-2) stride gathered while entry i computes (kernels with
+// registers to spare and few waves per SIMD, e.g. k_eval_pair)
+template <int NS, class Body>
+__device__ __forceinline__ void pipe_entries_ns(const int4* __restrict__ idx, const double2* __restrict__ xyv,
+                                                int i0, int e, int stride, const double* __restrict__ points,
+                                                Body body) {
+  static_assert(NS >= 3, "at least three slots");
+  int4 id[NS];
+  double2 xy[NS];
+  double X[NS][3];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    id[s] = make_int4(-1, 0, -1, 0);
+    xy[s] = make_double2(0.0, 0.0);
+    X[s][0] = X[s][1] = X[s][2] = 0.0;
+  }
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (i0 + s * stride < e) {
+      id[s] = idx[i0 + s * stride];
+      xy[s] = xyv[i0 + s * stride];
+    }
+#pragma unroll
+  for (int s = 0; s < NS - 2; ++s)
+    if (id[s].x >= 0) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) X[s][q] = points[3 * (size_t)id[s].x + q];
+    }
+  for (int i = i0; i < e; i += NS * stride) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int ii = i + u * stride;
+      if (ii >= e) break;
+      const int sg = (u + NS - 2) % NS, sl = (u + NS - 1) % NS;
+      if (id[sg].x >= 0 && ii + (NS - 2) * stride < e) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) X[sg][q] = points[3 * (size_t)id[sg].x + q];
+      }
+      if (ii + (NS - 1) * stride < e) {
+        id[sl] = idx[ii + (NS - 1) * stride];
+        xy[sl] = xyv[ii + (NS - 1) * stride];
+      }
+      body(id[u], xy[u], X[u]);
+    }
+  }
+}
+
 // UNI: the chunks of `list` are uniform (chunk_uni), tables read once per block
 template <bool UNI>
 __global__ __launch_bounds__(256) void k_eval_cams(DevView v, const int* __restrict__ chunk_beg,
@@ -2158,6 +2206,7 @@ __global__ __launch_bounds__(256) void k_eval_cross(DevView v, const int* __rest
 // sums). It replaces, for these observations, both camera-major entries and the separate
 // cross pass: one 56-B input per observation instead of three. k_cam_final adds the
 // camera halves to the camera-major partials of the remaining entries.
+template <int PNS>
 __global__ __launch_bounds__(256) void k_eval_pair(DevView v, const int* __restrict__ chunk_beg,
                                                    const int4* __restrict__ x_idx,
                                                    const double2* __restrict__ x_xy,
@@ -2183,7 +2232,7 @@ __global__ __launch_bounds__(256) void k_eval_pair(DevView v, const int* __restr
   double acc[90];
 #pragma unroll
   for (int i = 0; i < 90; ++i) acc[i] = 0.0;
-  pipe_entries(x_idx, x_xy, b + threadIdx.x, e, blockDim.x, points,
+  pipe_entries_ns<PNS>(x_idx, x_xy, b + threadIdx.x, e, blockDim.x, points,
                [&](const int4 id, const double2 xy, const double (&X)[3]) {
                  double Ta[12], Tb[12], Kr[6];
                  st.rt(id.y, Ta);
@@ -2289,8 +2338,10 @@ void launch_eval_pair(hipStream_t s, const DevView& v, int nchunk, const int* ch
                       double* cpart) {
   if (nchunk <= 0) return;
   // 90 sums per lane: ~300 VGPRs, one wave per SIMD (a 256-VGPR cap spills hundreds)
-  k_eval_pair<<<nchunk, 256, small_tabs_bytes(v.E, v.NI), s>>>(v, chunk_beg, x_idx, x_xy, points, camtab, xpart,
-                                                               cpart);
+  // four register slots: measured 285 us at C5 against 295 (three) and 286 (five); one
+  // wave per SIMD leaves the registers for it
+  k_eval_pair<4><<<nchunk, 256, small_tabs_bytes(v.E, v.NI), s>>>(v, chunk_beg, x_idx, x_xy, points, camtab, xpart,
+                                                                  cpart);
 }
 
 // ug[c] = its camera-major chunk partials (seg_chunk) + its halves of the pair chunks
