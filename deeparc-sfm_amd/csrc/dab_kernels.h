@@ -143,9 +143,9 @@ void launch_point_factor(hipStream_t s, const DevView& v, const double* V, const
 void launch_entry_y(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                     const double* scale_c, const double* PU, YBufs Y, bool with_pm);
 // S blocks (Y part): packed[blk][36] = - sum_pairs Y_row Y_col^T (pairs hold positions;
-// Y = the fp64 camera-major planes, stride NE)
+// Y = the fp64 camera-major planes, stride NE; Yr = scratch [NE][18] for the records)
 void launch_s_blocks(hipStream_t s, int nblk, const int* blk_pair_beg, const int2* pairs,
-                     const double* Y, int NE, double* packed);
+                     const double* Y, int NE, double* packed, double* Yr);
 // camera rhs partial: per position -Y q_p -> partial[chunk][6]
 void launch_cam_rhs_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
                             const double* Y, const double* q, double* partial);

@@ -2558,19 +2558,28 @@ void launch_entry_y(hipStream_t s, const DevView& v, const double* points, const
 }
 
 // one wave per S block; lane (a,b) < 36 accumulates -sum Y_row[a,:] . Y_col[b,:]
+// Y planes -> one contiguous 144-B record per entry: the S-block pairs gather whole
+// records (2 lines) instead of one 8-B element from each of 18 planes (18 lines)
+__global__ __launch_bounds__(256) void k_y_records(int NE, const double* __restrict__ Y, double* __restrict__ Yr) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)kYRec * NE) return;
+  const size_t i = t / kYRec, j = t - kYRec * (t / kYRec);
+  Yr[t] = Y[j * (size_t)NE + i];
+}
+
 __global__ __launch_bounds__(256) void k_s_blocks(int nblk, const int* __restrict__ blk_pair_beg,
                                                   const int2* __restrict__ pairs,
-                                                  const double* __restrict__ Y, int NE,
+                                                  const double* __restrict__ Yr,
                                                   double* __restrict__ packed) {
   const int blk = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (blk >= nblk || lane >= 36) return;
   const int a = lane / 6, b = lane - 6 * (lane / 6);
-  const size_t st = (size_t)NE;
   double acc = 0.0;
   auto term = [&](const int2 pr) {
-    return Y[(3 * a) * st + pr.x] * Y[(3 * b) * st + pr.y] + Y[(3 * a + 1) * st + pr.x] * Y[(3 * b + 1) * st + pr.y] +
-           Y[(3 * a + 2) * st + pr.x] * Y[(3 * b + 2) * st + pr.y];
+    const double* x = Yr + (size_t)kYRec * pr.x + 3 * a;
+    const double* y = Yr + (size_t)kYRec * pr.y + 3 * b;
+    return x[0] * y[0] + x[1] * y[1] + x[2] * y[2];
   };
   // four pairs' gathers in flight per step (the loop is latency bound); the sum keeps the
   // pair order, so the result is bitwise that of the one-pair loop
@@ -2589,9 +2598,10 @@ __global__ __launch_bounds__(256) void k_s_blocks(int nblk, const int* __restric
 }
 
 void launch_s_blocks(hipStream_t s, int nblk, const int* blk_pair_beg, const int2* pairs,
-                     const double* Y, int NE, double* packed) {
+                     const double* Y, int NE, double* packed, double* Yr) {
   if (nblk <= 0) return;
-  k_s_blocks<<<(nblk + 3) / 4, 256, 0, s>>>(nblk, blk_pair_beg, pairs, Y, NE, packed);
+  k_y_records<<<(unsigned)(((size_t)kYRec * NE + 255) / 256), 256, 0, s>>>(NE, Y, Yr);
+  k_s_blocks<<<(nblk + 3) / 4, 256, 0, s>>>(nblk, blk_pair_beg, pairs, Yr, packed);
 }
 
 __global__ __launch_bounds__(256) void k_cam_rhs_partial(DevView v, const int* __restrict__ chunk_beg,

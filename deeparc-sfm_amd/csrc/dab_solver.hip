@@ -167,6 +167,7 @@ struct dab_handle {
   double* d_Jfull = nullptr;  // parity API only (lazily allocated)
   double *d_V = nullptr, *d_g = nullptr, *d_scale_p = nullptr, *d_scale_c = nullptr;
   double *d_L = nullptr, *d_q = nullptr, *d_Y = nullptr, *d_Yp = nullptr;  // Y camera-/point-major
+  double* d_Yrec = nullptr;  // EXPLICIT: Y as [NE][18] records for k_s_blocks (lazy)
   float *d_Y32c = nullptr, *d_Y32p = nullptr;                                 // pcg_fp32 (lazy)
   double* d_camred = nullptr;  // [Ucc NC*21 | gc NC*6 | Ux ncross*36] (all-reduced)
   double* d_partial = nullptr; // chunk partials (max of chunk counts * 36)
@@ -457,6 +458,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   HIP_OK(hipSetDevice(h->device));
   HIP_OK(hipStreamSynchronize(h->stream));
   h->dev.release();
+  h->d_Yrec = nullptr;  // lazily allocated: reallocated by the next explicit step
   h->have_problem = false;
   h->prob = *p;
   const int N = p->num_obs;
@@ -1495,7 +1497,8 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
       pcg_fail = cg_status == kPcgFailure;
     } else if (NC > 0) {
       launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, yb, true);
-      launch_s_blocks(s, h->nblk, h->d_blk_pair_beg, h->d_pairs, h->d_Y, h->NE, h->packed());
+      if (!h->d_Yrec) CHECK_RC(h->dev.alloc(&h->d_Yrec, (size_t)kYRec * std::max(1, h->NE)));
+      launch_s_blocks(s, h->nblk, h->d_blk_pair_beg, h->d_pairs, h->d_Y, h->NE, h->packed(), h->d_Yrec);
       launch_cam_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_Y, h->d_q, h->d_partial);
       launch_seg_final(s, NC, 6, h->d_seg_chunk, h->d_partial, h->ybc(), h->max_seg_chunks);
       CHECK_RC(h->allreduce(h->d_spack, h->spack_count(), ncclSum));
