@@ -2581,17 +2581,16 @@ __global__ __launch_bounds__(256) void k_s_blocks(int nblk, const int* __restric
     const double* y = Yr + (size_t)kYRec * pr.y + 3 * b;
     return x[0] * y[0] + x[1] * y[1] + x[2] * y[2];
   };
-  // four pairs' gathers in flight per step (the loop is latency bound); the sum keeps the
+  // eight pairs' gathers in flight per step (the loop is latency bound); the sum keeps the
   // pair order, so the result is bitwise that of the one-pair loop
   const int e = blk_pair_beg[blk + 1];
   int i = blk_pair_beg[blk];
-  for (; i + 3 < e; i += 4) {
-    const int2 p0 = pairs[i], p1 = pairs[i + 1], p2 = pairs[i + 2], p3 = pairs[i + 3];
-    const double t0 = term(p0), t1 = term(p1), t2 = term(p2), t3 = term(p3);
-    acc += t0;
-    acc += t1;
-    acc += t2;
-    acc += t3;
+  for (; i + 7 < e; i += 8) {
+    double t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = term(pairs[i + u]);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += t[u];
   }
   for (; i < e; ++i) acc += term(pairs[i]);
   packed[36 * (size_t)blk + lane] = -acc;
