@@ -72,7 +72,8 @@ class DabSummary(C.Structure):
         ("linear_solver_time_in_seconds", C.c_double),
         ("message", C.c_char * 256),
         ("iterations", C.POINTER(DabIteration)), ("iterations_capacity", C.c_int32),
-        ("iterations_written", C.c_int32),
+        ("iterations_written", C.c_int32), ("linear_solver_type_used", C.c_int32),
+        ("schur_assembly", C.c_int32),
     ]
 
 
@@ -137,7 +138,7 @@ def load_library(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.dab_abi_version() != 1:
+    if lib.dab_abi_version() != 2:
         raise RuntimeError("libdab ABI version mismatch")
     if path is None:
         _LIB = lib

@@ -162,6 +162,7 @@ def summary_to_dict(s, its):
         jacobian_time=s.jacobian_evaluation_time_in_seconds,
         residual_time=s.residual_evaluation_time_in_seconds,
         linear_solver_time=s.linear_solver_time_in_seconds,
+        linear_solver_type_used=s.linear_solver_type_used, schur_assembly=s.schur_assembly,
         iterations=[dict(iteration=it.iteration, success=bool(it.step_is_successful),
                          valid=bool(it.step_is_valid), cost=it.cost, cost_change=it.cost_change,
                          gradient_max_norm=it.gradient_max_norm, step_norm=it.step_norm,

@@ -20,11 +20,27 @@ struct YBufs {
   bool f32;
 };
 constexpr int kRedBlock = 256;
-// fixed-point cost accumulators (cost_fx_add): kFxCopies shards of 128 B, each holding
-// {sum r^2 integer part, fraction * 2^52, non-finite count} as uint64 in words 0..2
+// fixed-point cost accumulators (cost_fx_commit): kFxCopies shards of 128 B. A work-group's
+// partial sum of r^2 is split into kFxLimbs integer limbs of 50 bits each, limb k in units
+// of 2^(50 * (2 - k)) (2^100, 2^50, 1, 2^-50, 2^-100), so any finite partial below 2^150
+// is held exactly down to 2^-100; word kFxBad counts non-finite partials. Integer adds are
+// associative: the total is the same in any arrival order and across ranks, and no word
+// can wrap (each limb < 2^50 + 1, at most 2^11 adds per word over every rank).
 constexpr int kFxStride = 16;   // 8-B words per shard
 constexpr int kFxCopies = 32;   // shards (work-group b adds into shard b % kFxCopies)
 constexpr int kFxWords = kFxStride * kFxCopies;
+constexpr int kFxLimbs = 5;
+constexpr int kFxBad = kFxLimbs;  // word of the non-finite count
+// host side: the summed shards of one set -> {sum r^2, non-finite count}
+inline void cost_fx_total(const unsigned long long* words, double& sum, double& bad) {
+  unsigned long long acc[kFxLimbs + 1] = {0, 0, 0, 0, 0, 0};
+  for (int c = 0; c < kFxCopies; ++c)
+    for (int i = 0; i <= kFxLimbs; ++i) acc[i] += words[kFxStride * c + i];
+  const double unit[kFxLimbs] = {0x1p100, 0x1p50, 1.0, 0x1p-50, 0x1p-100};
+  sum = 0.0;
+  for (int i = 0; i < kFxLimbs; ++i) sum += (double)acc[i] * unit[i];  // largest limb first
+  bad = (double)acc[kFxBad];
+}
 constexpr int kChunk = 4096;  // max entries per reduction chunk (C3: one chunk per camera)
 constexpr int kSlotBit = 1 << 30;  // cm_idx.w flag: the entry is the ring (slot 1) camera
 
@@ -146,6 +162,35 @@ void launch_entry_y(hipStream_t s, const DevView& v, const double* points, const
 // Y = the fp64 camera-major planes, stride NE; Yr = scratch [NE][18] for the records)
 void launch_s_blocks(hipStream_t s, int nblk, const int* blk_pair_beg, const int2* pairs,
                      const double* Y, int NE, double* packed, double* Yr);
+// Explicit S for small camera sets without pair tables (k_schur_tiles): tiles of the lower
+// block triangle of S in LDS, fixed-point 64-bit integer sums (exact, order-free). Element
+// (c, d <= c, r, s) of the Schur part sits at 36 (c (c+1)/2 + d) + 6 r + s, the rhs part of
+// row 6 c + r at nelem + 6 c + r, in units of 2^(kx[R] + kx[C] - 60) / 2^(kx[R] + kq - 60).
+constexpr size_t kTileLdsMax = 163840;  // dynamic LDS of one k_schur_tiles work-group
+constexpr int kTileBatch = 32;          // entries (and points) per wave batch
+__host__ __device__ inline long long tri_n(long long i) { return (i * (i + 1)) >> 1; }
+struct SchurTiles {
+  int ntile, ngroup, nbatch, nelem;  // nelem = 36 NC (NC + 1) / 2
+  const int* tile_c0;                // [ntile + 1] camera bounds of the tiles
+  const int* batch_pt;               // [nbatch + 1] first point of each batch (<= 32 entries, <= 32 points)
+  const int2* sch_ent;               // [NE] (ent_os, camera), sorted by camera inside each point
+  const double* scx;                 // [6 NC] s_c 2^(30 - kx)
+  double qscale;                     // 2^(30 - kq)
+  unsigned long long* partial;       // [ngroup][stride]
+  size_t stride;                     // nelem + 6 NC
+};
+size_t schur_tile_lds_fixed();       // LDS of the per-wave scratch (the tile gets the rest)
+void launch_schur_scale(hipStream_t s, int NC, const double* ug, const double* scale_c, double* scx, int* kx);
+void launch_schur_tiles(hipStream_t s, const DevView& v, const double* points, const double* camtab, const double* PU,
+                        const double* q, const SchurTiles& a, size_t lds_bytes);
+void launch_schur_sum(hipStream_t s, int ngroup, size_t stride, size_t count, const unsigned long long* partial,
+                      unsigned long long* out);
+// S lower rows 0..n-1 = -Schur part, ybc = -rhs part (then launch_s_add_u)
+void launch_schur_unpack(hipStream_t s, int NC, const unsigned long long* sfx, const int* kx, int kq, double* S,
+                         int lds, double* ybc);
+// adds the U part (+ D^2) and cross blocks, writes the rhs row n = s_c g_c + ybc
+void launch_s_add_u(hipStream_t s, int NC, const double* ug, int ncross, const int2* cross_cam, const double* Ucross,
+                    const double* scale_c, StepScalars sc, const double* ybc, double* S, int lds);
 // camera rhs partial: per position -Y q_p -> partial[chunk][6]
 void launch_cam_rhs_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
                             const double* Y, const double* q, double* partial);

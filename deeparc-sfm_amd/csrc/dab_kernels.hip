@@ -859,6 +859,32 @@ __global__ __launch_bounds__(1024) void k_eval_points_lds(DevView v, const doubl
 // between consecutive passes: block 0 of a pass zeroes the set the next pass adds into
 // (fx_next), so no memset or extra launch runs in front of the kernel; the set of a pass
 // stays valid until the pass after next.
+// One lane commits a work-group's cost partial p (sum r^2 >= 0) and its non-finite count b
+// to its shard as kFxLimbs 50-bit limbs (dab_kernels.h). Each limb is taken off the top with
+// a floor and an exact subtraction (the remainder of a double below 2^(50 (k+1)) after
+// removing its multiple of 2^(50 k) is representable), the last one rounded. A finite p of
+// 2^150 or more (a residual of ~1e22 px) cannot be held and is counted as non-finite.
+__device__ __forceinline__ void cost_fx_commit(double p, double b, unsigned long long* __restrict__ shard) {
+  unsigned long long limb[kFxLimbs] = {0, 0, 0, 0, 0};
+  if (!(p >= 0.0 && p < 0x1p150)) {
+    if (b == 0.0) b = 1.0;
+  } else {
+    double r = p;
+    const double scale[kFxLimbs - 1] = {0x1p-100, 0x1p-50, 1.0, 0x1p50};
+#pragma unroll
+    for (int k = 0; k < kFxLimbs - 1; ++k) {
+      const double l = floor(r * scale[k]);
+      limb[k] = (unsigned long long)l;
+      r -= l / scale[k];  // exact
+    }
+    limb[kFxLimbs - 1] = (unsigned long long)rint(r * 0x1p100);
+  }
+#pragma unroll
+  for (int k = 0; k < kFxLimbs; ++k)
+    if (limb[k]) __hip_atomic_fetch_add(shard + k, limb[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (b != 0.0) __hip_atomic_fetch_add(shard + kFxBad, (unsigned long long)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int NW>
 __device__ __forceinline__ void cost_fx_add(double (&acc)[2], unsigned long long* __restrict__ fx) {
   __shared__ double shp[NW][2];
@@ -876,18 +902,7 @@ __device__ __forceinline__ void cost_fx_add(double (&acc)[2], unsigned long long
       p += shp[q][0];
       b += shp[q][1];
     }
-    long long hi = 0, lo = 0;
-    if (p >= 0.0 && p < 0x1p62) {
-      const double ip = trunc(p);
-      hi = (long long)ip;
-      lo = (long long)rint((p - ip) * 0x1p52);
-    } else {
-      b += 1.0;  // non-finite (or absurd) partial: the evaluation is flagged bad
-    }
-    unsigned long long* sh = fx + kFxStride * (blockIdx.x % kFxCopies);
-    if (hi) __hip_atomic_fetch_add(sh, (unsigned long long)hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (lo) __hip_atomic_fetch_add(sh + 1, (unsigned long long)lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (b != 0.0) __hip_atomic_fetch_add(sh + 2, (unsigned long long)b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cost_fx_commit(p, b, fx + kFxStride * (blockIdx.x % kFxCopies));
   }
 }
 
@@ -1133,22 +1148,28 @@ void launch_eval_points(hipStream_t s, const DevView& v, const double* points, c
       case 23: launch_pf<2, 3>(s, v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next, grid); break;
       case 64012: launch_pf<1, 2, 64>(s, v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next, grid); break;
       case 64022: launch_pf<2, 2, 64>(s, v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next, grid); break;
+#ifdef DAB_ABLATIONS  // timing ablations (wrong results)
       case 2012: launch_pf<1, 2, 2>(s, v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next, grid); break;
       case 4012: launch_pf<1, 2, 4>(s, v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next, grid); break;
       case 1012: launch_pf<1, 2, 1>(s, v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next, grid); break;
+#endif
       default: launch_pf<2, 2>(s, v, points, ext, V, g, partial, arrivals, cost, costfx, fx_next, grid); break;
     }
     return;
   }
-  if (wps == -5) {  // ablation: intrinsic index masked to the 128 staged in LDS (timing only)
+#ifdef DAB_ABLATIONS  // timing ablations (wrong results)
+  if (wps == -5) {  // intrinsic index masked to the 128 staged in LDS
     k_eval_points_lds<128, 2, true><<<grid, 1024, 0, s>>>(v, points, ext, camtab, V, g, partial, arrivals, cost);
     return;
   }
-  if (wps == 41) {  // ablations
-    k_eval_points<4, 1><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);
-  } else if (wps == 42) {
-    k_eval_points<4, 2><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);
-  } else if (wps == 16) {
+  if (wps == 41 || wps == 42) {
+    if (wps == 41) k_eval_points<4, 1><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);
+    else k_eval_points<4, 2><<<grid, 256, 0, s>>>(v, points, camtab, V, g, partial);
+    launch_final_sum(s, grid, 2, partial, cost);
+    return;
+  }
+#endif
+  if (wps == 16) {
     k_eval_points<16><<<grid, 1024, 0, s>>>(v, points, camtab, V, g, partial);
   } else if (wps == 8) {
     k_eval_points<8><<<grid, 512, 0, s>>>(v, points, camtab, V, g, partial);
@@ -2009,18 +2030,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
     pc += shp[w][0];
     bc += shp[w][1];
   }
-  long long hi = 0, lo = 0;
-  if (pc >= 0.0 && pc < 0x1p62) {
-    const double ip = trunc(pc);
-    hi = (long long)ip;
-    lo = (long long)rint((pc - ip) * 0x1p52);
-  } else {
-    bc += 1.0;
-  }
-  unsigned long long* shd = costfx + kFxStride * (blockIdx.x % kFxCopies);
-  if (hi) __hip_atomic_fetch_add(shd, (unsigned long long)hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (lo) __hip_atomic_fetch_add(shd + 1, (unsigned long long)lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (bc != 0.0) __hip_atomic_fetch_add(shd + 2, (unsigned long long)bc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  cost_fx_commit(pc, bc, costfx + kFxStride * (blockIdx.x % kFxCopies));
 }
 
 bool fused_eval_fits(const DevView& v, int nchunk, int ngen, int ncross, int grid) {
@@ -2057,12 +2067,13 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
     k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
     return;
   }
-  const int abl = getenv("DAB_FUSED_ABL") ? atoi(getenv("DAB_FUSED_ABL")) : 0;  // timing ablations
+#ifdef DAB_ABLATIONS
+  // timing ablations (wrong results; built only with -DDAB_ABLATIONS, read once)
+  static const int abl = getenv("DAB_FUSED_ABL") ? atoi(getenv("DAB_FUSED_ABL")) : 0;
   if (abl == 5)
     k_eval_fused<2, 5><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
   else if (abl == 25)
     k_eval_fused<2, 25><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
-
   else if (abl == 1) k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
   else if (abl == 2) k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
   else if (abl == 3) k_eval_fused<2, 3><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
@@ -2072,7 +2083,9 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
   else if (abl == 35) k_eval_fused<2, 0, 5><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
   else if (abl == 234) k_eval_fused<2, 2, 4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
   else if (abl == 14) k_eval_fused<4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
-  else k_eval_fused<2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+  else
+#endif
+    k_eval_fused<2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
 }
 
 // arc∘ring cross blocks Jc0^T Jc1, one block per chunk of composed observations sorted
@@ -2666,15 +2679,242 @@ __global__ void k_s_cross(int ncross, const int2* __restrict__ cross_cam, const 
   else S[(size_t)(6 * cc.y + b) * lds + 6 * cc.x + a] += v;
 }
 
+void launch_s_add_u(hipStream_t s, int NC, const double* ug, int ncross, const int2* cross_cam, const double* Ucross,
+                    const double* scale_c, StepScalars sc, const double* ybc, double* S, int lds) {
+  if (NC > 0) k_s_diag<<<grid_for(NC * 36, 256, 1 << 20), 256, 0, s>>>(NC, ug, scale_c, sc, ybc, S, lds);
+  if (ncross > 0)
+    k_s_cross<<<grid_for(ncross * 36, 256, 1 << 20), 256, 0, s>>>(ncross, cross_cam, Ucross, scale_c, S, lds);
+}
 void launch_s_unpack(hipStream_t s, int NC, int nblk, const int2* blk_cam, const double* packed,
                      const double* ug, int ncross, const int2* cross_cam, const double* Ucross,
                      const double* scale_c, StepScalars sc, const double* ybc, double* S, int lds) {
   const size_t n = (size_t)6 * NC;
   (void)hipMemsetAsync(S, 0, sizeof(double) * (n + 1) * lds, s);
   if (nblk > 0) k_s_scatter<<<grid_for(nblk * 36, 256, 1 << 20), 256, 0, s>>>(nblk, blk_cam, packed, S, lds);
-  if (NC > 0) k_s_diag<<<grid_for(NC * 36, 256, 1 << 20), 256, 0, s>>>(NC, ug, scale_c, sc, ybc, S, lds);
-  if (ncross > 0)
-    k_s_cross<<<grid_for(ncross * 36, 256, 1 << 20), 256, 0, s>>>(ncross, cross_cam, Ucross, scale_c, S, lds);
+  launch_s_add_u(s, NC, ug, ncross, cross_cam, Ucross, scale_c, sc, ybc, S, lds);
+}
+
+// --- explicit reduced camera system for small camera sets: tiled fixed-point assembly ---
+// DENSE_SCHUR's S = U~ + D^2 - sum_p Y_p Y_p^T (rows of Y_p: the point's distinct free
+// cameras, Y_{p,c} = sum over the point's entries on camera c of s_c o (J_c^T J_p) PU_p,
+// 6x3) without pair tables: every work-group holds one tile of the lower block triangle of
+// S (the blocks (c, d <= c) of a camera range [ca, cb)) in LDS, streams a group of points,
+// re-evaluates their entries' Y from the 32-B observation inputs and adds every product
+// Y_{p,c} Y_{p,d}^T of the tile into LDS with 64-bit integer atomics. The sums are kept in
+// fixed point: row R of Y is pre-scaled by 2^(30 - k_R) with 2^k_R >= sqrt(U~_RR), and
+// since sum_p |Y_{p,R}| |Y_{p,C}| <= sqrt(U~_RR U~_CC) (Cauchy-Schwarz, and
+// W V^-1 W^T <= U for the damped V), every partial sum of element (R, C) stays below 2^60
+// in units of 2^(k_R + k_C - 60): integer adds cannot wrap, and the result is the same in
+// any order, on any number of work-groups and of ranks (integer all-reduce). The rhs
+// sum_p Y_{p,c} q_p is accumulated the same way (sum_p |q_p|^2 <= sum r^2 = 2 cost).
+constexpr int kTileWaves = 8;    // waves per work-group
+constexpr int kTileTri = kTileBatch * (kTileBatch + 1) / 2;  // (i, j <= i) pairs of 32 distinct cameras
+struct TileWave {                // per-wave LDS scratch
+  double y[kTileBatch][18];      // Y of the batch's entries (runs summed into their head)
+  int cam[kTileBatch], pt[kTileBatch];
+  int drow[kTileBatch], dcam[kTileBatch];  // distinct (point, camera) records: row of y, camera
+  int pd0[kTileBatch + 1];       // first distinct record of each point of the batch
+};
+constexpr size_t kTileLdsFixed = sizeof(TileWave) * kTileWaves + sizeof(unsigned) * kTileTri;
+size_t schur_tile_lds_fixed() { return kTileLdsFixed; }
+
+__global__ __launch_bounds__(512) void k_schur_tiles(DevView v, const double* __restrict__ points,
+                                                     const double* __restrict__ camtab,
+                                                     const double* __restrict__ PU, const double* __restrict__ q,
+                                                     SchurTiles a) {
+  extern __shared__ __align__(16) unsigned char tile_lds[];
+  TileWave* tw = reinterpret_cast<TileWave*>(tile_lds);
+  unsigned* tri_tab = reinterpret_cast<unsigned*>(tw + kTileWaves);  // pair p -> i | j << 16
+  unsigned long long* acc = reinterpret_cast<unsigned long long*>(tile_lds + kTileLdsFixed);
+  const int t = blockIdx.x % a.ntile, g = blockIdx.x / a.ntile;
+  const int ca = a.tile_c0[t], cb = a.tile_c0[t + 1];
+  const int ebase = 36 * (int)tri_n(ca), ecount = 36 * (int)tri_n(cb) - ebase, rcount = 6 * (cb - ca);
+  unsigned long long* rhs = acc + ecount;
+  for (int i = threadIdx.x; i < ecount + rcount; i += blockDim.x) acc[i] = 0ull;
+  for (int p = threadIdx.x; p < kTileTri; p += blockDim.x) {
+    int i = (int)((sqrtf(8.0f * p + 1.0f) - 1.0f) * 0.5f);
+    while (tri_n(i + 1) <= p) ++i;
+    while (tri_n(i) > p) --i;
+    tri_tab[p] = (unsigned)i | ((unsigned)(p - tri_n(i)) << 16);
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  TileWave& W = tw[wave];
+  const GlobalTabs tabs{camtab, v.intr};
+  const int b0 = (int)((long long)a.nbatch * g / a.ngroup), b1 = (int)((long long)a.nbatch * (g + 1) / a.ngroup);
+  for (int b = b0 + wave; b < b1; b += kTileWaves) {
+    const int p0 = a.batch_pt[b], np = a.batch_pt[b + 1] - p0;
+    const int e0 = v.pt_ent_ptr[p0], ne = v.pt_ent_ptr[p0 + np] - e0;  // both <= kTileBatch
+    // ---- entry phase: lane = entry; Y re-evaluated (both slots' rows, the entry's kept)
+    const bool live = lane < ne;
+    int mycam = -1, mypt = -1;
+    if (live) {
+      const int2 se = a.sch_ent[e0 + lane];
+      const int pt = v.ent_pt[e0 + lane];
+      const int s = se.x >> 1;
+      const int4 id = v.obs_idx[s];
+      const double X[3] = {points[3 * (size_t)pt], points[3 * (size_t)pt + 1], points[3 * (size_t)pt + 2]};
+      double ru, rv, jx0[3], jx1[3], ja[6], jb[6], da[6], db[6];
+      obs_rows<true, 2>(id, v.obs_xy[s], X, tabs, ru, rv, jx0, jx1, ja, jb, da, db);
+      if (se.x & 1) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          ja[k] = da[k];
+          jb[k] = db[k];
+        }
+      }
+      double y[18];
+      make_y(ja, jb, jx0, jx1, a.scx + 6 * se.y, PU + 6 * (size_t)pt, y);
+#pragma unroll
+      for (int k = 0; k < 18; ++k) W.y[lane][k] = y[k];
+      mycam = se.y;
+      mypt = pt - p0;
+      W.cam[lane] = mycam;
+      W.pt[lane] = mypt;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- runs of one (point, camera) summed into their head (entries are sorted by
+    // camera inside a point); heads become the distinct records and add the rhs
+    const bool head = live && (lane == 0 || W.cam[lane - 1] != mycam || W.pt[lane - 1] != mypt);
+    const unsigned long long hmask = __ballot(head);
+    const unsigned hm = (unsigned)hmask;  // ne <= 32
+    if (head) {
+      const int didx = __popc(hm & ((1u << lane) - 1u));
+      double y[18];
+#pragma unroll
+      for (int k = 0; k < 18; ++k) y[k] = W.y[lane][k];
+      for (int r = lane + 1; r < ne && W.cam[r] == mycam && W.pt[r] == mypt; ++r)
+#pragma unroll
+        for (int k = 0; k < 18; ++k) y[k] += W.y[r][k];
+#pragma unroll
+      for (int k = 0; k < 18; ++k) W.y[lane][k] = y[k];
+      W.drow[didx] = lane;
+      W.dcam[didx] = mycam;
+      if (mycam >= ca && mycam < cb) {
+        const size_t pg = (size_t)(p0 + mypt);
+        const double q0 = q[4 * pg] * a.qscale, q1 = q[4 * pg + 1] * a.qscale, q2 = q[4 * pg + 2] * a.qscale;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+          const double val = y[3 * r] * q0 + y[3 * r + 1] * q1 + y[3 * r + 2] * q2;
+          __hip_atomic_fetch_add(rhs + 6 * (mycam - ca) + r, (unsigned long long)__double2ll_rn(val),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    }
+    // distinct range of point l: the heads below its first and below its end entry
+    if (lane <= np) {
+      const int eb = lane < np ? v.pt_ent_ptr[p0 + lane] - e0 : ne;
+      W.pd0[lane] = __popc(hm & (eb >= 32 ? 0xffffffffu : ((1u << eb) - 1u)));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- pair phase, per point: lanes = (pair (i, j <= i) with camera i in the tile, row r)
+    for (int pl = 0; pl < np; ++pl) {
+      const int d0 = W.pd0[pl], m = W.pd0[pl + 1] - d0;
+      const int dc = lane < m ? W.dcam[d0 + lane] : 1 << 30;
+      const int i0 = __popcll(__ballot(dc < ca)), i1 = __popcll(__ballot(dc < cb));
+      const int pbase = (int)tri_n(i0), npair6 = 6 * ((int)tri_n(i1) - pbase);
+      for (int k = lane; k < npair6; k += 64) {
+        const int pi = k / 6, r = k - 6 * pi;
+        const unsigned ij = tri_tab[pbase + pi];
+        const int i = (int)(ij & 0xffffu), j = (int)(ij >> 16);
+        const int ri = W.drow[d0 + i], rj = W.drow[d0 + j];
+        const int ci = W.dcam[d0 + i], cj = W.dcam[d0 + j];
+        const double y0 = W.y[ri][3 * r], y1 = W.y[ri][3 * r + 1], y2 = W.y[ri][3 * r + 2];
+        unsigned long long* dst = acc + (36 * (int)tri_n(ci) + 36 * cj - ebase) + 6 * r;
+#pragma unroll
+        for (int s2 = 0; s2 < 6; ++s2) {
+          const double val = y0 * W.y[rj][3 * s2] + y1 * W.y[rj][3 * s2 + 1] + y2 * W.y[rj][3 * s2 + 2];
+          __hip_atomic_fetch_add(dst + s2, (unsigned long long)__double2ll_rn(val), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  __syncthreads();
+  // the group's tile and rhs partials: [group][elements (lower block triangle) | rhs (6 NC)]
+  unsigned long long* out = a.partial + (size_t)g * a.stride;
+  for (int i = threadIdx.x; i < ecount; i += blockDim.x) out[ebase + i] = acc[i];
+  for (int i = threadIdx.x; i < rcount; i += blockDim.x) out[a.nelem + 6 * ca + i] = rhs[i];
+}
+
+// Row exponents: k_R with 2^k_R >= sqrt(s_R^2 U_RR) (U from ug, all-reduced), scx = s_c 2^(30 - k)
+__global__ void k_schur_scale(int NC, const double* __restrict__ ug, const double* __restrict__ scc,
+                              double* __restrict__ scx, int* __restrict__ kx) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 6 * NC) return;
+  const int c = i / 6, a = i - 6 * c;
+  const double s = scc[i];
+  const double u = s * s * ug[27 * (size_t)c + a * 6 - (a * (a - 1)) / 2];
+  int k = 0;
+  if (u > 0.0 && isfinite(u)) {
+    int e;
+    (void)frexp(u, &e);  // u < 2^e, so sqrt(u) < 2^ceil(e/2)
+    k = (e + 1) >> 1;
+  }
+  kx[i] = k;
+  scx[i] = ldexp(s, 30 - k);
+}
+
+// integer sum over the groups' partials (fixed order irrelevant: exact)
+__global__ void k_schur_sum(int ngroup, size_t stride, size_t count, const unsigned long long* __restrict__ partial,
+                            unsigned long long* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  unsigned long long s = 0;
+  for (int g = 0; g < ngroup; ++g) s += partial[(size_t)g * stride + i];
+  out[i] = s;
+}
+
+// dense S lower (rows 0..n-1) = -(fixed-point Schur part), ybc = -(rhs part); the U part,
+// D^2 and the rhs row follow (k_s_diag, k_s_cross)
+__global__ void k_schur_unpack(int NC, const unsigned long long* __restrict__ sfx, const int* __restrict__ kx,
+                               int kq, double* __restrict__ S, int lds, double* __restrict__ ybc) {
+  const int n = 6 * NC;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nlow = (size_t)tri_n(n);
+  if (t < nlow) {
+    int R = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while (tri_n(R + 1) <= (long long)t) ++R;
+    while (tri_n(R) > (long long)t) --R;
+    const int C = (int)(t - tri_n(R));
+    const int c = R / 6, r = R - 6 * c, d = C / 6, s = C - 6 * d;
+    const long long v = (long long)sfx[36 * tri_n(c) + 36 * d + 6 * r + s];
+    S[(size_t)R * lds + C] = -ldexp((double)v, kx[R] + kx[C] - 60);
+  } else if (t < nlow + (size_t)n) {
+    const int R = (int)(t - nlow);
+    const long long v = (long long)sfx[36 * tri_n(NC) + R];
+    ybc[R] = -ldexp((double)v, kx[R] + kq - 60);
+  }
+}
+
+void launch_schur_tiles(hipStream_t s, const DevView& v, const double* points, const double* camtab, const double* PU,
+                        const double* q, const SchurTiles& a, size_t lds_bytes) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_schur_tiles), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kTileLdsMax);
+    attr = true;
+  }
+  k_schur_tiles<<<a.ntile * a.ngroup, 512, lds_bytes, s>>>(v, points, camtab, PU, q, a);
+}
+void launch_schur_scale(hipStream_t s, int NC, const double* ug, const double* scale_c, double* scx, int* kx) {
+  if (NC > 0) k_schur_scale<<<grid_for(6 * NC, 256, 1 << 20), 256, 0, s>>>(NC, ug, scale_c, scx, kx);
+}
+void launch_schur_sum(hipStream_t s, int ngroup, size_t stride, size_t count, const unsigned long long* partial,
+                      unsigned long long* out) {
+  if (count > 0) k_schur_sum<<<(unsigned)((count + 255) / 256), 256, 0, s>>>(ngroup, stride, count, partial, out);
+}
+void launch_schur_unpack(hipStream_t s, int NC, const unsigned long long* sfx, const int* kx, int kq, double* S,
+                         int lds, double* ybc) {
+  const size_t n = (size_t)6 * NC, cnt = (size_t)tri_n((long long)n) + n;
+  if (cnt > 0) k_schur_unpack<<<(unsigned)((cnt + 255) / 256), 256, 0, s>>>(NC, sfx, kx, kq, S, lds, ybc);
 }
 
 // delta_p = -PU (q - sum_e Y_e^T y_c): lane = point, walking its SELL observation slots

@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <array>
 #include <chrono>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -104,9 +105,42 @@ int upload(T** dptr, Dev& dev, const std::vector<T>& h, hipStream_t s) {
   return 0;
 }
 
+// Tuning / test knobs from the environment, read once when the handle is created (never
+// on a launch path). Unset = the production default.
+struct Knobs {
+  int chunk = 0;            // DAB_CHUNK: entries per camera-side reduction chunk (0: kChunk)
+  int pair_eval = -1;       // DAB_PAIR_EVAL=0: rig camera side camera-major + cross passes
+  int eval_wps = INT_MIN;   // DAB_EVAL_WPS: point-kernel variant of the two-kernel pass
+  int free_cus = 8;         // DAB_EVAL_FREE_CUS: CUs the multi-rank point kernel leaves free
+  int eval_fused = 1;       // DAB_EVAL_FUSED=0: two-kernel pass even where the fused one fits
+  int eval_split = 0;       // DAB_EVAL_SPLIT=1: the multi-rank split schedule on one rank
+  int pcg_fused = 1;        // DAB_PCG_FUSED=0
+  int pcg_mf = 1;           // DAB_PCG_MF=0: stored-Y PCG even for small camera sets
+  int cg_onewg = 0;         // DAB_CG_ONEWG=1: single-work-group CG update
+  int bench_sample = 8;     // DAB_BENCH_SAMPLE: timing-event stride of dab_bench_eval_pass
+  int schur_tiles = 1;      // DAB_SCHUR_TILES=0: explicit S from the pair tables even for small NC
+  void read() {
+    auto get = [](const char* name, int& out) {
+      if (const char* e = getenv(name)) out = atoi(e);
+    };
+    get("DAB_CHUNK", chunk);
+    get("DAB_PAIR_EVAL", pair_eval);
+    get("DAB_EVAL_WPS", eval_wps);
+    get("DAB_EVAL_FREE_CUS", free_cus);
+    get("DAB_EVAL_FUSED", eval_fused);
+    get("DAB_EVAL_SPLIT", eval_split);
+    get("DAB_PCG_FUSED", pcg_fused);
+    get("DAB_PCG_MF", pcg_mf);
+    get("DAB_CG_ONEWG", cg_onewg);
+    get("DAB_BENCH_SAMPLE", bench_sample);
+    get("DAB_SCHUR_TILES", schur_tiles);
+  }
+};
+
 }  // namespace
 
 struct dab_handle {
+  Knobs knobs;
   int device = 0;
   int rank = 0, world = 1;
   hipStream_t stream = nullptr;
@@ -138,7 +172,7 @@ struct dab_handle {
   bool schur_built = false;
   bool pcg_built = false;
   int nxlist = 0;
-  std::vector<int> h_pt_ent_ptr, h_ent_cam, h_ent_pos;  // kept for build_schur_tables
+  std::vector<int> h_pt_ent_ptr, h_ent_cam, h_ent_pos, h_ent_os;  // kept for build_schur_tables
 
   // ---- device buffers ----
   Dev dev;
@@ -182,6 +216,13 @@ struct dab_handle {
   double *d_partial2 = nullptr, *d_xcpart = nullptr;
   double* d_spack = nullptr;   // [packed nblk*36 | ybc NC*6] (all-reduced)
   double* d_S = nullptr;
+  // explicit S by fixed-point tiles (small camera sets, k_schur_tiles)
+  bool schur_tiles = false;
+  SchurTiles tiles{};
+  size_t tile_lds = 0;
+  double* d_scx = nullptr;
+  int* d_kx = nullptr;
+  unsigned long long* d_sfx = nullptr;  // [stride] group sums (all-reduced as integers)
   // implicit-Schur PCG (lazily allocated)
   double *d_pcg_b = nullptr, *d_pcg_r = nullptr, *d_pcg_z = nullptr, *d_pcg_p = nullptr, *d_pcg_q = nullptr,
          *d_pcg_w = nullptr, *d_pcg_Ad = nullptr, *d_pcg_Minv = nullptr, *d_pcg_red = nullptr,
@@ -339,6 +380,7 @@ static int create_common(int device, dab_handle** out) {
   HIP_OK(hipSetDevice(device));
   dab_handle* h = new dab_handle();
   h->device = device;
+  h->knobs.read();
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
     delete h;
     return set_error(DAB_E_DEVICE, "hipStreamCreate failed");
@@ -576,8 +618,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
     for (int e = 0; e < NE; ++e) cam_ent[fill[ent_cam[e]]++] = e;
   }
   // entries per reduction chunk (one block each); DAB_CHUNK is a tuning knob
-  const char* chunk_env = getenv("DAB_CHUNK");
-  const int chunk = std::max(64, chunk_env ? atoi(chunk_env) : kChunk);
+  const int chunk = std::max(64, h->knobs.chunk > 0 ? h->knobs.chunk : kChunk);
   std::vector<int> chunk_beg, seg_chunk(NC + 1, 0);
   for (int c = 0; c < NC; ++c) {
     seg_chunk[c] = (int)chunk_beg.size();
@@ -706,10 +747,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   std::vector<int4> cm2_idx;
   std::vector<double2> cm2_xy;
   std::vector<int> chunk2_beg, seg2_chunk(NC + 1, 0), xcam_ptr(NC + 1, 0), xcam_list;
-  {
-    const char* pe = getenv("DAB_PAIR_EVAL");
-    h->pair_eval = h->nxchunk > 0 && pair_eval_fits(h->E, h->NI) && !(pe && atoi(pe) == 0);
-  }
+  h->pair_eval = h->nxchunk > 0 && pair_eval_fits(h->E, h->NI) && h->knobs.pair_eval != 0;
   if (h->pair_eval) {
     for (int c = 0; c < NC; ++c) {
       seg2_chunk[c] = (int)chunk2_beg.size();
@@ -743,7 +781,9 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   h->h_pt_ent_ptr = pt_ent_ptr;
   h->h_ent_cam = ent_cam;
   h->h_ent_pos = ent_pos;
+  h->h_ent_os = ent_os;
   h->schur_built = false;
+  h->schur_tiles = false;
   h->pcg_built = false;
   h->nblk = 0;
   h->npairs = 0;
@@ -848,8 +888,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   {
     // point-side kernel: LDS-staged camera tables when they fit (persistent grid, one
     // 1024-thread work-group per CU), else global tables (one block per slice).
-    const char* env = getenv("DAB_EVAL_WPS");
-    h->eval_wps = env ? atoi(env) : (eval_points_lds_fits(h->E) ? -2 : 4);
+    h->eval_wps = h->knobs.eval_wps != INT_MIN ? h->knobs.eval_wps : (eval_points_lds_fits(h->E) ? -2 : 4);
     int ncu = 256;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, h->device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -862,15 +901,10 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
     // free for them (DAB_EVAL_FREE_CUS overrides; its slices are dealt round robin over
     // whatever grid it gets).
     int pcus = ncu;
-    if (h->world > 1 && h->eval_wps <= 0) {
-      const char* fc = getenv("DAB_EVAL_FREE_CUS");
-      pcus = std::max(1, ncu - (fc ? atoi(fc) : 8));
-    }
+    if (h->world > 1 && h->eval_wps <= 0) pcus = std::max(1, ncu - h->knobs.free_cus);
     h->eval_grid = h->eval_wps <= 0 ? std::max(1, std::min(pcus, h->nslice)) : std::max(1, h->nslice);
-    const char* fenv = getenv("DAB_EVAL_FUSED");
-    h->fused = !fenv || atoi(fenv) != 0;
-    const char* senv = getenv("DAB_EVAL_SPLIT");  // the split schedule on one rank too (tests)
-    h->fused_split = h->world > 1 || (senv && atoi(senv) != 0);
+    h->fused = h->knobs.eval_fused != 0;
+    h->fused_split = h->world > 1 || h->knobs.eval_split != 0;  // the split schedule on one rank too (tests)
   }
   CHECK_RC(d.alloc(&h->d_gpart, (size_t)std::max(h->red_grid, h->eval_grid) * 4));
   CHECK_RC(d.alloc(&h->d_scal, S_NSLOTS));
@@ -917,6 +951,82 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
 // sorted by block so each block is one deterministic segment. The block table is the
 // union over ranks so the all-reduced packed layout matches.
 static constexpr long long kMaxExplicitPairs = 200000000LL;
+static int max_all_ranks(dab_handle* h, double& x) {  // max over ranks of one host scalar
+  if (h->world <= 1) return 0;
+  hipStream_t s = h->stream;
+  double* d_f = nullptr;
+  CHECK_RC(h->dev.alloc(&d_f, 1));
+  HIP_OK(hipMemcpyAsync(d_f, &x, sizeof(double), hipMemcpyHostToDevice, s));
+  CHECK_RC(h->allreduce(d_f, 1, ncclMax));
+  HIP_OK(hipMemcpyAsync(&x, d_f, sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return 0;
+}
+
+// Explicit S by fixed-point tiles (k_schur_tiles) when the camera set is small (the
+// matrix-free criterion: tables in LDS, NC <= 160) and every point has at most kTileBatch
+// entries. Tables: each point's entries sorted by camera, batches of whole points (<= 32
+// entries and points), tiles of the lower block triangle sized to the LDS.
+static int build_schur_tiles(dab_handle* h) {
+  hipStream_t s = h->stream;
+  const int NP = h->NP, NC = h->NC;
+  const std::vector<int>& pt_ent_ptr = h->h_pt_ent_ptr;
+  const std::vector<int>& ent_cam = h->h_ent_cam;
+  const std::vector<int>& ent_os = h->h_ent_os;
+  std::vector<int2> sch(h->NE);
+  std::vector<int> batch{0};
+  int cur_e = 0, cur_p = 0;
+  for (int p = 0; p < NP; ++p) {
+    const int b = pt_ent_ptr[p], e = pt_ent_ptr[p + 1], m = e - b;
+    for (int i = b; i < e; ++i) sch[i] = make_int2(ent_os[i], ent_cam[i]);
+    std::sort(sch.begin() + b, sch.begin() + e, [](const int2& x, const int2& y) {
+      return x.y != y.y ? x.y < y.y : x.x < y.x;
+    });
+    if (cur_p > 0 && (cur_e + m > kTileBatch || cur_p + 1 > kTileBatch)) {
+      batch.push_back(p);
+      cur_e = cur_p = 0;
+    }
+    cur_e += m;
+    cur_p += 1;
+  }
+  batch.push_back(NP);
+  // tiles: camera ranges whose blocks (c, d <= c) and rhs rows fit the LDS left over
+  const size_t cap = (kTileLdsMax - schur_tile_lds_fixed()) / sizeof(unsigned long long);
+  std::vector<int> tc{0};
+  size_t maxuse = 0;
+  while (tc.back() < NC) {
+    const int ca = tc.back();
+    int cb = ca + 1;
+    auto use = [&](int hi) { return (size_t)(36 * (tri_n(hi) - tri_n(ca)) + 6 * (long long)(hi - ca)); };
+    while (cb < NC && use(cb + 1) <= cap) ++cb;
+    maxuse = std::max(maxuse, use(cb));
+    tc.push_back(cb);
+  }
+  SchurTiles& a = h->tiles;
+  a.ntile = (int)tc.size() - 1;
+  a.nbatch = (int)batch.size() - 1;
+  a.ngroup = std::max(1, std::min(h->ncu / a.ntile, a.nbatch));
+  a.nelem = (int)(36 * tri_n(NC));
+  a.stride = (size_t)a.nelem + 6 * (size_t)NC;
+  a.qscale = 1.0;
+  h->tile_lds = schur_tile_lds_fixed() + sizeof(unsigned long long) * maxuse;
+  Dev& d = h->dev;
+  int *d_tc = nullptr, *d_batch = nullptr;
+  int2* d_sch = nullptr;
+  CHECK_RC(upload(&d_tc, d, tc, s));
+  CHECK_RC(upload(&d_batch, d, batch, s));
+  CHECK_RC(upload(&d_sch, d, sch, s));
+  a.tile_c0 = d_tc;
+  a.batch_pt = d_batch;
+  a.sch_ent = d_sch;
+  CHECK_RC(d.alloc(&h->d_scx, (size_t)6 * NC));
+  CHECK_RC(d.alloc(&h->d_kx, (size_t)6 * NC));
+  CHECK_RC(d.alloc(&a.partial, (size_t)a.ngroup * a.stride));
+  CHECK_RC(d.alloc(&h->d_sfx, a.stride));
+  HIP_OK(hipStreamSynchronize(s));
+  return 0;
+}
+
 static int build_schur_tables(dab_handle* h) {
   if (h->schur_built) return 0;
   hipStream_t s = h->stream;
@@ -924,20 +1034,35 @@ static int build_schur_tables(dab_handle* h) {
   const std::vector<int>& pt_ent_ptr = h->h_pt_ent_ptr;
   const std::vector<int>& ent_cam = h->h_ent_cam;
   const std::vector<int>& ent_pos = h->h_ent_pos;
+  {
+    // tile mode: every rank must take the same branch (the all-reduced S layouts differ)
+    int maxm = 0;
+    for (int pt = 0; pt < NP; ++pt) maxm = std::max(maxm, pt_ent_ptr[pt + 1] - pt_ent_ptr[pt]);
+    double no_tiles = (h->knobs.schur_tiles != 0 && NC > 0 && mf_schur_fits(NC, h->E, h->NI) && maxm <= kTileBatch)
+                          ? 0.0 : 1.0;
+    CHECK_RC(max_all_ranks(h, no_tiles));
+    h->schur_tiles = no_tiles == 0.0;
+  }
+  if (h->schur_tiles) {
+    CHECK_RC(build_schur_tiles(h));
+    h->nblk = 0;
+    h->npairs = 0;
+    CHECK_RC(h->dev.alloc(&h->d_spack, h->spack_count()));  // ybc only
+    const int n = 6 * NC;
+    h->lds = ((n + 1 + 7) / 8) * 8;
+    if (h->lds % 512 == 0) h->lds += 8;
+    CHECK_RC(h->dev.alloc(&h->d_S, (size_t)(n + 1) * h->lds));
+    h->mf_grid_n = mf_grid(h->NP, h->ncu);
+    h->schur_built = true;
+    return 0;
+  }
   long long total = 0;
   for (int pt = 0; pt < NP; ++pt) {
     const long long m = pt_ent_ptr[pt + 1] - pt_ent_ptr[pt];
     total += m * (m + 1) / 2 + m;  // upper bound
   }
   double flag = total > kMaxExplicitPairs ? 1.0 : 0.0;
-  if (h->world > 1) {  // every rank must take the same branch
-    double* d_f = nullptr;
-    CHECK_RC(h->dev.alloc(&d_f, 1));
-    HIP_OK(hipMemcpyAsync(d_f, &flag, sizeof(double), hipMemcpyHostToDevice, s));
-    CHECK_RC(h->allreduce(d_f, 1, ncclMax));
-    HIP_OK(hipMemcpyAsync(&flag, d_f, sizeof(double), hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
-  }
+  CHECK_RC(max_all_ranks(h, flag));  // every rank must take the same branch
   if (flag != 0.0)
     return set_error(DAB_E_UNSUPPORTED,
                      "reduced camera system too large for explicit Schur pair tables (" +
@@ -1013,6 +1138,9 @@ static int build_schur_tables(dab_handle* h) {
   h->lds = ((n + 1 + 7) / 8) * 8;
   if (h->lds % 512 == 0) h->lds += 8;  // avoid power-of-two row strides
   CHECK_RC(d.alloc(&h->d_S, NC > 0 ? (size_t)(n + 1) * h->lds : 1));
+  // Y as [NE][18] records for k_s_blocks (allocated here so that an OOM surfaces before
+  // iteration 0, not mid-solve)
+  if (NC > 0) CHECK_RC(d.alloc(&h->d_Yrec, (size_t)kYRec * std::max(1, h->NE)));
   HIP_OK(hipStreamSynchronize(s));
   h->schur_built = true;
   return 0;
@@ -1034,14 +1162,12 @@ static int build_pcg_buffers(dab_handle* h) {
   CHECK_RC(d.alloc(&h->d_cg_cnt, 1));
   HIP_OK(hipMemsetAsync(h->d_cg_cnt, 0, sizeof(unsigned), h->stream));
   // the single-pass matvec when the camera system is small (DAB_PCG_FUSED=0 disables it)
-  const char* fz = getenv("DAB_PCG_FUSED");
-  const char* mfe = getenv("DAB_PCG_MF");
-  h->mf = mf_schur_fits(h->NC, h->E, h->NI) && h->NP > 0 && !(mfe && atoi(mfe) == 0);
+  h->mf = mf_schur_fits(h->NC, h->E, h->NI) && h->NP > 0 && h->knobs.pcg_mf != 0;
   if (h->mf) {
     h->mf_grid_n = mf_grid(h->NP, h->ncu);
     CHECK_RC(d.alloc(&h->d_mf_partial, (size_t)h->mf_grid_n * 6 * h->NC));
   }
-  if (pcg_fused_fits(h->NC) && h->NP > 0 && !(fz && atoi(fz) == 0)) {
+  if (pcg_fused_fits(h->NC) && h->NP > 0 && h->knobs.pcg_fused != 0) {
     h->fused_grid = pcg_fused_grid(h->NP, h->ncu);
     CHECK_RC(d.alloc(&h->d_fused_partial, (size_t)h->fused_grid * 6 * h->NC));
   }
@@ -1097,8 +1223,7 @@ static int pcg_solve(dab_handle* h, const dab_options& opt, StepScalars sc, YBuf
                   max_it, h->d_pcg_Minv, h->d_pcg_r, h->d_pcg_z, h->d_pcg_p);
   const int* xptr = h->nxlist > 0 ? h->d_xptr : nullptr;
   // the CG update: spread over work-groups (default) or one work-group (DAB_CG_ONEWG=1)
-  const char* one = getenv("DAB_CG_ONEWG");
-  const bool onewg = one && atoi(one) != 0;
+  const bool onewg = h->knobs.cg_onewg != 0;
   auto update = [&](int mode) {
     if (onewg)
       launch_pcg_update(s, NC, mode, h->d_pcg_Ad, h->d_pcg_w, xptr, h->d_xlist, h->d_cross_cam, h->Ux(),
@@ -1297,17 +1422,11 @@ static int read_scalars(dab_handle* h) {
   HIP_OK(hipMemcpyAsync(h->h_flags, h->d_flags, sizeof(int) * 4, hipMemcpyDeviceToHost, h->stream));
   HIP_OK(hipStreamSynchronize(h->stream));
   if (h->cost_fx_pending) {
-    // the last evaluation pass left its cost in fixed point (cost_fx_add): exact integer
-    // sums, converted once here
-    uint64_t fx[3] = {0, 0, 0};
-    for (int c = 0; c < kFxCopies; ++c)
-      for (int i = 0; i < 3; ++i) {
-        uint64_t w;
-        std::memcpy(&w, h->h_scal + S_CFX + (size_t)kFxWords * h->fx_last + kFxStride * c + i, sizeof(uint64_t));
-        fx[i] += w;
-      }
-    h->h_scal[S_COST] = (double)(int64_t)fx[0] + (double)(int64_t)fx[1] * 0x1p-52;
-    h->h_scal[S_COST_BAD] = (double)fx[2];
+    // the last evaluation pass left its cost in fixed point (cost_fx_commit): exact
+    // integer limb sums, converted once here
+    unsigned long long w[kFxWords];
+    std::memcpy(w, h->h_scal + S_CFX + (size_t)kFxWords * h->fx_last, sizeof(w));
+    cost_fx_total(w, h->h_scal[S_COST], h->h_scal[S_COST_BAD]);
     h->cost_fx_pending = false;
   }
   return 0;
@@ -1395,6 +1514,8 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
   sum->residual_evaluation_time_in_seconds = 0;
   sum->linear_solver_time_in_seconds = 0;
   sum->termination_type = DAB_FAILURE;
+  sum->linear_solver_type_used = opt.linear_solver_type;
+  sum->schur_assembly = use_pcg ? (h->mf ? 1 : 0) : (h->schur_tiles ? DAB_SCHUR_TILES : DAB_SCHUR_PAIRS);
   const bool verbose = opt.minimizer_progress_to_stdout && h->rank == 0;
   const bool in_global = true;  (void)in_global;
 
@@ -1495,9 +1616,28 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
       CHECK_RC(pcg_solve(h, opt, sc, yb, &cg_iters, &cg_status));
       it.linear_solver_iterations = cg_iters;
       pcg_fail = cg_status == kPcgFailure;
+    } else if (NC > 0 && h->schur_tiles) {
+      // S by fixed-point tiles: Y re-evaluated per tile, integer sums (all-reduced exactly)
+      SchurTiles a = h->tiles;
+      int kq = 0;
+      if (x_cost > 0.0 && std::isfinite(x_cost)) {
+        int e2;
+        (void)std::frexp(2.0 * x_cost, &e2);  // sum_p |q_p|^2 <= 2 cost < 2^e2
+        kq = (e2 + 1) >> 1;
+      }
+      a.qscale = std::ldexp(1.0, 30 - kq);
+      a.scx = h->d_scx;
+      launch_schur_scale(s, NC, h->ug(), h->d_scale_c, h->d_scx, h->d_kx);
+      launch_schur_tiles(s, v, h->d_points, h->d_camtab, h->d_L, h->d_q, a, h->tile_lds);
+      launch_schur_sum(s, a.ngroup, a.stride, a.stride, a.partial, h->d_sfx);
+      CHECK_RC(h->allreduce_u64(reinterpret_cast<uint64_t*>(h->d_sfx), a.stride));
+      HIP_OK(hipMemsetAsync(h->d_S, 0, sizeof(double) * (size_t)(n + 1) * h->lds, s));
+      launch_schur_unpack(s, NC, h->d_sfx, h->d_kx, kq, h->d_S, h->lds, h->ybc());
+      launch_s_add_u(s, NC, h->ug(), h->ncross, h->d_cross_cam, h->Ux(), h->d_scale_c, sc, h->ybc(), h->d_S, h->lds);
+      if (chol_factor_solve(h->chol, s, n, h->d_S, h->lds, h->d_yc, h->d_flags + 1) != 0)
+        return set_error(DAB_E_DEVICE, "dense Cholesky launch failed");
     } else if (NC > 0) {
       launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, yb, true);
-      if (!h->d_Yrec) CHECK_RC(h->dev.alloc(&h->d_Yrec, (size_t)kYRec * std::max(1, h->NE)));
       launch_s_blocks(s, h->nblk, h->d_blk_pair_beg, h->d_pairs, h->d_Y, h->NE, h->packed(), h->d_Yrec);
       launch_cam_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_Y, h->d_q, h->d_partial);
       launch_seg_final(s, NC, 6, h->d_seg_chunk, h->d_partial, h->ybc(), h->max_seg_chunks);
@@ -1507,7 +1647,7 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
       if (chol_factor_solve(h->chol, s, n, h->d_S, h->lds, h->d_yc, h->d_flags + 1) != 0)
         return set_error(DAB_E_DEVICE, "dense Cholesky launch failed");
     }
-    if (use_pcg && h->mf)
+    if ((use_pcg && h->mf) || (!use_pcg && h->schur_tiles))
       launch_mf_backsub(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, h->d_q, h->d_yc, h->d_dp, h->mf_grid_n);
     else
       launch_backsub(s, v, h->d_L, h->d_q, yb, NC > 0 ? h->d_yc : nullptr, h->d_dp);
@@ -1744,8 +1884,6 @@ extern "C" int dab_dense_spd_solve(dab_handle* h, int n, const double* A, const 
 // benchmark hooks
 // ------------------------------------------------------------------------------------
 // accumulate the timings of the recorded bench steps (waits for the last one)
-constexpr int kBenchSample = 8;
-
 static int collect_bench_events(dab_handle* h) {
   if (h->bench_pending == 0) return 0;
   HIP_OK(hipEventSynchronize(h->bench_ev[h->bench_pending - 1][3]));
@@ -1769,11 +1907,10 @@ extern "C" int dab_bench_eval_pass(dab_handle* h, int with_assembly, int count) 
   if (count < 0) return set_error(DAB_E_INVALID, "negative pass count");
   HIP_OK(hipSetDevice(h->device));
   hipStream_t s = h->stream;
-  // Timing events bracket every kBenchSample-th pass of the batch (the first one always):
+  // Timing events bracket every 8th pass (Knobs::bench_sample) of the batch (the first one always):
   // even fence-free, four event records add ~10 us to a ~40 us pass, so timing every pass
   // would distort the throughput it measures. DAB_BENCH_SAMPLE overrides (0 = no events).
-  const char* env = getenv("DAB_BENCH_SAMPLE");
-  const int sample = env ? atoi(env) : kBenchSample;
+  const int sample = h->knobs.bench_sample;
   for (int step = 0; step < count; ++step) {
     if (sample <= 0 || step % sample != 0) {
       CHECK_RC(eval_pass(h, false));

@@ -19,7 +19,12 @@ int solveWith(DeepArcManager& m, const dab_options& options, bool freeze_camera,
   dab_summary* s = summary ? summary : &local;
   rc = dab_solve(dh.h, &options, s);
   if (rc == DAB_E_UNSUPPORTED && options.linear_solver_type == DAB_LINEAR_SOLVER_EXPLICIT_SCHUR) {
-    // the explicit reduced system would not fit: same LM with the implicit-Schur PCG step
+    // The explicit reduced system is refused only when it is both too large for the LDS
+    // tiles (more than 160 free cameras) and too large for the pair tables (> 2e8 entry
+    // pairs). The step is then the inexact implicit-Schur PCG one: say so, and the summary
+    // records it (linear_solver_type_used), so the result is not read as DENSE_SCHUR parity.
+    std::fprintf(stderr, "solve: DENSE_SCHUR refused (%s); running ITERATIVE_SCHUR (PCG) instead\n",
+                 dab_last_error());
     dab_options o = options;
     o.linear_solver_type = DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG;
     rc = dab_solve(dh.h, &o, s);
@@ -39,7 +44,8 @@ void solve(DeepArcManager& deeparcManager, int max_iteration, int max_second, bo
   o.max_solver_time_in_seconds = max_second;                // sfm.cc:71
   dab_summary s{};
   dab_check(solveWith(deeparcManager, o, freeze_camera, &s));
-  std::printf("Solver Summary: initial cost %.6e, final cost %.6e, %d iterations (%d successful), %s\n",
+  std::printf("Solver Summary: %s, initial cost %.6e, final cost %.6e, %d iterations (%d successful), %s\n",
+              s.linear_solver_type_used == DAB_LINEAR_SOLVER_EXPLICIT_SCHUR ? "DENSE_SCHUR" : "ITERATIVE_SCHUR (PCG)",
               s.initial_cost, s.final_cost, s.num_iterations, s.num_successful_steps, s.message);
 }
 

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DAB_ABI_VERSION 1
+#define DAB_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define DAB_OK 0
@@ -155,7 +155,13 @@ typedef struct dab_summary {
   dab_iteration* iterations;       /* optional caller buffer (may be NULL) */
   int32_t iterations_capacity;     /* entries available in `iterations` */
   int32_t iterations_written;      /* entries filled */
+  int32_t linear_solver_type_used; /* the DAB_LINEAR_SOLVER_* that ran (the requested one) */
+  int32_t schur_assembly;          /* EXPLICIT_SCHUR: DAB_SCHUR_* (how S was assembled);
+                                      IMPLICIT_SCHUR_PCG: 1 matrix-free products, 0 stored Y */
 } dab_summary;
+/* schur_assembly values for DAB_LINEAR_SOLVER_EXPLICIT_SCHUR */
+#define DAB_SCHUR_PAIRS 0   /* per camera-pair block sums over entry-pair tables (large NC) */
+#define DAB_SCHUR_TILES 1   /* fixed-point LDS tiles of S, Y re-evaluated (NC <= 160) */
 
 typedef struct dab_handle dab_handle;
 

@@ -346,10 +346,11 @@ def test_fused_camera_frame_small_angles(pkg, gpu, monkeypatch):
         s.close()
     assert sched == [1, 0]
     a, b = res
-    assert [it["linear_solver_iterations"] for it in a["iterations"]] == \
-        [it["linear_solver_iterations"] for it in b["iterations"]]
-    np.testing.assert_allclose([it["cost"] for it in a["iterations"]], [it["cost"] for it in b["iterations"]],
-                               rtol=1e-10)
+    assert [it["success"] for it in a["iterations"]] == [it["success"] for it in b["iterations"]]
+    # accepted costs to 1e-10; the rejected candidates here are wild steps (costs ~1e23 from
+    # ~1e7) whose cost amplifies the regrouped U, g_c rounding, so they get 1e-8
+    for x, y in zip(a["iterations"], b["iterations"]):
+        assert x["cost"] == pytest.approx(y["cost"], rel=1e-10 if x["success"] else 1e-8), (x, y)
 
 
 @pytest.mark.parametrize("kind", ["bal", "c2"])
@@ -503,3 +504,59 @@ def test_full_size_c3_properties(pkg, orc, gpu):
     assert all(b < a for a, b in zip(acc, acc[1:]))
     assert summ["final_cost"] < 0.05 * summ["initial_cost"]
     np.testing.assert_array_equal(prob.ext[0], ext0)
+
+
+@pytest.mark.parametrize("kind", ["bal", "rig"])
+def test_schur_tiles_match_pair_tables(pkg, gpu, kind, monkeypatch):
+    """EXPLICIT_SCHUR on small camera sets assembles S from fixed-point LDS tiles
+    (k_schur_tiles, Y re-evaluated, integer sums); DAB_SCHUR_TILES=0 forces the camera-pair
+    block sums over entry-pair tables. Same LM trajectory (cost 1e-10 relative, same
+    iteration count and termination); the tile path is bitwise repeatable and the summary
+    names the assembly that ran."""
+    if kind == "bal":
+        prob = pkg.synth(kind=0, num_cameras=70, num_points=5000, obs_per_point=8, seed=71)
+    else:
+        prob = pkg.synth(kind=1, num_arcs=6, num_rings=16, num_points=3000, obs_per_point=8, seed=72)
+    res, pts = [], []
+    for tiles in ("1", "0", "1"):
+        monkeypatch.setenv("DAB_SCHUR_TILES", tiles)
+        p = prob.copy()
+        s = pkg.Solver(0)
+        s.set_problem(p)
+        res.append(s.solve(pkg.options(max_num_iterations=12)))
+        s.close()
+        pts.append(p.points.copy())
+    a, b = res[0], res[1]
+    assert a["schur_assembly"] == 1 and b["schur_assembly"] == 0
+    assert a["linear_solver_type_used"] == pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR
+    assert len(a["iterations"]) == len(b["iterations"]) and a["termination"] == b["termination"]
+    np.testing.assert_allclose([it["cost"] for it in a["iterations"]], [it["cost"] for it in b["iterations"]],
+                               rtol=1e-10)
+    np.testing.assert_array_equal(pts[0], pts[2])
+
+
+@pytest.mark.parametrize("kind", ["bal", "rig"])
+def test_large_initial_cost_matches_oracle(pkg, orc, gpu, kind):
+    """A finite cost far beyond the old fixed-point range is an ordinary evaluation for
+    Ceres: the solve proceeds. (1) The problem in pixel units scaled by 1e8 (focal lengths,
+    principal points and observations; the same problem up to the residual scale, initial
+    cost >= 1e20): the full trajectory must match the oracle's. (2) One observation 1e11 px
+    off: the initial cost matches and the solve is not a FAILURE (its rejected candidates
+    are too ill-conditioned to compare)."""
+    if kind == "bal":
+        prob = pkg.synth(kind=0, num_cameras=30, num_points=2000, obs_per_point=6, seed=73)
+    else:
+        prob = pkg.synth(kind=1, num_arcs=5, num_rings=10, num_points=2000, obs_per_point=6, seed=74)
+    big = prob.copy()
+    big.intr[:, :4] *= 1e8
+    big.obs_xy *= 1e8
+    g, o, ref = run_both(pkg, orc, big, max_num_iterations=10)
+    assert g["initial_cost"] >= 1e20
+    assert_same_trajectory(g, o, big, ref)
+    out = prob.copy()
+    out.obs_xy[17] = [1.0e11, -3.0e10]
+    g, o, ref = run_both(pkg, orc, out, max_num_iterations=10)
+    assert g["initial_cost"] >= 1e20
+    assert g["initial_cost"] == pytest.approx(o["initial_cost"], rel=1e-12)
+    assert g["termination"] != "FAILURE", g["message"]
+    assert [it["success"] for it in g["iterations"]] == [it["success"] for it in o["iterations"]]
