@@ -162,32 +162,41 @@ void launch_entry_y(hipStream_t s, const DevView& v, const double* points, const
 // Y = the fp64 camera-major planes, stride NE; Yr = scratch [NE][18] for the records)
 void launch_s_blocks(hipStream_t s, int nblk, const int* blk_pair_beg, const int2* pairs,
                      const double* Y, int NE, double* packed, double* Yr);
-// Explicit S for small camera sets without pair tables (k_schur_tiles): tiles of the lower
-// block triangle of S in LDS, fixed-point 64-bit integer sums (exact, order-free). Element
-// (c, d <= c, r, s) of the Schur part sits at 36 (c (c+1)/2 + d) + 6 r + s, the rhs part of
-// row 6 c + r at nelem + 6 c + r, in units of 2^(kx[R] + kx[C] - 60) / 2^(kx[R] + kq - 60).
-constexpr size_t kTileLdsMax = 163840;  // dynamic LDS of one k_schur_tiles work-group
-constexpr int kTileBatch = 32;          // entries (and points) per wave batch
+// Explicit S for small camera sets without pair tables (k_schur_y + k_schur_tiles): every
+// thread of a work-group owns one 6x6 block of the lower block triangle of S (numbered
+// row-major: block (c, d <= c) = c (c+1)/2 + d) and sums it in registers over the records of
+// its group of points; fp64, one fixed order per block. The rhs part is summed in fixed point:
+// row 6 c + r in units of 2^(kx[R] + kq - 60).
+constexpr int kMfCamsMax = 160;  // small camera sets (matrix-free PCG, explicit S tiles)
+constexpr int kTileMaxRec = 32;  // distinct free cameras per point (tile path limit)
 __host__ __device__ inline long long tri_n(long long i) { return (i * (i + 1)) >> 1; }
 struct SchurTiles {
   int ntile, ngroup, nbatch, nelem;  // nelem = 36 NC (NC + 1) / 2
-  const int* tile_c0;                // [ntile + 1] camera bounds of the tiles
-  const int* batch_pt;               // [nbatch + 1] first point of each batch (<= 32 entries, <= 32 points)
+  int nrec;                          // records: distinct (point, free camera) pairs
+  int kq;                            // rhs exponent: 2^kq >= sqrt(2 cost)
+  const int* tile_b0;                // [ntile + 1] block bounds of the tiles (<= 1024 blocks each)
+  const int* batch_rec;              // [nbatch + 1] first record of each batch (<= batch_cap, whole points)
+  const int* batch_pt;               // [nbatch] first point of each batch (<= 64 points)
+  int batch_cap;                     // records per batch (LDS capacity)
+  const int4* rec_info;              // [nrec] (first entry in sch_ent, entry count, point, camera)
+  const int* rec_cam;                // [nrec] camera of each record
   const int2* sch_ent;               // [NE] (ent_os, camera), sorted by camera inside each point
-  const double* scx;                 // [6 NC] s_c 2^(30 - kx)
-  double qscale;                     // 2^(30 - kq)
-  unsigned long long* partial;       // [ngroup][stride]
-  size_t stride;                     // nelem + 6 NC
+  const int* kx;                     // [6 NC] rhs row exponents (launch_schur_scale)
+  double* partial;                   // [ngroup][stride] per-group block sums
+  size_t stride;                     // nelem
 };
-size_t schur_tile_lds_fixed();       // LDS of the per-wave scratch (the tile gets the rest)
-void launch_schur_scale(hipStream_t s, int NC, const double* ug, const double* scale_c, double* scx, int* kx);
-void launch_schur_tiles(hipStream_t s, const DevView& v, const double* points, const double* camtab, const double* PU,
-                        const double* q, const SchurTiles& a, size_t lds_bytes);
-void launch_schur_sum(hipStream_t s, int ngroup, size_t stride, size_t count, const unsigned long long* partial,
-                      unsigned long long* out);
+constexpr size_t kTileLdsMax = 163840;            // LDS of one k_schur_tiles work-group (at most)
+int schur_tile_batch_cap(int NC);                 // records per batch that fit the LDS
+void launch_schur_scale(hipStream_t s, int NC, const double* ug, const double* scale_c, int* kx);
+// Y of every record -> yrec[nrec][18]; rhs fixed-point sums added into rhs_out[6 NC]
+void launch_schur_y(hipStream_t s, const DevView& v, const double* points, const double* camtab, const double* PU,
+                    const double* q, const double* scale_c, const SchurTiles& a, double* yrec,
+                    unsigned long long* rhs_out);
+void launch_schur_tiles(hipStream_t s, const double* yrec, const SchurTiles& a, int NC);
+void launch_schur_sum(hipStream_t s, int ngroup, size_t stride, size_t count, const double* partial, double* out);
 // S lower rows 0..n-1 = -Schur part, ybc = -rhs part (then launch_s_add_u)
-void launch_schur_unpack(hipStream_t s, int NC, const unsigned long long* sfx, const int* kx, int kq, double* S,
-                         int lds, double* ybc);
+void launch_schur_unpack(hipStream_t s, int NC, const double* sblk, const unsigned long long* rfx, const int* kx,
+                         int kq, double* S, int lds, double* ybc);
 // adds the U part (+ D^2) and cross blocks, writes the rhs row n = s_c g_c + ybc
 void launch_s_add_u(hipStream_t s, int NC, const double* ug, int ncross, const int2* cross_cam, const double* Ucross,
                     const double* scale_c, StepScalars sc, const double* ybc, double* S, int lds);

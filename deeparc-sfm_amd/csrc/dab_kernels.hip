@@ -2694,159 +2694,188 @@ void launch_s_unpack(hipStream_t s, int NC, int nblk, const int2* blk_cam, const
   launch_s_add_u(s, NC, ug, ncross, cross_cam, Ucross, scale_c, sc, ybc, S, lds);
 }
 
-// --- explicit reduced camera system for small camera sets: tiled fixed-point assembly ---
-// DENSE_SCHUR's S = U~ + D^2 - sum_p Y_p Y_p^T (rows of Y_p: the point's distinct free
-// cameras, Y_{p,c} = sum over the point's entries on camera c of s_c o (J_c^T J_p) PU_p,
-// 6x3) without pair tables: every work-group holds one tile of the lower block triangle of
-// S (the blocks (c, d <= c) of a camera range [ca, cb)) in LDS, streams a group of points,
-// re-evaluates their entries' Y from the 32-B observation inputs and adds every product
-// Y_{p,c} Y_{p,d}^T of the tile into LDS with 64-bit integer atomics. The sums are kept in
-// fixed point: row R of Y is pre-scaled by 2^(30 - k_R) with 2^k_R >= sqrt(U~_RR), and
-// since sum_p |Y_{p,R}| |Y_{p,C}| <= sqrt(U~_RR U~_CC) (Cauchy-Schwarz, and
-// W V^-1 W^T <= U for the damped V), every partial sum of element (R, C) stays below 2^60
-// in units of 2^(k_R + k_C - 60): integer adds cannot wrap, and the result is the same in
-// any order, on any number of work-groups and of ranks (integer all-reduce). The rhs
-// sum_p Y_{p,c} q_p is accumulated the same way (sum_p |q_p|^2 <= sum r^2 = 2 cost).
-constexpr int kTileWaves = 8;    // waves per work-group
-constexpr int kTileTri = kTileBatch * (kTileBatch + 1) / 2;  // (i, j <= i) pairs of 32 distinct cameras
-struct TileWave {                // per-wave LDS scratch
-  double y[kTileBatch][18];      // Y of the batch's entries (runs summed into their head)
-  int cam[kTileBatch], pt[kTileBatch];
-  int drow[kTileBatch], dcam[kTileBatch];  // distinct (point, camera) records: row of y, camera
-  int pd0[kTileBatch + 1];       // first distinct record of each point of the batch
-};
-constexpr size_t kTileLdsFixed = sizeof(TileWave) * kTileWaves + sizeof(unsigned) * kTileTri;
-size_t schur_tile_lds_fixed() { return kTileLdsFixed; }
+// --- explicit reduced camera system for small camera sets: register-owned block tiles ---
+// DENSE_SCHUR's S = U~ + D^2 - sum_p Y_p Y_p^T without pair tables. A record is one distinct
+// (point, free camera) pair, Y_{p,c} = sum over the point's entries on camera c of
+// s_c o (J_c^T J_p) PU_p (6x3). k_schur_y re-evaluates every record once per LM step into
+// HBM (records of a point contiguous, cameras ascending) and adds the rhs sum_p Y_{p,c} q_p
+// in fixed point. k_schur_tiles: the lower block triangle of S (blocks (c, d <= c), numbered
+// row-major) is cut into tiles of <= 1024 blocks; in a work-group every thread OWNS one block
+// and keeps its 36 sums in registers. The work-group streams the records of a group of points
+// in batches through LDS (with a per-camera bit mask of the batch's points and a (point,
+// camera) -> record table), and each thread walks the points that see both of its cameras in
+// batch order. No atomics: each block's sum has one fixed order (groups' partials then added
+// in group order), so the result is bitwise reproducible.
+constexpr int kTileThreads = 512;             // threads per work-group (two blocks each)
+// LDS of a work-group: y[batch records][18] | mask[NC] (points of the batch seeing camera c) |
+// recof[64][NC] ((point, camera) -> record of the batch); the batch capacity fills the rest
+size_t schur_tile_lds_bytes(int NC, int batch_rec) {
+  return sizeof(double) * 18 * (size_t)batch_rec + sizeof(unsigned long long) * NC + sizeof(unsigned short) * 64 * NC;
+}
+int schur_tile_batch_cap(int NC) {
+  const size_t fixed = schur_tile_lds_bytes(NC, 0);
+  return (int)((kTileLdsMax - fixed) / (18 * sizeof(double)));
+}
 
-__global__ __launch_bounds__(512) void k_schur_tiles(DevView v, const double* __restrict__ points,
-                                                     const double* __restrict__ camtab,
-                                                     const double* __restrict__ PU, const double* __restrict__ q,
-                                                     SchurTiles a) {
-  extern __shared__ __align__(16) unsigned char tile_lds[];
-  TileWave* tw = reinterpret_cast<TileWave*>(tile_lds);
-  unsigned* tri_tab = reinterpret_cast<unsigned*>(tw + kTileWaves);  // pair p -> i | j << 16
-  unsigned long long* acc = reinterpret_cast<unsigned long long*>(tile_lds + kTileLdsFixed);
-  const int t = blockIdx.x % a.ntile, g = blockIdx.x / a.ntile;
-  const int ca = a.tile_c0[t], cb = a.tile_c0[t + 1];
-  const int ebase = 36 * (int)tri_n(ca), ecount = 36 * (int)tri_n(cb) - ebase, rcount = 6 * (cb - ca);
-  unsigned long long* rhs = acc + ecount;
-  for (int i = threadIdx.x; i < ecount + rcount; i += blockDim.x) acc[i] = 0ull;
-  for (int p = threadIdx.x; p < kTileTri; p += blockDim.x) {
-    int i = (int)((sqrtf(8.0f * p + 1.0f) - 1.0f) * 0.5f);
-    while (tri_n(i + 1) <= p) ++i;
-    while (tri_n(i) > p) --i;
-    tri_tab[p] = (unsigned)i | ((unsigned)(p - tri_n(i)) << 16);
-  }
+// k_schur_y: thread per record; tables staged in LDS; rhs partials of the work-group in LDS
+// (fixed point, 2^(60 - kx[R] - kq) units), then one global integer atomic per rhs row.
+__global__ __launch_bounds__(256) void k_schur_y(DevView v, const double* __restrict__ points,
+                                                 const double* __restrict__ camtab, const double* __restrict__ PU,
+                                                 const double* __restrict__ q, const double* __restrict__ scc,
+                                                 SchurTiles a, double* __restrict__ yrec,
+                                                 unsigned long long* __restrict__ rhs_out) {
+  extern __shared__ __align__(16) double ylds[];
+  const SmallTabs st = stage_small_tabs(ylds, v.E, v.NI, camtab, v.intr);
+  unsigned long long* rhs = reinterpret_cast<unsigned long long*>(ylds + 30 * (size_t)v.E + 6 * (size_t)v.NI);
+  for (int i = threadIdx.x; i < 6 * v.NC; i += blockDim.x) rhs[i] = 0ull;
   __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  TileWave& W = tw[wave];
-  const GlobalTabs tabs{camtab, v.intr};
-  const int b0 = (int)((long long)a.nbatch * g / a.ngroup), b1 = (int)((long long)a.nbatch * (g + 1) / a.ngroup);
-  for (int b = b0 + wave; b < b1; b += kTileWaves) {
-    const int p0 = a.batch_pt[b], np = a.batch_pt[b + 1] - p0;
-    const int e0 = v.pt_ent_ptr[p0], ne = v.pt_ent_ptr[p0 + np] - e0;  // both <= kTileBatch
-    // ---- entry phase: lane = entry; Y re-evaluated (both slots' rows, the entry's kept)
-    const bool live = lane < ne;
-    int mycam = -1, mypt = -1;
-    if (live) {
-      const int2 se = a.sch_ent[e0 + lane];
-      const int pt = v.ent_pt[e0 + lane];
-      const int s = se.x >> 1;
-      const int4 id = v.obs_idx[s];
-      const double X[3] = {points[3 * (size_t)pt], points[3 * (size_t)pt + 1], points[3 * (size_t)pt + 2]};
+  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < a.nrec; r += gridDim.x * blockDim.x) {
+    const int4 ri = a.rec_info[r];  // (first sorted entry, count, point, camera)
+    const int pt = ri.z, cam = ri.w;
+    const double X[3] = {points[3 * (size_t)pt], points[3 * (size_t)pt + 1], points[3 * (size_t)pt + 2]};
+    double y[18];
+#pragma unroll
+    for (int k = 0; k < 18; ++k) y[k] = 0.0;
+    for (int e = ri.x; e < ri.x + ri.y; ++e) {
+      const int os = a.sch_ent[e].x, sl = os >> 1;
+      const int4 id = v.obs_idx[sl];
       double ru, rv, jx0[3], jx1[3], ja[6], jb[6], da[6], db[6];
-      obs_rows<true, 2>(id, v.obs_xy[s], X, tabs, ru, rv, jx0, jx1, ja, jb, da, db);
-      if (se.x & 1) {
+      obs_rows<true, 2>(id, v.obs_xy[sl], X, st, ru, rv, jx0, jx1, ja, jb, da, db);
+      if (os & 1) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
           ja[k] = da[k];
           jb[k] = db[k];
         }
       }
-      double y[18];
-      make_y(ja, jb, jx0, jx1, a.scx + 6 * se.y, PU + 6 * (size_t)pt, y);
+      double ye[18];
+      make_y(ja, jb, jx0, jx1, scc + 6 * cam, PU + 6 * (size_t)pt, ye);
 #pragma unroll
-      for (int k = 0; k < 18; ++k) W.y[lane][k] = y[k];
-      mycam = se.y;
-      mypt = pt - p0;
-      W.cam[lane] = mycam;
-      W.pt[lane] = mypt;
+      for (int k = 0; k < 18; ++k) y[k] += ye[k];
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- runs of one (point, camera) summed into their head (entries are sorted by
-    // camera inside a point); heads become the distinct records and add the rhs
-    const bool head = live && (lane == 0 || W.cam[lane - 1] != mycam || W.pt[lane - 1] != mypt);
-    const unsigned long long hmask = __ballot(head);
-    const unsigned hm = (unsigned)hmask;  // ne <= 32
-    if (head) {
-      const int didx = __popc(hm & ((1u << lane) - 1u));
-      double y[18];
+    double2* o = reinterpret_cast<double2*>(yrec + 18 * (size_t)r);
 #pragma unroll
-      for (int k = 0; k < 18; ++k) y[k] = W.y[lane][k];
-      for (int r = lane + 1; r < ne && W.cam[r] == mycam && W.pt[r] == mypt; ++r)
+    for (int k = 0; k < 9; ++k) o[k] = make_double2(y[2 * k], y[2 * k + 1]);
+    const double q0 = q[4 * (size_t)pt], q1 = q[4 * (size_t)pt + 1], q2 = q[4 * (size_t)pt + 2];
 #pragma unroll
-        for (int k = 0; k < 18; ++k) y[k] += W.y[r][k];
-#pragma unroll
-      for (int k = 0; k < 18; ++k) W.y[lane][k] = y[k];
-      W.drow[didx] = lane;
-      W.dcam[didx] = mycam;
-      if (mycam >= ca && mycam < cb) {
-        const size_t pg = (size_t)(p0 + mypt);
-        const double q0 = q[4 * pg] * a.qscale, q1 = q[4 * pg + 1] * a.qscale, q2 = q[4 * pg + 2] * a.qscale;
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-          const double val = y[3 * r] * q0 + y[3 * r + 1] * q1 + y[3 * r + 2] * q2;
-          __hip_atomic_fetch_add(rhs + 6 * (mycam - ca) + r, (unsigned long long)__double2ll_rn(val),
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      }
+    for (int k = 0; k < 6; ++k) {
+      const double val = ldexp(y[3 * k] * q0 + y[3 * k + 1] * q1 + y[3 * k + 2] * q2, 60 - a.kx[6 * cam + k] - a.kq);
+      __hip_atomic_fetch_add(rhs + 6 * cam + k, (unsigned long long)__double2ll_rn(val), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    // distinct range of point l: the heads below its first and below its end entry
-    if (lane <= np) {
-      const int eb = lane < np ? v.pt_ent_ptr[p0 + lane] - e0 : ne;
-      W.pd0[lane] = __popc(hm & (eb >= 32 ? 0xffffffffu : ((1u << eb) - 1u)));
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- pair phase, per point: lanes = (pair (i, j <= i) with camera i in the tile, row r)
-    for (int pl = 0; pl < np; ++pl) {
-      const int d0 = W.pd0[pl], m = W.pd0[pl + 1] - d0;
-      const int dc = lane < m ? W.dcam[d0 + lane] : 1 << 30;
-      const int i0 = __popcll(__ballot(dc < ca)), i1 = __popcll(__ballot(dc < cb));
-      const int pbase = (int)tri_n(i0), npair6 = 6 * ((int)tri_n(i1) - pbase);
-      for (int k = lane; k < npair6; k += 64) {
-        const int pi = k / 6, r = k - 6 * pi;
-        const unsigned ij = tri_tab[pbase + pi];
-        const int i = (int)(ij & 0xffffu), j = (int)(ij >> 16);
-        const int ri = W.drow[d0 + i], rj = W.drow[d0 + j];
-        const int ci = W.dcam[d0 + i], cj = W.dcam[d0 + j];
-        const double y0 = W.y[ri][3 * r], y1 = W.y[ri][3 * r + 1], y2 = W.y[ri][3 * r + 2];
-        unsigned long long* dst = acc + (36 * (int)tri_n(ci) + 36 * cj - ebase) + 6 * r;
-#pragma unroll
-        for (int s2 = 0; s2 < 6; ++s2) {
-          const double val = y0 * W.y[rj][3 * s2] + y1 * W.y[rj][3 * s2 + 1] + y2 * W.y[rj][3 * s2 + 2];
-          __hip_atomic_fetch_add(dst + s2, (unsigned long long)__double2ll_rn(val), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   __syncthreads();
-  // the group's tile and rhs partials: [group][elements (lower block triangle) | rhs (6 NC)]
-  unsigned long long* out = a.partial + (size_t)g * a.stride;
-  for (int i = threadIdx.x; i < ecount; i += blockDim.x) out[ebase + i] = acc[i];
-  for (int i = threadIdx.x; i < rcount; i += blockDim.x) out[a.nelem + 6 * ca + i] = rhs[i];
+  for (int i = threadIdx.x; i < 6 * v.NC; i += blockDim.x)
+    if (rhs[i]) __hip_atomic_fetch_add(rhs_out + i, rhs[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Row exponents: k_R with 2^k_R >= sqrt(s_R^2 U_RR) (U from ug, all-reduced), scx = s_c 2^(30 - k)
+// one owned block's sums over the batch's points that see both of its cameras (batch order)
+__device__ __forceinline__ void tile_block_hits(const double* __restrict__ ly, const unsigned short* __restrict__ recof,
+                                                const unsigned long long* __restrict__ mask, int NC, int c, int d,
+                                                double (&acc)[36]) {
+  unsigned long long m = mask[c] & mask[d];
+  while (m) {
+    const int pl = __builtin_ctzll(m);
+    m &= m - 1;
+    const double* pi = ly + 18 * recof[pl * NC + c];
+    const double2* pj = reinterpret_cast<const double2*>(ly + 18 * recof[pl * NC + d]);
+    double yj[18];
+#pragma unroll
+    for (int u = 0; u < 9; ++u) {
+      const double2 z = pj[u];
+      yj[2 * u] = z.x;
+      yj[2 * u + 1] = z.y;
+    }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const double y0 = pi[3 * r], y1 = pi[3 * r + 1], y2 = pi[3 * r + 2];
+#pragma unroll
+      for (int s2 = 0; s2 < 6; ++s2)
+        acc[6 * r + s2] = fma(y2, yj[3 * s2 + 2], fma(y1, yj[3 * s2 + 1], fma(y0, yj[3 * s2], acc[6 * r + s2])));
+    }
+  }
+}
+__device__ __forceinline__ int tri_row(int bl) {  // c with c (c+1)/2 <= bl < (c+1)(c+2)/2
+  int c = (int)((sqrtf(8.0f * bl + 1.0f) - 1.0f) * 0.5f);
+  while (tri_n(c + 1) <= bl) ++c;
+  while (tri_n(c) > bl) --c;
+  return c;
+}
+
+// Each thread owns two blocks of the tile (bl and bl + kTileThreads): 72 sums in registers,
+// and the two blocks' hit counts add up, which evens out the lanes' work per batch.
+__global__ __launch_bounds__(kTileThreads) void k_schur_tiles(const double* __restrict__ yrec, SchurTiles a, int NC) {
+  extern __shared__ __align__(16) unsigned char tile_lds[];
+  double* ly = reinterpret_cast<double*>(tile_lds);
+  unsigned long long* mask = reinterpret_cast<unsigned long long*>(ly + 18 * (size_t)a.batch_cap);
+  unsigned short* recof = reinterpret_cast<unsigned short*>(mask + NC);
+  // XCD-aware placement: the tiles of one group of points run on one XCD (blocks b and b + 8
+  // share one), so the group's records come from HBM once and from that L2 for the others
+  int t, g;
+  if (a.ngroup % 8 == 0) {
+    const int x = blockIdx.x & 7, y = blockIdx.x >> 3;
+    t = y % a.ntile;
+    g = (y / a.ntile) * 8 + x;
+  } else {
+    t = blockIdx.x % a.ntile;
+    g = blockIdx.x / a.ntile;
+  }
+  const int bt0 = a.tile_b0[t], bt1 = a.tile_b0[t + 1];
+  const int blA = bt0 + (int)threadIdx.x, blB = blA + kTileThreads;
+  const bool ownA = blA < bt1, ownB = blB < bt1;
+  int cA = 0, dA = 0, cB = 0, dB = 0;
+  if (ownA) {
+    cA = tri_row(blA);
+    dA = blA - (int)tri_n(cA);
+  }
+  if (ownB) {
+    cB = tri_row(blB);
+    dB = blB - (int)tri_n(cB);
+  }
+  const int clast = tri_row(bt1 - 1);  // the tile's last row camera
+  double accA[36], accB[36];
+#pragma unroll
+  for (int k = 0; k < 36; ++k) accA[k] = accB[k] = 0.0;
+  for (int i = threadIdx.x; i < NC; i += blockDim.x) mask[i] = 0ull;
+  const int b0 = (int)((long long)a.nbatch * g / a.ngroup), b1 = (int)((long long)a.nbatch * (g + 1) / a.ngroup);
+  for (int b = b0; b < b1; ++b) {
+    const int r0 = a.batch_rec[b], nr = a.batch_rec[b + 1] - r0, p0 = a.batch_pt[b];
+    __syncthreads();  // masks zeroed, previous batch consumed
+    // the batch's records on cameras up to the tile's last row camera into LDS
+    for (int i = threadIdx.x; i < nr; i += blockDim.x) {
+      const int4 ri = a.rec_info[r0 + i];
+      if (ri.w <= clast) {
+        recof[(ri.z - p0) * NC + ri.w] = (unsigned short)i;
+        __hip_atomic_fetch_or(&mask[ri.w], 1ull << (ri.z - p0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    for (int i = threadIdx.x; i < 9 * nr; i += blockDim.x) {
+      const int rr = i / 9, k = i - 9 * rr;
+      if (a.rec_cam[r0 + rr] <= clast)
+        reinterpret_cast<double2*>(ly + 18 * rr)[k] = reinterpret_cast<const double2*>(yrec + 18 * (size_t)(r0 + rr))[k];
+    }
+    __syncthreads();
+    if (ownA) tile_block_hits(ly, recof, mask, NC, cA, dA, accA);
+    if (ownB) tile_block_hits(ly, recof, mask, NC, cB, dB, accB);
+    __syncthreads();
+    for (int i = threadIdx.x; i < NC; i += blockDim.x) mask[i] = 0ull;
+  }
+  double* out = a.partial + (size_t)g * a.stride;
+  if (ownA) {
+    double2* o = reinterpret_cast<double2*>(out + 36 * (size_t)blA);
+#pragma unroll
+    for (int k = 0; k < 18; ++k) o[k] = make_double2(accA[2 * k], accA[2 * k + 1]);
+  }
+  if (ownB) {
+    double2* o = reinterpret_cast<double2*>(out + 36 * (size_t)blB);
+#pragma unroll
+    for (int k = 0; k < 18; ++k) o[k] = make_double2(accB[2 * k], accB[2 * k + 1]);
+  }
+}
+
+// Row exponents of the fixed-point rhs: 2^kx[R] >= sqrt(s_R^2 U_RR) (U from ug, all-reduced)
 __global__ void k_schur_scale(int NC, const double* __restrict__ ug, const double* __restrict__ scc,
-                              double* __restrict__ scx, int* __restrict__ kx) {
+                              int* __restrict__ kx) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 6 * NC) return;
   const int c = i / 6, a = i - 6 * c;
@@ -2859,23 +2888,23 @@ __global__ void k_schur_scale(int NC, const double* __restrict__ ug, const doubl
     k = (e + 1) >> 1;
   }
   kx[i] = k;
-  scx[i] = ldexp(s, 30 - k);
 }
 
-// integer sum over the groups' partials (fixed order irrelevant: exact)
-__global__ void k_schur_sum(int ngroup, size_t stride, size_t count, const unsigned long long* __restrict__ partial,
-                            unsigned long long* __restrict__ out) {
+// sum over the groups' partials in group order (fixed: bitwise reproducible)
+__global__ void k_schur_sum(int ngroup, size_t stride, size_t count, const double* __restrict__ partial,
+                            double* __restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
-  unsigned long long s = 0;
+  double s = 0.0;
   for (int g = 0; g < ngroup; ++g) s += partial[(size_t)g * stride + i];
   out[i] = s;
 }
 
-// dense S lower (rows 0..n-1) = -(fixed-point Schur part), ybc = -(rhs part); the U part,
-// D^2 and the rhs row follow (k_s_diag, k_s_cross)
-__global__ void k_schur_unpack(int NC, const unsigned long long* __restrict__ sfx, const int* __restrict__ kx,
-                               int kq, double* __restrict__ S, int lds, double* __restrict__ ybc) {
+// dense S lower (rows 0..n-1) = -(Schur part), ybc = -(fixed-point rhs part); the U part, D^2
+// and the rhs row follow (launch_s_add_u)
+__global__ void k_schur_unpack(int NC, const double* __restrict__ sblk, const unsigned long long* __restrict__ rfx,
+                               const int* __restrict__ kx, int kq, double* __restrict__ S, int lds,
+                               double* __restrict__ ybc) {
   const int n = 6 * NC;
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t nlow = (size_t)tri_n(n);
@@ -2885,36 +2914,40 @@ __global__ void k_schur_unpack(int NC, const unsigned long long* __restrict__ sf
     while (tri_n(R) > (long long)t) --R;
     const int C = (int)(t - tri_n(R));
     const int c = R / 6, r = R - 6 * c, d = C / 6, s = C - 6 * d;
-    const long long v = (long long)sfx[36 * tri_n(c) + 36 * d + 6 * r + s];
-    S[(size_t)R * lds + C] = -ldexp((double)v, kx[R] + kx[C] - 60);
+    S[(size_t)R * lds + C] = -sblk[36 * tri_n(c) + 36 * d + 6 * r + s];
   } else if (t < nlow + (size_t)n) {
     const int R = (int)(t - nlow);
-    const long long v = (long long)sfx[36 * tri_n(NC) + R];
-    ybc[R] = -ldexp((double)v, kx[R] + kq - 60);
+    ybc[R] = -ldexp((double)(long long)rfx[R], kx[R] + kq - 60);
   }
 }
 
-void launch_schur_tiles(hipStream_t s, const DevView& v, const double* points, const double* camtab, const double* PU,
-                        const double* q, const SchurTiles& a, size_t lds_bytes) {
+void launch_schur_y(hipStream_t s, const DevView& v, const double* points, const double* camtab, const double* PU,
+                    const double* q, const double* scale_c, const SchurTiles& a, double* yrec,
+                    unsigned long long* rhs_out) {
+  if (a.nrec <= 0) return;
+  const size_t lds = small_tabs_bytes(v.E, v.NI) + sizeof(unsigned long long) * 6 * (size_t)v.NC;
+  k_schur_y<<<std::min(grid_for(a.nrec, 256, 1 << 20), kSmallGrid), 256, lds, s>>>(v, points, camtab, PU, q, scale_c,
+                                                                                   a, yrec, rhs_out);
+}
+void launch_schur_tiles(hipStream_t s, const double* yrec, const SchurTiles& a, int NC) {
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_schur_tiles), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)kTileLdsMax);
     attr = true;
   }
-  k_schur_tiles<<<a.ntile * a.ngroup, 512, lds_bytes, s>>>(v, points, camtab, PU, q, a);
+  k_schur_tiles<<<a.ntile * a.ngroup, kTileThreads, schur_tile_lds_bytes(NC, a.batch_cap), s>>>(yrec, a, NC);
 }
-void launch_schur_scale(hipStream_t s, int NC, const double* ug, const double* scale_c, double* scx, int* kx) {
-  if (NC > 0) k_schur_scale<<<grid_for(6 * NC, 256, 1 << 20), 256, 0, s>>>(NC, ug, scale_c, scx, kx);
+void launch_schur_scale(hipStream_t s, int NC, const double* ug, const double* scale_c, int* kx) {
+  if (NC > 0) k_schur_scale<<<grid_for(6 * NC, 256, 1 << 20), 256, 0, s>>>(NC, ug, scale_c, kx);
 }
-void launch_schur_sum(hipStream_t s, int ngroup, size_t stride, size_t count, const unsigned long long* partial,
-                      unsigned long long* out) {
+void launch_schur_sum(hipStream_t s, int ngroup, size_t stride, size_t count, const double* partial, double* out) {
   if (count > 0) k_schur_sum<<<(unsigned)((count + 255) / 256), 256, 0, s>>>(ngroup, stride, count, partial, out);
 }
-void launch_schur_unpack(hipStream_t s, int NC, const unsigned long long* sfx, const int* kx, int kq, double* S,
-                         int lds, double* ybc) {
+void launch_schur_unpack(hipStream_t s, int NC, const double* sblk, const unsigned long long* rfx, const int* kx,
+                         int kq, double* S, int lds, double* ybc) {
   const size_t n = (size_t)6 * NC, cnt = (size_t)tri_n((long long)n) + n;
-  if (cnt > 0) k_schur_unpack<<<(unsigned)((cnt + 255) / 256), 256, 0, s>>>(NC, sfx, kx, kq, S, lds, ybc);
+  if (cnt > 0) k_schur_unpack<<<(unsigned)((cnt + 255) / 256), 256, 0, s>>>(NC, sblk, rfx, kx, kq, S, lds, ybc);
 }
 
 // delta_p = -PU (q - sum_e Y_e^T y_c): lane = point, walking its SELL observation slots
@@ -2974,7 +3007,7 @@ __global__ __launch_bounds__(256) void k_backsub(DevView v, const double* __rest
 // sweeps over a point's SELL rows (lane = point); the camera sums go to per-wave LDS
 // accumulators (LDS atomics only between the lanes of one instruction; waves, then
 // work-groups, summed in fixed order: bitwise repeatable). All arithmetic fp64.
-constexpr int kMfCams = 160;
+constexpr int kMfCams = kMfCamsMax;
 constexpr int kMfBlock = 256;
 bool mf_schur_fits(int NC, int E, int NI) { return NC > 0 && NC <= kMfCams && small_tabs_fit(E, NI); }
 // LDS: tables | s_c o vec [NC][6] | per-wave camera sums [4][NC][6] (products): <= 40 KB for

@@ -219,10 +219,10 @@ struct dab_handle {
   // explicit S by fixed-point tiles (small camera sets, k_schur_tiles)
   bool schur_tiles = false;
   SchurTiles tiles{};
-  size_t tile_lds = 0;
-  double* d_scx = nullptr;
-  int* d_kx = nullptr;
-  unsigned long long* d_sfx = nullptr;  // [stride] group sums (all-reduced as integers)
+  int* d_kx = nullptr;                  // [6 NC] rhs row exponents
+  double* d_sblk = nullptr;             // [nelem] Schur part of S by block (group sums, all-reduced)
+  unsigned long long* d_rfx = nullptr;  // [6 NC] fixed-point rhs part (all-reduced as integers)
+  double* d_yrec = nullptr;             // [nrec][18] Y of every record (this LM step)
   // implicit-Schur PCG (lazily allocated)
   double *d_pcg_b = nullptr, *d_pcg_r = nullptr, *d_pcg_z = nullptr, *d_pcg_p = nullptr, *d_pcg_q = nullptr,
          *d_pcg_w = nullptr, *d_pcg_Ad = nullptr, *d_pcg_Minv = nullptr, *d_pcg_red = nullptr,
@@ -963,10 +963,11 @@ static int max_all_ranks(dab_handle* h, double& x) {  // max over ranks of one h
   return 0;
 }
 
-// Explicit S by fixed-point tiles (k_schur_tiles) when the camera set is small (the
-// matrix-free criterion: tables in LDS, NC <= 160) and every point has at most kTileBatch
-// entries. Tables: each point's entries sorted by camera, batches of whole points (<= 32
-// entries and points), tiles of the lower block triangle sized to the LDS.
+// Explicit S by block tiles (k_schur_y + k_schur_tiles) when the camera set is small (the
+// matrix-free criterion: tables in LDS, NC <= 160) and no point sees more than kTileMaxRec
+// free cameras. Tables: each point's entries sorted by camera, records (distinct point-camera
+// pairs), batches of whole points (<= 640 records, <= 64 points), tiles of <= 1024 blocks.
+static constexpr int kBatchPts = 64, kTileBlocks = 1024;
 static int build_schur_tiles(dab_handle* h) {
   hipStream_t s = h->stream;
   const int NP = h->NP, NC = h->NC;
@@ -974,55 +975,76 @@ static int build_schur_tiles(dab_handle* h) {
   const std::vector<int>& ent_cam = h->h_ent_cam;
   const std::vector<int>& ent_os = h->h_ent_os;
   std::vector<int2> sch(h->NE);
-  std::vector<int> batch{0};
-  int cur_e = 0, cur_p = 0;
+  std::vector<int4> rec;
+  rec.reserve(h->NE);
+  std::vector<int> batch_rec{0}, batch_pt{0};
+  const int kBatchRec = schur_tile_batch_cap(NC);
+  int cur = 0, curp = 0;
   for (int p = 0; p < NP; ++p) {
-    const int b = pt_ent_ptr[p], e = pt_ent_ptr[p + 1], m = e - b;
+    const int b = pt_ent_ptr[p], e = pt_ent_ptr[p + 1];
     for (int i = b; i < e; ++i) sch[i] = make_int2(ent_os[i], ent_cam[i]);
     std::sort(sch.begin() + b, sch.begin() + e, [](const int2& x, const int2& y) {
       return x.y != y.y ? x.y < y.y : x.x < y.x;
     });
-    if (cur_p > 0 && (cur_e + m > kTileBatch || cur_p + 1 > kTileBatch)) {
-      batch.push_back(p);
-      cur_e = cur_p = 0;
+    const int r0 = (int)rec.size();
+    for (int i = b; i < e; ++i) {
+      if (i > b && sch[i].y == sch[i - 1].y) {
+        rec.back().y++;
+        continue;
+      }
+      rec.push_back(make_int4(i, 1, p, sch[i].y));
     }
-    cur_e += m;
-    cur_p += 1;
+    const int m = (int)rec.size() - r0;
+    if (curp > 0 && (cur + m > kBatchRec || curp + 1 > kBatchPts)) {
+      batch_rec.push_back(r0);
+      batch_pt.push_back(p);
+      cur = curp = 0;
+    }
+    cur += m;
+    curp += 1;
   }
-  batch.push_back(NP);
-  // tiles: camera ranges whose blocks (c, d <= c) and rhs rows fit the LDS left over
-  const size_t cap = (kTileLdsMax - schur_tile_lds_fixed()) / sizeof(unsigned long long);
-  std::vector<int> tc{0};
-  size_t maxuse = 0;
-  while (tc.back() < NC) {
-    const int ca = tc.back();
-    int cb = ca + 1;
-    auto use = [&](int hi) { return (size_t)(36 * (tri_n(hi) - tri_n(ca)) + 6 * (long long)(hi - ca)); };
-    while (cb < NC && use(cb + 1) <= cap) ++cb;
-    maxuse = std::max(maxuse, use(cb));
-    tc.push_back(cb);
-  }
+  batch_rec.push_back((int)rec.size());
+  // tiles: equal block ranges of <= kTileBlocks
+  const int nb = (int)tri_n(NC);
+  const int ntile = std::max(1, (nb + kTileBlocks - 1) / kTileBlocks);
+  std::vector<int> tb(ntile + 1);
+  for (int t = 0; t <= ntile; ++t) tb[t] = (int)((long long)nb * t / ntile);
   SchurTiles& a = h->tiles;
-  a.ntile = (int)tc.size() - 1;
-  a.nbatch = (int)batch.size() - 1;
-  a.ngroup = std::max(1, std::min(h->ncu / a.ntile, a.nbatch));
-  a.nelem = (int)(36 * tri_n(NC));
-  a.stride = (size_t)a.nelem + 6 * (size_t)NC;
-  a.qscale = 1.0;
-  h->tile_lds = schur_tile_lds_fixed() + sizeof(unsigned long long) * maxuse;
+  a.ntile = ntile;
+  a.nbatch = (int)batch_rec.size() - 1;
+  a.nrec = (int)rec.size();
+  // one work-group per CU (1024 threads); groups in multiples of 8 (one XCD per group)
+  int ng = std::max(1, h->ncu / a.ntile);
+  if (ng >= 8) ng -= ng % 8;
+  a.ngroup = std::max(1, std::min(ng, a.nbatch));
+  a.nelem = 36 * nb;
+  a.stride = (size_t)a.nelem;
+  a.kq = 0;
+  a.batch_cap = kBatchRec;
+  std::vector<int> rcam(rec.size());
+  for (size_t i = 0; i < rec.size(); ++i) rcam[i] = rec[i].w;
   Dev& d = h->dev;
-  int *d_tc = nullptr, *d_batch = nullptr;
+  int *d_tb = nullptr, *d_br = nullptr, *d_bp = nullptr, *d_rcam = nullptr;
+  CHECK_RC(upload(&d_rcam, d, rcam, s));
+  a.rec_cam = d_rcam;
   int2* d_sch = nullptr;
-  CHECK_RC(upload(&d_tc, d, tc, s));
-  CHECK_RC(upload(&d_batch, d, batch, s));
+  int4* d_rec = nullptr;
+  CHECK_RC(upload(&d_tb, d, tb, s));
+  CHECK_RC(upload(&d_br, d, batch_rec, s));
+  CHECK_RC(upload(&d_bp, d, batch_pt, s));
   CHECK_RC(upload(&d_sch, d, sch, s));
-  a.tile_c0 = d_tc;
-  a.batch_pt = d_batch;
+  CHECK_RC(upload(&d_rec, d, rec, s));
+  a.tile_b0 = d_tb;
+  a.batch_rec = d_br;
+  a.batch_pt = d_bp;
   a.sch_ent = d_sch;
-  CHECK_RC(d.alloc(&h->d_scx, (size_t)6 * NC));
+  a.rec_info = d_rec;
   CHECK_RC(d.alloc(&h->d_kx, (size_t)6 * NC));
+  a.kx = h->d_kx;
   CHECK_RC(d.alloc(&a.partial, (size_t)a.ngroup * a.stride));
-  CHECK_RC(d.alloc(&h->d_sfx, a.stride));
+  CHECK_RC(d.alloc(&h->d_sblk, a.stride));
+  CHECK_RC(d.alloc(&h->d_rfx, (size_t)6 * NC));
+  CHECK_RC(d.alloc(&h->d_yrec, (size_t)18 * std::max(1, a.nrec)));
   HIP_OK(hipStreamSynchronize(s));
   return 0;
 }
@@ -1036,9 +1058,18 @@ static int build_schur_tables(dab_handle* h) {
   const std::vector<int>& ent_pos = h->h_ent_pos;
   {
     // tile mode: every rank must take the same branch (the all-reduced S layouts differ)
-    int maxm = 0;
-    for (int pt = 0; pt < NP; ++pt) maxm = std::max(maxm, pt_ent_ptr[pt + 1] - pt_ent_ptr[pt]);
-    double no_tiles = (h->knobs.schur_tiles != 0 && NC > 0 && mf_schur_fits(NC, h->E, h->NI) && maxm <= kTileBatch)
+    int maxm = 0;  // distinct free cameras of one point
+    std::vector<int> seen(std::max(1, NC), -1);
+    for (int pt = 0; pt < NP; ++pt) {
+      int m = 0;
+      for (int e = pt_ent_ptr[pt]; e < pt_ent_ptr[pt + 1]; ++e)
+        if (seen[ent_cam[e]] != pt) {
+          seen[ent_cam[e]] = pt;
+          ++m;
+        }
+      maxm = std::max(maxm, m);
+    }
+    double no_tiles = (h->knobs.schur_tiles != 0 && NC > 0 && mf_schur_fits(NC, h->E, h->NI) && maxm <= kTileMaxRec)
                           ? 0.0 : 1.0;
     CHECK_RC(max_all_ranks(h, no_tiles));
     h->schur_tiles = no_tiles == 0.0;
@@ -1617,22 +1648,23 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
       it.linear_solver_iterations = cg_iters;
       pcg_fail = cg_status == kPcgFailure;
     } else if (NC > 0 && h->schur_tiles) {
-      // S by fixed-point tiles: Y re-evaluated per tile, integer sums (all-reduced exactly)
+      // S by register-owned block tiles over the records' Y (re-evaluated once per step)
       SchurTiles a = h->tiles;
-      int kq = 0;
+      a.kq = 0;
       if (x_cost > 0.0 && std::isfinite(x_cost)) {
         int e2;
         (void)std::frexp(2.0 * x_cost, &e2);  // sum_p |q_p|^2 <= 2 cost < 2^e2
-        kq = (e2 + 1) >> 1;
+        a.kq = (e2 + 1) >> 1;
       }
-      a.qscale = std::ldexp(1.0, 30 - kq);
-      a.scx = h->d_scx;
-      launch_schur_scale(s, NC, h->ug(), h->d_scale_c, h->d_scx, h->d_kx);
-      launch_schur_tiles(s, v, h->d_points, h->d_camtab, h->d_L, h->d_q, a, h->tile_lds);
-      launch_schur_sum(s, a.ngroup, a.stride, a.stride, a.partial, h->d_sfx);
-      CHECK_RC(h->allreduce_u64(reinterpret_cast<uint64_t*>(h->d_sfx), a.stride));
+      launch_schur_scale(s, NC, h->ug(), h->d_scale_c, h->d_kx);
+      HIP_OK(hipMemsetAsync(h->d_rfx, 0, sizeof(unsigned long long) * 6 * (size_t)NC, s));
+      launch_schur_y(s, v, h->d_points, h->d_camtab, h->d_L, h->d_q, h->d_scale_c, a, h->d_yrec, h->d_rfx);
+      launch_schur_tiles(s, h->d_yrec, a, NC);
+      launch_schur_sum(s, a.ngroup, a.stride, (size_t)a.nelem, a.partial, h->d_sblk);
+      CHECK_RC(h->allreduce(h->d_sblk, (size_t)a.nelem, ncclSum));
+      CHECK_RC(h->allreduce_u64(reinterpret_cast<uint64_t*>(h->d_rfx), (size_t)6 * NC));
       HIP_OK(hipMemsetAsync(h->d_S, 0, sizeof(double) * (size_t)(n + 1) * h->lds, s));
-      launch_schur_unpack(s, NC, h->d_sfx, h->d_kx, kq, h->d_S, h->lds, h->ybc());
+      launch_schur_unpack(s, NC, h->d_sblk, h->d_rfx, h->d_kx, a.kq, h->d_S, h->lds, h->ybc());
       launch_s_add_u(s, NC, h->ug(), h->ncross, h->d_cross_cam, h->Ux(), h->d_scale_c, sc, h->ybc(), h->d_S, h->lds);
       if (chol_factor_solve(h->chol, s, n, h->d_S, h->lds, h->d_yc, h->d_flags + 1) != 0)
         return set_error(DAB_E_DEVICE, "dense Cholesky launch failed");

@@ -161,7 +161,7 @@ typedef struct dab_summary {
 } dab_summary;
 /* schur_assembly values for DAB_LINEAR_SOLVER_EXPLICIT_SCHUR */
 #define DAB_SCHUR_PAIRS 0   /* per camera-pair block sums over entry-pair tables (large NC) */
-#define DAB_SCHUR_TILES 1   /* fixed-point LDS tiles of S, Y re-evaluated (NC <= 160) */
+#define DAB_SCHUR_TILES 1   /* register-owned block tiles over per-step Y records (NC <= 160) */
 
 typedef struct dab_handle dab_handle;
 

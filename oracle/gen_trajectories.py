@@ -1,0 +1,93 @@
+"""TEST INFRASTRUCTURE ONLY: oracle LM trajectories of the BASELINE configurations at full
+size, committed as tests/golden/trajectories.json (the -m gpu full-size parity tests compare
+the HIP path against them; the CPU oracle takes seconds to minutes per iteration at these
+sizes, too long to rerun inside a test).
+
+The problems come from libdab's deterministic host generator (dab_synth_fill: splitmix64 /
+xoshiro256** streams), so the GPU box regenerates the identical problem; each
+record carries a digest of the generated arrays that the tests verify first.
+
+Usage: python oracle/gen_trajectories.py [record ...]   (default: every record below)
+"""
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+import _pkgload  # noqa: E402
+import oracle  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden", "trajectories.json")
+
+# (record name, config, linear solver, LM iterations). Tolerances are zeroed so that every
+# iteration runs, as in bench.py.
+CASES = [
+    ("c2_explicit", "c2_100cam", "explicit", 4),
+    ("c2_pcg", "c2_100cam", "pcg", 4),
+    ("c3_explicit", "c3_1kcam", "explicit", 3),
+    ("c3_pcg", "c3_1kcam", "pcg", 3),
+    ("c5_explicit", "c5_rig_16x64", "explicit", 2),
+    ("c5_pcg", "c5_rig_16x64", "pcg", 2),
+]
+
+
+def problem_digest(prob):
+    """sha256 over the generated arrays (bit patterns), so the tests know they regenerated
+    exactly the problem the trajectory was computed on."""
+    h = hashlib.sha256()
+    for a in (prob.obs_xy, prob.obs_point, prob.obs_ext0, prob.obs_ext1, prob.obs_intr, prob.points,
+              prob.ext, prob.intr, prob.intr_nf, prob.intr_nk, prob.ext_const):
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def case_options(pkg, solver, iters, threads=8):
+    lst = (pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR if solver == "explicit"
+           else pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)
+    return pkg.options(max_num_iterations=iters, function_tolerance=0.0, gradient_tolerance=0.0,
+                       parameter_tolerance=0.0, linear_solver_type=lst, num_threads=threads)
+
+
+def sample_rows(a, n):
+    return a[:: max(1, a.shape[0] // n)][:n]
+
+
+def main(names):
+    pkg = _pkgload.load()
+    threads = min(16, os.cpu_count() or 1)
+    out = json.load(open(OUT)) if os.path.exists(OUT) else {}
+    probs = {}
+    for name, cfg, solver, iters in CASES:
+        if names and name not in names:
+            continue
+        if cfg not in probs:
+            probs = {cfg: pkg.synth(**pkg.CONFIGS[cfg])}
+        prob = probs[cfg].copy()
+        digest = problem_digest(prob)
+        t = time.perf_counter()
+        o = oracle.solve(pkg, prob, case_options(pkg, solver, iters, threads))
+        wall = time.perf_counter() - t
+        out[name] = dict(
+            config=cfg, solver=solver, max_num_iterations=iters, digest=digest, num_obs=prob.num_obs,
+            termination=o["termination"], num_iterations=o["num_iterations"],
+            costs=[it["cost"] for it in o["iterations"]],
+            success=[bool(it["success"]) for it in o["iterations"]],
+            linear_iterations=[it["linear_solver_iterations"] for it in o["iterations"]],
+            final_cost=o["final_cost"],
+            points_sample=sample_rows(prob.points, 64).tolist(), ext_sample=prob.ext[:16].tolist(),
+            oracle_wall_s=wall, oracle_threads=threads)
+        print(f"{name}: {o['num_iterations']} its, costs {out[name]['costs']}, "
+              f"cg {out[name]['linear_iterations']}, {wall:.1f} s", flush=True)
+        with open(OUT, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
