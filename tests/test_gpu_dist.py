@@ -23,3 +23,22 @@ def test_two_ranks_match_single_handle(gpu):
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     assert "DIST_CHECK OK" in p.stdout, p.stdout[-3000:]
+
+
+def test_rccl_one_rank_per_gpu(gpu):
+    """The product multi-GPU path: one process per GPU, dab_create_dist (RCCL over xGMI),
+    every collective on RCCL. Runs whenever the box shows two or more devices (the driver's
+    8-GPU node); a one-GPU box skips it (RCCL refuses two ranks per device)."""
+    import torch
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip(f"{n} device(s) visible: the RCCL path needs two")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "scripts", "dist_check.py")]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "DIST_CHECK OK" in p.stdout, p.stdout[-3000:]
