@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-lm", action="store_true")
     ap.add_argument("--no-rig", action="store_true", help="skip the config-5 rig LM measurement")
+    ap.add_argument("--no-c4", action="store_true", help="skip the config-4 strong-scaling lines")
+    ap.add_argument("--no-c1", action="store_true", help="skip the config-1 CPU-path record")
     ap.add_argument("--no-c2", action="store_true", help="skip the config-2 evaluation pass (PMC passes: "
                     "its launches share the kernel name)")
     ap.add_argument("--rig-config", default="c5_rig_16x64")
@@ -98,7 +100,9 @@ def main():
             dist.all_reduce(torch.from_numpy(arr),
                             op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
     solver = pkg.Solver(device, rank, world, uid, host_allreduce=host_ar)
+    t_sp = time.perf_counter()
     solver.set_problem(prob)
+    set_problem_s = time.perf_counter() - t_sp
     n_obs = prob.num_obs
 
     def barrier():
@@ -165,6 +169,45 @@ def main():
         prob.points[:], prob.ext[:] = pts0, ext0
         solver.update_parameters(pts0, ext0)
 
+    # ---- BASELINE config 4: the 1M-observation C3 problem point-sharded over the N ranks
+    # (strong scaling; the headline above is weak scaling, 1M observations per rank). At N = 1
+    # it is the headline problem itself, so the numbers are the headline's.
+    c4 = {}
+    if not args.no_c4:
+        if world == 1:
+            c4 = {"c4_eval_mobs_per_s": value, "c4_eval_ms_per_step": ms_per_step,
+                  "c4_lm_iter_ms_median": lm.get("lm_iter_ms_median"),
+                  "c4_lm_pcg_iter_ms_median": lm.get("lm_pcg_iter_ms_median")}
+        else:
+            gprob = pkg.synth(**pkg.CONFIGS[args.config])
+            sprob = gprob.shard(rank, world)
+            csolver = pkg.Solver(device, rank, world, make_uid(), host_allreduce=host_ar)
+            csolver.set_problem(sprob)
+            csolver.bench_eval_pass(True, 5)
+            csolver.sync()
+            barrier()
+            t4 = time.perf_counter()
+            csolver.bench_eval_pass(True, 50)
+            csolver.sync()
+            barrier()
+            d4 = max_over_ranks(time.perf_counter() - t4) / 50
+            c4 = {"c4_eval_mobs_per_s": gprob.num_obs / d4 / 1e6, "c4_eval_ms_per_step": 1e3 * d4}
+            if not args.no_lm:
+                p40, e40 = sprob.points.copy(), sprob.ext.copy()
+                for tag, lst in (("c4_lm", pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR),
+                                 ("c4_lm_pcg", pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)):
+                    csolver.update_parameters(p40, e40)
+                    barrier()
+                    summ4 = csolver.solve(pkg.options(max_num_iterations=args.lm_iters, function_tolerance=0.0,
+                                                      gradient_tolerance=0.0, parameter_tolerance=0.0,
+                                                      linear_solver_type=lst))
+                    its4 = [it["time"] for it in summ4["iterations"][1:]]
+                    c4[f"{tag}_iter_ms_median"] = max_over_ranks(1e3 * float(np.median(its4))) if its4 else None
+                    c4[f"{tag}_final_cost"] = summ4["final_cost"]
+            csolver.close()
+            del gprob, sprob
+        c4["c4_config"] = f"{args.config} global problem point-sharded over {world} rank(s) (strong scaling)"
+
     # ---- BASELINE config 5: the 10M-observation rig, point-sharded over the N ranks
     # (strong scaling), PCG step as BASELINE names it (pcg_fp32 requested; the rig's 79
     # cameras take the matrix-free PCG, which stores no Schur factors and runs all fp64).
@@ -200,9 +243,23 @@ def main():
         opts = pkg.options(max_num_iterations=args.lm_iters, function_tolerance=0.0, gradient_tolerance=0.0,
                            parameter_tolerance=0.0, linear_solver_type=pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG,
                            pcg_fp32=1)
+        rp0, re0 = rprob.points.copy(), rprob.ext.copy()
         summ = rsolver.solve(opts)
         its = [it["time"] for it in summ["iterations"][1:]]
         mf = rsolver.pcg_matrix_free()
+        # the exact step (DENSE_SCHUR): S from the block tiles, dense Cholesky of 474 x 474
+        rsolver.update_parameters(rp0, re0)
+        barrier()
+        t_x = time.perf_counter()
+        sx = rsolver.solve(pkg.options(max_num_iterations=args.lm_iters, function_tolerance=0.0,
+                                       gradient_tolerance=0.0, parameter_tolerance=0.0,
+                                       linear_solver_type=pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR))
+        t_x = max_over_ranks(time.perf_counter() - t_x)
+        itx = [it["time"] for it in sx["iterations"][1:]]
+        rig_x = {"rig_lm_explicit_iter_ms_median": max_over_ranks(1e3 * float(np.median(itx))) if itx else None,
+                 "rig_lm_explicit_first_solve_ms_per_iter": 1e3 * t_x / max(1, sx["num_iterations"]),
+                 "rig_lm_explicit_costs": [it["cost"] for it in sx["iterations"]],
+                 "rig_lm_explicit_schur_assembly": {0: "pair tables", 1: "block tiles"}[sx["schur_assembly"]]}
         rig = {"rig_config": args.rig_config, "rig_global_obs": gprob.num_obs,
                "rig_lm_pcg_iter_ms_median": max_over_ranks(1e3 * float(np.median(its))) if its else None,
                "rig_linear_solver": ("implicit-Schur PCG, matrix-free Schur products (fp64, no stored factors)"
@@ -210,7 +267,7 @@ def main():
                "rig_lm_iterations": summ["num_iterations"],
                "rig_lm_linear_iterations": [it["linear_solver_iterations"] for it in summ["iterations"][1:]],
                "rig_initial_cost": summ["initial_cost"], "rig_final_cost": summ["final_cost"],
-               "rig_set_problem_s": max_over_ranks(t_set), **rig_eval}
+               "rig_set_problem_s": max_over_ranks(t_set), **rig_eval, **rig_x}
         rsolver.close()
         del gprob, rprob
 
@@ -257,17 +314,48 @@ def main():
                                                parameter_tolerance=0.0))
         it1 = o["iterations"][1]["time"] if len(o["iterations"]) > 1 else None
         cpu = dict(value=len(idx) / cpu_jac_s / 1e6, unit="M obs/s", cores=threads, kind="port",
+                   nproc=os.cpu_count(), affinity=len(os.sched_getaffinity(0)),
                    sample=(f"residual+autodiff-Jacobian of {len(idx)} obs (every 5th obs of "
                            f"{args.config}); LM iteration 1 on the full problem"),
                    lm_iter_ms=1e3 * it1 if it1 else None)
 
+    # ---- BASELINE config 1: the reference's CPU path (sfm.cc solve(), DENSE_SCHUR) on the
+    # synthetic rig .deeparc stand-in (8 x 36 rig, 20k points; the reference's data files are
+    # stripped): wall-clock per LM iteration and the cost after the same LM iterations, CPU
+    # oracle and GPU side by side (rank 0 at N = 1).
+    c1 = {}
+    if rank == 0 and world == 1 and not args.no_c1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        threads = min(16, os.cpu_count() or 1)
+        c1prob = pkg.synth(**pkg.CONFIGS["c1_rig_8x36"])
+        o1 = pkg.options(max_num_iterations=10, num_threads=threads)
+        c1g = c1prob.copy()
+        g1s = pkg.Solver(device)
+        g1s.set_problem(c1g)
+        gsum = g1s.solve(o1)
+        g1s.close()
+        c1c = c1prob.copy()
+        t1 = time.perf_counter()
+        csum = oracle.solve(pkg, c1c, o1)
+        t1 = time.perf_counter() - t1
+        c1 = {"c1_config": "c1_rig_8x36: rig 8 x 36, 20000 points, 160000 observations, DENSE_SCHUR, "
+                           "up to 10 LM iterations (Ceres defaults)",
+              "c1_gpu_lm_iter_ms_median": 1e3 * float(np.median([it["time"] for it in gsum["iterations"][1:]])),
+              "c1_cpu_lm_iter_ms": 1e3 * t1 / max(1, csum["num_iterations"]), "c1_cpu_threads": threads,
+              "c1_gpu_final_cost": gsum["final_cost"], "c1_cpu_final_cost": csum["final_cost"],
+              "c1_iterations": [gsum["num_iterations"], csum["num_iterations"]],
+              "c1_termination": [gsum["termination"], csum["termination"]]}
+
     traffic = None
+    valu = None
     if os.path.exists(args.traffic_json):
         try:
             t = json.load(open(args.traffic_json))
             if (t.get("config") == args.config and t.get("n_obs") == n_obs
                     and str(t.get("kernel", "")).startswith(eval_kernel)):
                 traffic = t.get("bytes_per_launch")
+                valu = t.get("valu_insts_per_launch")
         except Exception:
             traffic = None
 
@@ -285,7 +373,12 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": eval_kernel, "kernel_ms": jac_ms,
-                         "algorithmic_bytes_per_launch": jac_bytes},
+                         "algorithmic_bytes_per_launch": jac_bytes,
+                         # fp64 VALU issue: PMC SQ_INSTS_VALU per launch against one wave-
+                         # instruction per CU and cycle (the fp64 rate of 4 SIMD-32s) at 2.4 GHz
+                         "valu_insts_per_launch": valu,
+                         "valu_frac": (valu / (256 * 2.4e9 * jac_ms * 1e-3)) if valu else None},
+            "set_problem_s": set_problem_s,
             "eval_kernel_mobs_per_s": n_obs / (jac_ms * 1e-3) / 1e6,
             "eval_schedule": {1: "fused: camera and point side in one launch",
                               2: "fused kernel split: camera side, then point side beside the all-reduce",
@@ -295,8 +388,12 @@ def main():
         }
         if lm:
             line.update(lm)
+        if c4:
+            line.update(c4)
         if rig:
             line.update(rig)
+        if c1:
+            line.update(c1)
         if c2:
             line.update(c2)
         print(json.dumps(line), flush=True)

@@ -38,24 +38,29 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--config", default="c3_1kcam")
     ap.add_argument("--n-obs", type=int, default=1000000)
+    ap.add_argument("--valu-dir", default="", help="a third PMC pass with SQ_INSTS_VALU (wave-instructions)")
     ap.add_argument("--kernel", default="auto", help="kernel name prefix (auto: k_eval_fused if it ran, "
                     "else k_eval_points)")
     a = ap.parse_args()
     fetch, write = load(a.fetch_dir, "FETCH_SIZE"), load(a.write_dir, "WRITE_SIZE")
+    valu = load(a.valu_dir, "SQ_INSTS_VALU") if a.valu_dir else {}
     table = {}
     for k in sorted(set(fetch) | set(write)):
         f = fetch.get(k, [])
         w = write.get(k, [])
         fb = 2.0 * 1024 * sum(f) / len(f) if f else None
         wb = 1024.0 * sum(w) / len(w) if w else None
+        v = valu.get(k, [])
         table[short(k)] = dict(launches=max(len(f), len(w)), fetch_bytes_x2=fb, write_bytes=wb,
-                               bytes_per_launch=(fb or 0.0) + (wb or 0.0))
+                               bytes_per_launch=(fb or 0.0) + (wb or 0.0),
+                               valu_insts=(sum(v) / len(v)) if v else None)
     if a.kernel == "auto":
         a.kernel = "k_eval_fused" if any(k.startswith("k_eval_fused") for k in table) else "k_eval_points"
     # the evaluation-kernel variant the bench ran (most launches among the matching names)
     main_k = sorted((k for k in table if k.startswith(a.kernel)), key=lambda k: -table[k]["launches"])
     out = dict(config=a.config, n_obs=a.n_obs, kernel=main_k[0] if main_k else None,
                bytes_per_launch=table[main_k[0]]["bytes_per_launch"] if main_k else None,
+               valu_insts_per_launch=table[main_k[0]]["valu_insts"] if main_k else None,
                correction="FETCH_SIZE x2 (gfx950 wide-load tally), WRITE_SIZE x1, KiB->B",
                kernels=table)
     with open(a.out, "w") as fh:
