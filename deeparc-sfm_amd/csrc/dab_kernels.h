@@ -71,6 +71,8 @@ struct DevView {
   const int* ext_col;       // [E] free camera index or -1
   const double* intr;       // [NI][kIntr]
   const int2* chunk_uni;    // [nchunk] (ext, intr) shared by every entry of the chunk, or (-1, -1)
+  const int* obs_e;         // [N] (streamed fused pass; null otherwise) ext0 | intr << 16 of a
+                            // single-extrinsic slot, -1 for padding
 };
 
 // camera-side chunks split by whether one camera/intrinsic serves the whole chunk
@@ -115,9 +117,14 @@ void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, con
 // point waves side by side. fused_eval_fits: whether the problem qualifies for `grid`.
 bool fused_eval_fits(const DevView& v, int nchunk, int ngen, int ncross, int grid);
 // side: 0 both halves; 1 the point side only (V, g, cost); 2 the camera side only (ug)
+// cmx (nullable): the camera-major point copy [3][NE] (launch_cmx_gather of the current
+// points) together with v.obs_e selects the streamed form; variant = its pipeline depths
+// (DAB_ABLATIONS builds; 0 = default)
 void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
                        double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
-                       int grid, int side);
+                       int grid, int side, const double* cmx = nullptr, int variant = 0,
+                       const double* camtab = nullptr);
+void launch_cmx_gather(hipStream_t s, const DevView& v, const double* points, double* cmx);
 //  arc∘ring cross blocks Jc0^T Jc1 over composed observations (pair-major copy) -> partial[chunk][36]
 void launch_eval_cross(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
                        const double2* x_xy, const double* points, const double* camtab, double* partial);

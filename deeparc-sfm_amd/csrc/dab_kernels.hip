@@ -1484,6 +1484,33 @@ struct UniFrame {
       for (int q = 0; q < 9; ++q) jl[q] = J[q];
     }
   }
+  // the same from the precomputed table camtab[e] (k_cam_tables: R t Rd Jd), scalar loads
+  struct FromTable {};
+  __device__ __forceinline__ UniFrame(FromTable, const double* __restrict__ camtab,
+                                      const double* __restrict__ intr, int e, int i, double* jl) {
+    const double* F = camtab + (size_t)kCamTab * e;
+    double Fr[30];
+#pragma unroll
+    for (int q = 0; q < 30; ++q) Fr[q] = UniTabs::uniform(F[q]);
+    small = Fr[12] == 1.0 && Fr[13] == 0.0 && Fr[14] == 0.0 && Fr[15] == 0.0 && Fr[16] == 1.0 && Fr[17] == 0.0 &&
+            Fr[18] == 0.0 && Fr[19] == 0.0 && Fr[20] == 1.0 && Fr[21] == 1.0 && Fr[25] == 1.0 && Fr[29] == 1.0;
+#pragma unroll
+    for (int q = 0; q < 12; ++q) T[q] = Fr[q];
+    const double* k = intr + (size_t)kIntr * i;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) K[q] = UniTabs::uniform(k[q]);
+    double J[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        J[3 * r + c] = UniTabs::uniform(Fr[12 + 3 * r] * Fr[21 + c] + Fr[12 + 3 * r + 1] * Fr[24 + c] +
+                                        Fr[12 + 3 * r + 2] * Fr[27 + c]);
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+      for (int q = 0; q < 9; ++q) jl[q] = J[q];
+    }
+  }
 };
 
 __device__ __forceinline__ void frame_rows_acc(const double2 xy, const double (&X)[3], const UniFrame& f,
@@ -1583,6 +1610,49 @@ __device__ __forceinline__ void eval_cams_uni_frame(const DevView& v, int i0, in
   const UniFrame f(ext, v.intr, ext_i, intr_i, jl);  // built while the first loads fly
   DAB_STAMP_ANY(1);
   frame_pipe<NS>(v, i0, e, stride, points, f, pt, xy, X, acc);
+}
+
+// The fused pass's camera loop over a STREAMED camera-major copy of the point coordinates
+// (cmx, planar [3][NE], refreshed whenever the points change: launch_cmx_gather): every
+// load is a coalesced stream, none depends on another, so the pipeline is NS - 1 steps of
+// 64 entries deep (10 VGPRs per slot) instead of the index -> point gather chain of
+// eval_cams_uni_frame, whose every step waited one dependent L2 round trip.
+template <int NS, bool TAB = false>
+__device__ __forceinline__ void eval_cams_stream(const double* __restrict__ cmx, size_t NE,
+                                                 const double2* __restrict__ cmxy, int i0, int e, int ext_i,
+                                                 int intr_i, const double* __restrict__ ext,
+                                                 const double* __restrict__ intr, double (&acc)[27], double* jl,
+                                                 const double* __restrict__ camtab = nullptr) {
+  static_assert(NS >= 2, "at least two slots");
+  // Every load is unconditional (entries past the range re-read the last one, which is
+  // then not used), so the number of loads in flight is the same on every path and the
+  // compiler's wait before slot u covers exactly that slot (vmcnt((NS-1) x 4)), not every
+  // outstanding load; the step count is wave-uniform.
+  const int lo = i0 - (int)(threadIdx.x & 63);
+  const int n = (e - lo + 63) >> 6;  // steps of 64 entries
+  double2 xy[NS];
+  double X[NS][3];
+  auto load = [&](int slot, int step) {
+    const int i = min(i0 + 64 * step, e - 1);
+    xy[slot] = cmxy[i];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) X[slot][q] = cmx[q * NE + i];
+  };
+  if (n > 0) {
+#pragma unroll
+    for (int st = 0; st < NS - 1; ++st) load(st, st);
+  }
+  // built while the first loads fly
+  const UniFrame f = TAB ? UniFrame(UniFrame::FromTable{}, camtab, intr, ext_i, intr_i, jl)
+                         : UniFrame(ext, intr, ext_i, intr_i, jl);
+  DAB_STAMP_ANY(1);
+  for (int st0 = 0; st0 < n; st0 += NS) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      load((u + NS - 1) % NS, st0 + u + NS - 1);
+      if (i0 + 64 * (st0 + u) < e) frame_rows_acc(xy[u], X[u], f, acc);
+    }
+  }
 }
 
 // entry k (< 27) of the camera's [U upper-packed | g_c] from the point-frame sums s
@@ -1790,23 +1860,31 @@ void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, con
 // uniform chunk per free camera, E, NI <= kLdsCams, NC <= (camera waves / 2) x grid.
 constexpr int kFusedPW = 8;               // point waves per work-group
 constexpr int kFusedCW = 16 - kFusedPW;   // camera waves (kFusedCW / 2 cameras per round)
-template <int D, int ABL = 0, int NS = 3>  // ABL: 1 camera waves exit at once (point side only), 2 point
-                                          // waves do (camera side only) — the multi-rank split schedule;
-                                          // timing ablations: 3 no trig in the staging, 21 / 22 point /
-                                          // camera waves at raised priority; NS: camera-entry pipeline slots
+// ST: the streamed form — camera waves read the camera-major point copy cmx (eval_cams_stream,
+// NS slots) and point waves the packed 4-B slot records v.obs_e (ext | intr << 16, a D-deep
+// queue at 5 VGPRs per row) instead of the 16-B obs_idx records.
+template <int D, int ABL = 0, int NS = 3, bool ST = false, bool TAB = false>  // ABL: 1 camera waves exit at once (point side
+                                          // only), 2 point waves do (camera side only) — the multi-rank split
+                                          // schedule; timing ablations: 3 no trig in the staging, 21 / 22
+                                          // point / camera waves at raised priority; NS: camera-entry slots
 __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __restrict__ chunk_beg,
                                                      const double* __restrict__ points,
                                                      const double* __restrict__ ext, double* __restrict__ V,
                                                      double* __restrict__ g, double* __restrict__ ug,
                                                      unsigned long long* __restrict__ costfx,
-                                                     unsigned long long* __restrict__ fx_next, int wpc, int wps) {
+                                                     unsigned long long* __restrict__ fx_next,
+                                                     const double* __restrict__ cmx,
+                                                     const double* __restrict__ camtab, int wpc, int wps,
+                                                     int wxor) {
   __shared__ double rt_s[kLdsCams * 12];
   __shared__ double k_s[kLdsCams * 6];
   __shared__ double csum[kFusedCW][27];     // camera waves' sums: [camera slot * wpc + part][component]
   __shared__ double cjl[kFusedCW][9];       // camera waves' J_l (eval_cams_uni_frame)
   __shared__ double shp[kFusedPW][2];       // point waves' cost partials
   __shared__ unsigned ccount[kFusedCW + kFusedPW], pbar, pdone;  // camera slots | point slots
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // wxor = 8: the camera side runs on hardware waves 0-7 (the older waves, which the issue
+  // arbiter serves first) and the point side on 8-15; `wave` is the logical index
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) ^ wxor);
   DAB_STAMP(0);
   if (threadIdx.x < kFusedCW + kFusedPW) ccount[threadIdx.x] = 0u;
   if (threadIdx.x == 0) pbar = pdone = 0u;
@@ -1831,6 +1909,9 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
       eval_cams_uni_pipe<NS>(v, lo + lane, hi, 64, points, [&]() { return UniTabs(ext, v.intr, u.x, u.y); },
                              acc);
       if (lane < 9) cjl[cw][lane] = (lane % 4 == 0) ? 1.0 : 0.0;
+    } else if constexpr (ST) {
+      eval_cams_stream<NS, TAB>(cmx, (size_t)v.NE, v.cm_xy, lo + lane, hi, u.x, u.y, ext, v.intr, acc, cjl[cw],
+                                camtab);
     } else {
       eval_cams_uni_frame<NS>(v, lo + lane, hi, 64, points, u.x, u.y, ext, acc, cjl[cw]);
     }
@@ -1870,14 +1951,22 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
   // part, part + wps, ...; the parts are combined in LDS by the last one to finish
   const int pw = wave, pslots = kFusedPW / wps, slot = pw / wps, part = pw - slot * wps;
   const int rounds = (v.nslice + pslots * gridDim.x - 1) / (pslots * gridDim.x);
-  RowQueue<D> q;
+  RowQueue<ST ? 1 : D> q;
+  int qe[ST ? D : 1];      // ST: packed records (ext | intr << 16, -1 = padding)
+  double2 qxy[ST ? D : 1];
   double X[3] = {0.0, 0.0, 0.0};
   int sl = slot * gridDim.x + blockIdx.x, off = 0, len = 0;
   auto fill_q = [&]() {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const int k = part + d * wps;
-      if (k < len) {
+      if constexpr (ST) {
+        // unconditional (rows past the slice re-read its last row, never used): the same
+        // number of loads on every path, so each row's wait covers that row only
+        const int kk = max(0, min(k, len - 1));
+        qe[d] = v.obs_e[off + 64 * kk + lane];
+        qxy[d] = v.obs_xy[off + 64 * kk + lane];
+      } else if (k < len) {
         q.id[d] = v.obs_idx[off + 64 * k + lane];
         q.xy[d] = v.obs_xy[off + 64 * k + lane];
       } else {
@@ -1886,28 +1975,62 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
       }
     }
   };
-  if (sl < v.nslice) {
-    off = v.slice_off[sl];
-    len = (v.slice_off[sl + 1] - off) >> 6;
-    const int p = 64 * sl + lane;
-    if (p < v.NP) {
+  // ST: every load of a round's set-up is unconditional (clamped to valid addresses; a
+  // lane past the points or a wave past the slices computes nothing from what it read), so
+  // the row queue's waits count exactly
+  auto setup_round = [&]() {
+    if constexpr (ST) {
+      const bool has = sl < v.nslice;
+      const int slc = min(sl, v.nslice - 1);
+      const int o0 = v.slice_off[slc], o1 = v.slice_off[slc + 1];
+      off = has ? o0 : 0;
+      len = has ? (o1 - o0) >> 6 : 0;
+      const int p = min(64 * slc + lane, v.NP - 1);
       X[0] = points[3 * (size_t)p];
       X[1] = points[3 * (size_t)p + 1];
       X[2] = points[3 * (size_t)p + 2];
+    } else if (sl < v.nslice) {
+      off = v.slice_off[sl];
+      len = (v.slice_off[sl + 1] - off) >> 6;
+      const int p = 64 * sl + lane;
+      if (p < v.NP) {
+        X[0] = points[3 * (size_t)p];
+        X[1] = points[3 * (size_t)p + 1];
+        X[2] = points[3 * (size_t)p + 2];
+      }
     }
-  }
-  fill_q();
-  // intrinsics: LDS-DMA straight into k_s (no registers), 16 B per lane, k_s is lane-linear
-  {
-    const int npiece = 3 * v.NI;
-    for (int base = pw * 64; base < npiece; base += kFusedPW * 64) {
-      const int i = min(base + lane, npiece - 1);  // tail lanes repeat the last piece (same bytes, same place)
-      const double* src = v.intr + (size_t)kIntr * (i / 3) + 2 * (i % 3);
-      __builtin_amdgcn_global_load_lds(src, k_s + 2 * (size_t)base, 16, 0, 0);
+    fill_q();
+  };
+  setup_round();
+  // Table staging. Every CU reads the same tables; in one order the 32 CUs of an XCD would
+  // ask for the same L2 lines at the same moment (one L2 channel at a time), and the
+  // camera waves' first loads would queue behind that in each CU. So each CU of an XCD
+  // starts at its own 1/32 of the table (blockIdx / 8: work-groups are dealt to the XCDs
+  // round robin).
+  const unsigned xrot = blockIdx.x >> 3;
+  // LDS-DMA of 16-B pieces (no registers), 64 lane-linear pieces per instruction; tail lanes
+  // repeat the last piece into the padding after it. Intrinsics: K of intrinsic i / 3,
+  // piece i % 3; tables (TAB): R, t of ext i / 6, piece i % 6 from k_cam_tables' output.
+#pragma unroll
+  for (int which = 0; which < (TAB ? 2 : 1); ++which) {
+    const int per = which ? 6 : 3, npiece = per * (which ? v.E : v.NI);
+    const double* src0 = which ? camtab : v.intr;
+    const int stride = which ? kCamTab : kIntr;
+    double* dst = which ? rt_s : k_s;
+    const int nch = (npiece + 63) >> 6;
+    const int rot = (int)((xrot * (unsigned)nch) >> 5);
+    for (int j = pw; j < nch; j += kFusedPW) {
+      int jr = j + rot;
+      if (jr >= nch) jr -= nch;
+      const int i = min(jr * 64 + lane, npiece - 1);
+      __builtin_amdgcn_global_load_lds(src0 + (size_t)stride * (i / per) + 2 * (i % per), dst + 2 * (size_t)(jr * 64),
+                                       16, 0, 0);
     }
   }
   // R, t of every extrinsic from the parameters (point threads only)
-  for (int e0 = threadIdx.x; e0 < v.E; e0 += kFusedPW * 64) {
+  const int erot = (int)((xrot * (unsigned)v.E) >> 5);
+  for (int e1 = pw * 64 + lane; e1 < (TAB ? 0 : v.E); e1 += kFusedPW * 64) {
+    const int e0 = e1 + erot < v.E ? e1 + erot : e1 + erot - v.E;
     double2 xw[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) xw[i] = reinterpret_cast<const double2*>(ext + 6 * (size_t)e0)[i];
@@ -1936,17 +2059,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
       sl = (r * pslots + slot) * gridDim.x + blockIdx.x;
       off = len = 0;
       X[0] = X[1] = X[2] = 0.0;
-      if (sl < v.nslice) {
-        off = v.slice_off[sl];
-        len = (v.slice_off[sl + 1] - off) >> 6;
-        const int p = 64 * sl + lane;
-        if (p < v.NP) {
-          X[0] = points[3 * (size_t)p];
-          X[1] = points[3 * (size_t)p + 1];
-          X[2] = points[3 * (size_t)p + 2];
-        }
-      }
-      fill_q();
+      setup_round();
     }
     double c[9];
 #pragma unroll
@@ -1956,12 +2069,24 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         const int k = k0 + d * wps;
-        if (k >= len) break;
-        const int4 id = q.id[d];
-        const double2 xy = q.xy[d];
-        if (k + D * wps < len) {
-          q.id[d] = v.obs_idx[off + 64 * (k + D * wps) + lane];
-          q.xy[d] = v.obs_xy[off + 64 * (k + D * wps) + lane];
+        if (!ST && k >= len) break;
+        int4 id;
+        double2 xy;
+        if constexpr (ST) {
+          const int pk = qe[d], pe = pk >= 0 ? pk : 0;
+          id = make_int4(pk >= 0 ? 0 : -1, pe & 0xffff, -1, pe >> 16);
+          xy = qxy[d];
+          const int kn = min(k + D * wps, len - 1);
+          qe[d] = v.obs_e[off + 64 * kn + lane];
+          qxy[d] = v.obs_xy[off + 64 * kn + lane];
+          if (k >= len) continue;  // wave-uniform; no load below
+        } else {
+          id = q.id[d];
+          xy = q.xy[d];
+          if (k + D * wps < len) {
+            q.id[d] = v.obs_idx[off + 64 * (k + D * wps) + lane];
+            q.xy[d] = v.obs_xy[off + 64 * (k + D * wps) + lane];
+          }
         }
         const bool live = id.x >= 0;
         double ru, rv, jx0[3], jx1[3];
@@ -2055,37 +2180,80 @@ static int fused_wps(int nslice, int E, int grid) {
 }
 void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
                        double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
-                       int grid, int side) {
+                       int grid, int side, const double* cmx, int variant, const double* camtab) {
   const int wpc = fused_wpc(v.NC, grid), wps = fused_wps(v.nslice, v.E, grid);
+  const int wxor = variant >= 1000 ? 8 : 0;  // camera side on the older hardware waves
+  variant %= 1000;
+#define DAB_FUSED_ARGS v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, cmx, camtab, wpc, wps, wxor
+  if (cmx && v.obs_e) {
+    // streamed form: variant = 10 D + NS (point queue depth, camera slots)
+    // D = 3 point rows and NS = 2 camera slots in flight: the measured best at C3 (deeper
+    // queues cost registers the loops need: 20.5 us against 20.8-21.6 us)
+#ifdef DAB_ABLATIONS
+    if (camtab) {  // tables read from k_cam_tables' output
+      if (side == 1) k_eval_fused<3, 1, 2, true, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+      else if (side == 2) k_eval_fused<3, 2, 2, true, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+      else if (variant == 23) k_eval_fused<2, 0, 3, true, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+      else k_eval_fused<3, 0, 2, true, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+      return;
+    }
+    if (side == 0 && variant != 0) {
+      if (variant == 23) k_eval_fused<2, 0, 3, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+      else if (variant == 24) k_eval_fused<2, 0, 4, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+      else if (variant == 43) k_eval_fused<4, 0, 3, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+      else if (variant == 44) k_eval_fused<4, 0, 4, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+      else k_eval_fused<3, 0, 2, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+      return;
+    }
+#endif
+    if (side == 1) k_eval_fused<3, 1, 2, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+    else if (side == 2) k_eval_fused<3, 2, 2, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+    else k_eval_fused<3, 0, 2, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+    return;
+  }
   // one side only (the multi-rank split schedule): the same kernel with the other side's
   // waves leaving at once
   if (side == 1) {
-    k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+    k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
     return;
   }
   if (side == 2) {
-    k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+    k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
     return;
   }
 #ifdef DAB_ABLATIONS
   // timing ablations (wrong results; built only with -DDAB_ABLATIONS, read once)
   static const int abl = getenv("DAB_FUSED_ABL") ? atoi(getenv("DAB_FUSED_ABL")) : 0;
-  if (abl == 5)
-    k_eval_fused<2, 5><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
-  else if (abl == 25)
-    k_eval_fused<2, 25><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
-  else if (abl == 1) k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
-  else if (abl == 2) k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
-  else if (abl == 3) k_eval_fused<2, 3><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
-  else if (abl == 21) k_eval_fused<2, 21><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
-  else if (abl == 22) k_eval_fused<2, 22><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
-  else if (abl == 34) k_eval_fused<2, 0, 4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
-  else if (abl == 35) k_eval_fused<2, 0, 5><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
-  else if (abl == 234) k_eval_fused<2, 2, 4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
-  else if (abl == 14) k_eval_fused<4><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+  if (abl == 5) k_eval_fused<2, 5><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+  else if (abl == 25) k_eval_fused<2, 25><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+  else if (abl == 1) k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+  else if (abl == 2) k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+  else if (abl == 3) k_eval_fused<2, 3><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+  else if (abl == 21) k_eval_fused<2, 21><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+  else if (abl == 22) k_eval_fused<2, 22><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+  else if (abl == 34) k_eval_fused<2, 0, 4><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+  else if (abl == 35) k_eval_fused<2, 0, 5><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+  else if (abl == 234) k_eval_fused<2, 2, 4><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+  else if (abl == 14) k_eval_fused<4><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
   else
 #endif
-    k_eval_fused<2><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, wpc, wps);
+    k_eval_fused<2><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+#undef DAB_FUSED_ARGS
+}
+
+// camera-major point copy for the streamed fused pass: cmx[q][i] = points[cm_pt[i]][q]
+__global__ __launch_bounds__(256) void k_cmx_gather(int NE, const int* __restrict__ cm_pt,
+                                                    const double* __restrict__ points, double* __restrict__ cmx) {
+  const size_t NEs = (size_t)NE;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < NE; i += gridDim.x * blockDim.x) {
+    const int p = cm_pt[i];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) cmx[q * NEs + i] = points[3 * (size_t)p + q];
+  }
+}
+void launch_cmx_gather(hipStream_t s, const DevView& v, const double* points, double* cmx) {
+  if (v.NE <= 0) return;
+  k_cmx_gather<<<grid_for(v.NE, 256, 8192), 256, 0, s>>>(v.NE, v.cm_pt, points, cmx);
 }
 
 // arc∘ring cross blocks Jc0^T Jc1, one block per chunk of composed observations sorted

@@ -119,6 +119,11 @@ struct Knobs {
   int cg_onewg = 0;         // DAB_CG_ONEWG=1: single-work-group CG update
   int bench_sample = 8;     // DAB_BENCH_SAMPLE: timing-event stride of dab_bench_eval_pass
   int schur_tiles = 1;      // DAB_SCHUR_TILES=0: explicit S from the pair tables even for small NC
+  int fused_stream = 1;     // DAB_FUSED_STREAM=0: the fused pass without the streamed camera-major point copy
+  int fused_variant = 0;    // DAB_FUSED_V: pipeline depths of the streamed fused pass (DAB_ABLATIONS builds)
+  int fused_tab = 0;        // DAB_FUSED_TAB=1 (DAB_ABLATIONS builds): the streamed fused pass reads the
+                            // k_cam_tables output instead of building its tables (kernel -0.9 us at C3,
+                            // but the extra launch in front costs more)
   void read() {
     auto get = [](const char* name, int& out) {
       if (const char* e = getenv(name)) out = atoi(e);
@@ -134,6 +139,9 @@ struct Knobs {
     get("DAB_CG_ONEWG", cg_onewg);
     get("DAB_BENCH_SAMPLE", bench_sample);
     get("DAB_SCHUR_TILES", schur_tiles);
+    get("DAB_FUSED_STREAM", fused_stream);
+    get("DAB_FUSED_V", fused_variant);
+    get("DAB_FUSED_TAB", fused_tab);
   }
 };
 
@@ -179,6 +187,11 @@ struct dab_handle {
   DevView view{};
   int4* d_obs_idx = nullptr;
   double2* d_obs_xy = nullptr;
+  // streamed fused pass: packed slot records (DevView::obs_e) and the camera-major point copy
+  // cmx [3][NE], re-gathered in eval_pass whenever the points changed (pts_version)
+  int* d_obs_e = nullptr;
+  double* d_cmx = nullptr;
+  long long pts_version = 0, cmx_version = -1;
   int4* d_cm_idx = nullptr;
   double2* d_cm_xy = nullptr;
   int4* d_x_idx = nullptr;
@@ -860,6 +873,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   }
   CHECK_RC(upload(&h->d_intr, d, intr, s));
   CHECK_RC(upload(&h->d_points, d, points, s));
+  ++h->pts_version;
   CHECK_RC(upload(&h->d_ext, d, ext, s));
   CHECK_RC(d.alloc(&h->d_points_c, (size_t)3 * NP));
   CHECK_RC(d.alloc(&h->d_ext_c, (size_t)6 * h->E));
@@ -940,6 +954,20 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   v.ext_col = h->d_ext_col;
   v.intr = h->d_intr;
   h->fused = h->fused && fused_eval_fits(v, h->nchunk, h->chunks.ngen, h->ncross, h->ncu);
+  v.obs_e = nullptr;
+  h->d_obs_e = nullptr;
+  h->d_cmx = nullptr;
+  h->cmx_version = -1;
+  if (h->fused && h->knobs.fused_stream != 0 && h->E < 0x8000 && h->NI < 0x8000) {
+    // streamed fused pass: 4-B slot records and the camera-major point copy
+    std::vector<int> obs_e(NS, -1);
+    for (int i = 0; i < NS; ++i)
+      if (obs_idx[i].x >= 0) obs_e[i] = obs_idx[i].y | (obs_idx[i].w << 16);
+    CHECK_RC(upload(&h->d_obs_e, d, obs_e, s));
+    CHECK_RC(d.alloc(&h->d_cmx, (size_t)3 * std::max(1, NE)));
+    HIP_OK(hipStreamSynchronize(s));
+    v.obs_e = h->d_obs_e;
+  }
   h->have_problem = true;
   return 0;
 }
@@ -1302,6 +1330,7 @@ extern "C" int dab_update_parameters(dab_handle* h, const double* points, const 
       for (int k = 0; k < 3; ++k) pts[3 * (size_t)i + k] = points[3 * (size_t)h->pt_of[i] + k];
     HIP_OK(hipMemcpyAsync(h->d_points, pts.data(), pts.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
     HIP_OK(hipStreamSynchronize(h->stream));
+    ++h->pts_version;
   }
   if (ext) {
     HIP_OK(hipMemcpyAsync(h->d_ext, ext, sizeof(double) * 6 * (size_t)h->E, hipMemcpyHostToDevice, h->stream));
@@ -1342,15 +1371,29 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
   hipStream_t s = h->stream;
   const DevView& v = h->view;
   bool overlapped = false;
-  const bool need_tab = (h->NC > 0 && (h->chunks.ngen > 0 || h->ncross > 0)) || eval_points_needs_camtab(h->eval_wps);
+  // the streamed fused pass reads R, t (point side) and R, t, Rd, Jd (camera side) from the
+  // tables of the current x instead of building them in every work-group
+#ifdef DAB_ABLATIONS
+  const bool fused_tab = h->fused && h->d_cmx && h->knobs.fused_tab != 0;
+#else
+  const bool fused_tab = false;
+#endif
+  const bool need_tab = (h->NC > 0 && (h->chunks.ngen > 0 || h->ncross > 0)) || eval_points_needs_camtab(h->eval_wps) ||
+                        fused_tab;
   if (!camtab_ready && need_tab) launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
   const bool fx = h->fused || eval_points_fx(h->eval_wps);
   if (fx) h->fx_last ^= 1;  // this pass adds into set fx_last and zeroes the other
   h->cost_fx_pending = fx;
+  if (h->d_cmx && h->cmx_version != h->pts_version) {
+    // the points changed since the camera-major copy was taken (set-up, accepted step)
+    launch_cmx_gather(s, v, h->d_points, h->d_cmx);
+    h->cmx_version = h->pts_version;
+  }
   if (h->fused && !h->fused_split) {  // both halves of the pass in one launch (launch_eval_fused)
     if (ev_mid) HIP_OK(hipEventRecord(ev_mid, s));
     launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
-                      h->cost_fx(h->fx_last ^ 1), h->ncu, 0);
+                      h->cost_fx(h->fx_last ^ 1), h->ncu, 0, h->d_cmx, h->knobs.fused_variant,
+                      fused_tab ? h->d_camtab : nullptr);
     if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
     if (h->NC > 0) CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
     return 0;
@@ -1361,7 +1404,7 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
     // leaves one CU per XCD free for it: eval_grid)
     if (ev_mid) HIP_OK(hipEventRecord(ev_mid, s));
     launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
-                      h->cost_fx(h->fx_last ^ 1), h->ncu, 2);
+                      h->cost_fx(h->fx_last ^ 1), h->ncu, 2, h->d_cmx, 0, fused_tab ? h->d_camtab : nullptr);
     bool ovl = false;
     if (h->comm && !h->host_cb) {
       HIP_OK(hipEventRecord(h->ev_cam, s));
@@ -1374,7 +1417,7 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
       CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
     }
     launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
-                      h->cost_fx(h->fx_last ^ 1), h->eval_grid, 1);
+                      h->cost_fx(h->fx_last ^ 1), h->eval_grid, 1, h->d_cmx, 0, fused_tab ? h->d_camtab : nullptr);
     if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
     if (ovl) HIP_OK(hipStreamWaitEvent(s, h->ev_comm, 0));
     return 0;
@@ -1744,6 +1787,7 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
       const double xc_norm = std::sqrt(h->h_scal[S_XCNORM_P] + h->h_scal[S_CAM0 + 1]);
       std::swap(h->d_points, h->d_points_c);
       std::swap(h->d_ext, h->d_ext_c);
+      ++h->pts_version;
       x_norm = xc_norm;
       const double tj = now_s();
       CHECK_RC(eval_jacobian_and_blocks(h, true));
@@ -2015,10 +2059,17 @@ extern "C" int dab_jacobian_bytes(dab_handle* h, double* bytes) {
   // point index + pixel; the chunk's camera and intrinsic are per block). A deterministic
   // matrix-free pass needs both traversal orders (point-major for V, g; camera-major for
   // U, g_c: no atomics, no per-observation partials), so both reads are algorithmic.
+  // The streamed fused form reads, per observation, a packed 4-B record (ext | intr) + the
+  // 16-B pixel on the point side and, per entry, the camera-major point copy (24 B) + the
+  // pixel on the camera side (no index, no gather).
   const double ext_b = eval_points_needs_camtab(h->eval_wps) ? 96.0 : 48.0;
   double b = (24.0 + 72.0) * h->NP + ext_b * h->E + 48.0 * h->NI;
-  if (h->fused) b += 216.0 * h->NC + 20.0 * h->NE;
-  for (int o = 0; o < h->N; ++o) b += 16.0 + 4.0 * (h->prob.obs_ext1[o] >= 0 ? 3 : 2);
+  if (h->fused && h->d_cmx) {
+    b += 216.0 * h->NC + 40.0 * h->NE + 20.0 * h->N;
+  } else {
+    if (h->fused) b += 216.0 * h->NC + 20.0 * h->NE;
+    for (int o = 0; o < h->N; ++o) b += 16.0 + 4.0 * (h->prob.obs_ext1[o] >= 0 ? 3 : 2);
+  }
   *bytes = b;
   return 0;
 }
