@@ -34,6 +34,7 @@ constexpr int LDP = 66;  // padded LDS row stride (doubles): conflict-free fragm
 constexpr int kBlk = 1024 + NB * NB;
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
+__constant__ int g_chol_prio = 1;  // DAB_CHOL_PRIO=0: no wave priority for the panel chain (A/B)
 
 struct CholCtx {
   double* blk = nullptr;  // per block column: D [4][16][16] (inverses of the 16x16 diagonal
@@ -46,13 +47,45 @@ struct CholCtx {
   hipGraphExec_t exec = nullptr;
   int g_n = -1, g_lda = -1;
   const void *g_A = nullptr, *g_y = nullptr, *g_flag = nullptr;
+  int bulk_grid = 0;  // work-groups of the persistent bulk update (0: one per tile)
+  int ncu = 256;
+  size_t bulk_pad = 0;      // DAB_CHOL_BULK_PAD (KB): dynamic LDS padding of the bulk work-groups
+  int bulk_kc = 16;         // DAB_CHOL_BULK_KC: K chunk of the bulk update (16 | 32)
+  int bulk_occ = 4;         // DAB_CHOL_BULK_OCC: waves per SIMD the bulk update is compiled for (2 | 4)
+  unsigned* bar = nullptr;  // grid-barrier counter of k_trsv_back_all (zeroed per solve)
+  bool v1 = false;          // DAB_CHOL_V1=1: the per-step schedule (one bulk update per panel, one
+                            // back-substitution launch per block)
 };
 
-CholCtx* chol_create() { return new CholCtx(); }
+CholCtx* chol_create() {
+  CholCtx* c = new CholCtx();
+  // DAB_CHOL_BULK_GRID: work-groups of the bulk trailing update (default: one per CU, so
+  // every CU keeps LDS room for a panel-chain work-group beside it)
+  int ncu = 256;
+  hipDeviceProp_t prop;
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+    ncu = prop.multiProcessorCount;
+  // two 512-thread bulk work-groups per CU, 32 CUs left for the panel chain (measured at
+  // n = 5994: 6.74 ms against 6.88-6.93 ms for one per CU or all CUs)
+  c->bulk_grid = std::max(1, 2 * ncu - 64);
+  c->ncu = ncu;
+  if (const char* e = getenv("DAB_CHOL_BULK_GRID")) c->bulk_grid = atoi(e);
+  if (const char* e = getenv("DAB_CHOL_V1")) c->v1 = atoi(e) != 0;
+  if (const char* e = getenv("DAB_CHOL_BULK_PAD")) c->bulk_pad = (size_t)atoi(e) * 1024;
+  if (const char* e = getenv("DAB_CHOL_BULK_KC")) c->bulk_kc = atoi(e);
+  if (const char* e = getenv("DAB_CHOL_BULK_OCC")) c->bulk_occ = atoi(e);
+  if (const char* e = getenv("DAB_CHOL_PRIO")) {
+    const int v = atoi(e);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chol_prio), &v, sizeof(int));
+  }
+  return c;
+}
 void chol_destroy(CholCtx* c) {
   if (!c) return;
   if (c->exec) (void)hipGraphExecDestroy(c->exec);
   if (c->blk) (void)hipFree(c->blk);
+  if (c->bar) (void)hipFree(c->bar);
   for (hipEvent_t e : c->ev_panel) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_bulk) (void)hipEventDestroy(e);
   if (c->side) (void)hipStreamDestroy(c->side);
@@ -210,6 +243,9 @@ __global__ __launch_bounds__(kThreads) void k_panel(double* __restrict__ A, int 
   __shared__ double L[NB][LS];
   __shared__ double P[NB][LS];
   __shared__ double D[4][16][DS];
+  // the panel chain is the critical path: its waves win the issue arbitration against the
+  // bulk update's waves on shared CUs
+  if (g_chol_prio) __builtin_amdgcn_s_setprio(3);
   const int tid = threadIdx.x, w = tid >> 6;
   const int row0 = r0 + NB * blockIdx.x;
 #pragma unroll
@@ -268,11 +304,17 @@ __global__ __launch_bounds__(kThreads) void k_panel(double* __restrict__ A, int 
 
 // col_only: just the first tile column of the trailing matrix (tile (t, 0)), the block
 // column the next panel step factors; otherwise the whole lower triangle of tiles.
-__global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, int lda, int r0, int m, int k,
-                                                        int kb, int col_only) {
+// ntiles: tiles of the launch; the grid may be smaller (a persistent bulk update that leaves
+// every CU room for the panel chain's work-groups), each work-group loops over its tiles.
+// The update has rank kk: panel columns [k, k + kk) in chunks of NB (kk = kb of one panel,
+// or two panels' 128 for the column after a panel pair).
+__global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, int lda, int r0, int m, int k0,
+                                                        int kk, int col_only, int ntiles) {
   __shared__ double Pa[NB * LDP];
   __shared__ double Pb[NB * LDP];
-  const int t = blockIdx.x;
+  if (col_only && g_chol_prio) __builtin_amdgcn_s_setprio(3);  // on the panel chain
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  if (t != (int)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
   int bi = t, bj = 0;
   if (!col_only) {
     bi = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
@@ -299,6 +341,9 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
         const int col = bj * NB + wc * 32 + b2 * 16 + li;
         acc[a2][b2][reg] = (!skip && row < m && col < m) ? A[(size_t)(r0 + row) * lda + r0 + col] : 0.0;
       }
+  for (int k = k0; k < k0 + kk; k += NB) {
+  const int kb = min(NB, k0 + kk - k);
+  if (k != k0) __syncthreads();  // the previous chunk's LDS reads are done
   // coalesced tile loads: 8 rows per pass, 32 double2 per row
 #pragma unroll
   for (int q = 0; q < NB / 8; ++q) {
@@ -320,7 +365,7 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
   }
   __syncthreads();
   const double* PB = diag ? Pa : Pb;
-  if (skip) return;
+  if (skip) continue;
 #pragma unroll 4
   for (int ks = 0; ks < NB / 4; ++ks) {
     double fa[2], fb[2];
@@ -334,6 +379,7 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
       for (int b2 = 0; b2 < 2; ++b2)
         acc[a2][b2] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a2], fb[b2], acc[a2][b2], 0, 0, 0);
   }
+  }
   // D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * reg
 #pragma unroll
   for (int a2 = 0; a2 < 2; ++a2)
@@ -343,8 +389,9 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
       for (int reg = 0; reg < 4; ++reg) {
         const int row = bi * NB + wr * 32 + a2 * 16 + lk + 4 * reg;
         const int col = bj * NB + wc * 32 + b2 * 16 + li;
-        if (row < m && col < m) A[(size_t)(r0 + row) * lda + r0 + col] = acc[a2][b2][reg];
+        if (!skip && row < m && col < m) A[(size_t)(r0 + row) * lda + r0 + col] = acc[a2][b2][reg];
       }
+  }
 }
 
 // back substitution step for block [k, k+kb): y_k = L_kk^-T z_k by 16-blocks with the
@@ -409,6 +456,232 @@ __global__ __launch_bounds__(kThreads) void k_trsv_back(const double* __restrict
   if (part == 0 && i < k) z[i] -= ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
 }
 
+
+// Bulk trailing update of a panel PAIR on 128 x 128 super-tiles (rank kk <= 128: the two
+// 64-wide panels of the pair, so the trailing matrix is read and written once per two
+// panel steps): C(i, j) -= sum_{q in [k0, k0 + kk)} A(i, q) A(j, q) for c0 <= j <= i <
+// c0 + m. Persistent: work-group g walks the lower super-tiles t = g, g + grid, ...; per
+// tile the product streams through LDS in 16-wide K chunks, double-buffered (the next
+// chunk's global loads are in flight during the current chunk's MFMAs). Wave w owns the
+// 64 x 64 quadrant (w >> 1, w & 1): 4 x 4 tiles of v_mfma_f64_16x16x4f64, 64 fp64
+// accumulators per lane; a diagonal super-tile skips its strictly upper quadrant. All LDS
+// is one __shared__ array (a second one can make hipcc drain vmcnt before every ds_read).
+constexpr int TB = 128;  // super-tile
+constexpr int kBigThreads = 512;
+// 8 waves: wave w owns the 64 x 32 half (w & 1) of quadrant w >> 1 (rows 64 (q >> 1), cols
+// 64 (q & 1)): 4 x 2 MFMA tiles, 32 accumulators per lane, so that ~110 VGPRs give 4 waves per
+// SIMD (two work-groups per CU) and one wave's waits are covered by another's MFMAs.
+template <int KC, int OCC>  // K chunk, waves per SIMD
+__global__ __launch_bounds__(kBigThreads, OCC) void k_syrk_big(double* __restrict__ A, int lda, int c0, int m, int k0,
+                                                            int kk, int ntiles) {
+  constexpr int LKC = KC + 2;                   // LDS row stride (doubles)
+  constexpr int PER = KC / 4;                   // doubles per thread and operand per chunk
+  constexpr int TPR = KC / PER;                 // loader threads per row (4)
+  __shared__ double sm[2 * 2 * TB * LKC];       // [stage][A | B][row][LKC]
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+  const int qd = w >> 1, wr = qd >> 1, wc = qd & 1, half = w & 1;
+  const int lr = tid / TPR, lh = (tid % TPR) * PER;  // loader: row lr, k columns lh .. lh + PER - 1
+  const int nch = (kk + KC - 1) / KC;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    int bi = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
+    while (bi * (bi + 1) / 2 > t) --bi;
+    const int bj = t - bi * (bi + 1) / 2;
+    const bool diag = bi == bj;
+    const bool skip = diag && wr < wc;
+    const int ri0 = bi * TB, rj0 = bj * TB;  // relative to c0
+    double ra[PER], rb[PER];
+    auto gload = [&](int ch) {
+      const int ia = ri0 + lr, ib = rj0 + lr;
+#pragma unroll
+      for (int q = 0; q < PER; q += 2) {
+        const int kc = ch * KC + lh + q;
+        ra[q] = ra[q + 1] = rb[q] = rb[q + 1] = 0.0;
+        if (ia < m) {
+          const double* src = A + (size_t)(c0 + ia) * lda + k0 + kc;
+          ra[q] = kc < kk ? src[0] : 0.0;
+          ra[q + 1] = kc + 1 < kk ? src[1] : 0.0;
+        }
+        if (!diag && ib < m) {
+          const double* src = A + (size_t)(c0 + ib) * lda + k0 + kc;
+          rb[q] = kc < kk ? src[0] : 0.0;
+          rb[q + 1] = kc + 1 < kk ? src[1] : 0.0;
+        }
+      }
+    };
+    auto sstore = [&](int st) {
+      double* a = sm + (size_t)(2 * st) * TB * LKC + lr * LKC + lh;
+#pragma unroll
+      for (int q = 0; q < PER; q += 2) *reinterpret_cast<double2*>(a + q) = make_double2(ra[q], ra[q + 1]);
+      if (!diag) {
+        double* b = a + TB * LKC;
+#pragma unroll
+        for (int q = 0; q < PER; q += 2) *reinterpret_cast<double2*>(b + q) = make_double2(rb[q], rb[q + 1]);
+      }
+    };
+    dbl4 acc[4][2];
+#pragma unroll
+    for (int tr = 0; tr < 4; ++tr)
+#pragma unroll
+      for (int tc = 0; tc < 2; ++tc)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int row = ri0 + 64 * wr + 16 * tr + lk + 4 * reg, col = rj0 + 64 * wc + 32 * half + 16 * tc + li;
+          acc[tr][tc][reg] = (!skip && row < m && col < m) ? A[(size_t)(c0 + row) * lda + c0 + col] : 0.0;
+        }
+    gload(0);
+    __syncthreads();  // the previous tile's LDS reads are done
+    sstore(0);
+    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) {
+      const int st = ch & 1;
+      if (ch + 1 < nch) gload(ch + 1);
+      if (!skip) {
+        const double* As = sm + (size_t)(2 * st) * TB * LKC;
+        const double* Bs = diag ? As : As + TB * LKC;
+#pragma unroll
+        for (int ks = 0; ks < KC / 4; ++ks) {
+          double fa[4], fb[2];
+#pragma unroll
+          for (int tr = 0; tr < 4; ++tr) fa[tr] = -As[(64 * wr + 16 * tr + li) * LKC + 4 * ks + lk];
+#pragma unroll
+          for (int tc = 0; tc < 2; ++tc) fb[tc] = Bs[(64 * wc + 32 * half + 16 * tc + li) * LKC + 4 * ks + lk];
+#pragma unroll
+          for (int tr = 0; tr < 4; ++tr)
+#pragma unroll
+            for (int tc = 0; tc < 2; ++tc)
+              acc[tr][tc] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[tr], fb[tc], acc[tr][tc], 0, 0, 0);
+        }
+      }
+      if (ch + 1 < nch) sstore(st ^ 1);
+      __syncthreads();
+    }
+    if (!skip) {
+#pragma unroll
+      for (int tr = 0; tr < 4; ++tr)
+#pragma unroll
+        for (int tc = 0; tc < 2; ++tc)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) {
+            const int row = ri0 + 64 * wr + 16 * tr + lk + 4 * reg, col = rj0 + 64 * wc + 32 * half + 16 * tc + li;
+            if (row < m && col < m) A[(size_t)(c0 + row) * lda + c0 + col] = acc[tr][tc][reg];
+          }
+    }
+  }
+}
+
+// Back substitution L^T y = z in ONE launch (instead of one per block): grid G <= CUs,
+// every work-group resident. Per block b, last first, every work-group computes y_b =
+// L_bb^-T z_b from the stored 16x16 inverses (redundantly: no hand-off needed for it),
+// work-group 0 writes y_b, and each work-group updates its 64-column shares of z[0:k_b]
+// with L[k_b : k_b + kb, shares]^T y_b; then a grid barrier (the counter form of the
+// agent-scope release/acquire hand-off; bounded spin: on timeout flag |= 2 and the kernel
+// ends instead of hanging).
+__global__ __launch_bounds__(kThreads) void k_trsv_back_all(const double* __restrict__ A, int lda, int n, int nblk,
+                                                            const double* __restrict__ blk, double* __restrict__ z,
+                                                            double* __restrict__ y, unsigned* __restrict__ bar,
+                                                            int* __restrict__ flag) {
+  __shared__ double Lk[NB][LS];
+  __shared__ double Dq[4][16][DS];
+  __shared__ double yy[NB];
+  __shared__ double tt[16];
+  __shared__ double red[4][64];
+  __shared__ int abort_s;
+  const int tid = threadIdx.x, G = gridDim.x;
+  if (tid == 0) abort_s = 0;
+  for (int b = nblk - 1; b >= 0; --b) {
+    const int k = b * NB, kb = min(NB, n - k);
+    const double* bk = blk + (size_t)b * kBlk;
+#pragma unroll
+    for (int q = 0; q < NB * NB / kThreads; ++q) {
+      const int idx = tid + q * kThreads, i = idx >> 6, j = idx & 63;
+      Lk[i][j] = bk[1024 + idx];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = tid + q * kThreads;
+      Dq[idx >> 8][(idx >> 4) & 15][idx & 15] = bk[idx];
+    }
+    // z_b: written by its owner with agent-scope (L2-bypassing) stores, read likewise
+    if (tid < NB) yy[tid] = tid < kb ? __hip_atomic_load(z + k + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    __syncthreads();
+    // y_b by 16-blocks, q = 3..0, with all 256 threads (c = tid & 15, part = tid >> 4):
+    // t_c = z_c - sum_{j >= 16 (q+1)} L[j][16 q + c] y_j (terms j = 16 (q+1) + part + 16 u),
+    // then y_{16 q + c} = sum_{mm >= c} D_q[mm][c] t_mm (term mm = part); both sums in a fixed
+    // order through LDS
+    {
+      const int c = tid & 15, part = tid >> 4;
+#pragma unroll
+      for (int q = 3; q >= 0; --q) {
+        double acc = 0.0;
+        for (int j = 16 * (q + 1) + part; j < NB; j += 16) acc = fma(-Lk[j][16 * q + c], yy[j], acc);
+        red[part >> 2][(part & 3) * 16 + c] = acc;
+        __syncthreads();
+        if (tid < 16) {
+          double t = yy[16 * q + c];
+#pragma unroll
+          for (int p2 = 0; p2 < 16; ++p2) t += red[p2 >> 2][(p2 & 3) * 16 + c];
+          tt[c] = t;
+        }
+        __syncthreads();
+        red[part >> 2][(part & 3) * 16 + c] = part >= c ? Dq[q][part][c] * tt[part] : 0.0;
+        __syncthreads();
+        if (tid < 16) {
+          double sacc = 0.0;
+#pragma unroll
+          for (int p2 = 0; p2 < 16; ++p2) sacc += red[p2 >> 2][(p2 & 3) * 16 + c];
+          yy[16 * q + c] = sacc;
+        }
+        __syncthreads();
+      }
+    }
+    if (blockIdx.x == 0 && tid < kb) y[k + tid] = yy[tid];
+    if (b == 0) break;
+    // z[i] -= sum_mm L[k + mm][i] y[mm] for this work-group's 64-column shares of [0, k)
+    const int part = tid >> 6;
+    for (int i0 = blockIdx.x * 64; i0 < k; i0 += 64 * G) {
+      const int i = i0 + (tid & 63);
+      double sacc = 0.0;
+      if (i < k) {
+#pragma unroll
+        for (int q = 0; q < NB / 4; ++q) {
+          const int mm = part * (NB / 4) + q;
+          if (mm < kb) sacc += A[(size_t)(k + mm) * lda + i] * yy[mm];
+        }
+      }
+      red[part][tid & 63] = sacc;
+      __syncthreads();
+      if (part == 0 && i < k) {
+        // z[i] has one writer (this work-group, every step): the current value is its own
+        const double zi = __hip_atomic_load(z + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(z + i, zi - (((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+    }
+    // grid barrier: every wave's (agent-scope) z stores complete before the ticket; a
+    // bounded relaxed poll. No cache-wide release/acquire: z moves by agent-scope accesses
+    // only, and L_bb, D_b, A stay cached.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned target = (unsigned)G * (unsigned)(nblk - b);
+      int spins = 0;
+      while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1 << 22)) {
+          abort_s = 1;
+          atomicOr(flag, 2);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (abort_s) return;
+  }
+}
+
 static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y,
                                  int* d_flag);
 
@@ -424,6 +697,7 @@ int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
     c->nblk_alloc = nblk;
   }
   if (!c->side && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) return -3;
+  if (!c->bar && hipMalloc(&c->bar, sizeof(unsigned)) != hipSuccess) return -2;
   while ((int)c->ev_panel.size() < nblk) {
     hipEvent_t a, b;
     if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess) return -3;
@@ -458,8 +732,71 @@ int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
   return hipGraphLaunch(c->exec, s) == hipSuccess ? 0 : -3;
 }
 
+static void enqueue_factor_solve_v1(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y,
+                                    int* d_flag);
+// Panel PAIRS with lookahead. Chain stream s, per pair (b, b+1): [wait the previous pair's
+// bulk] column b+1 with panel b -> panel b+1 -> column b+2 with panels b, b+1 -> panel b+2;
+// bulk stream s2: after panel b+1, the rank-128 update of columns >= b+3 (k_syrk_big),
+// overlapping the chain. The trailing matrix is streamed once per two panel steps. Then
+// the back substitution in one launch (k_trsv_back_all).
 static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y,
                                  int* d_flag) {
+  if (c->v1) {
+    enqueue_factor_solve_v1(c, s, n, A, lda, y, d_flag);
+    return;
+  }
+  const int nblk = (n + NB - 1) / NB;
+  hipStream_t s2 = getenv("DAB_CHOL_SERIAL") ? s : c->side;  // serial: debugging aid
+  auto kb_of = [&](int b) { return std::min(NB, n - b * NB); };
+  auto panel = [&](int b) {
+    const int k = b * NB, kb = kb_of(b);
+    const int r0 = k + kb, r1 = n + 1;  // includes the rhs row n
+    const int grid = std::max(1, (r1 - r0 + NB - 1) / NB);
+    k_panel<<<grid, kThreads, 0, s>>>(A, lda, k, kb, r0, r1, c->blk + (size_t)b * kBlk, d_flag);
+  };
+  // column block cb (rows >= its first row, through the rhs row) with panel columns [k, k + kk)
+  auto col = [&](int cb, int k, int kk) {
+    const int r0 = cb * NB, m = n + 1 - r0;
+    if (m <= 1) return;
+    const int nt = (m + NB - 1) / NB;
+    k_syrk_mfma<<<nt, kThreads, 0, s>>>(A, lda, r0, m, k, kk, 1, nt);
+  };
+  panel(0);
+  int pending = -1;  // pair whose bulk update is still running on s2
+  for (int b = 0; b + 1 < nblk; b += 2) {
+    if (pending >= 0) (void)hipStreamWaitEvent(s, c->ev_bulk[pending], 0);
+    pending = -1;
+    col(b + 1, b * NB, kb_of(b));
+    panel(b + 1);
+    if (b + 2 >= nblk) break;  // panel b + 1 was the last (its solve covered the rhs row)
+    const int kk = kb_of(b) + kb_of(b + 1);
+    const int c0 = (b + 3) * NB, m = n + 1 - c0;
+    if (m > 1) {
+      (void)hipEventRecord(c->ev_panel[b], s);
+      (void)hipStreamWaitEvent(s2, c->ev_panel[b], 0);
+      const int t2 = (m + TB - 1) / TB, ntb = t2 * (t2 + 1) / 2;
+      // bulk_pad: extra (unused) LDS so that no panel-chain work-group shares a CU with the
+      // bulk (its dependent MFMA chain would queue behind the bulk's MFMAs); the bulk grid
+      // leaves CUs free for the chain instead
+      const int g = std::min(ntb, c->bulk_grid > 0 ? c->bulk_grid : ntb);
+      if (c->bulk_kc == 32) k_syrk_big<32, 2><<<g, kBigThreads, c->bulk_pad, s2>>>(A, lda, c0, m, b * NB, kk, ntb);
+      else if (c->bulk_occ == 4) k_syrk_big<16, 4><<<g, kBigThreads, c->bulk_pad, s2>>>(A, lda, c0, m, b * NB, kk, ntb);
+      else k_syrk_big<16, 2><<<g, kBigThreads, c->bulk_pad, s2>>>(A, lda, c0, m, b * NB, kk, ntb);
+      (void)hipEventRecord(c->ev_bulk[b], s2);
+      pending = b;
+    }
+    col(b + 2, b * NB, kk);
+    panel(b + 2);
+  }
+  if (pending >= 0) (void)hipStreamWaitEvent(s, c->ev_bulk[pending], 0);
+  double* z = A + (size_t)n * lda;
+  (void)hipMemsetAsync(c->bar, 0, sizeof(unsigned), s);
+  const int G = std::max(1, std::min(c->ncu / 2, (n + 63) / 64));
+  k_trsv_back_all<<<G, kThreads, 0, s>>>(A, lda, n, nblk, c->blk, z, y, c->bar, d_flag);
+}
+
+static void enqueue_factor_solve_v1(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y,
+                                    int* d_flag) {
   // Lookahead by one block column. Chain stream s: P(0), then per step b
   // [wait bulk(b-1)] col-update(b) -> P(b+1); bulk stream s2: bulk(b) after P(b). The
   // bulk trailing update of step b overlaps the next panel step.
@@ -483,12 +820,14 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
       (void)hipEventRecord(c->ev_panel[b], s);
       (void)hipStreamWaitEvent(s2, c->ev_panel[b], 0);
       const int m2 = m - NB, nt2 = (m2 + NB - 1) / NB;
-      k_syrk_mfma<<<nt2 * (nt2 + 1) / 2, kThreads, 0, s2>>>(A, lda, r0 + NB, m2, k, kb, 0);
+      const int ntb = nt2 * (nt2 + 1) / 2;
+      k_syrk_mfma<<<std::min(ntb, c->bulk_grid > 0 ? c->bulk_grid : ntb), kThreads, 0, s2>>>(A, lda, r0 + NB, m2, k,
+                                                                                         kb, 0, ntb);
       (void)hipEventRecord(c->ev_bulk[b], s2);
       bulk = true;
     }
     if (bulk_prev) (void)hipStreamWaitEvent(s, c->ev_bulk[b - 1], 0);
-    if (m > 1) k_syrk_mfma<<<nt, kThreads, 0, s>>>(A, lda, r0, m, k, kb, 1);
+    if (m > 1) k_syrk_mfma<<<nt, kThreads, 0, s>>>(A, lda, r0, m, k, kb, 1, nt);
     if (b + 1 < nblk) panel(b + 1);
     bulk_prev = bulk;
   }

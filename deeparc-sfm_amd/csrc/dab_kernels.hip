@@ -2241,19 +2241,33 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
 #undef DAB_FUSED_ARGS
 }
 
-// camera-major point copy for the streamed fused pass: cmx[q][i] = points[cm_pt[i]][q]
+// camera-major point copy for the streamed fused pass: cmx[q][i] = points[cm_pt[i]][q].
+// Four entries per thread (stride one grid row), every index load issued before the
+// gathers and every gather before the stores, so each thread has 4 x 3 loads in flight.
 __global__ __launch_bounds__(256) void k_cmx_gather(int NE, const int* __restrict__ cm_pt,
                                                     const double* __restrict__ points, double* __restrict__ cmx) {
   const size_t NEs = (size_t)NE;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < NE; i += gridDim.x * blockDim.x) {
-    const int p = cm_pt[i];
+  const int row = gridDim.x * blockDim.x;
+  for (int i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < NE; i0 += 4 * row) {
+    int p[4];
+    double x[4][3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) cmx[q * NEs + i] = points[3 * (size_t)p + q];
+    for (int k = 0; k < 4; ++k) p[k] = cm_pt[min(i0 + k * row, NE - 1)];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) x[k][q] = points[3 * (size_t)p[k] + q];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i0 + k * row < NE) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) cmx[q * NEs + i0 + k * row] = x[k][q];
+      }
   }
 }
 void launch_cmx_gather(hipStream_t s, const DevView& v, const double* points, double* cmx) {
   if (v.NE <= 0) return;
-  k_cmx_gather<<<grid_for(v.NE, 256, 8192), 256, 0, s>>>(v.NE, v.cm_pt, points, cmx);
+  k_cmx_gather<<<grid_for((v.NE + 3) / 4, 256, 4096), 256, 0, s>>>(v.NE, v.cm_pt, points, cmx);
 }
 
 // arc∘ring cross blocks Jc0^T Jc1, one block per chunk of composed observations sorted

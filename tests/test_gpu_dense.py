@@ -7,7 +7,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n", [1, 6, 63, 64, 65, 130, 384, 1000])
+@pytest.mark.parametrize("n", [1, 6, 63, 64, 65, 127, 128, 130, 191, 192, 193, 256, 257, 384, 449, 1000, 2048])
 def test_dense_spd_solve_matches_numpy(pkg, gpu, n):
     rng = np.random.default_rng(n)
     M = rng.standard_normal((n, n))
