@@ -247,6 +247,11 @@ def main():
         summ = rsolver.solve(opts)
         its = [it["time"] for it in summ["iterations"][1:]]
         mf = rsolver.pcg_matrix_free()
+        # the same LM with fp64 products, for comparison with the mixed-precision line
+        rsolver.update_parameters(rp0, re0)
+        opts.pcg_fp32 = 0
+        s64 = rsolver.solve(opts)
+        its64 = [it["time"] for it in s64["iterations"][1:]]
         # the exact step (DENSE_SCHUR): S from the block tiles, dense Cholesky of 474 x 474
         rsolver.update_parameters(rp0, re0)
         barrier()
@@ -262,8 +267,13 @@ def main():
                  "rig_lm_explicit_schur_assembly": {0: "pair tables", 1: "block tiles"}[sx["schur_assembly"]]}
         rig = {"rig_config": args.rig_config, "rig_global_obs": gprob.num_obs,
                "rig_lm_pcg_iter_ms_median": max_over_ranks(1e3 * float(np.median(its))) if its else None,
-               "rig_linear_solver": ("implicit-Schur PCG, matrix-free Schur products (fp64, no stored factors)"
-                                     if mf else "implicit-Schur PCG, fp32 Schur factors"),
+               "rig_linear_solver": {2: "implicit-Schur PCG, mixed precision: matrix-free Schur products in fp32 "
+                                        "arithmetic, fp64 sums, CG recurrences and true residuals (every 10th CG "
+                                        "iteration, fp64 product)",
+                                     1: "implicit-Schur PCG, matrix-free Schur products (fp64, no stored factors)",
+                                     0: "implicit-Schur PCG, fp32 Schur factors"}[mf],
+               "rig_lm_pcg64_iter_ms_median": max_over_ranks(1e3 * float(np.median(its64))) if its64 else None,
+               "rig_lm_pcg64_linear_iterations": [it["linear_solver_iterations"] for it in s64["iterations"][1:]],
                "rig_lm_iterations": summ["num_iterations"],
                "rig_lm_linear_iterations": [it["linear_solver_iterations"] for it in summ["iterations"][1:]],
                "rig_initial_cost": summ["initial_cost"], "rig_final_cost": summ["final_cost"],

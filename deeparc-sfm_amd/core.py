@@ -290,9 +290,10 @@ class Solver:
         return b.value
 
     def pcg_matrix_free(self):
+        """0: stored-Y products; 1: matrix-free fp64; 2: matrix-free mixed precision (pcg_fp32)"""
         f = C.c_int32()
         check(self.lib.dab_pcg_schedule(self.h, C.byref(f)), self.lib)
-        return bool(f.value)
+        return int(f.value)
 
     def eval_fused(self):
         f = C.c_int32()

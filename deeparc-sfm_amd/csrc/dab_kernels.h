@@ -286,6 +286,10 @@ int mf_grid(int NP, int ncu);
 void launch_mf_product(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                        const double* scale_c, const double* PU, const double* vec, double* partial, double* w,
                        int grid, const PcgState* st);
+// the same product with fp32 per-observation arithmetic and fp64 sums (mixed precision)
+void launch_mf_product32(hipStream_t s, const DevView& v, const double* points, const double* camtab,
+                         const double* scale_c, const double* PU, const double* vec, double* partial, double* w,
+                         int grid, const PcgState* st);
 // dp[3][NP] = -PU (q - sum_e Y_e^T y_c)
 void launch_mf_backsub(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                        const double* scale_c, const double* PU, const double* q, const double* yc, double* dp,

@@ -3443,7 +3443,7 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_points(DevView v, const doub
 static size_t mf2_lds_bytes(int E, int NI, int NC, bool product) {
   return sizeof(double) * (12 * (size_t)E + 6 * (size_t)NI + 6 * (size_t)NC + 9 * (size_t)NC +
                            (product ? (kMfBlock / 64) * 6 * (size_t)NC : 0)) +
-         sizeof(int) * (size_t)E;
+         2 * sizeof(int) * (size_t)E;
 }
 template <int MODE>
 __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const double* __restrict__ points,
@@ -3462,6 +3462,7 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const doubl
   double* jl_s = dv_s + NC6;                           // [NC][9]: J_l (MODE 0, 2)
   double* accs = jl_s + 9 * (size_t)v.NC;              // [waves][NC][6] (MODE 0, 2)
   int* sm_s = reinterpret_cast<int*>(accs + (MODE != 1 ? (kMfBlock / 64) * NC6 : 0));  // [E]
+  int* col_s = sm_s + v.E;                             // [E] ext_col: no dependent global load per slot
   for (int i = threadIdx.x; i < 12 * v.E; i += blockDim.x) rt_s[i] = camtab[(size_t)kCamTab * (i / 12) + i % 12];
   for (int i = threadIdx.x; i < 6 * v.NI; i += blockDim.x) k_s[i] = v.intr[(size_t)kIntr * (i / 6) + i % 6];
   for (int e = threadIdx.x; e < v.E; e += blockDim.x) {
@@ -3471,6 +3472,7 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const doubl
                   ? 1
                   : 0;  // Rd = I: the small-angle tables
     const int c = v.ext_col[e];
+    col_s[e] = c;
     if (c < 0) continue;
     double J[9];
 #pragma unroll
@@ -3573,13 +3575,15 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const doubl
       up[1] = pu[3] * q1 + pu[4] * q2;
       up[2] = pu[5] * q2;
     } else {
-      // sweep 1: a = sum_e J_p^T (J_c (s_c o v_c))
+      // sweep 1: a = sum_e J_p^T (J_c (s_c o v_c)); the next slot's index is in flight
       double a[3] = {0.0, 0.0, 0.0};
+      int4 nid = len > 0 ? v.obs_idx[off + lane] : make_int4(-1, 0, -1, 0);
       for (int k = 0; k < len; ++k) {
         const int s = off + 64 * k + lane;
-        const int4 id = v.obs_idx[s];
+        const int4 id = nid;
+        if (k + 1 < len) nid = v.obs_idx[s + 64];
         if (id.x < 0) continue;
-        const int c0 = v.ext_col[id.y], c1 = id.z >= 0 ? v.ext_col[id.z] : -1;
+        const int c0 = col_s[id.y], c1 = id.z >= 0 ? col_s[id.z] : -1;
         if (c0 < 0 && c1 < 0) continue;
         double A0[3], A1[3], Ra[9], Z0[3], Z1[3], unused[3];
         bool comp;
@@ -3635,11 +3639,13 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const doubl
     }
     if constexpr (MODE != 1) {
       // sweep 2: per camera, sum [Z x g | g] (J_l^T and -s_c applied after the sums)
+      int4 nid = len > 0 ? v.obs_idx[off + lane] : make_int4(-1, 0, -1, 0);
       for (int k = 0; k < len; ++k) {
         const int s = off + 64 * k + lane;
-        const int4 id = v.obs_idx[s];
+        const int4 id = nid;
+        if (k + 1 < len) nid = v.obs_idx[s + 64];
         if (id.x < 0) continue;
-        const int c0 = v.ext_col[id.y], c1 = id.z >= 0 ? v.ext_col[id.z] : -1;
+        const int c0 = col_s[id.y], c1 = id.z >= 0 ? col_s[id.z] : -1;
         if (c0 < 0 && c1 < 0) continue;
         double A0[3], A1[3], Ra[9], Z0[3], Z1[3], kk[3];
         bool comp;
@@ -3690,6 +3696,264 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const doubl
       }
       out[(size_t)blockIdx.x * NC6 + i] = -scc[i] * x;
     }
+  }
+}
+
+// ---- mixed precision (BASELINE config 5): the Schur product in fp32 arithmetic ----------
+// k_mf_frame<0> with every per-observation operation in fp32: the R, t tables, the focal and
+// distortion terms, w~ and dt per camera are staged in LDS as floats (24 instead of 48 B per
+// table read), the point, PU_p and the projection Jacobian A are fp32, and so are the two
+// sweeps' 3-vectors. Accumulation stays fp64: each observation's camera terms are widened
+// before the per-wave LDS sums, J_l^T and -s_c are applied to the fp64 sums, and the
+// work-group partials are added in fixed order (launch_pcg_fused_final). The product is
+// accurate to ~1e-7 relative; the PCG keeps its recurrences, dot products and the periodic
+// true residual r = b - S x in fp64 (that product is the fp64 k_mf_frame<0>), which is the
+// iterative refinement that bounds the drift of the fp32 products. The observed pixel is
+// not read: the products need the Jacobian only.
+__device__ __forceinline__ void mv3f(const float* __restrict__ M, const float (&x)[3], float (&o)[3]) {
+  o[0] = M[0] * x[0] + M[1] * x[1] + M[2] * x[2];
+  o[1] = M[3] * x[0] + M[4] * x[1] + M[5] * x[2];
+  o[2] = M[6] * x[0] + M[7] * x[1] + M[8] * x[2];
+}
+__device__ __forceinline__ void mtv3f(const float* __restrict__ M, const float (&x)[3], float (&o)[3]) {
+  o[0] = M[0] * x[0] + M[3] * x[1] + M[6] * x[2];
+  o[1] = M[1] * x[0] + M[4] * x[1] + M[7] * x[2];
+  o[2] = M[2] * x[0] + M[5] * x[1] + M[8] * x[2];
+}
+__device__ __forceinline__ void cross3f(const float (&a)[3], const float (&b)[3], float (&o)[3]) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+// d (ru, rv) / d P of projectPoint (the Jacobian half of `project`), K = fx fy k0 k1
+__device__ __forceinline__ void proj_jac32(const float (&P)[3], const float4 K, float (&A0)[3], float (&A1)[3]) {
+  float iz = __builtin_amdgcn_rcpf(P[2]);
+  iz = fmaf(iz, fmaf(-P[2], iz, 1.0f), iz);
+  const float xp = P[0] * iz, yp = P[1] * iz;
+  const float r2 = xp * xp + yp * yp;
+  const float d = 1.0f + r2 * (K.z + K.w * r2);
+  const float dd = K.z + 2.0f * K.w * r2;
+  const float du_dx = K.x * (d + 2.0f * xp * xp * dd), du_dy = K.x * (2.0f * xp * yp * dd);
+  const float dv_dx = K.y * (2.0f * xp * yp * dd), dv_dy = K.y * (d + 2.0f * yp * yp * dd);
+  A0[0] = du_dx * iz;
+  A0[1] = du_dy * iz;
+  A0[2] = -(du_dx * xp + du_dy * yp) * iz;
+  A1[0] = dv_dx * iz;
+  A1[1] = dv_dy * iz;
+  A1[2] = -(dv_dx * xp + dv_dy * yp) * iz;
+}
+static size_t mf32_lds_bytes(int E, int NI, int NC) {
+  return sizeof(double) * (9 * (size_t)NC + (kMfBlock / 64) * 6 * (size_t)NC) +
+         sizeof(float) * (12 * (size_t)E + 4 * (size_t)NI + 6 * (size_t)NC) + 2 * sizeof(int) * (size_t)E;
+}
+__global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame32(DevView v, const double* __restrict__ points,
+                                                         const double* __restrict__ camtab,
+                                                         const double* __restrict__ scc,
+                                                         const double* __restrict__ PU,
+                                                         const double* __restrict__ vec, double* __restrict__ out,
+                                                         const PcgState* st) {
+  extern __shared__ double mf_lds[];
+  if (st->status != kPcgRunning) return;
+  const int NC6 = 6 * v.NC;
+  double* jl_s = mf_lds;                                        // [NC][9] J_l (fp64, applied to the sums)
+  double* accs = jl_s + 9 * (size_t)v.NC;                       // [waves][NC][6] fp64 sums
+  float* rt_s = reinterpret_cast<float*>(accs + (kMfBlock / 64) * NC6);  // [E][12] R | t
+  float* k_s = rt_s + 12 * (size_t)v.E;                         // [NI][4] fx fy k0 k1
+  float* dv_s = k_s + 4 * (size_t)v.NI;                         // [NC][6] w~ | dt
+  int* sm_s = reinterpret_cast<int*>(dv_s + NC6);               // [E] small-angle tables
+  int* col_s = sm_s + v.E;                                      // [E] ext_col
+  for (int i = threadIdx.x; i < 12 * v.E; i += blockDim.x)
+    rt_s[i] = (float)camtab[(size_t)kCamTab * (i / 12) + i % 12];
+  for (int i = threadIdx.x; i < 4 * v.NI; i += blockDim.x) k_s[i] = (float)v.intr[(size_t)kIntr * (i / 4) + 2 + i % 4];
+  for (int e = threadIdx.x; e < v.E; e += blockDim.x) {
+    const double* T = camtab + (size_t)kCamTab * e;  // R t Rd Jd
+    sm_s[e] = (T[12] == 1.0 && T[13] == 0.0 && T[14] == 0.0 && T[15] == 0.0 && T[16] == 1.0 && T[17] == 0.0 &&
+               T[18] == 0.0 && T[19] == 0.0 && T[20] == 1.0)
+                  ? 1
+                  : 0;
+    const int c = v.ext_col[e];
+    col_s[e] = c;
+    if (c < 0) continue;
+    double J[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc)
+        J[3 * r + cc] = T[12 + 3 * r] * T[21 + cc] + T[12 + 3 * r + 1] * T[24 + cc] + T[12 + 3 * r + 2] * T[27 + cc];
+    double d[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) d[k] = scc[6 * c + k] * vec[6 * c + k];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) dv_s[6 * c + r] = (float)(J[3 * r] * d[0] + J[3 * r + 1] * d[1] + J[3 * r + 2] * d[2]);
+#pragma unroll
+    for (int k = 3; k < 6; ++k) dv_s[6 * c + k] = (float)d[k];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) jl_s[9 * c + k] = J[k];
+  }
+  for (int i = threadIdx.x; i < (kMfBlock / 64) * NC6; i += blockDim.x) accs[i] = 0.0;
+  __syncthreads();
+  double* acc = accs + (threadIdx.x >> 6) * NC6;
+  auto add = [&](int i, float x) { atomicAdd(acc + i, (double)x); };  // fp64 per-wave camera sums
+  auto sum_of = [&](int i) {  // fixed order over the waves
+    double t = accs[i];
+#pragma unroll
+    for (int w = 1; w < kMfBlock / 64; ++w) t += accs[w * NC6 + i];
+    return t;
+  };
+  auto rt = [&](int e, float (&o)[12]) {
+    const float4* pp = reinterpret_cast<const float4*>(rt_s + 12 * e);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float4 u = pp[k];
+      o[4 * k] = u.x;
+      o[4 * k + 1] = u.y;
+      o[4 * k + 2] = u.z;
+      o[4 * k + 3] = u.w;
+    }
+  };
+  // one observation's geometry (as k_mf_frame's geo): A (2 x 3), R_a, the rotated-frame
+  // points Z of both slots, and vout = R_b vin while the ring table is in registers
+  auto geo = [&](const int4 id, const float (&X)[3], float (&A0)[3], float (&A1)[3], float (&Ra)[12],
+                 float (&Z0)[3], float (&Z1)[3], bool& comp, const float (&vin)[3], float (&vout)[3]) {
+    rt(id.y, Ra);
+    const float4 K = *reinterpret_cast<const float4*>(k_s + 4 * id.w);
+    comp = id.z >= 0;
+    float Q[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) vout[k] = vin[k];
+    if (comp) {
+      float Tb[12];
+      rt(id.z, Tb);
+      float RX[3];
+      mv3f(Tb, X, RX);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) Q[k] = RX[k] + Tb[9 + k];
+      mv3f(Tb, vin, vout);
+      const bool sb = sm_s[id.z] != 0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) Z1[k] = sb ? X[k] : RX[k];  // Q - t_b
+    } else {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) Q[k] = X[k];
+    }
+    float RQ[3], P[3];
+    mv3f(Ra, Q, RQ);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) P[k] = RQ[k] + Ra[9 + k];
+    const bool sa = sm_s[id.y] != 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) Z0[k] = sa ? Q[k] : RQ[k];  // P - t_a
+    proj_jac32(P, K, A0, A1);
+  };
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < v.NP; p += gridDim.x * blockDim.x) {
+    const int sl = p >> 6, lane = p & 63;
+    const int off = v.slice_off[sl], len = (v.slice_off[sl + 1] - off) >> 6;
+    const float X[3] = {(float)points[3 * (size_t)p], (float)points[3 * (size_t)p + 1],
+                        (float)points[3 * (size_t)p + 2]};
+    float pu[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) pu[k] = (float)PU[6 * (size_t)p + k];
+    // sweep 1: a = sum_e J_p^T (J_c (s_c o v_c))
+    float a[3] = {0.0f, 0.0f, 0.0f};
+    const float zero3[3] = {0.0f, 0.0f, 0.0f};
+    int4 nid = len > 0 ? v.obs_idx[off + lane] : make_int4(-1, 0, -1, 0);
+    for (int k = 0; k < len; ++k) {
+      const int s = off + 64 * k + lane;
+      const int4 id = nid;
+      if (k + 1 < len) nid = v.obs_idx[s + 64];
+      if (id.x < 0) continue;
+      const int c0 = col_s[id.y], c1 = id.z >= 0 ? col_s[id.z] : -1;
+      if (c0 < 0 && c1 < 0) continue;
+      float A0[3], A1[3], Ra[12], Z0[3], Z1[3], unused[3];
+      bool comp;
+      geo(id, X, A0, A1, Ra, Z0, Z1, comp, zero3, unused);
+      float dP[3] = {0.0f, 0.0f, 0.0f};
+      if (c0 >= 0) {
+        const float* d = dv_s + 6 * c0;
+        const float w[3] = {d[0], d[1], d[2]};
+        float cz[3];
+        cross3f(Z0, w, cz);
+#pragma unroll
+        for (int k2 = 0; k2 < 3; ++k2) dP[k2] = d[3 + k2] - cz[k2];
+      }
+      if (c1 >= 0) {
+        const float* d = dv_s + 6 * c1;
+        const float w[3] = {d[0], d[1], d[2]};
+        float cz[3], r[3], r2[3];
+        cross3f(Z1, w, cz);
+#pragma unroll
+        for (int k2 = 0; k2 < 3; ++k2) r[k2] = d[3 + k2] - cz[k2];
+        mv3f(Ra, r, r2);
+#pragma unroll
+        for (int k2 = 0; k2 < 3; ++k2) dP[k2] += r2[k2];
+      }
+      const float u0 = A0[0] * dP[0] + A0[1] * dP[1] + A0[2] * dP[2];
+      const float u1 = A1[0] * dP[0] + A1[1] * dP[1] + A1[2] * dP[2];
+      const float au[3] = {u0 * A0[0] + u1 * A1[0], u0 * A0[1] + u1 * A1[1], u0 * A0[2] + u1 * A1[2]};
+      float h[3];
+      mtv3f(Ra, au, h);
+      if (comp) {
+        float Rb[12], h2[3];
+        rt(id.z, Rb);
+        mtv3f(Rb, h, h2);
+#pragma unroll
+        for (int k2 = 0; k2 < 3; ++k2) h[k2] = h2[k2];
+      }
+      a[0] += h[0];
+      a[1] += h[1];
+      a[2] += h[2];
+    }
+    const float t0 = pu[0] * a[0], t1 = pu[1] * a[0] + pu[3] * a[1];
+    const float t2 = pu[2] * a[0] + pu[4] * a[1] + pu[5] * a[2];
+    const float up[3] = {pu[0] * t0 + pu[1] * t1 + pu[2] * t2, pu[3] * t1 + pu[4] * t2, pu[5] * t2};
+    // sweep 2: per camera, sum [Z x g | g] (fp64 sums; J_l^T and -s_c after the sums)
+    nid = len > 0 ? v.obs_idx[off + lane] : make_int4(-1, 0, -1, 0);
+    for (int k = 0; k < len; ++k) {
+      const int s = off + 64 * k + lane;
+      const int4 id = nid;
+      if (k + 1 < len) nid = v.obs_idx[s + 64];
+      if (id.x < 0) continue;
+      const int c0 = col_s[id.y], c1 = id.z >= 0 ? col_s[id.z] : -1;
+      if (c0 < 0 && c1 < 0) continue;
+      float A0[3], A1[3], Ra[12], Z0[3], Z1[3], kk[3];
+      bool comp;
+      geo(id, X, A0, A1, Ra, Z0, Z1, comp, up, kk);
+      float m[3];
+      mv3f(Ra, kk, m);
+      const float z0 = A0[0] * m[0] + A0[1] * m[1] + A0[2] * m[2];
+      const float z1 = A1[0] * m[0] + A1[1] * m[1] + A1[2] * m[2];
+      const float gz[3] = {z0 * A0[0] + z1 * A1[0], z0 * A0[1] + z1 * A1[1], z0 * A0[2] + z1 * A1[2]};
+      if (c0 >= 0) {
+        float cz[3];
+        cross3f(Z0, gz, cz);
+#pragma unroll
+        for (int a2 = 0; a2 < 3; ++a2) add(6 * c0 + a2, cz[a2]);
+#pragma unroll
+        for (int a2 = 0; a2 < 3; ++a2) add(6 * c0 + 3 + a2, gz[a2]);
+      }
+      if (c1 >= 0) {
+        float hz[3], cz[3];
+        mtv3f(Ra, gz, hz);
+        cross3f(Z1, hz, cz);
+#pragma unroll
+        for (int a2 = 0; a2 < 3; ++a2) add(6 * c1 + a2, cz[a2]);
+#pragma unroll
+        for (int a2 = 0; a2 < 3; ++a2) add(6 * c1 + 3 + a2, hz[a2]);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NC6; i += blockDim.x) {
+    const int c = i / 6, k = i - 6 * c;
+    double x;
+    if (k < 3) {
+      x = 0.0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) x += jl_s[9 * c + 3 * r + k] * sum_of(6 * c + r);
+    } else {
+      x = sum_of(i);
+    }
+    out[(size_t)blockIdx.x * NC6 + i] = -scc[i] * x;
   }
 }
 
@@ -3773,6 +4037,13 @@ void launch_mf_product(hipStream_t s, const DevView& v, const double* points, co
     k_mf_frame<0><<<grid, kMfBlock, mf2_lds_bytes(v.E, v.NI, v.NC, true), s>>>(v, points, camtab, scale_c, PU, vec,
                                                                               nullptr, partial, st);
   }
+  launch_pcg_fused_final(s, grid, 6 * v.NC, partial, w, st);
+}
+void launch_mf_product32(hipStream_t s, const DevView& v, const double* points, const double* camtab,
+                         const double* scale_c, const double* PU, const double* vec, double* partial, double* w,
+                         int grid, const PcgState* st) {
+  k_mf_frame32<<<grid, kMfBlock, mf32_lds_bytes(v.E, v.NI, v.NC), s>>>(v, points, camtab, scale_c, PU, vec, partial,
+                                                                      st);
   launch_pcg_fused_final(s, grid, 6 * v.NC, partial, w, st);
 }
 void launch_mf_backsub(hipStream_t s, const DevView& v, const double* points, const double* camtab,

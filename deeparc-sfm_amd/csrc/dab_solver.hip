@@ -257,6 +257,7 @@ struct dab_handle {
   int ncu = 256;      // compute units of the device
   int fused_grid = 0;  // > 0: single-pass PCG matvec (small camera systems)
   bool mf = false;     // matrix-free implicit Schur (no Y records; DAB_PCG_MF=0 disables)
+  bool mf32 = false;   // this solve's matrix-free products in fp32 arithmetic (pcg_fp32)
   int mf_grid_n = 0;
   double* d_mf_partial = nullptr;
   int pcg_hint = 2;    // CG iterations of the previous solve (first batch size)
@@ -1238,11 +1239,16 @@ static int build_pcg_buffers(dab_handle* h) {
 }
 
 // S vec (Y part) -> d_pcg_w, all-reduced across ranks
-static int pcg_matvec(dab_handle* h, YBufs yb, const double* vec) {
+// exact: the fp64 product even in a mixed-precision solve (the true residual r = b - S x)
+static int pcg_matvec(dab_handle* h, YBufs yb, const double* vec, bool exact = false) {
   hipStream_t s = h->stream;
   if (h->mf) {
-    launch_mf_product(s, h->view, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, vec, h->d_mf_partial, h->d_pcg_w,
-                      h->mf_grid_n, h->d_pcg_state);
+    if (h->mf32 && !exact)
+      launch_mf_product32(s, h->view, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, vec, h->d_mf_partial,
+                          h->d_pcg_w, h->mf_grid_n, h->d_pcg_state);
+    else
+      launch_mf_product(s, h->view, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, vec, h->d_mf_partial,
+                        h->d_pcg_w, h->mf_grid_n, h->d_pcg_state);
     CHECK_RC(h->allreduce(h->d_pcg_w, (size_t)6 * h->NC, ncclSum));
     return 0;
   }
@@ -1305,7 +1311,7 @@ static int pcg_solve(dab_handle* h, const dab_options& opt, StepScalars sc, YBuf
       const bool reset = done % 10 == 0;  // r = b - S x every 10th iteration
       update(reset ? 1 : 0);
       if (reset) {
-        CHECK_RC(pcg_matvec(h, yb, h->d_yc));
+        CHECK_RC(pcg_matvec(h, yb, h->d_yc, true));
         update(2);
       }
     }
@@ -1567,6 +1573,8 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
   // (Jacobians, residuals, V/U/g, the CG vectors and scalars stay fp64)
   // (the matrix-free PCG of small camera sets stores no Y and is all fp64)
   const bool y32 = use_pcg && opt.pcg_fp32 != 0 && !h->mf;
+  // matrix-free mixed precision: fp32 products, fp64 sums, recurrences and true residuals
+  h->mf32 = use_pcg && opt.pcg_fp32 != 0 && h->mf;
   if (y32 && !h->d_Y32c) {
     CHECK_RC(h->dev.alloc(&h->d_Y32c, (size_t)kYRec * std::max(1, h->NE)));
     CHECK_RC(h->dev.alloc(&h->d_Y32p, (size_t)kYRec * std::max(1, h->NS) * (h->any_compose ? 2 : 1)));
@@ -1589,7 +1597,8 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
   sum->linear_solver_time_in_seconds = 0;
   sum->termination_type = DAB_FAILURE;
   sum->linear_solver_type_used = opt.linear_solver_type;
-  sum->schur_assembly = use_pcg ? (h->mf ? 1 : 0) : (h->schur_tiles ? DAB_SCHUR_TILES : DAB_SCHUR_PAIRS);
+  sum->schur_assembly = use_pcg ? (h->mf ? (h->mf32 ? DAB_PCG_MATRIX_FREE_FP32 : DAB_PCG_MATRIX_FREE) : DAB_PCG_STORED_Y)
+                                : (h->schur_tiles ? DAB_SCHUR_TILES : DAB_SCHUR_PAIRS);
   const bool verbose = opt.minimizer_progress_to_stdout && h->rank == 0;
   const bool in_global = true;  (void)in_global;
 
@@ -2077,7 +2086,7 @@ extern "C" int dab_jacobian_bytes(dab_handle* h, double* bytes) {
 extern "C" int dab_pcg_schedule(dab_handle* h, int32_t* matrix_free) {
   clear_error();
   if (!h || !h->have_problem || !matrix_free) return set_error(DAB_E_STATE, "no problem set");
-  *matrix_free = h->pcg_built && h->mf ? 1 : 0;
+  *matrix_free = h->pcg_built && h->mf ? (h->mf32 ? 2 : 1) : 0;
   return 0;
 }
 

@@ -157,11 +157,16 @@ typedef struct dab_summary {
   int32_t iterations_written;      /* entries filled */
   int32_t linear_solver_type_used; /* the DAB_LINEAR_SOLVER_* that ran (the requested one) */
   int32_t schur_assembly;          /* EXPLICIT_SCHUR: DAB_SCHUR_* (how S was assembled);
-                                      IMPLICIT_SCHUR_PCG: 1 matrix-free products, 0 stored Y */
+                                      IMPLICIT_SCHUR_PCG: DAB_PCG_* (the Schur products) */
 } dab_summary;
 /* schur_assembly values for DAB_LINEAR_SOLVER_EXPLICIT_SCHUR */
 #define DAB_SCHUR_PAIRS 0   /* per camera-pair block sums over entry-pair tables (large NC) */
 #define DAB_SCHUR_TILES 1   /* register-owned block tiles over per-step Y records (NC <= 160) */
+/* schur_assembly values for DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG */
+#define DAB_PCG_STORED_Y 0          /* products over stored Y records (fp32 records with pcg_fp32) */
+#define DAB_PCG_MATRIX_FREE 1       /* rows re-evaluated per product, all fp64 (NC <= 160) */
+#define DAB_PCG_MATRIX_FREE_FP32 2  /* as 1 with pcg_fp32: fp32 per-observation arithmetic, fp64
+                                       sums, fp64 CG recurrences and true residuals */
 
 typedef struct dab_handle dab_handle;
 
@@ -249,8 +254,9 @@ int dab_jacobian_bytes(dab_handle* h, double* bytes);
  * k_eval_points). */
 int dab_eval_schedule(dab_handle* h, int32_t* fused);
 /* After an IMPLICIT_SCHUR_PCG solve: *matrix_free = 1 when the Schur products re-evaluate
- * the observation rows in every pass (small camera sets: all fp64, no Y records, so
- * pcg_fp32 has nothing to store in fp32), 0 for the stored-Y products. */
+ * the observation rows in every pass (small camera sets, fp64, no Y records), 2 for the
+ * same with pcg_fp32 (fp32 per-observation arithmetic, fp64 sums and true residuals), 0 for
+ * the stored-Y products. */
 int dab_pcg_schedule(dab_handle* h, int32_t* matrix_free);
 
 /* ---- host utilities (no device needed) ----------------------------------------------- */

@@ -72,6 +72,30 @@ def test_full_size_trajectory_matches_oracle(pkg, gpu, name):
     np.testing.assert_allclose(prob.ext[:16], rec["ext_sample"], rtol=0, atol=1e-6)
 
 
+def test_c5_mixed_precision_pcg_matches_oracle(pkg, gpu):
+    """BASELINE config 5 as named: the 10M-observation rig with the mixed-precision PCG
+    (fp32 matrix-free products, fp64 sums / recurrences / true residuals) against the
+    oracle's fp64 CG trajectory (c5_pcg): identical CG counts, cost 1e-7 relative."""
+    import gen_trajectories as gt
+    rec = TRAJ["c5_pcg"]
+    prob = _problem(pkg, rec["config"])
+    assert gt.problem_digest(prob) == rec["digest"]
+    opts = gt.case_options(pkg, "pcg", rec["max_num_iterations"])
+    opts.pcg_fp32 = 1
+    s = pkg.Solver(0)
+    try:
+        s.set_problem(prob)
+        g = s.solve(opts)
+        assert s.pcg_matrix_free() == 2
+    finally:
+        s.close()
+    assert g["termination"] == rec["termination"] and g["num_iterations"] == rec["num_iterations"]
+    assert [it["linear_solver_iterations"] for it in g["iterations"]] == rec["linear_iterations"]
+    for a, b in zip([it["cost"] for it in g["iterations"]], rec["costs"]):
+        assert abs(a - b) <= 1e-7 * abs(b), (a, b)
+    np.testing.assert_allclose(gt.sample_rows(prob.points, 64), rec["points_sample"], rtol=0, atol=1e-5)
+
+
 def test_c4_shape_two_ranks_match_single_handle(gpu):
     """BASELINE config 4's partition at full size: C3 point-sharded over two ranks."""
     with socket.socket() as sk:

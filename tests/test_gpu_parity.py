@@ -273,6 +273,43 @@ def test_matrix_free_pcg_matches_stored_y(pkg, gpu, kind, monkeypatch):
 
 
 @pytest.mark.parametrize("kind", ["bal", "rig"])
+def test_matrix_free_mixed_precision_pcg_matches_oracle(pkg, orc, gpu, kind):
+    """BASELINE config 5's mixed-precision PCG where the products are matrix-free (small
+    camera sets, the rig): pcg_fp32 runs the Schur products with fp32 per-observation
+    arithmetic (k_mf_frame32) and keeps the sums, the CG recurrences and the true residual
+    r = b - S x of every 10th CG iteration in fp64 (the refinement step). Against the oracle's
+    fp64 CG trajectory: identical CG iteration counts and termination, per-iteration cost
+    within 1e-6 relative (the fp32 products perturb each step at ~1e-7), points within 1e-5.
+    The run reports the mixed schedule."""
+    if kind == "bal":
+        prob = pkg.synth(kind=0, num_cameras=60, num_points=4000, obs_per_point=7, seed=61)
+    else:
+        prob = pkg.synth(kind=1, num_arcs=6, num_rings=16, num_points=3000, obs_per_point=8, seed=62)
+    opts = pkg.options(max_num_iterations=12, pcg_fp32=1, num_threads=8,
+                       linear_solver_type=pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)
+    ref = prob.copy()
+    s = pkg.Solver(0)
+    try:
+        s.set_problem(prob)
+        g = s.solve(opts)
+        assert s.pcg_matrix_free() == 2 and g["schur_assembly"] == 2
+    finally:
+        s.close()
+    o = orc.solve(pkg, ref, opts)
+    assert g["termination"] == o["termination"] and len(g["iterations"]) == len(o["iterations"])
+    assert [it["linear_solver_iterations"] for it in g["iterations"]] == \
+        [it["linear_solver_iterations"] for it in o["iterations"]]
+    dev = 0.0
+    for a, b in zip(g["iterations"], o["iterations"]):
+        assert a["success"] == b["success"]
+        dev = max(dev, abs(a["cost"] - b["cost"]) / abs(b["cost"]))
+    print(f"mixed-precision PCG vs oracle fp64 CG: max relative cost deviation {dev:.2e}, "
+          f"max |dX| {np.abs(prob.points - ref.points).max():.2e}")
+    assert dev <= 1e-6
+    np.testing.assert_allclose(prob.points, ref.points, rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("kind", ["bal", "rig"])
 def test_cg_update_work_groups_match_single(pkg, gpu, kind, monkeypatch):
     """The CG update spread over work-groups (last-arriver grid sums) against the
     single-work-group kernel (DAB_CG_ONEWG=1): same CG iteration counts, costs 1e-10."""
