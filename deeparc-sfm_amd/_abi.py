@@ -116,6 +116,7 @@ SIGNATURES = {
     "dab_jacobian_bytes": (C.c_int, [C.c_void_p, _dp]),
     "dab_eval_schedule": (C.c_int, [C.c_void_p, _ip]),
     "dab_pcg_schedule": (C.c_int, [C.c_void_p, _ip]),
+    "dab_comm_schedule": (C.c_int, [C.c_void_p, _ip]),
     "dab_synth_sizes": (C.c_int, [C.POINTER(DabSynthConfig), _ip, _ip, _ip, _ip]),
     "dab_synth_fill": (C.c_int, [C.POINTER(DabSynthConfig), C.POINTER(DabProblem), _u8p]),
 }

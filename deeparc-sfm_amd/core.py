@@ -289,6 +289,12 @@ class Solver:
         check(self.lib.dab_jacobian_bytes(self.h, C.byref(b)), self.lib)
         return b.value
 
+    def comm_p2p(self):
+        """1 when the one-shot xGMI peer-to-peer all-reduce carries the sums over ranks"""
+        f = C.c_int32()
+        check(self.lib.dab_comm_schedule(self.h, C.byref(f)), self.lib)
+        return int(f.value)
+
     def pcg_matrix_free(self):
         """0: stored-Y products; 1: matrix-free fp64; 2: matrix-free mixed precision (pcg_fp32)"""
         f = C.c_int32()

@@ -31,6 +31,7 @@
 
 #include "dab_internal.h"
 #include "dab_kernels.h"
+#include "dab_p2p.h"
 
 using namespace dab;
 
@@ -119,6 +120,8 @@ struct Knobs {
   int cg_onewg = 0;         // DAB_CG_ONEWG=1: single-work-group CG update
   int bench_sample = 8;     // DAB_BENCH_SAMPLE: timing-event stride of dab_bench_eval_pass
   int schur_tiles = 1;      // DAB_SCHUR_TILES=0: explicit S from the pair tables even for small NC
+  int p2p = -1;             // DAB_P2P: one-shot xGMI all-reduce of small sums (-1 auto: RCCL handles
+                            // only; 1 also on host-staged handles, the one-GPU rehearsal; 0 off)
   int fused_stream = 1;     // DAB_FUSED_STREAM=0: the fused pass without the streamed camera-major point copy
   int fused_variant = 0;    // DAB_FUSED_V: pipeline depths of the streamed fused pass (DAB_ABLATIONS builds)
   int fused_tab = 0;        // DAB_FUSED_TAB=1 (DAB_ABLATIONS builds): the streamed fused pass reads the
@@ -139,6 +142,7 @@ struct Knobs {
     get("DAB_CG_ONEWG", cg_onewg);
     get("DAB_BENCH_SAMPLE", bench_sample);
     get("DAB_SCHUR_TILES", schur_tiles);
+    get("DAB_P2P", p2p);
     get("DAB_FUSED_STREAM", fused_stream);
     get("DAB_FUSED_V", fused_variant);
     get("DAB_FUSED_TAB", fused_tab);
@@ -283,6 +287,8 @@ struct dab_handle {
     if (ev_cam) (void)hipEventDestroy(ev_cam);
     if (ev_comm) (void)hipEventDestroy(ev_comm);
     if (comm_stream) (void)hipStreamDestroy(comm_stream);
+    p2p_destroy(p2p_main);
+    p2p_destroy(p2p_comm);
     if (comm) ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -293,6 +299,20 @@ struct dab_handle {
   double* packed() { return d_spack; }
   double* ybc() { return d_spack + (size_t)36 * nblk; }
   size_t spack_count() const { return (size_t)36 * nblk + (size_t)6 * NC; }
+
+  // one-shot xGMI all-reduce (dab_p2p.hip) of sums up to kP2pWords, one context per stream
+  // (the main stream and the communication stream of the overlapped camera all-reduce)
+  P2pComm* p2p_main = nullptr;
+  P2pComm* p2p_comm = nullptr;
+  static constexpr size_t kP2pWords = 65536;
+  // an all-reduce on comm_stream can overlap the point-side kernel (RCCL or peer-to-peer)
+  bool can_overlap() const { return world > 1 && ((comm && !host_cb) || p2p_comm); }
+  int allreduce_comm_stream(double* buf, size_t n) {
+    if (p2p_comm && n <= kP2pWords) return p2p_allreduce_sum(p2p_comm, comm_stream, buf, n);
+    if (!comm || host_cb) return set_error(DAB_E_STATE, "no collective for the communication stream");
+    NCCL_OK(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, comm, comm_stream));
+    return 0;
+  }
 
   // host-staged collective (dab_create_dist_host): rehearsal path, not the product path
   dab_host_allreduce_fn host_cb = nullptr;
@@ -325,6 +345,8 @@ struct dab_handle {
   // moves each word as three 22-bit pieces, which gloo's double sum adds exactly
   int allreduce_u64(uint64_t* buf, size_t n) {
     if (world <= 1 || n == 0) return 0;
+    if (p2p_main && n <= kP2pWords)
+      return p2p_allreduce_sum_u64(p2p_main, stream, reinterpret_cast<unsigned long long*>(buf), n);
     if (!host_cb) {
       NCCL_OK(ncclAllReduce(buf, buf, n, ncclUint64, ncclSum, comm, stream));
       return 0;
@@ -357,6 +379,7 @@ struct dab_handle {
 
   int allreduce(double* buf, size_t n, ncclRedOp_t op) {
     if (world <= 1 || n == 0) return 0;
+    if (p2p_main && op == ncclSum && n <= kP2pWords) return p2p_allreduce_sum(p2p_main, stream, buf, n);
     if (host_cb) return host_allreduce(buf, n, op == ncclMax ? 1 : 0);
     NCCL_OK(ncclAllReduce(buf, buf, n, ncclDouble, op, comm, stream));
     return 0;
@@ -436,6 +459,84 @@ extern "C" int dab_comm_unique_id(uint8_t out_id[128]) {
   return 0;
 }
 
+// The one-shot all-reduce contexts: every rank maps every peer's region (IPC handles
+// gathered through the handle's own collective). Needs every pair of devices to be
+// peer-accessible (one xGMI node); otherwise the sums stay on RCCL.
+static int setup_p2p(dab_handle* h) {
+  const bool want = h->knobs.p2p > 0 || (h->knobs.p2p < 0 && !h->host_cb);
+  if (!want || h->world < 2 || h->world > kP2pMaxRanks) return 0;
+  P2pAllgather gather;
+  if (h->host_cb) {
+    gather = [h](unsigned char* buf) -> int {
+      const size_t n = (size_t)h->world * kP2pHandleBytes;
+      if (h->stage(n) != 0) return -1;
+      for (size_t i = 0; i < n; ++i) h->h_stage[i] = buf[i];
+      if (h->host_cb(h->h_stage, (int64_t)n, 0, h->host_user) != 0) return -1;
+      for (size_t i = 0; i < n; ++i) buf[i] = (unsigned char)h->h_stage[i];
+      return 0;
+    };
+  } else {
+    int ok = 1;  // peer access between this device and every other one of the node
+    int ndev = 0;
+    (void)hipGetDeviceCount(&ndev);
+    for (int d = 0; d < ndev; ++d) {
+      int a = 1;
+      if (d != h->device && hipDeviceCanAccessPeer(&a, h->device, d) == hipSuccess && !a) ok = 0;
+    }
+    double f = ok ? 0.0 : 1.0;  // every rank must take the same branch
+    double* d_f = nullptr;
+    HIP_OK(hipMalloc(&d_f, sizeof(double)));
+    HIP_OK(hipMemcpy(d_f, &f, sizeof(double), hipMemcpyHostToDevice));
+    NCCL_OK(ncclAllReduce(d_f, d_f, 1, ncclDouble, ncclMax, h->comm, h->stream));
+    HIP_OK(hipMemcpyAsync(&f, d_f, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    (void)hipFree(d_f);
+    if (f != 0.0) return 0;
+    gather = [h](unsigned char* buf) -> int {
+      const size_t n = (size_t)h->world * kP2pHandleBytes;
+      unsigned char* d = nullptr;
+      if (hipMalloc(&d, n) != hipSuccess) return -1;
+      int rc = 0;
+      if (hipMemcpy(d, buf, n, hipMemcpyHostToDevice) != hipSuccess ||
+          ncclAllGather(d + (size_t)h->rank * kP2pHandleBytes, d, kP2pHandleBytes, ncclUint8, h->comm, h->stream) !=
+              ncclSuccess ||
+          hipMemcpyAsync(buf, d, n, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+          hipStreamSynchronize(h->stream) != hipSuccess)
+        rc = -1;
+      (void)hipFree(d);
+      return rc;
+    };
+  }
+  P2pComm* ctx[2] = {nullptr, nullptr};
+  const int rc = p2p_create_group(h->rank, h->world, dab_handle::kP2pWords, 2, gather, ctx);
+  // every rank must agree: if the contexts could not be set up anywhere, all ranks keep
+  // their sums on RCCL (or the host path) instead
+  double bad = rc != 0 ? 1.0 : 0.0;
+  if (h->host_cb) {
+    CHECK_RC(h->stage(1));
+    h->h_stage[0] = bad;
+    if (h->host_cb(h->h_stage, 1, 1, h->host_user) != 0) return set_error(DAB_E_COMM, "host all-reduce failed");
+    bad = h->h_stage[0];
+  } else {
+    double* d_f = nullptr;
+    HIP_OK(hipMalloc(&d_f, sizeof(double)));
+    HIP_OK(hipMemcpy(d_f, &bad, sizeof(double), hipMemcpyHostToDevice));
+    NCCL_OK(ncclAllReduce(d_f, d_f, 1, ncclDouble, ncclMax, h->comm, h->stream));
+    HIP_OK(hipMemcpyAsync(&bad, d_f, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    (void)hipFree(d_f);
+  }
+  if (bad != 0.0) {
+    p2p_destroy(ctx[0]);
+    p2p_destroy(ctx[1]);
+    clear_error();
+    return 0;
+  }
+  h->p2p_main = ctx[0];
+  h->p2p_comm = ctx[1];
+  return 0;
+}
+
 extern "C" int dab_create_dist(int device, int rank, int world_size, const uint8_t unique_id[128],
                                dab_handle** out) {
   clear_error();
@@ -455,6 +556,11 @@ extern "C" int dab_create_dist(int device, int rank, int world_size, const uint8
       *out = nullptr;
       return set_error(DAB_E_COMM, msg);
     }
+    if (setup_p2p(h) != 0) {
+      delete h;
+      *out = nullptr;
+      return -1;
+    }
   }
   return 0;
 }
@@ -470,6 +576,11 @@ extern "C" int dab_create_dist_host(int device, int rank, int world_size, dab_ho
   h->world = world_size;
   h->host_cb = cb;
   h->host_user = user;
+  if (world_size > 1 && setup_p2p(h) != 0) {
+    delete h;
+    *out = nullptr;
+    return -1;
+  }
   return 0;
 }
 
@@ -1412,11 +1523,10 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
     launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
                       h->cost_fx(h->fx_last ^ 1), h->ncu, 2, h->d_cmx, 0, fused_tab ? h->d_camtab : nullptr);
     bool ovl = false;
-    if (h->comm && !h->host_cb) {
+    if (h->can_overlap()) {
       HIP_OK(hipEventRecord(h->ev_cam, s));
       HIP_OK(hipStreamWaitEvent(h->comm_stream, h->ev_cam, 0));
-      NCCL_OK(ncclAllReduce(h->d_camred, h->d_camred, h->camred_count(), ncclDouble, ncclSum, h->comm,
-                            h->comm_stream));
+      CHECK_RC(h->allreduce_comm_stream(h->d_camred, h->camred_count()));
       HIP_OK(hipEventRecord(h->ev_comm, h->comm_stream));
       ovl = true;
     } else {
@@ -1456,11 +1566,10 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
         HIP_OK(hipMemsetAsync(h->Ux(), 0, sizeof(double) * 36 * (size_t)h->ncross, s));
       }
     }
-    if (h->world > 1 && h->comm && !h->host_cb) {
+    if (h->can_overlap()) {
       HIP_OK(hipEventRecord(h->ev_cam, s));
       HIP_OK(hipStreamWaitEvent(h->comm_stream, h->ev_cam, 0));
-      NCCL_OK(ncclAllReduce(h->d_camred, h->d_camred, h->camred_count(), ncclDouble, ncclSum, h->comm,
-                            h->comm_stream));
+      CHECK_RC(h->allreduce_comm_stream(h->d_camred, h->camred_count()));
       HIP_OK(hipEventRecord(h->ev_comm, h->comm_stream));
       overlapped = true;
     } else {
@@ -1830,6 +1939,8 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
   // the accepted iterate is always the lowest-cost one (steps are monotone), so the
   // device-resident x is Ceres' parameters_; write it back (sfm.cc:47-48 semantics)
   CHECK_RC(dab_get_parameters(h, h->prob.points, h->prob.ext));
+  CHECK_RC(p2p_check(h->p2p_main));  // a one-shot all-reduce that gave up waiting for a peer
+  CHECK_RC(p2p_check(h->p2p_comm));
   sum->total_time_in_seconds = now_s() - t_start;
   return 0;
 }
@@ -2080,6 +2191,13 @@ extern "C" int dab_jacobian_bytes(dab_handle* h, double* bytes) {
     for (int o = 0; o < h->N; ++o) b += 16.0 + 4.0 * (h->prob.obs_ext1[o] >= 0 ? 3 : 2);
   }
   *bytes = b;
+  return 0;
+}
+
+extern "C" int dab_comm_schedule(dab_handle* h, int32_t* p2p) {
+  clear_error();
+  if (!h || !p2p) return set_error(DAB_E_INVALID, "null argument");
+  *p2p = (h->p2p_main || h->p2p_comm) ? 1 : 0;
   return 0;
 }
 

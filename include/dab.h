@@ -258,6 +258,11 @@ int dab_eval_schedule(dab_handle* h, int32_t* fused);
  * same with pcg_fp32 (fp32 per-observation arithmetic, fp64 sums and true residuals), 0 for
  * the stored-Y products. */
 int dab_pcg_schedule(dab_handle* h, int32_t* matrix_free);
+/* How the handle's sums over ranks run: *p2p = 1 when the one-shot peer-to-peer all-reduce
+ * over xGMI (IPC-mapped peer regions, fixed rank order) carries the camera-sized sums (every
+ * pair of devices peer-accessible; environment DAB_P2P=0 disables it, DAB_P2P=1 also enables
+ * it on host-staged handles), 0 when every collective is RCCL or host-staged. */
+int dab_comm_schedule(dab_handle* h, int32_t* p2p);
 
 /* ---- host utilities (no device needed) ----------------------------------------------- */
 /* Deterministic synthetic problems. kind 0: BAL-shaped (non-shared, one

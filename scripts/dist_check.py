@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--config", default="", help="a named configuration (core.CONFIGS) instead of "
                     "the small BAL and rig problems, e.g. c3_1kcam: BASELINE config 4's partition")
     ap.add_argument("--iters", type=int, default=12)
+    ap.add_argument("--expect-p2p", action="store_true",
+                    help="fail unless the one-shot peer-to-peer all-reduce carried the sums")
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dev = a.device if a.device >= 0 else int(os.environ.get("LOCAL_RANK", "0"))
@@ -69,6 +71,7 @@ def main():
             s = pkg.Solver(dev, rank, world, uid, host_allreduce=gloo_allreduce if a.host_collective else None)
             s.set_problem(mine)
             sched = s.eval_fused()
+            p2p = s.comm_p2p()
             summ = s.solve(opts)
             s.close()
             pts = torch.from_numpy(np.where((owner == rank)[:, None], mine.points, 0.0))
@@ -90,13 +93,14 @@ def main():
                     dpts=float(np.abs(pts.numpy() - rp).max()),
                     dext=float(np.abs(ext.numpy() - re).max()),
                     ext_ranks_equal=bool(torch.equal(ext, ext_min)),
-                    eval_schedule=sched)
+                    eval_schedule=sched, p2p=p2p)
     if rank == 0:
         print(json.dumps(out, indent=1))
         bad = [k for k, v in out.items()
                if v["iters"][0] != v["iters"][1] or v["max_rel_cost"] > 1e-8 or v["dpts"] > 1e-6
                or v["dext"] > 1e-6 or not v["ext_ranks_equal"]
-               or (not k.startswith("rig") and v["eval_schedule"] != 2)]  # BAL shards: the split fused pass
+               or (not k.startswith("rig") and v["eval_schedule"] != 2)  # BAL shards: the split fused pass
+               or (a.expect_p2p and v["p2p"] != 1)]
         print("DIST_CHECK", "FAIL " + ",".join(bad) if bad else "OK")
     dist.destroy_process_group()
 

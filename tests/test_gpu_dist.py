@@ -25,6 +25,25 @@ def test_two_ranks_match_single_handle(gpu):
     assert "DIST_CHECK OK" in p.stdout, p.stdout[-3000:]
 
 
+def test_two_ranks_p2p_allreduce_match_single_handle(gpu):
+    """The one-shot peer-to-peer all-reduce (dab_p2p.hip: IPC-mapped peer regions, flags,
+    fixed rank-order sums) on the one-GPU rehearsal: two processes on one device map each
+    other's regions (DAB_P2P=1 enables it on host-staged handles), so every camera-sized sum
+    of the sharded solve (camera blocks on the communication stream beside the point side,
+    PCG products, Schur-Jacobi blocks, fixed-point cost words) goes through the kernel,
+    the rest through gloo. Same trajectories as the single handle."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, DAB_P2P="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "scripts", "dist_check.py"), "--device", "0", "--host-collective", "--expect-p2p"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "DIST_CHECK OK" in p.stdout, p.stdout[-3000:]
+
+
 def test_rccl_one_rank_per_gpu(gpu):
     """The product multi-GPU path: one process per GPU, dab_create_dist (RCCL over xGMI),
     every collective on RCCL. Runs whenever the box shows two or more devices (the driver's
