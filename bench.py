@@ -103,6 +103,7 @@ def main():
     t_sp = time.perf_counter()
     solver.set_problem(prob)
     set_problem_s = time.perf_counter() - t_sp
+    comm_p2p = world > 1 and solver.comm_p2p() == 1
     n_obs = prob.num_obs
 
     def barrier():
@@ -379,7 +380,9 @@ def main():
             "config": {"workload": args.config + " per GPU: 1000 cameras, 100000 points, "
                        "1000000 observations, BAL-shaped, eval pass = residual+Jacobian reduced "
                        "into the JtJ/Jtr blocks", "global_obs": world * n_obs,
-                       "parallelism": f"point-sharded x{world}, RCCL all-reduce of camera blocks"},
+                       "parallelism": (f"point-sharded x{world}, " + (
+                           "one-shot xGMI peer-to-peer all-reduce of the camera blocks (RCCL for large sums)"
+                           if comm_p2p else "RCCL all-reduce of camera blocks"))},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": eval_kernel, "kernel_ms": jac_ms,
