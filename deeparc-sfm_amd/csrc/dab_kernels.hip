@@ -2986,6 +2986,7 @@ __device__ __forceinline__ int tri_row(int bl) {  // c with c (c+1)/2 <= bl < (c
 
 // Each thread owns two blocks of the tile (bl and bl + kTileThreads): 72 sums in registers,
 // and the two blocks' hit counts add up, which evens out the lanes' work per batch.
+template <int ABL>
 __global__ __launch_bounds__(kTileThreads) void k_schur_tiles(const double* __restrict__ yrec, SchurTiles a, int NC) {
   extern __shared__ __align__(16) unsigned char tile_lds[];
   double* ly = reinterpret_cast<double*>(tile_lds);
@@ -3031,14 +3032,14 @@ __global__ __launch_bounds__(kTileThreads) void k_schur_tiles(const double* __re
         __hip_atomic_fetch_or(&mask[ri.w], 1ull << (ri.z - p0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
-    for (int i = threadIdx.x; i < 9 * nr; i += blockDim.x) {
+    for (int i = threadIdx.x; i < (ABL == 2 ? 0 : 9 * nr); i += blockDim.x) {
       const int rr = i / 9, k = i - 9 * rr;
       if (a.rec_cam[r0 + rr] <= clast)
         reinterpret_cast<double2*>(ly + 18 * rr)[k] = reinterpret_cast<const double2*>(yrec + 18 * (size_t)(r0 + rr))[k];
     }
     __syncthreads();
-    if (ownA) tile_block_hits(ly, recof, mask, NC, cA, dA, accA);
-    if (ownB) tile_block_hits(ly, recof, mask, NC, cB, dB, accB);
+    if (ABL != 1 && ownA) tile_block_hits(ly, recof, mask, NC, cA, dA, accA);
+    if (ABL != 1 && ownB) tile_block_hits(ly, recof, mask, NC, cB, dB, accB);
     __syncthreads();
     for (int i = threadIdx.x; i < NC; i += blockDim.x) mask[i] = 0ull;
   }
@@ -3114,11 +3115,15 @@ void launch_schur_y(hipStream_t s, const DevView& v, const double* points, const
 void launch_schur_tiles(hipStream_t s, const double* yrec, const SchurTiles& a, int NC) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_schur_tiles), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kTileLdsMax);
+    for (const void* f : {reinterpret_cast<const void*>(k_schur_tiles<0>), reinterpret_cast<const void*>(k_schur_tiles<1>),
+                          reinterpret_cast<const void*>(k_schur_tiles<2>)})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTileLdsMax);
     attr = true;
   }
-  k_schur_tiles<<<a.ntile * a.ngroup, kTileThreads, schur_tile_lds_bytes(NC, a.batch_cap), s>>>(yrec, a, NC);
+  static const int abl = getenv("DAB_TILES_ABL") ? atoi(getenv("DAB_TILES_ABL")) : 0;
+  if (abl == 1) k_schur_tiles<1><<<a.ntile * a.ngroup, kTileThreads, schur_tile_lds_bytes(NC, a.batch_cap), s>>>(yrec, a, NC);
+  else if (abl == 2) k_schur_tiles<2><<<a.ntile * a.ngroup, kTileThreads, schur_tile_lds_bytes(NC, a.batch_cap), s>>>(yrec, a, NC);
+  else k_schur_tiles<0><<<a.ntile * a.ngroup, kTileThreads, schur_tile_lds_bytes(NC, a.batch_cap), s>>>(yrec, a, NC);
 }
 void launch_schur_scale(hipStream_t s, int NC, const double* ug, const double* scale_c, int* kx) {
   if (NC > 0) k_schur_scale<<<grid_for(6 * NC, 256, 1 << 20), 256, 0, s>>>(NC, ug, scale_c, kx);
