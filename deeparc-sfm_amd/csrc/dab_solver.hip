@@ -1292,36 +1292,49 @@ static int build_schur_tiles(dab_handle* h) {
   const std::vector<int>& pt_ent_ptr = h->h_pt_ent_ptr;
   const big_vec<int>& ent_cam = h->h_ent_cam;
   const big_vec<int>& ent_os = h->h_ent_os;
-  std::vector<int2> sch(h->NE);
-  std::vector<int4> rec;
-  rec.reserve(h->NE);
+  big_vec<int2> sch(h->NE);
+  std::vector<int> rec_ptr(NP + 1, 0);
+  // per point (threads): entries sorted by (camera, slot), distinct cameras counted
+  par_for(NP, [&](long long pb, long long pe, int) {
+    for (int p = (int)pb; p < (int)pe; ++p) {
+      const int b = pt_ent_ptr[p], e = pt_ent_ptr[p + 1];
+      for (int i = b; i < e; ++i) sch[i] = make_int2(ent_os[i], ent_cam[i]);
+      std::sort(sch.begin() + b, sch.begin() + e, [](const int2& x, const int2& y) {
+        return x.y != y.y ? x.y < y.y : x.x < y.x;
+      });
+      int m = 0;
+      for (int i = b; i < e; ++i) m += (i == b || sch[i].y != sch[i - 1].y);
+      rec_ptr[p + 1] = m;
+    }
+  });
+  for (int p = 0; p < NP; ++p) rec_ptr[p + 1] += rec_ptr[p];
+  big_vec<int4> rec(rec_ptr[NP]);
+  par_for(NP, [&](long long pb, long long pe, int) {
+    for (int p = (int)pb; p < (int)pe; ++p) {
+      int r = rec_ptr[p] - 1;
+      for (int i = pt_ent_ptr[p]; i < pt_ent_ptr[p + 1]; ++i) {
+        if (i > pt_ent_ptr[p] && sch[i].y == sch[i - 1].y) {
+          rec[r].y++;
+          continue;
+        }
+        rec[++r] = make_int4(i, 1, p, sch[i].y);
+      }
+    }
+  });
   std::vector<int> batch_rec{0}, batch_pt{0};
   const int kBatchRec = schur_tile_batch_cap(NC);
   int cur = 0, curp = 0;
   for (int p = 0; p < NP; ++p) {
-    const int b = pt_ent_ptr[p], e = pt_ent_ptr[p + 1];
-    for (int i = b; i < e; ++i) sch[i] = make_int2(ent_os[i], ent_cam[i]);
-    std::sort(sch.begin() + b, sch.begin() + e, [](const int2& x, const int2& y) {
-      return x.y != y.y ? x.y < y.y : x.x < y.x;
-    });
-    const int r0 = (int)rec.size();
-    for (int i = b; i < e; ++i) {
-      if (i > b && sch[i].y == sch[i - 1].y) {
-        rec.back().y++;
-        continue;
-      }
-      rec.push_back(make_int4(i, 1, p, sch[i].y));
-    }
-    const int m = (int)rec.size() - r0;
+    const int m = rec_ptr[p + 1] - rec_ptr[p];
     if (curp > 0 && (cur + m > kBatchRec || curp + 1 > kBatchPts)) {
-      batch_rec.push_back(r0);
+      batch_rec.push_back(rec_ptr[p]);
       batch_pt.push_back(p);
       cur = curp = 0;
     }
     cur += m;
     curp += 1;
   }
-  batch_rec.push_back((int)rec.size());
+  batch_rec.push_back(rec_ptr[NP]);
   // tiles: equal block ranges of <= kTileBlocks
   const int nb = (int)tri_n(NC);
   const int ntile = std::max(1, (nb + kTileBlocks - 1) / kTileBlocks);
@@ -1339,8 +1352,10 @@ static int build_schur_tiles(dab_handle* h) {
   a.stride = (size_t)a.nelem;
   a.kq = 0;
   a.batch_cap = kBatchRec;
-  std::vector<int> rcam(rec.size());
-  for (size_t i = 0; i < rec.size(); ++i) rcam[i] = rec[i].w;
+  big_vec<int> rcam(rec.size());
+  par_for((long long)rec.size(), [&](long long b, long long e, int) {
+    for (long long i = b; i < e; ++i) rcam[i] = rec[i].w;
+  });
   Dev& d = h->dev;
   int *d_tb = nullptr, *d_br = nullptr, *d_bp = nullptr, *d_rcam = nullptr;
   CHECK_RC(upload(&d_rcam, d, rcam, s));
@@ -1376,17 +1391,20 @@ static int build_schur_tables(dab_handle* h) {
   const big_vec<int>& ent_pos = h->h_ent_pos;
   {
     // tile mode: every rank must take the same branch (the all-reduced S layouts differ)
-    int maxm = 0;  // distinct free cameras of one point
-    std::vector<int> seen(std::max(1, NC), -1);
-    for (int pt = 0; pt < NP; ++pt) {
-      int m = 0;
-      for (int e = pt_ent_ptr[pt]; e < pt_ent_ptr[pt + 1]; ++e)
-        if (seen[ent_cam[e]] != pt) {
-          seen[ent_cam[e]] = pt;
-          ++m;
-        }
-      maxm = std::max(maxm, m);
-    }
+    std::vector<int> tmax(setup_threads(), 0);  // distinct free cameras of one point
+    par_for(NP, [&](long long pb, long long pe, int t) {
+      std::vector<int> seen(std::max(1, NC), -1);
+      for (int pt = (int)pb; pt < (int)pe; ++pt) {
+        int m = 0;
+        for (int e = pt_ent_ptr[pt]; e < pt_ent_ptr[pt + 1]; ++e)
+          if (seen[ent_cam[e]] != pt) {
+            seen[ent_cam[e]] = pt;
+            ++m;
+          }
+        tmax[t] = std::max(tmax[t], m);
+      }
+    });
+    const int maxm = *std::max_element(tmax.begin(), tmax.end());
     double no_tiles = (h->knobs.schur_tiles != 0 && NC > 0 && mf_schur_fits(NC, h->E, h->NI) && maxm <= kTileMaxRec)
                           ? 0.0 : 1.0;
     CHECK_RC(max_all_ranks(h, no_tiles));
