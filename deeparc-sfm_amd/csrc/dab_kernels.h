@@ -181,19 +181,27 @@ struct SchurTiles {
   int ntile, ngroup, nbatch, nelem;  // nelem = 36 NC (NC + 1) / 2
   int nrec;                          // records: distinct (point, free camera) pairs
   int kq;                            // rhs exponent: 2^kq >= sqrt(2 cost)
-  const int* tile_b0;                // [ntile + 1] block bounds of the tiles (<= 1024 blocks each)
-  const int* batch_rec;              // [nbatch + 1] first record of each batch (<= batch_cap, whole points)
-  const int* batch_pt;               // [nbatch] first point of each batch (<= 64 points)
-  int batch_cap;                     // records per batch (LDS capacity)
+  // records are ordered by (batch, camera, point): inside a batch the records of cameras
+  // 0..c form a prefix, and the record of (point pl, camera c) is
+  // off[c] + popcount(mask[c] & ((1 << pl) - 1)) from the batch start
+  const int* batch_rec;              // [nbatch + 1] first record of each batch (<= batch_cap records)
+  const unsigned char* hdr;          // [nbatch][hdr_bytes]: mask[NC] (u64, bit = point of the batch) |
+                                     // off[NC + 1] (int, records before camera c in the batch)
+  int hdr_bytes;                     // 16-B multiple
+  int batch_cap;                     // records per batch (one LDS buffer)
+  const int* tile_clast;             // [ntile] last row camera of the tile (its records: a batch prefix)
+  const int* tile_slot;              // [ntile][2 kTileThreads] block owned by (thread, half) or -1,
+                                     // balanced by the blocks' sampled hit counts
   const int4* rec_info;              // [nrec] (first entry in sch_ent, entry count, point, camera)
-  const int* rec_cam;                // [nrec] camera of each record
   const int2* sch_ent;               // [NE] (ent_os, camera), sorted by camera inside each point
   const int* kx;                     // [6 NC] rhs row exponents (launch_schur_scale)
   double* partial;                   // [ngroup][stride] per-group block sums
   size_t stride;                     // nelem
 };
+constexpr int kTileThreads = 512;     // threads of a k_schur_tiles work-group (two blocks each)
 constexpr size_t kTileLdsMax = 163840;            // LDS of one k_schur_tiles work-group (at most)
-int schur_tile_batch_cap(int NC);                 // records per batch that fit the LDS
+int schur_tile_batch_cap(int NC);                 // records per batch (one of two LDS buffers)
+int schur_tile_hdr_bytes(int NC);                 // batch header bytes (16-B multiple)
 void launch_schur_scale(hipStream_t s, int NC, const double* ug, const double* scale_c, int* kx);
 // Y of every record -> yrec[nrec][18]; rhs fixed-point sums added into rhs_out[6 NC]
 void launch_schur_y(hipStream_t s, const DevView& v, const double* points, const double* camtab, const double* PU,

@@ -2880,23 +2880,26 @@ void launch_s_unpack(hipStream_t s, int NC, int nblk, const int2* blk_cam, const
 // DENSE_SCHUR's S = U~ + D^2 - sum_p Y_p Y_p^T without pair tables. A record is one distinct
 // (point, free camera) pair, Y_{p,c} = sum over the point's entries on camera c of
 // s_c o (J_c^T J_p) PU_p (6x3). k_schur_y re-evaluates every record once per LM step into
-// HBM (records of a point contiguous, cameras ascending) and adds the rhs sum_p Y_{p,c} q_p
-// in fixed point. k_schur_tiles: the lower block triangle of S (blocks (c, d <= c), numbered
-// row-major) is cut into tiles of <= 1024 blocks; in a work-group every thread OWNS one block
-// and keeps its 36 sums in registers. The work-group streams the records of a group of points
-// in batches through LDS (with a per-camera bit mask of the batch's points and a (point,
-// camera) -> record table), and each thread walks the points that see both of its cameras in
-// batch order. No atomics: each block's sum has one fixed order (groups' partials then added
-// in group order), so the result is bitwise reproducible.
-constexpr int kTileThreads = 512;             // threads per work-group (two blocks each)
-// LDS of a work-group: y[batch records][18] | mask[NC] (points of the batch seeing camera c) |
-// recof[64][NC] ((point, camera) -> record of the batch); the batch capacity fills the rest
-size_t schur_tile_lds_bytes(int NC, int batch_rec) {
-  return sizeof(double) * 18 * (size_t)batch_rec + sizeof(unsigned long long) * NC + sizeof(unsigned short) * 64 * NC;
-}
+// HBM and adds the rhs sum_p Y_{p,c} q_p in fixed point. k_schur_tiles: the lower block
+// triangle of S (blocks (c, d <= c)) is cut into tiles of row ranges (<= 1024 blocks); in a
+// work-group every thread OWNS two blocks of the tile and keeps their 72 sums in registers
+// (the pair of a heavy and a light block by sampled hit counts, so the lanes of a wave have
+// similar work). The records are ordered (batch, camera, point), so a tile whose last row
+// camera is c needs only a prefix of each batch; batches stream through two LDS buffers by
+// LDS-DMA (global_load_lds, no registers): batch b + 1 is in flight while batch b is
+// summed. Per batch, a per-camera mask of the batch's points and per-camera record offsets
+// (the batch header, DMA'd with it) give the records of a (point, camera) pair by a popcount.
+// Each thread walks the points that see both of its cameras in batch order. No atomics:
+// each block's sum has one fixed order (groups' partials then added in group order), so the
+// result is bitwise reproducible.
+constexpr size_t kTileBufBytes = kTileLdsMax / 2;  // one LDS buffer: header area + records
+__host__ __device__ inline int tile_hdr_bytes(int NC) { return (int)(((size_t)8 * NC + (size_t)4 * (NC + 1) + 15) / 16 * 16); }
+int schur_tile_hdr_bytes(int NC) { return tile_hdr_bytes(NC); }
+__host__ __device__ inline size_t tile_hdr_area(int NC) { return ((size_t)tile_hdr_bytes(NC) + 1023) / 1024 * 1024; }
 int schur_tile_batch_cap(int NC) {
-  const size_t fixed = schur_tile_lds_bytes(NC, 0);
-  return (int)((kTileLdsMax - fixed) / (18 * sizeof(double)));
+  // records land in whole 1-KB DMA chunks (a chunk's tail lanes repeat its last piece)
+  const size_t area = (kTileBufBytes - tile_hdr_area(NC)) / 1024 * 1024;
+  return (int)(area / (18 * sizeof(double)));
 }
 
 // k_schur_y: thread per record; tables staged in LDS; rhs partials of the work-group in LDS
@@ -2952,29 +2955,32 @@ __global__ __launch_bounds__(256) void k_schur_y(DevView v, const double* __rest
 }
 
 // one owned block's sums over the batch's points that see both of its cameras (batch order)
-__device__ __forceinline__ void tile_block_hits(const double* __restrict__ ly, const unsigned short* __restrict__ recof,
-                                                const unsigned long long* __restrict__ mask, int NC, int c, int d,
-                                                double (&acc)[36]) {
-  unsigned long long m = mask[c] & mask[d];
+__device__ __forceinline__ void tile_block_hits(const double* __restrict__ ly, const unsigned long long* __restrict__ mask,
+                                                const int* __restrict__ off, int c, int d, double (&acc)[36]) {
+  const unsigned long long mc = mask[c], md = mask[d];
+  const int oc = off[c], od = off[d];
+  unsigned long long m = mc & md;
   while (m) {
     const int pl = __builtin_ctzll(m);
     m &= m - 1;
-    const double* pi = ly + 18 * recof[pl * NC + c];
-    const double2* pj = reinterpret_cast<const double2*>(ly + 18 * recof[pl * NC + d]);
-    double yj[18];
+    const unsigned long long below = (1ull << pl) - 1ull;
+    const double2* pi = reinterpret_cast<const double2*>(ly + 18 * (oc + __builtin_popcountll(mc & below)));
+    const double2* pj = reinterpret_cast<const double2*>(ly + 18 * (od + __builtin_popcountll(md & below)));
+    double yi[18], yj[18];
 #pragma unroll
     for (int u = 0; u < 9; ++u) {
-      const double2 z = pj[u];
-      yj[2 * u] = z.x;
-      yj[2 * u + 1] = z.y;
+      const double2 zi = pi[u], zj = pj[u];
+      yi[2 * u] = zi.x;
+      yi[2 * u + 1] = zi.y;
+      yj[2 * u] = zj.x;
+      yj[2 * u + 1] = zj.y;
     }
 #pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      const double y0 = pi[3 * r], y1 = pi[3 * r + 1], y2 = pi[3 * r + 2];
+    for (int r = 0; r < 6; ++r)
 #pragma unroll
       for (int s2 = 0; s2 < 6; ++s2)
-        acc[6 * r + s2] = fma(y2, yj[3 * s2 + 2], fma(y1, yj[3 * s2 + 1], fma(y0, yj[3 * s2], acc[6 * r + s2])));
-    }
+        acc[6 * r + s2] =
+            fma(yi[3 * r + 2], yj[3 * s2 + 2], fma(yi[3 * r + 1], yj[3 * s2 + 1], fma(yi[3 * r], yj[3 * s2], acc[6 * r + s2])));
   }
 }
 __device__ __forceinline__ int tri_row(int bl) {  // c with c (c+1)/2 <= bl < (c+1)(c+2)/2
@@ -2984,14 +2990,28 @@ __device__ __forceinline__ int tri_row(int bl) {  // c with c (c+1)/2 <= bl < (c
   return c;
 }
 
-// Each thread owns two blocks of the tile (bl and bl + kTileThreads): 72 sums in registers,
-// and the two blocks' hit counts add up, which evens out the lanes' work per batch.
-template <int ABL>
+// LDS-DMA of batch b into buffer dst: the header, then the records of cameras 0..clast
+// (a prefix of the batch). 16-B pieces, 64 lane-linear pieces (1 KB) per wave instruction,
+// chunks dealt to the waves round robin; a partial chunk's tail lanes repeat its last piece.
+__device__ __forceinline__ void tile_dma_batch(const SchurTiles& a, const double* __restrict__ yrec, int NC, int clast,
+                                               int b, unsigned char* dst) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int kWaves = kTileThreads / 64;
+  const unsigned char* h = a.hdr + (size_t)b * a.hdr_bytes;
+  // the prefix length first: an ordinary load's use waits for every load in flight
+  const int nrec = reinterpret_cast<const int*>(h + 8 * (size_t)NC)[clast + 1];
+  const int hp = a.hdr_bytes / 16;  // header pieces
+  for (int j = wave; j * 64 < hp; j += kWaves)
+    __builtin_amdgcn_global_load_lds(h + 16 * (size_t)min(j * 64 + lane, hp - 1), dst + 1024 * (size_t)j, 16, 0, 0);
+  const int np = 9 * nrec;  // record pieces
+  const unsigned char* src = reinterpret_cast<const unsigned char*>(yrec + 18 * (size_t)a.batch_rec[b]);
+  unsigned char* rdst = dst + tile_hdr_area(NC);
+  for (int j = wave; j * 64 < np; j += kWaves)
+    __builtin_amdgcn_global_load_lds(src + 16 * (size_t)min(j * 64 + lane, np - 1), rdst + 1024 * (size_t)j, 16, 0, 0);
+}
+
 __global__ __launch_bounds__(kTileThreads) void k_schur_tiles(const double* __restrict__ yrec, SchurTiles a, int NC) {
   extern __shared__ __align__(16) unsigned char tile_lds[];
-  double* ly = reinterpret_cast<double*>(tile_lds);
-  unsigned long long* mask = reinterpret_cast<unsigned long long*>(ly + 18 * (size_t)a.batch_cap);
-  unsigned short* recof = reinterpret_cast<unsigned short*>(mask + NC);
   // XCD-aware placement: the tiles of one group of points run on one XCD (blocks b and b + 8
   // share one), so the group's records come from HBM once and from that L2 for the others
   int t, g;
@@ -3003,53 +3023,43 @@ __global__ __launch_bounds__(kTileThreads) void k_schur_tiles(const double* __re
     t = blockIdx.x % a.ntile;
     g = blockIdx.x / a.ntile;
   }
-  const int bt0 = a.tile_b0[t], bt1 = a.tile_b0[t + 1];
-  const int blA = bt0 + (int)threadIdx.x, blB = blA + kTileThreads;
-  const bool ownA = blA < bt1, ownB = blB < bt1;
+  const int clast = a.tile_clast[t];
+  const int blA = a.tile_slot[(size_t)t * 2 * kTileThreads + threadIdx.x];
+  const int blB = a.tile_slot[(size_t)t * 2 * kTileThreads + kTileThreads + threadIdx.x];
   int cA = 0, dA = 0, cB = 0, dB = 0;
-  if (ownA) {
+  if (blA >= 0) {
     cA = tri_row(blA);
     dA = blA - (int)tri_n(cA);
   }
-  if (ownB) {
+  if (blB >= 0) {
     cB = tri_row(blB);
     dB = blB - (int)tri_n(cB);
   }
-  const int clast = tri_row(bt1 - 1);  // the tile's last row camera
   double accA[36], accB[36];
 #pragma unroll
   for (int k = 0; k < 36; ++k) accA[k] = accB[k] = 0.0;
-  for (int i = threadIdx.x; i < NC; i += blockDim.x) mask[i] = 0ull;
   const int b0 = (int)((long long)a.nbatch * g / a.ngroup), b1 = (int)((long long)a.nbatch * (g + 1) / a.ngroup);
+  if (b0 < b1) tile_dma_batch(a, yrec, NC, clast, b0, tile_lds);
+  __syncthreads();  // drains the DMA (vmcnt) and publishes buffer 0
   for (int b = b0; b < b1; ++b) {
-    const int r0 = a.batch_rec[b], nr = a.batch_rec[b + 1] - r0, p0 = a.batch_pt[b];
-    __syncthreads();  // masks zeroed, previous batch consumed
-    // the batch's records on cameras up to the tile's last row camera into LDS
-    for (int i = threadIdx.x; i < nr; i += blockDim.x) {
-      const int4 ri = a.rec_info[r0 + i];
-      if (ri.w <= clast) {
-        recof[(ri.z - p0) * NC + ri.w] = (unsigned short)i;
-        __hip_atomic_fetch_or(&mask[ri.w], 1ull << (ri.z - p0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-    for (int i = threadIdx.x; i < (ABL == 2 ? 0 : 9 * nr); i += blockDim.x) {
-      const int rr = i / 9, k = i - 9 * rr;
-      if (a.rec_cam[r0 + rr] <= clast)
-        reinterpret_cast<double2*>(ly + 18 * rr)[k] = reinterpret_cast<const double2*>(yrec + 18 * (size_t)(r0 + rr))[k];
-    }
-    __syncthreads();
-    if (ABL != 1 && ownA) tile_block_hits(ly, recof, mask, NC, cA, dA, accA);
-    if (ABL != 1 && ownB) tile_block_hits(ly, recof, mask, NC, cB, dB, accB);
-    __syncthreads();
-    for (int i = threadIdx.x; i < NC; i += blockDim.x) mask[i] = 0ull;
+    unsigned char* cur = tile_lds + kTileBufBytes * ((b - b0) & 1);
+    // the next batch streams into the other buffer while this one is summed (the sums
+    // below touch only LDS and registers, so nothing waits for the DMA before the barrier)
+    if (b + 1 < b1) tile_dma_batch(a, yrec, NC, clast, b + 1, tile_lds + kTileBufBytes * ((b + 1 - b0) & 1));
+    const unsigned long long* mask = reinterpret_cast<const unsigned long long*>(cur);
+    const int* off = reinterpret_cast<const int*>(cur + 8 * (size_t)NC);
+    const double* ly = reinterpret_cast<const double*>(cur + tile_hdr_area(NC));
+    if (blA >= 0) tile_block_hits(ly, mask, off, cA, dA, accA);
+    if (blB >= 0) tile_block_hits(ly, mask, off, cB, dB, accB);
+    __syncthreads();  // batch b consumed, batch b + 1 landed
   }
   double* out = a.partial + (size_t)g * a.stride;
-  if (ownA) {
+  if (blA >= 0) {
     double2* o = reinterpret_cast<double2*>(out + 36 * (size_t)blA);
 #pragma unroll
     for (int k = 0; k < 18; ++k) o[k] = make_double2(accA[2 * k], accA[2 * k + 1]);
   }
-  if (ownB) {
+  if (blB >= 0) {
     double2* o = reinterpret_cast<double2*>(out + 36 * (size_t)blB);
 #pragma unroll
     for (int k = 0; k < 18; ++k) o[k] = make_double2(accB[2 * k], accB[2 * k + 1]);
@@ -3115,15 +3125,11 @@ void launch_schur_y(hipStream_t s, const DevView& v, const double* points, const
 void launch_schur_tiles(hipStream_t s, const double* yrec, const SchurTiles& a, int NC) {
   static bool attr = false;
   if (!attr) {
-    for (const void* f : {reinterpret_cast<const void*>(k_schur_tiles<0>), reinterpret_cast<const void*>(k_schur_tiles<1>),
-                          reinterpret_cast<const void*>(k_schur_tiles<2>)})
-      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTileLdsMax);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_schur_tiles), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kTileLdsMax);
     attr = true;
   }
-  static const int abl = getenv("DAB_TILES_ABL") ? atoi(getenv("DAB_TILES_ABL")) : 0;
-  if (abl == 1) k_schur_tiles<1><<<a.ntile * a.ngroup, kTileThreads, schur_tile_lds_bytes(NC, a.batch_cap), s>>>(yrec, a, NC);
-  else if (abl == 2) k_schur_tiles<2><<<a.ntile * a.ngroup, kTileThreads, schur_tile_lds_bytes(NC, a.batch_cap), s>>>(yrec, a, NC);
-  else k_schur_tiles<0><<<a.ntile * a.ngroup, kTileThreads, schur_tile_lds_bytes(NC, a.batch_cap), s>>>(yrec, a, NC);
+  k_schur_tiles<<<a.ntile * a.ngroup, kTileThreads, kTileLdsMax, s>>>(yrec, a, NC);
 }
 void launch_schur_scale(hipStream_t s, int NC, const double* ug, const double* scale_c, int* kx) {
   if (NC > 0) k_schur_scale<<<grid_for(6 * NC, 256, 1 << 20), 256, 0, s>>>(NC, ug, scale_c, kx);

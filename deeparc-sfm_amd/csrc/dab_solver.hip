@@ -1308,68 +1308,123 @@ static int build_schur_tiles(dab_handle* h) {
     }
   });
   for (int p = 0; p < NP; ++p) rec_ptr[p + 1] += rec_ptr[p];
-  big_vec<int4> rec(rec_ptr[NP]);
-  par_for(NP, [&](long long pb, long long pe, int) {
-    for (int p = (int)pb; p < (int)pe; ++p) {
-      int r = rec_ptr[p] - 1;
-      for (int i = pt_ent_ptr[p]; i < pt_ent_ptr[p + 1]; ++i) {
-        if (i > pt_ent_ptr[p] && sch[i].y == sch[i - 1].y) {
-          rec[r].y++;
-          continue;
+  const int nrec = rec_ptr[NP];
+  // batches of whole points: <= kBatchPts points (one mask word) and <= cap records
+  std::vector<int> batch_rec{0}, batch_pt{0};
+  const int cap = schur_tile_batch_cap(NC);
+  {
+    int cur = 0, curp = 0;
+    for (int p = 0; p < NP; ++p) {
+      const int m = rec_ptr[p + 1] - rec_ptr[p];
+      if (curp > 0 && (cur + m > cap || curp + 1 > kBatchPts)) {
+        batch_rec.push_back(rec_ptr[p]);
+        batch_pt.push_back(p);
+        cur = curp = 0;
+      }
+      cur += m;
+      curp += 1;
+    }
+    batch_rec.push_back(nrec);
+    batch_pt.push_back(NP);
+  }
+  const int nbatch = (int)batch_rec.size() - 1;
+  // records ordered (batch, camera, point) and the batch headers: mask[NC] | off[NC + 1]
+  const int hdr_bytes = schur_tile_hdr_bytes(NC);
+  big_vec<int4> rec(nrec);
+  std::vector<unsigned char> hdr((size_t)nbatch * hdr_bytes, 0);
+  par_for(nbatch, [&](long long bb, long long be, int) {
+    std::vector<int> pos(NC + 1);
+    for (int b = (int)bb; b < (int)be; ++b) {
+      unsigned long long* mask = reinterpret_cast<unsigned long long*>(&hdr[(size_t)b * hdr_bytes]);
+      int* off = reinterpret_cast<int*>(&hdr[(size_t)b * hdr_bytes + 8 * (size_t)NC]);
+      for (int p = batch_pt[b]; p < batch_pt[b + 1]; ++p)
+        for (int i = pt_ent_ptr[p]; i < pt_ent_ptr[p + 1]; ++i)
+          if (i == pt_ent_ptr[p] || sch[i].y != sch[i - 1].y) {
+            off[sch[i].y + 1]++;
+            mask[sch[i].y] |= 1ull << (p - batch_pt[b]);
+          }
+      for (int c = 0; c < NC; ++c) off[c + 1] += off[c];
+      for (int c = 0; c <= NC; ++c) pos[c] = off[c];
+      for (int p = batch_pt[b]; p < batch_pt[b + 1]; ++p) {
+        int r = -1;
+        for (int i = pt_ent_ptr[p]; i < pt_ent_ptr[p + 1]; ++i) {
+          if (i > pt_ent_ptr[p] && sch[i].y == sch[i - 1].y) {
+            rec[r].y++;
+            continue;
+          }
+          r = batch_rec[b] + pos[sch[i].y]++;
+          rec[r] = make_int4(i, 1, p, sch[i].y);
         }
-        rec[++r] = make_int4(i, 1, p, sch[i].y);
       }
     }
-  });
-  std::vector<int> batch_rec{0}, batch_pt{0};
-  const int kBatchRec = schur_tile_batch_cap(NC);
-  int cur = 0, curp = 0;
-  for (int p = 0; p < NP; ++p) {
-    const int m = rec_ptr[p + 1] - rec_ptr[p];
-    if (curp > 0 && (cur + m > kBatchRec || curp + 1 > kBatchPts)) {
-      batch_rec.push_back(rec_ptr[p]);
-      batch_pt.push_back(p);
-      cur = curp = 0;
-    }
-    cur += m;
-    curp += 1;
-  }
-  batch_rec.push_back(rec_ptr[NP]);
-  // tiles: equal block ranges of <= kTileBlocks
+  }, 1024);
+  // tiles: equal block ranges of <= kTileBlocks (rows up to the tile's last camera)
   const int nb = (int)tri_n(NC);
   const int ntile = std::max(1, (nb + kTileBlocks - 1) / kTileBlocks);
-  std::vector<int> tb(ntile + 1);
+  std::vector<int> tb(ntile + 1), clast(ntile);
   for (int t = 0; t <= ntile; ++t) tb[t] = (int)((long long)nb * t / ntile);
+  // hit counts of every block from a sample of the points (every 4th): the points that see
+  // both of its cameras
+  std::vector<long long> hits(std::max(1, nb), 0);
+  {
+    std::vector<std::vector<long long>> th(setup_threads(), std::vector<long long>(std::max(1, nb), 0));
+    par_for(NP, [&](long long pb, long long pe, int t) {
+      std::vector<int> cams;
+      for (int p = (int)pb; p < (int)pe; ++p) {
+        if (p % 4) continue;
+        cams.clear();
+        for (int i = pt_ent_ptr[p]; i < pt_ent_ptr[p + 1]; ++i)
+          if (i == pt_ent_ptr[p] || sch[i].y != sch[i - 1].y) cams.push_back(sch[i].y);
+        for (size_t x = 0; x < cams.size(); ++x)  // ascending: block (cams[x], cams[y <= x])
+          for (size_t y = 0; y <= x; ++y) th[t][tri_n(cams[x]) + cams[y]]++;
+      }
+    });
+    for (auto& v : th)
+      for (int k = 0; k < nb; ++k) hits[k] += v[k];
+  }
+  // slots: per tile, blocks by hit count (descending); thread i owns the i-th heaviest and
+  // the (1023 - i)-th, so the pairs' sums are even and a wave's threads have similar work
+  std::vector<int> slot((size_t)ntile * 2 * kTileThreads, -1);
+  for (int t = 0; t < ntile; ++t) {
+    std::vector<int> bl;
+    for (int k = tb[t]; k < tb[t + 1]; ++k) bl.push_back(k);
+    std::stable_sort(bl.begin(), bl.end(), [&](int x, int y) { return hits[x] > hits[y]; });
+    for (int i = 0; i < (int)bl.size(); ++i) {
+      const int th2 = i < kTileThreads ? i : 2 * kTileThreads - 1 - i;
+      slot[(size_t)t * 2 * kTileThreads + (i < kTileThreads ? 0 : kTileThreads) + th2] = bl[i];
+    }
+    int c = 0;
+    while (tri_n(c + 1) <= tb[t + 1] - 1) ++c;
+    clast[t] = c;
+  }
   SchurTiles& a = h->tiles;
   a.ntile = ntile;
-  a.nbatch = (int)batch_rec.size() - 1;
-  a.nrec = (int)rec.size();
-  // one work-group per CU (1024 threads); groups in multiples of 8 (one XCD per group)
+  a.nbatch = nbatch;
+  a.nrec = nrec;
+  // one work-group per CU; groups in multiples of 8 (one XCD per group)
   int ng = std::max(1, h->ncu / a.ntile);
   if (ng >= 8) ng -= ng % 8;
   a.ngroup = std::max(1, std::min(ng, a.nbatch));
   a.nelem = 36 * nb;
   a.stride = (size_t)a.nelem;
   a.kq = 0;
-  a.batch_cap = kBatchRec;
-  big_vec<int> rcam(rec.size());
-  par_for((long long)rec.size(), [&](long long b, long long e, int) {
-    for (long long i = b; i < e; ++i) rcam[i] = rec[i].w;
-  });
+  a.batch_cap = cap;
+  a.hdr_bytes = hdr_bytes;
   Dev& d = h->dev;
-  int *d_tb = nullptr, *d_br = nullptr, *d_bp = nullptr, *d_rcam = nullptr;
-  CHECK_RC(upload(&d_rcam, d, rcam, s));
-  a.rec_cam = d_rcam;
+  int *d_br = nullptr, *d_cl = nullptr, *d_slot = nullptr;
+  unsigned char* d_hdr = nullptr;
   int2* d_sch = nullptr;
   int4* d_rec = nullptr;
-  CHECK_RC(upload(&d_tb, d, tb, s));
   CHECK_RC(upload(&d_br, d, batch_rec, s));
-  CHECK_RC(upload(&d_bp, d, batch_pt, s));
+  CHECK_RC(upload(&d_cl, d, clast, s));
+  CHECK_RC(upload(&d_slot, d, slot, s));
+  CHECK_RC(upload(&d_hdr, d, hdr, s));
   CHECK_RC(upload(&d_sch, d, sch, s));
   CHECK_RC(upload(&d_rec, d, rec, s));
-  a.tile_b0 = d_tb;
   a.batch_rec = d_br;
-  a.batch_pt = d_bp;
+  a.tile_clast = d_cl;
+  a.tile_slot = d_slot;
+  a.hdr = d_hdr;
   a.sch_ent = d_sch;
   a.rec_info = d_rec;
   CHECK_RC(d.alloc(&h->d_kx, (size_t)6 * NC));
