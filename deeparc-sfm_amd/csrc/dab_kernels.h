@@ -193,6 +193,8 @@ struct SchurTiles {
   const int* tile_slot;              // [ntile][2 kTileThreads] block owned by (thread, half) or -1,
                                      // balanced by the blocks' sampled hit counts
   const int4* rec_info;              // [nrec] (first entry in sch_ent, entry count, point, camera)
+  const int4* rec_obs;               // [nrec] the first entry's (observation slot 2 s + camera slot,
+                                     // ext0, ext1, intr): k_schur_y streams it instead of two gathers
   const int2* sch_ent;               // [NE] (ent_os, camera), sorted by camera inside each point
   const int* kx;                     // [6 NC] rhs row exponents (launch_schur_scale)
   double* partial;                   // [ngroup][stride] per-group block sums

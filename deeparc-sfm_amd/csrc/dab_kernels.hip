@@ -2914,40 +2914,86 @@ __global__ __launch_bounds__(256) void k_schur_y(DevView v, const double* __rest
   unsigned long long* rhs = reinterpret_cast<unsigned long long*>(ylds + 30 * (size_t)v.E + 6 * (size_t)v.NI);
   for (int i = threadIdx.x; i < 6 * v.NC; i += blockDim.x) rhs[i] = 0ull;
   __syncthreads();
-  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < a.nrec; r += gridDim.x * blockDim.x) {
+  // a wave's 64 consecutive records leave through LDS: each lane builds its record, then the
+  // wave stores the 9 KB as lane-contiguous 16-B pieces (whole lines, instead of 64 lines
+  // touched 16 B at a time by every store)
+  const int lane = threadIdx.x & 63;
+  double* stage = reinterpret_cast<double*>(rhs + 6 * (size_t)v.NC) + (size_t)(threadIdx.x >> 6) * 64 * 18;
+  for (int rb = blockIdx.x * blockDim.x + (threadIdx.x & ~63); rb < a.nrec; rb += gridDim.x * blockDim.x) {
+    const int r = rb + lane;
+    const int nvalid = min(64, a.nrec - rb);
+    double rq[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // this record's rhs terms (Y q per row)
+    int rcam = -1;
+    if (r < a.nrec) {
     const int4 ri = a.rec_info[r];  // (first sorted entry, count, point, camera)
     const int pt = ri.z, cam = ri.w;
     const double X[3] = {points[3 * (size_t)pt], points[3 * (size_t)pt + 1], points[3 * (size_t)pt + 2]};
-    double y[18];
+    // W = sum over the record's entries of J_c^T J_p (6 x 3); Y = s_c o (W PU) once after
+    double w[18];
 #pragma unroll
-    for (int k = 0; k < 18; ++k) y[k] = 0.0;
+    for (int k = 0; k < 18; ++k) w[k] = 0.0;
+    const int4 ro = a.rec_obs[r];
     for (int e = ri.x; e < ri.x + ri.y; ++e) {
-      const int os = a.sch_ent[e].x, sl = os >> 1;
-      const int4 id = v.obs_idx[sl];
-      double ru, rv, jx0[3], jx1[3], ja[6], jb[6], da[6], db[6];
-      obs_rows<true, 2>(id, v.obs_xy[sl], X, st, ru, rv, jx0, jx1, ja, jb, da, db);
-      if (os & 1) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-          ja[k] = da[k];
-          jb[k] = db[k];
-        }
+      // the first entry's observation comes with the record; further ones (a point seen by
+      // one camera twice: the rig's arc through several rings) are gathered
+      int os;
+      int4 id;
+      if (e == ri.x) {
+        os = ro.x;
+        id = make_int4(pt, ro.y, ro.z, ro.w);
+      } else {
+        os = a.sch_ent[e].x;
+        id = v.obs_idx[os >> 1];
       }
-      double ye[18];
-      make_y(ja, jb, jx0, jx1, scc + 6 * cam, PU + 6 * (size_t)pt, ye);
+      const double2 xy0 = make_double2(0.0, 0.0);  // the residual is not used
+      double ru, rv, jx0[3], jx1[3], ja[6], jb[6];  // the rows of the record's camera slot only
+      if (os & 1) obs_rows<true, 1>(id, xy0, X, st, ru, rv, jx0, jx1, ja, jb);
+      else obs_rows<true, 0>(id, xy0, X, st, ru, rv, jx0, jx1, ja, jb);
 #pragma unroll
-      for (int k = 0; k < 18; ++k) y[k] += ye[k];
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) w[3 * r + k] = fma(jb[r], jx1[k], fma(ja[r], jx0[k], w[3 * r + k]));
     }
-    double2* o = reinterpret_cast<double2*>(yrec + 18 * (size_t)r);
+    double y[18];
+    {
+      const double* pu = PU + 6 * (size_t)pt;
+      const double u00 = pu[0], u01 = pu[1], u02 = pu[2], u11 = pu[3], u12 = pu[4], u22 = pu[5];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        const double sa = scc[6 * cam + r];
+        y[3 * r] = sa * (w[3 * r] * u00);
+        y[3 * r + 1] = sa * (w[3 * r] * u01 + w[3 * r + 1] * u11);
+        y[3 * r + 2] = sa * (w[3 * r] * u02 + w[3 * r + 1] * u12 + w[3 * r + 2] * u22);
+      }
+    }
+    double2* o = reinterpret_cast<double2*>(stage + 18 * lane);
 #pragma unroll
     for (int k = 0; k < 9; ++k) o[k] = make_double2(y[2 * k], y[2 * k + 1]);
     const double q0 = q[4 * (size_t)pt], q1 = q[4 * (size_t)pt + 1], q2 = q[4 * (size_t)pt + 2];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const double val = ldexp(y[3 * k] * q0 + y[3 * k + 1] * q1 + y[3 * k + 2] * q2, 60 - a.kx[6 * cam + k] - a.kq);
-      __hip_atomic_fetch_add(rhs + 6 * cam + k, (unsigned long long)__double2ll_rn(val), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (int k = 0; k < 6; ++k) rq[k] = y[3 * k] * q0 + y[3 * k + 1] * q1 + y[3 * k + 2] * q2;
+    rcam = cam;
     }
+    if (rcam >= 0) {  // rhs in fixed point (integer adds: the order does not matter)
+#pragma unroll
+      for (int k = 0; k < 6; ++k)
+        __hip_atomic_fetch_add(rhs + 6 * rcam + k,
+                               (unsigned long long)__double2ll_rn(ldexp(rq[k], 60 - a.kx[6 * rcam + k] - a.kq)),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double2* dst = reinterpret_cast<double2*>(yrec + 18 * (size_t)rb);
+    const double2* src = reinterpret_cast<const double2*>(stage);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int piece = 64 * j + lane;
+      if (piece < 9 * nvalid) dst[piece] = src[piece];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 6 * v.NC; i += blockDim.x)
@@ -3118,7 +3164,8 @@ void launch_schur_y(hipStream_t s, const DevView& v, const double* points, const
                     const double* q, const double* scale_c, const SchurTiles& a, double* yrec,
                     unsigned long long* rhs_out) {
   if (a.nrec <= 0) return;
-  const size_t lds = small_tabs_bytes(v.E, v.NI) + sizeof(unsigned long long) * 6 * (size_t)v.NC;
+  const size_t lds = small_tabs_bytes(v.E, v.NI) + sizeof(unsigned long long) * 6 * (size_t)v.NC +
+                     sizeof(double) * 4 * 64 * 18;  // + a record stage per wave
   k_schur_y<<<std::min(grid_for(a.nrec, 256, 1 << 20), kSmallGrid), 256, lds, s>>>(v, points, camtab, PU, q, scale_c,
                                                                                    a, yrec, rhs_out);
 }

@@ -1330,7 +1330,7 @@ static int build_schur_tiles(dab_handle* h) {
   const int nbatch = (int)batch_rec.size() - 1;
   // records ordered (batch, camera, point) and the batch headers: mask[NC] | off[NC + 1]
   const int hdr_bytes = schur_tile_hdr_bytes(NC);
-  big_vec<int4> rec(nrec);
+  big_vec<int4> rec(nrec), robs(nrec);
   std::vector<unsigned char> hdr((size_t)nbatch * hdr_bytes, 0);
   par_for(nbatch, [&](long long bb, long long be, int) {
     std::vector<int> pos(NC + 1);
@@ -1354,6 +1354,8 @@ static int build_schur_tiles(dab_handle* h) {
           }
           r = batch_rec[b] + pos[sch[i].y]++;
           rec[r] = make_int4(i, 1, p, sch[i].y);
+          const int o = h->perm[sch[i].x >> 1];  // the caller's observation of the slot
+          robs[r] = make_int4(sch[i].x, h->prob.obs_ext0[o], h->prob.obs_ext1[o], h->prob.obs_intr[o]);
         }
       }
     }
@@ -1421,6 +1423,9 @@ static int build_schur_tiles(dab_handle* h) {
   CHECK_RC(upload(&d_hdr, d, hdr, s));
   CHECK_RC(upload(&d_sch, d, sch, s));
   CHECK_RC(upload(&d_rec, d, rec, s));
+  int4* d_robs = nullptr;
+  CHECK_RC(upload(&d_robs, d, robs, s));
+  a.rec_obs = d_robs;
   a.batch_rec = d_br;
   a.tile_clast = d_cl;
   a.tile_slot = d_slot;
