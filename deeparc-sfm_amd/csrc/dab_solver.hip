@@ -1288,6 +1288,14 @@ static int max_all_ranks(dab_handle* h, double& x) {  // max over ranks of one h
 static constexpr int kBatchPts = 64, kTileBlocks = 1024;
 static int build_schur_tiles(dab_handle* h) {
   hipStream_t s = h->stream;
+  static const bool timing = getenv("DAB_SETUP_TIMING") != nullptr;
+  double t_ph = now_s();
+  auto phase = [&](const char* name) {
+    if (!timing) return;
+    const double t = now_s();
+    fprintf(stderr, "schur_tiles %-22s %8.1f ms\n", name, 1e3 * (t - t_ph));
+    t_ph = t;
+  };
   const int NP = h->NP, NC = h->NC;
   const std::vector<int>& pt_ent_ptr = h->h_pt_ent_ptr;
   const big_vec<int>& ent_cam = h->h_ent_cam;
@@ -1306,9 +1314,10 @@ static int build_schur_tiles(dab_handle* h) {
       for (int i = b; i < e; ++i) m += (i == b || sch[i].y != sch[i - 1].y);
       rec_ptr[p + 1] = m;
     }
-  });
+  }, 2048);
   for (int p = 0; p < NP; ++p) rec_ptr[p + 1] += rec_ptr[p];
   const int nrec = rec_ptr[NP];
+  phase("sort entries");
   // batches of whole points: <= kBatchPts points (one mask word) and <= cap records
   std::vector<int> batch_rec{0}, batch_pt{0};
   const int cap = schur_tile_batch_cap(NC);
@@ -1359,7 +1368,8 @@ static int build_schur_tiles(dab_handle* h) {
         }
       }
     }
-  }, 1024);
+  }, 16);
+  phase("records, headers");
   // tiles: equal block ranges of <= kTileBlocks (rows up to the tile's last camera)
   const int nb = (int)tri_n(NC);
   const int ntile = std::max(1, (nb + kTileBlocks - 1) / kTileBlocks);
@@ -1399,6 +1409,7 @@ static int build_schur_tiles(dab_handle* h) {
     while (tri_n(c + 1) <= tb[t + 1] - 1) ++c;
     clast[t] = c;
   }
+  phase("hits, slots");
   SchurTiles& a = h->tiles;
   a.ntile = ntile;
   a.nbatch = nbatch;
@@ -1406,7 +1417,8 @@ static int build_schur_tiles(dab_handle* h) {
   // one work-group per CU; groups in multiples of 8 (one XCD per group)
   int ng = std::max(1, h->ncu / a.ntile);
   if (ng >= 8) ng -= ng % 8;
-  a.ngroup = std::max(1, std::min(ng, a.nbatch));
+  // at least 8 batches per group: small problems keep few partials for k_schur_sum
+  a.ngroup = std::max(1, std::min(ng, a.nbatch / 8));
   a.nelem = 36 * nb;
   a.stride = (size_t)a.nelem;
   a.kq = 0;
@@ -1439,11 +1451,21 @@ static int build_schur_tiles(dab_handle* h) {
   CHECK_RC(d.alloc(&h->d_rfx, (size_t)6 * NC));
   CHECK_RC(d.alloc(&h->d_yrec, (size_t)18 * std::max(1, a.nrec)));
   HIP_OK(hipStreamSynchronize(s));
+  phase("upload, alloc");
   return 0;
 }
 
 static int build_schur_tables(dab_handle* h) {
   if (h->schur_built) return 0;
+  static const bool timing = getenv("DAB_SETUP_TIMING") != nullptr;
+  const double t_b = now_s();
+  struct Report {
+    bool on;
+    double t0;
+    ~Report() {
+      if (on) fprintf(stderr, "build_schur_tables %8.1f ms\n", 1e3 * (now_s() - t0));
+    }
+  } report{timing, t_b};
   hipStream_t s = h->stream;
   const int NP = h->NP, NC = h->NC;
   const std::vector<int>& pt_ent_ptr = h->h_pt_ent_ptr;
