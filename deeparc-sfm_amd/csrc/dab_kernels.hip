@@ -3500,7 +3500,7 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_points(DevView v, const doub
 // flags [E] | w~, dt per camera [NC][6] | J_l per camera [NC][9] | per-wave sums [4][NC][6].
 static size_t mf2_lds_bytes(int E, int NI, int NC, bool product) {
   return sizeof(double) * (12 * (size_t)E + 6 * (size_t)NI + 6 * (size_t)NC + 9 * (size_t)NC +
-                           (product ? (kMfBlock / 64) * 6 * (size_t)NC : 0)) +
+                           (product ? (kMfBlock / 64) * 6 * (size_t)(NC | 1) : 0)) +
          2 * sizeof(int) * (size_t)E;
 }
 template <int MODE>
@@ -3518,8 +3518,11 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const doubl
   double* k_s = rt_s + 12 * (size_t)v.E;               // [NI][6]
   double* dv_s = k_s + 6 * (size_t)v.NI;               // [NC][6]: w~ | dt (MODE 0, 1)
   double* jl_s = dv_s + NC6;                           // [NC][9]: J_l (MODE 0, 2)
-  double* accs = jl_s + 9 * (size_t)v.NC;              // [waves][NC][6] (MODE 0, 2)
-  int* sm_s = reinterpret_cast<int*>(accs + (MODE != 1 ? (kMfBlock / 64) * NC6 : 0));  // [E]
+  // per-wave camera sums (MODE 0, 2), component-major [waves][6][NCP], odd NCP: the lanes of
+  // one atomic add one component of their cameras, which fall in different banks
+  const int NCP = v.NC | 1;
+  double* accs = jl_s + 9 * (size_t)v.NC;
+  int* sm_s = reinterpret_cast<int*>(accs + (MODE != 1 ? (kMfBlock / 64) * 6 * NCP : 0));  // [E]
   int* col_s = sm_s + v.E;                             // [E] ext_col: no dependent global load per slot
   for (int i = threadIdx.x; i < 12 * v.E; i += blockDim.x) rt_s[i] = camtab[(size_t)kCamTab * (i / 12) + i % 12];
   for (int i = threadIdx.x; i < 6 * v.NI; i += blockDim.x) k_s[i] = v.intr[(size_t)kIntr * (i / 6) + i % 6];
@@ -3551,7 +3554,7 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const doubl
     for (int k = 0; k < 9; ++k) jl_s[9 * c + k] = J[k];
   }
   if constexpr (MODE != 1)
-    for (int i = threadIdx.x; i < (kMfBlock / 64) * NC6; i += blockDim.x) accs[i] = 0.0;
+    for (int i = threadIdx.x; i < (kMfBlock / 64) * 6 * NCP; i += blockDim.x) accs[i] = 0.0;
   __syncthreads();
   const SmallTabs tabs{nullptr, k_s};
   auto rt = [&](int e, double (&o)[12]) {
@@ -3563,7 +3566,7 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const doubl
       o[2 * k + 1] = u.y;
     }
   };
-  double* acc = accs + (threadIdx.x >> 6) * NC6;
+  double* acc = accs + (threadIdx.x >> 6) * 6 * NCP;
   const size_t NPs = (size_t)v.NP;
   auto rot9 = [&](int e, double (&o)[9]) {
     const double2* pp = reinterpret_cast<const double2*>(rt_s + 12 * e);
@@ -3717,18 +3720,18 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const doubl
           double cz[3];
           cross3(Z0, gz, cz);
 #pragma unroll
-          for (int a = 0; a < 3; ++a) atomicAdd(acc + 6 * c0 + a, cz[a]);
+          for (int a = 0; a < 3; ++a) atomicAdd(acc + a * NCP + c0, cz[a]);
 #pragma unroll
-          for (int a = 0; a < 3; ++a) atomicAdd(acc + 6 * c0 + 3 + a, gz[a]);
+          for (int a = 0; a < 3; ++a) atomicAdd(acc + (3 + a) * NCP + c0, gz[a]);
         }
         if (c1 >= 0) {
           double hz[3], cz[3];
           mtv3(Ra, gz, hz);
           cross3(Z1, hz, cz);
 #pragma unroll
-          for (int a = 0; a < 3; ++a) atomicAdd(acc + 6 * c1 + a, cz[a]);
+          for (int a = 0; a < 3; ++a) atomicAdd(acc + a * NCP + c1, cz[a]);
 #pragma unroll
-          for (int a = 0; a < 3; ++a) atomicAdd(acc + 6 * c1 + 3 + a, hz[a]);
+          for (int a = 0; a < 3; ++a) atomicAdd(acc + (3 + a) * NCP + c1, hz[a]);
         }
       }
     }
@@ -3742,15 +3745,15 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const doubl
         x = 0.0;
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
-          double t = accs[6 * c + r];
+          double t = accs[r * NCP + c];
 #pragma unroll
-          for (int w = 1; w < kMfBlock / 64; ++w) t += accs[w * NC6 + 6 * c + r];
+          for (int w = 1; w < kMfBlock / 64; ++w) t += accs[(w * 6 + r) * NCP + c];
           x += jl_s[9 * c + 3 * r + k] * t;
         }
       } else {
-        x = accs[i];
+        x = accs[k * NCP + c];
 #pragma unroll
-        for (int w = 1; w < kMfBlock / 64; ++w) x += accs[w * NC6 + i];
+        for (int w = 1; w < kMfBlock / 64; ++w) x += accs[(w * 6 + k) * NCP + c];
       }
       out[(size_t)blockIdx.x * NC6 + i] = -scc[i] * x;
     }
@@ -3801,7 +3804,7 @@ __device__ __forceinline__ void proj_jac32(const float (&P)[3], const float4 K, 
   A1[2] = -(dv_dx * xp + dv_dy * yp) * iz;
 }
 static size_t mf32_lds_bytes(int E, int NI, int NC) {
-  return sizeof(double) * (9 * (size_t)NC + (kMfBlock / 64) * 6 * (size_t)NC) +
+  return sizeof(double) * (9 * (size_t)NC + (kMfBlock / 64) * 6 * (size_t)(NC | 1)) +
          sizeof(float) * (12 * (size_t)E + 4 * (size_t)NI + 6 * (size_t)NC) + 2 * sizeof(int) * (size_t)E;
 }
 __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame32(DevView v, const double* __restrict__ points,
@@ -3814,8 +3817,12 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame32(DevView v, const dou
   if (st->status != kPcgRunning) return;
   const int NC6 = 6 * v.NC;
   double* jl_s = mf_lds;                                        // [NC][9] J_l (fp64, applied to the sums)
-  double* accs = jl_s + 9 * (size_t)v.NC;                       // [waves][NC][6] fp64 sums
-  float* rt_s = reinterpret_cast<float*>(accs + (kMfBlock / 64) * NC6);  // [E][12] R | t
+  // per-wave fp64 camera sums, component-major [waves][6][NCP] with an odd row length: the
+  // 64 lanes of one atomic add the same component of their cameras, which then fall in
+  // different banks (camera-major [NC][6] put 6 doubles per camera, 16 bank offsets)
+  const int NCP = v.NC | 1;
+  double* accs = jl_s + 9 * (size_t)v.NC;
+  float* rt_s = reinterpret_cast<float*>(accs + (kMfBlock / 64) * 6 * NCP);  // [E][12] R | t
   float* k_s = rt_s + 12 * (size_t)v.E;                         // [NI][4] fx fy k0 k1
   float* dv_s = k_s + 4 * (size_t)v.NI;                         // [NC][6] w~ | dt
   int* sm_s = reinterpret_cast<int*>(dv_s + NC6);               // [E] small-angle tables
@@ -3848,14 +3855,14 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame32(DevView v, const dou
 #pragma unroll
     for (int k = 0; k < 9; ++k) jl_s[9 * c + k] = J[k];
   }
-  for (int i = threadIdx.x; i < (kMfBlock / 64) * NC6; i += blockDim.x) accs[i] = 0.0;
+  for (int i = threadIdx.x; i < (kMfBlock / 64) * 6 * NCP; i += blockDim.x) accs[i] = 0.0;
   __syncthreads();
-  double* acc = accs + (threadIdx.x >> 6) * NC6;
-  auto add = [&](int i, float x) { atomicAdd(acc + i, (double)x); };  // fp64 per-wave camera sums
-  auto sum_of = [&](int i) {  // fixed order over the waves
-    double t = accs[i];
+  double* acc = accs + (threadIdx.x >> 6) * 6 * NCP;
+  auto add = [&](int c, int a, float x) { atomicAdd(acc + a * NCP + c, (double)x); };  // fp64 per-wave sums
+  auto sum_of = [&](int c, int a) {  // fixed order over the waves
+    double t = accs[a * NCP + c];
 #pragma unroll
-    for (int w = 1; w < kMfBlock / 64; ++w) t += accs[w * NC6 + i];
+    for (int w = 1; w < kMfBlock / 64; ++w) t += accs[(w * 6 + a) * NCP + c];
     return t;
   };
   auto rt = [&](int e, float (&o)[12]) {
@@ -3985,18 +3992,18 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame32(DevView v, const dou
         float cz[3];
         cross3f(Z0, gz, cz);
 #pragma unroll
-        for (int a2 = 0; a2 < 3; ++a2) add(6 * c0 + a2, cz[a2]);
+        for (int a2 = 0; a2 < 3; ++a2) add(c0, a2, cz[a2]);
 #pragma unroll
-        for (int a2 = 0; a2 < 3; ++a2) add(6 * c0 + 3 + a2, gz[a2]);
+        for (int a2 = 0; a2 < 3; ++a2) add(c0, 3 + a2, gz[a2]);
       }
       if (c1 >= 0) {
         float hz[3], cz[3];
         mtv3f(Ra, gz, hz);
         cross3f(Z1, hz, cz);
 #pragma unroll
-        for (int a2 = 0; a2 < 3; ++a2) add(6 * c1 + a2, cz[a2]);
+        for (int a2 = 0; a2 < 3; ++a2) add(c1, a2, cz[a2]);
 #pragma unroll
-        for (int a2 = 0; a2 < 3; ++a2) add(6 * c1 + 3 + a2, hz[a2]);
+        for (int a2 = 0; a2 < 3; ++a2) add(c1, 3 + a2, hz[a2]);
       }
     }
   }
@@ -4007,9 +4014,9 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame32(DevView v, const dou
     if (k < 3) {
       x = 0.0;
 #pragma unroll
-      for (int r = 0; r < 3; ++r) x += jl_s[9 * c + 3 * r + k] * sum_of(6 * c + r);
+      for (int r = 0; r < 3; ++r) x += jl_s[9 * c + 3 * r + k] * sum_of(c, r);
     } else {
-      x = sum_of(i);
+      x = sum_of(c, k);
     }
     out[(size_t)blockIdx.x * NC6 + i] = -scc[i] * x;
   }
