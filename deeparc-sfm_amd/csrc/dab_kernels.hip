@@ -3498,8 +3498,11 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_points(DevView v, const doub
 // need only R, t (and K) from LDS: the 18 Rd | Jd doubles per slot of k_mf_points, the
 // s_c reads and the 3 x 3 products with them drop out. LDS: rt [E][12] | small-angle
 // flags [E] | w~, dt per camera [NC][6] | J_l per camera [NC][9] | per-wave sums [4][NC][6].
+// R | t rows of 14 doubles (12 used): 112 B = 28 banks apart, so the 16-B reads of 16
+// different cameras fall in 16 disjoint bank quads (a 12-double row gives only 8)
+constexpr int kRtStride = 14;
 static size_t mf2_lds_bytes(int E, int NI, int NC, bool product) {
-  return sizeof(double) * (12 * (size_t)E + 6 * (size_t)NI + 6 * (size_t)NC + 9 * (size_t)NC +
+  return sizeof(double) * (kRtStride * (size_t)E + 6 * (size_t)NI + 6 * (size_t)NC + 9 * (size_t)NC +
                            (product ? (kMfBlock / 64) * 6 * (size_t)(NC | 1) : 0)) +
          2 * sizeof(int) * (size_t)E;
 }
@@ -3515,7 +3518,7 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const doubl
   if (MODE == 0 && st->status != kPcgRunning) return;
   const int NC6 = 6 * v.NC;
   double* rt_s = mf_lds;                               // [E][12]
-  double* k_s = rt_s + 12 * (size_t)v.E;               // [NI][6]
+  double* k_s = rt_s + kRtStride * (size_t)v.E;        // [NI][6]
   double* dv_s = k_s + 6 * (size_t)v.NI;               // [NC][6]: w~ | dt (MODE 0, 1)
   double* jl_s = dv_s + NC6;                           // [NC][9]: J_l (MODE 0, 2)
   // per-wave camera sums (MODE 0, 2), component-major [waves][6][NCP], odd NCP: the lanes of
@@ -3524,7 +3527,7 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const doubl
   double* accs = jl_s + 9 * (size_t)v.NC;
   int* sm_s = reinterpret_cast<int*>(accs + (MODE != 1 ? (kMfBlock / 64) * 6 * NCP : 0));  // [E]
   int* col_s = sm_s + v.E;                             // [E] ext_col: no dependent global load per slot
-  for (int i = threadIdx.x; i < 12 * v.E; i += blockDim.x) rt_s[i] = camtab[(size_t)kCamTab * (i / 12) + i % 12];
+  for (int i = threadIdx.x; i < 12 * v.E; i += blockDim.x) rt_s[kRtStride * (i / 12) + i % 12] = camtab[(size_t)kCamTab * (i / 12) + i % 12];
   for (int i = threadIdx.x; i < 6 * v.NI; i += blockDim.x) k_s[i] = v.intr[(size_t)kIntr * (i / 6) + i % 6];
   for (int e = threadIdx.x; e < v.E; e += blockDim.x) {
     const double* T = camtab + (size_t)kCamTab * e;  // R t Rd Jd
@@ -3558,7 +3561,7 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const doubl
   __syncthreads();
   const SmallTabs tabs{nullptr, k_s};
   auto rt = [&](int e, double (&o)[12]) {
-    const double2* pp = reinterpret_cast<const double2*>(rt_s + 12 * e);
+    const double2* pp = reinterpret_cast<const double2*>(rt_s + kRtStride * e);
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
       const double2 u = pp[k];
@@ -3569,14 +3572,14 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const doubl
   double* acc = accs + (threadIdx.x >> 6) * 6 * NCP;
   const size_t NPs = (size_t)v.NP;
   auto rot9 = [&](int e, double (&o)[9]) {
-    const double2* pp = reinterpret_cast<const double2*>(rt_s + 12 * e);
+    const double2* pp = reinterpret_cast<const double2*>(rt_s + kRtStride * e);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const double2 u = pp[k];
       o[2 * k] = u.x;
       o[2 * k + 1] = u.y;
     }
-    o[8] = rt_s[12 * e + 8];
+    o[8] = rt_s[kRtStride * e + 8];
   };
   // one observation's geometry: A (2 x 3), R_a, and the rotated-frame points Z of both
   // slots; with RB, vout = R_b vin (vin for single-extrinsic observations) while the ring
