@@ -4298,13 +4298,13 @@ __global__ __launch_bounds__(256) void k_candidate_frame(DevView v, const double
                                                          double* __restrict__ partial) {
   extern __shared__ double cf_lds[];
   double* rt_s = cf_lds;
-  double* rtc_s = rt_s + 12 * (size_t)v.E;
-  double* k_s = rtc_s + 12 * (size_t)v.E;
+  double* rtc_s = rt_s + kRtStride * (size_t)v.E;  // rows padded (bank quads, see kRtStride)
+  double* k_s = rtc_s + kRtStride * (size_t)v.E;
   double* dv_s = k_s + 6 * (size_t)v.NI;
   int* sm_s = reinterpret_cast<int*>(dv_s + 6 * (size_t)v.NC);
   for (int i = threadIdx.x; i < 12 * v.E; i += blockDim.x) {
-    rt_s[i] = camtab[(size_t)kCamTab * (i / 12) + i % 12];
-    rtc_s[i] = camtab_c[(size_t)kCamTab * (i / 12) + i % 12];
+    rt_s[kRtStride * (i / 12) + i % 12] = camtab[(size_t)kCamTab * (i / 12) + i % 12];
+    rtc_s[kRtStride * (i / 12) + i % 12] = camtab_c[(size_t)kCamTab * (i / 12) + i % 12];
   }
   for (int i = threadIdx.x; i < 6 * v.NI; i += blockDim.x) k_s[i] = v.intr[(size_t)kIntr * (i / 6) + i % 6];
   for (int e = threadIdx.x; e < v.E; e += blockDim.x) {
@@ -4331,7 +4331,7 @@ __global__ __launch_bounds__(256) void k_candidate_frame(DevView v, const double
   __syncthreads();
   const SmallTabs tk{nullptr, k_s};
   auto rt = [&](const double* base, int e, double (&o)[12]) {
-    const double2* pp = reinterpret_cast<const double2*>(base + 12 * e);
+    const double2* pp = reinterpret_cast<const double2*>(base + kRtStride * e);
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
       const double2 u = pp[k];
@@ -4428,7 +4428,7 @@ void launch_candidate(hipStream_t s, const DevView& v, const double* points, con
                       int grid) {
   static const bool rows = getenv("DAB_CAND_ROWS") && atoi(getenv("DAB_CAND_ROWS")) != 0;  // A/B: row form
   if (small_tabs_fit(v.E, v.NI) && !rows) {
-    const size_t lds = sizeof(double) * (24 * (size_t)v.E + 6 * (size_t)v.NI + 6 * (size_t)v.NC) +
+    const size_t lds = sizeof(double) * (2 * kRtStride * (size_t)v.E + 6 * (size_t)v.NI + 6 * (size_t)v.NC) +
                        sizeof(int) * (size_t)v.E;
     k_candidate_frame<<<grid, 256, lds, s>>>(v, points, camtab, delta_p, delta_c, camtab_c, partial);
   } else if (small_tabs_fit(v.E, v.NI)) {
