@@ -56,3 +56,11 @@ for r, t in enumerate(runs):
         print(f"  {name:6s} loopend {q(x[:, :, 2])}")
         print(f"  {name:6s} exit    {q(x[:, :, 3])}")
         print(f"  {name:6s} loop    {q(x[:, :, 2] - x[:, :, 1])}   (per wave, percentiles 0/10/50/90/100)")
+if os.environ.get("DAB_TRACE_PER_WAVE"):
+    t = runs[-1]
+    have = t[:, :, 0] > 0
+    t0 = t[:, :, 0][have].min()
+    rel = np.where(t > 0, (t - t0) * 0.01, np.nan)
+    print("per logical wave: median staged / loop end / exit (us)")
+    for w in range(16):
+        print(f"  wave {w:2d}: " + " ".join(f"{np.nanmedian(rel[:, w, k]):6.2f}" for k in (1, 2, 3)))
