@@ -597,3 +597,28 @@ def test_large_initial_cost_matches_oracle(pkg, orc, gpu, kind):
     assert g["initial_cost"] == pytest.approx(o["initial_cost"], rel=1e-12)
     assert g["termination"] != "FAILURE", g["message"]
     assert [it["success"] for it in g["iterations"]] == [it["success"] for it in o["iterations"]]
+
+
+@pytest.mark.parametrize("kind", ["bal", "rig"])
+def test_noise_free_problem_matches_oracle(pkg, orc, gpu, kind):
+    """Observations without pixel noise: the cost falls towards zero, where a coarse
+    fixed-point cost would quantise the function-tolerance and relative-decrease tests.
+    The cost accumulator holds partials exactly down to 2^-100, so the GPU's iterations
+    match the oracle's while the cost is above 1e-12 of the initial one (below that both
+    are rounding noise), both converge, and the parameters agree to 1e-9."""
+    if kind == "bal":
+        prob = pkg.synth(kind=0, num_cameras=30, num_points=2000, obs_per_point=6, seed=81, pixel_noise=0.0)
+    else:
+        prob = pkg.synth(kind=1, num_arcs=5, num_rings=10, num_points=2000, obs_per_point=6, seed=82,
+                         pixel_noise=0.0)
+    g, o, ref = run_both(pkg, orc, prob, max_num_iterations=30)
+    c0 = o["initial_cost"]
+    assert g["initial_cost"] == pytest.approx(c0, rel=1e-12)
+    for a, b in zip(g["iterations"], o["iterations"]):
+        if b["cost"] < 1e-12 * c0:
+            break
+        assert a["success"] == b["success"]
+        assert a["cost"] == pytest.approx(b["cost"], rel=1e-6), (a["cost"], b["cost"])
+    assert g["termination"] == "CONVERGENCE" and o["termination"] == "CONVERGENCE"
+    assert g["final_cost"] < 1e-12 * c0 and o["final_cost"] < 1e-12 * c0
+    np.testing.assert_allclose(prob.points, ref.points, rtol=0, atol=1e-9)
