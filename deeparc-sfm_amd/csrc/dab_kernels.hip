@@ -4040,43 +4040,61 @@ __global__ __launch_bounds__(256) void k_mf_diag_rhs(DevView v, int nchunk, cons
   __shared__ double wsum[kRedBlock / 64][27];
   for (int c = blockIdx.x; c < nchunk; c += gridDim.x) {
   const int b = chunk_beg[c], e = chunk_beg[c + 1];
-  auto entry_y = [&](int i, int& pt, double (&y)[18]) {
-    int4 id = v.cm_idx[i];
-    const bool slot1 = (id.w & kSlotBit) != 0;
-    id.w &= ~kSlotBit;
-    const int cam = v.ext_col[slot1 ? id.z : id.y];
-    pt = id.x;
-    const double X[3] = {points[3 * (size_t)id.x], points[3 * (size_t)id.x + 1], points[3 * (size_t)id.x + 2]};
-    double ru, rv, jx0[3], jx1[3], ja[6], jb[6];
-    if (slot1) obs_rows<true, 1>(id, v.cm_xy[i], X, tabs, ru, rv, jx0, jx1, ja, jb);
-    else obs_rows<true, 0>(id, v.cm_xy[i], X, tabs, ru, rv, jx0, jx1, ja, jb);
-    make_y(ja, jb, jx0, jx1, scc + 6 * cam, PU + 6 * (size_t)id.x, y);
-  };
   double acc[27];
 #pragma unroll
   for (int i = 0; i < 27; ++i) acc[i] = 0.0;
   for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
-    int p;
+    // one run (the entries of one point on this camera; usually one entry): W = sum of
+    // J_c^T J_p over the run, then Z = s_c o (W PU) once. Run members are skipped here.
+    const int len = run[i];
+    if (len == 0) continue;
     double y[18];
-    entry_y(i, p, y);
+#pragma unroll
+    for (int k = 0; k < 18; ++k) y[k] = 0.0;
+    int p = 0, cam = 0;
+    double X[3] = {0.0, 0.0, 0.0};
+    for (int j = 0; j < len; ++j) {
+      int4 id = v.cm_idx[i + j];
+      const bool slot1 = (id.w & kSlotBit) != 0;
+      id.w &= ~kSlotBit;
+      if (j == 0) {
+        p = id.x;
+        cam = v.ext_col[slot1 ? id.z : id.y];
+        X[0] = points[3 * (size_t)p];
+        X[1] = points[3 * (size_t)p + 1];
+        X[2] = points[3 * (size_t)p + 2];
+      }
+      const double2 xy0 = make_double2(0.0, 0.0);  // the residual is not used
+      double ru, rv, jx0[3], jx1[3], ja[6], jb[6];
+      if (slot1) obs_rows<true, 1>(id, xy0, X, tabs, ru, rv, jx0, jx1, ja, jb);
+      else obs_rows<true, 0>(id, xy0, X, tabs, ru, rv, jx0, jx1, ja, jb);
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) y[3 * r + k] = fma(jb[r], jx1[k], fma(ja[r], jx0[k], y[3 * r + k]));
+    }
+    {  // in place: y = s_c o (W PU), PU upper triangular (00 01 02 11 12 22)
+      const double* pu = PU + 6 * (size_t)p;
+      const double u00 = pu[0], u01 = pu[1], u02 = pu[2], u11 = pu[3], u12 = pu[4], u22 = pu[5];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        const double sa = scc[6 * cam + r];
+        const double w0 = y[3 * r], w1 = y[3 * r + 1], w2 = y[3 * r + 2];
+        y[3 * r] = sa * (w0 * u00);
+        y[3 * r + 1] = sa * (w0 * u01 + w1 * u11);
+        y[3 * r + 2] = sa * (w0 * u02 + w1 * u12 + w2 * u22);
+      }
+    }
+    // the run's Y_e sum is Z (Y is linear in W): -Z q_p and Z Z^T
     const double q0 = q[4 * (size_t)p], q1 = q[4 * (size_t)p + 1], q2 = q[4 * (size_t)p + 2];
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[21 + a] -= y[3 * a] * q0 + y[3 * a + 1] * q1 + y[3 * a + 2] * q2;
-    const int len = run[i];
-    if (len == 0) continue;
-    for (int j = 1; j < len; ++j) {  // rare (rig): fold the run into Z
-      int pj;
-      double w[18];
-      entry_y(i + j, pj, w);
-#pragma unroll
-      for (int k = 0; k < 18; ++k) y[k] += w[k];
-    }
-    int k = 0;
+    int t = 0;
 #pragma unroll
     for (int a = 0; a < 6; ++a)
 #pragma unroll
       for (int bb = a; bb < 6; ++bb)
-        acc[k++] += y[3 * a] * y[3 * bb] + y[3 * a + 1] * y[3 * bb + 1] + y[3 * a + 2] * y[3 * bb + 2];
+        acc[t++] += y[3 * a] * y[3 * bb] + y[3 * a + 1] * y[3 * bb + 1] + y[3 * a + 2] * y[3 * bb + 2];
   }
   wave_sums_transposed<27>(acc, wsum[threadIdx.x >> 6]);
   __syncthreads();
