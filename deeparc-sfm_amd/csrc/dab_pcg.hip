@@ -802,7 +802,9 @@ void launch_cg_update(hipStream_t s, int NC, int mode, const double* Ad, const d
                       const double* bvec, double* p, double* q, double* x, double* r, PcgState* st,
                       const double* Minv, double* z, double* partial, unsigned* cnt) {
   if (NC <= 0) return;
-  const int L = xptr ? 16 : 1;
+  // with cross blocks a wave per camera: its cross blocks' loads all in flight at once (the
+  // rig: 63 per arc camera; 16 lanes per camera walked them in 4 dependent rounds)
+  const int L = xptr ? 64 : 1;
   const int gq = (NC + kCgBlock / L - 1) / (kCgBlock / L), gx = (NC + kCgBlock - 1) / kCgBlock;
   if (mode != 2)
     k_cg_q<<<gq, kCgBlock, 0, s>>>(NC, mode, L, Ad, w, xptr, xlist, xcam, X, scale_c, bvec, p, q, x, r, st, partial, cnt);
