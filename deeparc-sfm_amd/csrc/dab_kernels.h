@@ -305,7 +305,8 @@ void launch_mf_backsub(hipStream_t s, const DevView& v, const double* points, co
                        const double* scale_c, const double* PU, const double* q, const double* yc, double* dp,
                        int grid);
 // per chunk: 21 of sum Z Z^T over same-point runs | 6 of -sum Y q -> partial[chunk][27]
-void launch_mf_diag_rhs(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int* run,
+// run_beg[nchunk + 1]: each chunk's runs in run_rec {first position, length, point, camera}
+void launch_mf_diag_rhs(hipStream_t s, const DevView& v, int nchunk, const int* run_beg, const int4* run_rec,
                         const double* points, const double* camtab, const double* scale_c, const double* PU,
                         const double* q, double* partial);
 // fixed-order sum of the per-work-group product partials (dab_pcg.hip)

@@ -4028,8 +4028,8 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame32(DevView v, const dou
 // Per chunk of camera-major positions, Y re-evaluated: 21 upper of sum Z Z^T over
 // same-point runs (Z = sum of the run's Y_e; the diagonal block of the Schur term) | 6 of
 // -sum Y_e q_p -> partial[chunk][27]. Replaces k_entry_y + k_pcg_diag_rhs_partial.
-__global__ __launch_bounds__(256) void k_mf_diag_rhs(DevView v, int nchunk, const int* __restrict__ chunk_beg,
-                                                     const int* __restrict__ run,
+__global__ __launch_bounds__(256) void k_mf_diag_rhs(DevView v, int nchunk, const int* __restrict__ run_beg,
+                                                     const int4* __restrict__ run_rec,
                                                      const double* __restrict__ points,
                                                      const double* __restrict__ camtab,
                                                      const double* __restrict__ scc,
@@ -4039,31 +4039,33 @@ __global__ __launch_bounds__(256) void k_mf_diag_rhs(DevView v, int nchunk, cons
   const SmallTabs tabs = stage_small_tabs(mf_lds, v.E, v.NI, camtab, v.intr);  // once per block
   __shared__ double wsum[kRedBlock / 64][27];
   for (int c = blockIdx.x; c < nchunk; c += gridDim.x) {
-  const int b = chunk_beg[c], e = chunk_beg[c + 1];
+  const int b = run_beg[c], e = run_beg[c + 1];
   double acc[27];
 #pragma unroll
   for (int i = 0; i < 27; ++i) acc[i] = 0.0;
-  for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
+  // the chunk's camera scales (uniform: a chunk lies in one camera)
+  const int cam = b < e ? __builtin_amdgcn_readfirstlane(run_rec[b].w) : 0;
+  double sc[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) sc[r] = scc[6 * cam + r];
+  for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
     // one run (the entries of one point on this camera; usually one entry): W = sum of
-    // J_c^T J_p over the run, then Z = s_c o (W PU) once. Run members are skipped here.
-    const int len = run[i];
-    if (len == 0) continue;
+    // J_c^T J_p over the run, then Z = s_c o (W PU) once. The record carries the point, so
+    // the point's loads go out with the first entry's index.
+    const int4 rr = run_rec[k];
+    const int i = rr.x, len = rr.y, p = rr.z;
+    const double X[3] = {points[3 * (size_t)p], points[3 * (size_t)p + 1], points[3 * (size_t)p + 2]};
+    // PU_p and q_p in flight during the entries
+    const double* pu = PU + 6 * (size_t)p;
+    const double u00 = pu[0], u01 = pu[1], u02 = pu[2], u11 = pu[3], u12 = pu[4], u22 = pu[5];
+    const double q0 = q[4 * (size_t)p], q1 = q[4 * (size_t)p + 1], q2 = q[4 * (size_t)p + 2];
     double y[18];
 #pragma unroll
-    for (int k = 0; k < 18; ++k) y[k] = 0.0;
-    int p = 0, cam = 0;
-    double X[3] = {0.0, 0.0, 0.0};
+    for (int t = 0; t < 18; ++t) y[t] = 0.0;
     for (int j = 0; j < len; ++j) {
       int4 id = v.cm_idx[i + j];
       const bool slot1 = (id.w & kSlotBit) != 0;
       id.w &= ~kSlotBit;
-      if (j == 0) {
-        p = id.x;
-        cam = v.ext_col[slot1 ? id.z : id.y];
-        X[0] = points[3 * (size_t)p];
-        X[1] = points[3 * (size_t)p + 1];
-        X[2] = points[3 * (size_t)p + 2];
-      }
       const double2 xy0 = make_double2(0.0, 0.0);  // the residual is not used
       double ru, rv, jx0[3], jx1[3], ja[6], jb[6];
       if (slot1) obs_rows<true, 1>(id, xy0, X, tabs, ru, rv, jx0, jx1, ja, jb);
@@ -4071,22 +4073,18 @@ __global__ __launch_bounds__(256) void k_mf_diag_rhs(DevView v, int nchunk, cons
 #pragma unroll
       for (int r = 0; r < 6; ++r)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) y[3 * r + k] = fma(jb[r], jx1[k], fma(ja[r], jx0[k], y[3 * r + k]));
+        for (int t = 0; t < 3; ++t) y[3 * r + t] = fma(jb[r], jx1[t], fma(ja[r], jx0[t], y[3 * r + t]));
     }
     {  // in place: y = s_c o (W PU), PU upper triangular (00 01 02 11 12 22)
-      const double* pu = PU + 6 * (size_t)p;
-      const double u00 = pu[0], u01 = pu[1], u02 = pu[2], u11 = pu[3], u12 = pu[4], u22 = pu[5];
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
-        const double sa = scc[6 * cam + r];
         const double w0 = y[3 * r], w1 = y[3 * r + 1], w2 = y[3 * r + 2];
-        y[3 * r] = sa * (w0 * u00);
-        y[3 * r + 1] = sa * (w0 * u01 + w1 * u11);
-        y[3 * r + 2] = sa * (w0 * u02 + w1 * u12 + w2 * u22);
+        y[3 * r] = sc[r] * (w0 * u00);
+        y[3 * r + 1] = sc[r] * (w0 * u01 + w1 * u11);
+        y[3 * r + 2] = sc[r] * (w0 * u02 + w1 * u12 + w2 * u22);
       }
     }
     // the run's Y_e sum is Z (Y is linear in W): -Z q_p and Z Z^T
-    const double q0 = q[4 * (size_t)p], q1 = q[4 * (size_t)p + 1], q2 = q[4 * (size_t)p + 2];
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[21 + a] -= y[3 * a] * q0 + y[3 * a + 1] * q1 + y[3 * a + 2] * q2;
     int t = 0;
@@ -4143,13 +4141,13 @@ void launch_mf_backsub(hipStream_t s, const DevView& v, const double* points, co
                                                                                q, dp, nullptr);
   }
 }
-void launch_mf_diag_rhs(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int* run,
+void launch_mf_diag_rhs(hipStream_t s, const DevView& v, int nchunk, const int* run_beg, const int4* run_rec,
                         const double* points, const double* camtab, const double* scale_c, const double* PU,
                         const double* q, double* partial) {
   if (nchunk <= 0) return;
   const size_t lds = small_tabs_bytes(v.E, v.NI);
   // persistent blocks: the 20-KB tables are staged once per block, not once per chunk
-  k_mf_diag_rhs<<<std::min(nchunk, kSmallGrid), 256, lds, s>>>(v, nchunk, chunk_beg, run, points, camtab, scale_c,
+  k_mf_diag_rhs<<<std::min(nchunk, kSmallGrid), 256, lds, s>>>(v, nchunk, run_beg, run_rec, points, camtab, scale_c,
                                                                 PU, q, partial);
 }
 

@@ -345,6 +345,8 @@ struct dab_handle {
   PcgState* d_pcg_state = nullptr;
   PcgState* h_pcg_state = nullptr;  // pinned
   int *d_xptr = nullptr, *d_xlist = nullptr, *d_run = nullptr;
+  int* d_run_beg = nullptr;  // per chunk: its runs in d_run_rec
+  int4* d_run_rec = nullptr;
   double *d_yc = nullptr, *d_dp = nullptr, *d_dc = nullptr;
   double* d_gpart = nullptr;   // grid partials
   double* d_scal = nullptr;    // S_NSLOTS
@@ -913,6 +915,18 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   }, 1);
   // static camera-major copy of the entries' observation inputs (matrix-free camera passes)
   big_vec<int4> cm_idx(NE);
+  // the runs of each chunk as records {first position, length, point, camera} in position
+  // order (k_mf_diag_rhs: its loads need no dependent index load; run_beg[nchunk + 1])
+  std::vector<int> run_beg(h->nchunk + 1, 0);
+  par_for(h->nchunk, [&](long long b, long long e, int) {
+    for (int c = (int)b; c < (int)e; ++c) {
+      int n = 0;
+      for (int i = chunk_beg[c]; i < chunk_beg[c + 1]; ++i) n += run[i] > 0;
+      run_beg[c + 1] = n;
+    }
+  }, 64);
+  for (int c = 0; c < h->nchunk; ++c) run_beg[c + 1] += run_beg[c];
+  big_vec<int4> run_rec(std::max(1, run_beg[h->nchunk]));
   big_vec<double2> cm_xy(NE);
   par_for(NE, [&](long long b, long long en, int) {
     for (long long i = b; i < en; ++i) {
@@ -923,6 +937,14 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
       cm_xy[i] = obs_xy[s2];
     }
   });
+  par_for(NC, [&](long long b, long long e, int) {
+    for (int c = (int)b; c < (int)e; ++c)
+      for (int q = seg_chunk[c]; q < seg_chunk[c + 1]; ++q) {
+        int k = run_beg[q];
+        for (int i = chunk_beg[q]; i < chunk_beg[q + 1]; ++i)
+          if (run[i] > 0) run_rec[k++] = make_int4(i, run[i], cm_pt[i], c);
+      }
+  }, 1);
   // chunks whose entries all see one camera through one intrinsic (single-extrinsic
   // observations): the camera passes read that camera's tables once per block
   std::vector<int2> chunk_uni(h->nchunk, make_int2(-1, -1));
@@ -1142,6 +1164,8 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   CHECK_RC(upload(&h->d_cross_cam, d, cross_cam, s));
   CHECK_RC(upload(&h->d_xptr, d, xptr, s));
   CHECK_RC(upload(&h->d_run, d, run, s));
+  CHECK_RC(upload(&h->d_run_beg, d, run_beg, s));
+  CHECK_RC(upload(&h->d_run_rec, d, run_rec, s));
   CHECK_RC(upload(&h->d_xlist, d, xlist, s));
   if (h->pair_eval) {
     if (!cm2_idx.empty()) {
@@ -1663,7 +1687,7 @@ static int pcg_solve(dab_handle* h, const dab_options& opt, StepScalars sc, YBuf
   const int NC = h->NC;
   const bool direct = h->nchunk == h->NC;
   if (h->mf)
-    launch_mf_diag_rhs(s, v, h->nchunk, h->d_chunk_beg, h->d_run, h->d_points, h->d_camtab, h->d_scale_c, h->d_L,
+    launch_mf_diag_rhs(s, v, h->nchunk, h->d_run_beg, h->d_run_rec, h->d_points, h->d_camtab, h->d_scale_c, h->d_L,
                        h->d_q, direct ? h->d_pcg_red : h->d_partial);
   else
     launch_pcg_diag_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_run, yb, h->d_q,
