@@ -53,6 +53,8 @@ struct CholCtx {
   int bulk_kc = 16;         // DAB_CHOL_BULK_KC: K chunk of the bulk update (16 | 32)
   int bulk_occ = 4;         // DAB_CHOL_BULK_OCC: waves per SIMD the bulk update is compiled for (2 | 4)
   unsigned* bar = nullptr;  // grid-barrier counter of k_trsv_back_all (zeroed per solve)
+  unsigned* ready = nullptr;  // per block: y_b published (k_trsv_back_flow; zeroed per solve)
+  bool back_flow = true;      // DAB_CHOL_BACK_FLOW=0: the grid-barrier back substitution
   bool v1 = false;          // DAB_CHOL_V1=1: the per-step schedule (one bulk update per panel, one
                             // back-substitution launch per block)
 };
@@ -72,6 +74,7 @@ CholCtx* chol_create() {
   c->ncu = ncu;
   if (const char* e = getenv("DAB_CHOL_BULK_GRID")) c->bulk_grid = atoi(e);
   if (const char* e = getenv("DAB_CHOL_V1")) c->v1 = atoi(e) != 0;
+  if (const char* e = getenv("DAB_CHOL_BACK_FLOW")) c->back_flow = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_BULK_PAD")) c->bulk_pad = (size_t)atoi(e) * 1024;
   if (const char* e = getenv("DAB_CHOL_BULK_KC")) c->bulk_kc = atoi(e);
   if (const char* e = getenv("DAB_CHOL_BULK_OCC")) c->bulk_occ = atoi(e);
@@ -86,6 +89,7 @@ void chol_destroy(CholCtx* c) {
   if (c->exec) (void)hipGraphExecDestroy(c->exec);
   if (c->blk) (void)hipFree(c->blk);
   if (c->bar) (void)hipFree(c->bar);
+  if (c->ready) (void)hipFree(c->ready);
   for (hipEvent_t e : c->ev_panel) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_bulk) (void)hipEventDestroy(e);
   if (c->side) (void)hipStreamDestroy(c->side);
@@ -682,6 +686,147 @@ __global__ __launch_bounds__(kThreads) void k_trsv_back_all(const double* __rest
   }
 }
 
+// Back substitution L^T y = z as a dataflow over the blocks (no grid barrier): work-group
+// w owns the blocks s = w, w + G, ... and keeps their z_s in LDS. For b = last .. 1 it
+// waits for y_b (published by b's owner: agent-scope stores, then ready[b]), subtracts
+// L_bs^T y_b from each owned z_s with s < b, and when it owns b - 1 — whose z is then
+// final — solves y_{b-1} = L^-T z from the stored 16x16 inverses and publishes it. Only
+// that owner is on the critical path per block; everyone else consumes y_b in parallel.
+// The A block of the critical owned column is loaded before the wait. Waits are bounded
+// (flag |= 2 and the work-group ends). Every work-group must be resident (G <= CUs).
+constexpr int kMaxOwned = 4;
+__global__ __launch_bounds__(kThreads) void k_trsv_back_flow(const double* __restrict__ A, int lda, int n, int nblk,
+                                                             const double* __restrict__ blk,
+                                                             const double* __restrict__ z, double* __restrict__ y,
+                                                             unsigned* __restrict__ ready, int* __restrict__ flag) {
+  __shared__ double Lk[NB][LS];
+  __shared__ double Dq[4][16][DS];
+  __shared__ double zs[kMaxOwned][NB];
+  __shared__ double yy[NB];
+  __shared__ double tt[16];
+  __shared__ double red[4][64];
+  __shared__ int abort_s;
+  const int tid = threadIdx.x, G = gridDim.x, w = blockIdx.x;
+  const int nown = w < nblk ? (nblk - 1 - w) / G + 1 : 0;  // owned: s_j = w + G j
+  if (tid == 0) abort_s = 0;
+  for (int j = 0; j < nown; ++j) {
+    const int k = (w + G * j) * NB, kb = min(NB, n - k);
+    if (tid < NB) zs[j][tid] = tid < kb ? z[k + tid] : 0.0;
+  }
+  auto load_tabs = [&](int sb) {  // L_bb and the inverses of block sb
+    const double* bk = blk + (size_t)sb * kBlk;
+#pragma unroll
+    for (int q = 0; q < NB * NB / kThreads; ++q) {
+      const int idx = tid + q * kThreads, i = idx >> 6, jj = idx & 63;
+      Lk[i][jj] = bk[1024 + idx];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = tid + q * kThreads;
+      Dq[idx >> 8][(idx >> 4) & 15][idx & 15] = bk[idx];
+    }
+  };
+  // y_sb = L_bb^-T zs[j] by 16-blocks (as k_trsv_back_all), then publish
+  auto solve_publish = [&](int j) {
+    const int sb = w + G * j, k = sb * NB, kb = min(NB, n - k);
+    if (tid < NB) yy[tid] = zs[j][tid];
+    __syncthreads();
+    const int c = tid & 15, part = tid >> 4;
+#pragma unroll
+    for (int q = 3; q >= 0; --q) {
+      double acc = 0.0;
+      for (int r = 16 * (q + 1) + part; r < NB; r += 16) acc = fma(-Lk[r][16 * q + c], yy[r], acc);
+      red[part >> 2][(part & 3) * 16 + c] = acc;
+      __syncthreads();
+      if (tid < 16) {
+        double t = yy[16 * q + c];
+#pragma unroll
+        for (int p2 = 0; p2 < 16; ++p2) t += red[p2 >> 2][(p2 & 3) * 16 + c];
+        tt[c] = t;
+      }
+      __syncthreads();
+      red[part >> 2][(part & 3) * 16 + c] = part >= c ? Dq[q][part][c] * tt[part] : 0.0;
+      __syncthreads();
+      if (tid < 16) {
+        double sacc = 0.0;
+#pragma unroll
+        for (int p2 = 0; p2 < 16; ++p2) sacc += red[p2 >> 2][(p2 & 3) * 16 + c];
+        yy[16 * q + c] = sacc;
+      }
+      __syncthreads();
+    }
+    if (tid < 64) {  // wave 0: the stores, drained, then the flag
+      if (tid < kb) __hip_atomic_store(y + k + tid, yy[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (tid == 0) __hip_atomic_store(ready + sb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+  };
+  if (nown == 0) return;
+  int jn = nown - 1;  // the next owned block to solve (largest s first)
+  load_tabs(w + G * jn);
+  __syncthreads();
+  if (w + G * jn == nblk - 1) {
+    solve_publish(jn);
+    --jn;
+    if (jn >= 0) load_tabs(w + G * jn);
+  }
+  const int i = tid & 63, part = tid >> 6;
+  for (int b = nblk - 1; b >= 1 && jn >= 0; --b) {
+    // owned blocks below b: j = 0 .. jmax (s_j < b)
+    const int jmax = min(nown - 1, (b - 1 - w) / G);
+    if (b - 1 < w) break;
+    const int kbk = b * NB, kbb = min(NB, n - kbk);
+    // the critical owned column (the largest s < b) is loaded before the wait
+    double pa[NB / 4];
+    {
+      const int col = (w + G * jmax) * NB + i;
+#pragma unroll
+      for (int q = 0; q < NB / 4; ++q) {
+        const int mm = part * (NB / 4) + q;
+        pa[q] = (mm < kbb && col < n) ? A[(size_t)(kbk + mm) * lda + col] : 0.0;
+      }
+    }
+    if (tid == 0) {
+      int spins = 0;
+      while (__hip_atomic_load(ready + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1 << 22)) {
+          abort_s = 1;
+          atomicOr(flag, 2);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (abort_s) return;
+    if (tid < NB) yy[tid] = tid < kbb ? __hip_atomic_load(y + kbk + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    __syncthreads();
+    for (int j = jmax; j >= 0; --j) {
+      const int col = (w + G * j) * NB + i;
+      double sacc = 0.0;
+#pragma unroll
+      for (int q = 0; q < NB / 4; ++q) {
+        const int mm = part * (NB / 4) + q;
+        const double a = j == jmax ? pa[q] : ((mm < kbb && col < n) ? A[(size_t)(kbk + mm) * lda + col] : 0.0);
+        sacc = fma(a, yy[mm], sacc);
+      }
+      red[part][i] = sacc;
+      __syncthreads();
+      if (part == 0) zs[j][i] -= ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+      __syncthreads();
+    }
+    if (jmax == jn && w + G * jn == b - 1) {  // z_{b-1} is final
+      solve_publish(jn);
+      --jn;
+      if (jn >= 0) {
+        load_tabs(w + G * jn);
+        __syncthreads();
+      }
+    }
+  }
+}
+
 static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y,
                                  int* d_flag);
 
@@ -693,7 +838,10 @@ int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
     c->exec = nullptr;
     if (c->blk) (void)hipFree(c->blk);
     c->blk = nullptr;
+    if (c->ready) (void)hipFree(c->ready);
+    c->ready = nullptr;
     if (hipMalloc(&c->blk, sizeof(double) * kBlk * (size_t)nblk) != hipSuccess) return -2;
+    if (hipMalloc(&c->ready, sizeof(unsigned) * (size_t)nblk) != hipSuccess) return -2;
     c->nblk_alloc = nblk;
   }
   if (!c->side && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) return -3;
@@ -790,8 +938,13 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
   }
   if (pending >= 0) (void)hipStreamWaitEvent(s, c->ev_bulk[pending], 0);
   double* z = A + (size_t)n * lda;
-  (void)hipMemsetAsync(c->bar, 0, sizeof(unsigned), s);
   const int G = std::max(1, std::min(c->ncu / 2, (n + 63) / 64));
+  if (c->back_flow && nblk <= G * kMaxOwned) {
+    (void)hipMemsetAsync(c->ready, 0, sizeof(unsigned) * (size_t)nblk, s);
+    k_trsv_back_flow<<<G, kThreads, 0, s>>>(A, lda, n, nblk, c->blk, z, y, c->ready, d_flag);
+    return;
+  }
+  (void)hipMemsetAsync(c->bar, 0, sizeof(unsigned), s);
   k_trsv_back_all<<<G, kThreads, 0, s>>>(A, lda, n, nblk, c->blk, z, y, c->bar, d_flag);
 }
 
