@@ -700,10 +700,10 @@ __global__ __launch_bounds__(kThreads) void k_trsv_back_flow(const double* __res
                                                              const double* __restrict__ z, double* __restrict__ y,
                                                              unsigned* __restrict__ ready, int* __restrict__ flag) {
   __shared__ double Lk[NB][LS];
+  __shared__ double Li[NB][LS];  // L_bb^-1 of the next owned block (built off the critical path)
   __shared__ double Dq[4][16][DS];
   __shared__ double zs[kMaxOwned][NB];
   __shared__ double yy[NB];
-  __shared__ double tt[16];
   __shared__ double red[4][64];
   __shared__ int abort_s;
   const int tid = threadIdx.x, G = gridDim.x, w = blockIdx.x;
@@ -713,48 +713,74 @@ __global__ __launch_bounds__(kThreads) void k_trsv_back_flow(const double* __res
     const int k = (w + G * j) * NB, kb = min(NB, n - k);
     if (tid < NB) zs[j][tid] = tid < kb ? z[k + tid] : 0.0;
   }
-  auto load_tabs = [&](int sb) {  // L_bb and the inverses of block sb
+  // L_bb^-1 of block sb from L_bb and the inverses D_q of its 16x16 diagonal blocks, by
+  // 16-block rows: Li_qq = D_q, Li_pq = -D_p sum_{q <= r < p} L_pr Li_rq (ends with a barrier)
+  auto load_tabs = [&](int sb) {
     const double* bk = blk + (size_t)sb * kBlk;
 #pragma unroll
     for (int q = 0; q < NB * NB / kThreads; ++q) {
       const int idx = tid + q * kThreads, i = idx >> 6, jj = idx & 63;
       Lk[i][jj] = bk[1024 + idx];
+      Li[i][jj] = 0.0;
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int idx = tid + q * kThreads;
       Dq[idx >> 8][(idx >> 4) & 15][idx & 15] = bk[idx];
     }
-  };
-  // y_sb = L_bb^-T zs[j] by 16-blocks (as k_trsv_back_all), then publish
-  auto solve_publish = [&](int j) {
-    const int sb = w + G * j, k = sb * NB, kb = min(NB, n - k);
-    if (tid < NB) yy[tid] = zs[j][tid];
     __syncthreads();
-    const int c = tid & 15, part = tid >> 4;
 #pragma unroll
-    for (int q = 3; q >= 0; --q) {
-      double acc = 0.0;
-      for (int r = 16 * (q + 1) + part; r < NB; r += 16) acc = fma(-Lk[r][16 * q + c], yy[r], acc);
-      red[part >> 2][(part & 3) * 16 + c] = acc;
-      __syncthreads();
-      if (tid < 16) {
-        double t = yy[16 * q + c];
+    for (int q = 0; q < 4; ++q) {
+      const int idx = tid + q * kThreads, qq = idx >> 8, i = (idx >> 4) & 15, jj = idx & 15;
+      Li[16 * qq + i][16 * qq + jj] = i >= jj ? Dq[qq][i][jj] : 0.0;  // lower part only
+    }
+    __syncthreads();
+    for (int p = 1; p < 4; ++p) {
+      // T = sum_r L_pr Li_rq for the p blocks q < p (16 x 16 each): 256 threads over (q, i, j)
+      double T[3];
 #pragma unroll
-        for (int p2 = 0; p2 < 16; ++p2) t += red[p2 >> 2][(p2 & 3) * 16 + c];
-        tt[c] = t;
+      for (int u = 0; u < 3; ++u) {
+        const int idx = tid + u * kThreads, q = idx >> 8, i = (idx >> 4) & 15, jj = idx & 15;
+        double t = 0.0;
+        if (q < p)
+          for (int m = 16 * q; m < 16 * p; ++m) t = fma(Lk[16 * p + i][m], Li[m][16 * q + jj], t);
+        T[u] = t;
       }
       __syncthreads();
-      red[part >> 2][(part & 3) * 16 + c] = part >= c ? Dq[q][part][c] * tt[part] : 0.0;
-      __syncthreads();
-      if (tid < 16) {
-        double sacc = 0.0;
 #pragma unroll
-        for (int p2 = 0; p2 < 16; ++p2) sacc += red[p2 >> 2][(p2 & 3) * 16 + c];
-        yy[16 * q + c] = sacc;
+      for (int u = 0; u < 3; ++u) {  // park T in the (still zero) block Li_pq
+        const int idx = tid + u * kThreads, q = idx >> 8, i = (idx >> 4) & 15, jj = idx & 15;
+        if (q < p) Li[16 * p + i][16 * q + jj] = T[u];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int idx = tid + u * kThreads, q = idx >> 8, i = (idx >> 4) & 15, jj = idx & 15;
+        double t = 0.0;
+        if (q < p)
+          for (int m = 0; m <= i; ++m) t = fma(Dq[p][i][m], Li[16 * p + m][16 * q + jj], t);
+        T[u] = -t;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int idx = tid + u * kThreads, q = idx >> 8, i = (idx >> 4) & 15, jj = idx & 15;
+        if (q < p) Li[16 * p + i][16 * q + jj] = T[u];
       }
       __syncthreads();
     }
+  };
+  // y_sb = (L_bb^-1)^T zs[j] (4 lanes per row, fixed-order sum), then publish
+  auto solve_publish = [&](int j) {
+    const int sb = w + G * j, k = sb * NB, kb = min(NB, n - k);
+    {
+      const int i = tid & 63, part = tid >> 6;
+      double acc = 0.0;
+      for (int m = i + part; m < NB; m += 4) acc = fma(Li[m][i], zs[j][m], acc);
+      red[part][i] = acc;
+    }
+    __syncthreads();
+    if (tid < NB) yy[tid] = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
     if (tid < 64) {  // wave 0: the stores, drained, then the flag
       if (tid < kb) __hip_atomic_store(y + k + tid, yy[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -765,7 +791,6 @@ __global__ __launch_bounds__(kThreads) void k_trsv_back_flow(const double* __res
   if (nown == 0) return;
   int jn = nown - 1;  // the next owned block to solve (largest s first)
   load_tabs(w + G * jn);
-  __syncthreads();
   if (w + G * jn == nblk - 1) {
     solve_publish(jn);
     --jn;
@@ -819,10 +844,7 @@ __global__ __launch_bounds__(kThreads) void k_trsv_back_flow(const double* __res
     if (jmax == jn && w + G * jn == b - 1) {  // z_{b-1} is final
       solve_publish(jn);
       --jn;
-      if (jn >= 0) {
-        load_tabs(w + G * jn);
-        __syncthreads();
-      }
+      if (jn >= 0) load_tabs(w + G * jn);
     }
   }
 }
