@@ -55,6 +55,9 @@ struct CholCtx {
   unsigned* bar = nullptr;  // grid-barrier counter of k_trsv_back_all (zeroed per solve)
   unsigned* ready = nullptr;  // per block: y_b published (k_trsv_back_flow; zeroed per solve)
   bool back_flow = true;      // DAB_CHOL_BACK_FLOW=0: the grid-barrier back substitution
+  bool prefactor = true;      // DAB_CHOL_PREFACTOR=0: every panel work-group factors the diagonal block
+  bool fuse_panel = true;     // DAB_CHOL_FUSE_PANEL=0: the panel step as its own launch after the column update
+  unsigned* pready = nullptr; // per block: L_kk published by the fused column update (zeroed per factorisation)
   bool v1 = false;          // DAB_CHOL_V1=1: the per-step schedule (one bulk update per panel, one
                             // back-substitution launch per block)
 };
@@ -75,6 +78,8 @@ CholCtx* chol_create() {
   if (const char* e = getenv("DAB_CHOL_BULK_GRID")) c->bulk_grid = atoi(e);
   if (const char* e = getenv("DAB_CHOL_V1")) c->v1 = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_BACK_FLOW")) c->back_flow = atoi(e) != 0;
+  if (const char* e = getenv("DAB_CHOL_PREFACTOR")) c->prefactor = atoi(e) != 0;
+  if (const char* e = getenv("DAB_CHOL_FUSE_PANEL")) c->fuse_panel = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_BULK_PAD")) c->bulk_pad = (size_t)atoi(e) * 1024;
   if (const char* e = getenv("DAB_CHOL_BULK_KC")) c->bulk_kc = atoi(e);
   if (const char* e = getenv("DAB_CHOL_BULK_OCC")) c->bulk_occ = atoi(e);
@@ -90,6 +95,7 @@ void chol_destroy(CholCtx* c) {
   if (c->blk) (void)hipFree(c->blk);
   if (c->bar) (void)hipFree(c->bar);
   if (c->ready) (void)hipFree(c->ready);
+  if (c->pready) (void)hipFree(c->pready);
   for (hipEvent_t e : c->ev_panel) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_bulk) (void)hipEventDestroy(e);
   if (c->side) (void)hipStreamDestroy(c->side);
@@ -242,8 +248,11 @@ __device__ __forceinline__ void factor64(double (*L)[LS], double (*D)[16][DS], b
 
 // panel rows [r0, r1) (64 per work-group): P <- P L_kk^-T ; work-group 0 stores D and L_kk
 // to the block scratch
+// pre: the diagonal block was factored by the column update in front (k_syrk_mfma with
+// fblk), so L_kk and the inverses are read from the block scratch instead
 __global__ __launch_bounds__(kThreads) void k_panel(double* __restrict__ A, int lda, int k, int kb, int r0,
-                                                    int r1, double* __restrict__ blk, int* __restrict__ flag) {
+                                                    int r1, double* __restrict__ blk, int* __restrict__ flag,
+                                                    int pre) {
   __shared__ double L[NB][LS];
   __shared__ double P[NB][LS];
   __shared__ double D[4][16][DS];
@@ -252,8 +261,24 @@ __global__ __launch_bounds__(kThreads) void k_panel(double* __restrict__ A, int 
   if (g_chol_prio) __builtin_amdgcn_s_setprio(3);
   const int tid = threadIdx.x, w = tid >> 6;
   const int row0 = r0 + NB * blockIdx.x;
+  if (pre) {
+    if (row0 >= r1) return;
+#pragma unroll
+    for (int q = 0; q < NB * NB / kThreads; ++q) {
+      const int idx = tid + q * kThreads, i = idx >> 6, j = idx & 63;
+      L[i][j] = blk[1024 + idx];
+      P[i][j] = (row0 + i < r1 && j < kb) ? A[(size_t)(row0 + i) * lda + k + j] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = tid + q * kThreads;
+      D[idx >> 8][(idx >> 4) & 15][idx & 15] = blk[idx];
+    }
+    __syncthreads();
+  }
 #pragma unroll
   for (int q = 0; q < NB * NB / kThreads; ++q) {
+    if (pre) break;
     const int idx = tid + q * kThreads, i = idx >> 6, j = idx & 63;
     double v = (i == j) ? 1.0 : 0.0;
     if (i < kb && j <= i) v = A[(size_t)(k + i) * lda + k + j];
@@ -261,11 +286,11 @@ __global__ __launch_bounds__(kThreads) void k_panel(double* __restrict__ A, int 
     P[i][j] = (row0 + i < r1 && j < kb) ? A[(size_t)(row0 + i) * lda + k + j] : 0.0;
   }
   PROF_MARK(0);
-  __syncthreads();
+  if (!pre) __syncthreads();
   PROF_MARK(1);
   bool bad = false;
-  factor64(L, D, bad);
-  if (blockIdx.x == 0) {
+  if (!pre) factor64(L, D, bad);
+  if (blockIdx.x == 0 && !pre) {
     // L_kk goes to the scratch, not back into A: the other work-groups of this launch
     // may not have read the original diagonal block yet
     if (tid == 0 && bad) atomicOr(flag, 1);
@@ -312,10 +337,22 @@ __global__ __launch_bounds__(kThreads) void k_panel(double* __restrict__ A, int 
 // every CU room for the panel chain's work-groups), each work-group loops over its tiles.
 // The update has rank kk: panel columns [k, k + kk) in chunks of NB (kk = kb of one panel,
 // or two panels' 128 for the column after a panel pair).
+// fblk (col_only): the work-group of the diagonal tile then factors it (factor64, the first
+// kb_next rows; identity below) and stores L_kk and the 16x16 inverses there, so that the
+// next panel (k_panel pre) reads them instead of every work-group factoring the block.
+// ready (with fblk): the panel step is fused in as well — the diagonal work-group publishes
+// L_kk and the inverses (agent-scope stores, then ready = 1) and every other work-group
+// keeps its updated tile, which is its 64 panel rows, waits for ready (bounded: flag |= 2)
+// and solves the rows P <- P L_kk^-T (as k_panel), so the chain loses a launch per block.
 __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, int lda, int r0, int m, int k0,
-                                                        int kk, int col_only, int ntiles) {
+                                                        int kk, int col_only, int ntiles,
+                                                        double* __restrict__ fblk = nullptr, int kb_next = 0,
+                                                        int* __restrict__ flag = nullptr,
+                                                        unsigned* __restrict__ ready = nullptr) {
   __shared__ double Pa[NB * LDP];
   __shared__ double Pb[NB * LDP];
+  __shared__ double Dsh[4][16][DS];
+  __shared__ int abort_s;
   if (col_only && g_chol_prio) __builtin_amdgcn_s_setprio(3);  // on the panel chain
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
   if (t != (int)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
@@ -395,6 +432,107 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
         const int col = bj * NB + wc * 32 + b2 * 16 + li;
         if (!skip && row < m && col < m) A[(size_t)(r0 + row) * lda + r0 + col] = acc[a2][b2][reg];
       }
+  if (fblk && col_only && bi == 0) {
+    // Pb is free on a diagonal tile: it holds L [NB][LS]
+    double (*L)[LS] = reinterpret_cast<double (*)[LS]>(Pb);
+    double (*D)[16][DS] = Dsh;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NB * NB / kThreads; ++q) {
+      const int idx = tid + q * kThreads, i = idx >> 6, j = idx & 63;
+      L[i][j] = (i == j) ? 1.0 : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+      for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int i = wr * 32 + a2 * 16 + lk + 4 * reg, j = wc * 32 + b2 * 16 + li;
+          if (!skip && i < kb_next && j <= i) L[i][j] = acc[a2][b2][reg];
+        }
+    __syncthreads();
+    bool bad = false;
+    factor64(L, D, bad);
+    if (tid == 0 && bad) atomicOr(flag, 1);
+#pragma unroll
+    for (int q = 0; q < NB * NB / kThreads; ++q) {
+      const int idx = tid + q * kThreads, i = idx >> 6, j = idx & 63;
+      __hip_atomic_store(fblk + 1024 + idx, (j <= i) ? L[i][j] : 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = tid + q * kThreads;  // [4][16][16]
+      __hip_atomic_store(fblk + idx, D[idx >> 8][(idx >> 4) & 15][idx & 15], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (ready) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else if (ready && col_only) {
+    // the fused panel step on this tile's rows
+    double (*P)[LS] = reinterpret_cast<double (*)[LS]>(Pb);
+    double (*L)[LS] = reinterpret_cast<double (*)[LS]>(Pa);
+    __syncthreads();  // the MFMA loop's LDS reads are done
+#pragma unroll
+    for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+      for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int i = wr * 32 + a2 * 16 + lk + 4 * reg, j = wc * 32 + b2 * 16 + li;
+          P[i][j] = j < kb_next ? acc[a2][b2][reg] : 0.0;
+        }
+    if (tid == 0) {
+      abort_s = 0;
+      int spins = 0;
+      while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1 << 22)) {
+          abort_s = 1;
+          atomicOr(flag, 2);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (abort_s) return;
+#pragma unroll
+    for (int q = 0; q < NB * NB / kThreads; ++q) {
+      const int idx = tid + q * kThreads, i = idx >> 6, j = idx & 63;
+      L[i][j] = __hip_atomic_load(fblk + 1024 + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = tid + q * kThreads;
+      Dsh[idx >> 8][(idx >> 4) & 15][idx & 15] = __hip_atomic_load(fblk + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    double* Pf = &P[0][0];
+    const double* Lf = &L[0][0];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // wave w: rows [16 w, 16 w + 16), as k_panel
+      dbl4 t = tile_load<LS>(Pf, 16 * w, 16 * q);
+      if (q > 0) mma_nt<LS, LS>(16 * q, t, Pf, 16 * w, 0, Lf, 16 * q, 0, -1.0);
+      __builtin_amdgcn_wave_barrier();
+      tile_store<LS>(Pf, 16 * w, 16 * q, t);
+      __builtin_amdgcn_wave_barrier();
+      dbl4 x = {0.0, 0.0, 0.0, 0.0};
+      mma_nt<LS, DS>(16, x, Pf, 16 * w, 16 * q, &Dsh[q][0][0], 0, 0, 1.0);
+      __builtin_amdgcn_wave_barrier();
+      tile_store<LS>(Pf, 16 * w, 16 * q, x);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NB * NB / kThreads; ++q) {
+      const int idx = tid + q * kThreads, i = idx >> 6, j = idx & 63;
+      const int row = bi * NB + i;
+      if (row < m && j < kb_next) A[(size_t)(r0 + row) * lda + r0 + j] = P[i][j];
+    }
+  }
   }
 }
 
@@ -862,8 +1000,11 @@ int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
     c->blk = nullptr;
     if (c->ready) (void)hipFree(c->ready);
     c->ready = nullptr;
+    if (c->pready) (void)hipFree(c->pready);
+    c->pready = nullptr;
     if (hipMalloc(&c->blk, sizeof(double) * kBlk * (size_t)nblk) != hipSuccess) return -2;
     if (hipMalloc(&c->ready, sizeof(unsigned) * (size_t)nblk) != hipSuccess) return -2;
+    if (hipMalloc(&c->pready, sizeof(unsigned) * (size_t)nblk) != hipSuccess) return -2;
     c->nblk_alloc = nblk;
   }
   if (!c->side && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) return -3;
@@ -918,18 +1059,26 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
   const int nblk = (n + NB - 1) / NB;
   hipStream_t s2 = getenv("DAB_CHOL_SERIAL") ? s : c->side;  // serial: debugging aid
   auto kb_of = [&](int b) { return std::min(NB, n - b * NB); };
+  // every panel after the first follows the column update of its block, which factors the
+  // diagonal block (DAB_CHOL_PREFACTOR=0: each panel work-group factors it itself)
+  const bool pre = c->prefactor, fuse = pre && c->fuse_panel;
+  if (fuse) (void)hipMemsetAsync(c->pready, 0, sizeof(unsigned) * (size_t)nblk, s);
   auto panel = [&](int b) {
+    // done inside the column update in front, except for a last block shorter than NB,
+    // whose rows below (the rhs row) sit in the diagonal tile
+    if (fuse && b > 0 && kb_of(b) == NB) return;
     const int k = b * NB, kb = kb_of(b);
     const int r0 = k + kb, r1 = n + 1;  // includes the rhs row n
     const int grid = std::max(1, (r1 - r0 + NB - 1) / NB);
-    k_panel<<<grid, kThreads, 0, s>>>(A, lda, k, kb, r0, r1, c->blk + (size_t)b * kBlk, d_flag);
+    k_panel<<<grid, kThreads, 0, s>>>(A, lda, k, kb, r0, r1, c->blk + (size_t)b * kBlk, d_flag, pre && b > 0);
   };
   // column block cb (rows >= its first row, through the rhs row) with panel columns [k, k + kk)
   auto col = [&](int cb, int k, int kk) {
     const int r0 = cb * NB, m = n + 1 - r0;
     if (m <= 1) return;
     const int nt = (m + NB - 1) / NB;
-    k_syrk_mfma<<<nt, kThreads, 0, s>>>(A, lda, r0, m, k, kk, 1, nt);
+    k_syrk_mfma<<<nt, kThreads, 0, s>>>(A, lda, r0, m, k, kk, 1, nt, pre ? c->blk + (size_t)cb * kBlk : nullptr,
+                                        kb_of(cb), d_flag, fuse ? c->pready + cb : nullptr);
   };
   panel(0);
   int pending = -1;  // pair whose bulk update is still running on s2
@@ -981,7 +1130,7 @@ static void enqueue_factor_solve_v1(CholCtx* c, hipStream_t s, int n, double* A,
     const int k = b * NB, kb = (n - k < NB) ? n - k : NB;
     const int r0 = k + kb, r1 = n + 1;  // includes the rhs row n
     const int grid = std::max(1, (r1 - r0 + NB - 1) / NB);
-    k_panel<<<grid, kThreads, 0, s>>>(A, lda, k, kb, r0, r1, c->blk + (size_t)b * kBlk, d_flag);
+    k_panel<<<grid, kThreads, 0, s>>>(A, lda, k, kb, r0, r1, c->blk + (size_t)b * kBlk, d_flag, 0);
   };
   panel(0);
   bool bulk_prev = false;

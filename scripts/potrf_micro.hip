@@ -55,7 +55,7 @@ int main() {
   (void)hipMemset(flag, 0, 4);
   hipStream_t s;
   (void)hipStreamCreate(&s);
-  k_panel<<<1, kThreads, 0, s>>>(A, lda, 0, 64, 64, 65, blk, flag);
+  k_panel<<<1, kThreads, 0, s>>>(A, lda, 0, 64, 64, 65, blk, flag, 0);
   (void)hipStreamSynchronize(s);
   std::vector<double> hb(kBlk), ha(h.size());
   (void)hipMemcpy(hb.data(), blk, kBlk * 8, hipMemcpyDeviceToHost);
@@ -83,8 +83,8 @@ int main() {
       (void)hipEventRecord(e0, s);
       for (int it = 0; it < 100; ++it) {
         if (var == 0) k_empty<<<1, 64, 0, s>>>();
-        if (var == 1) k_panel<<<1, kThreads, 0, s>>>(A, lda, 0, 64, 64, 65, blk, flag);
-        if (var == 2) k_panel<<<94, kThreads, 0, s>>>(Big, 6008, 0, 64, 64, 6000, blk, flag);
+        if (var == 1) k_panel<<<1, kThreads, 0, s>>>(A, lda, 0, 64, 64, 65, blk, flag, 0);
+        if (var == 2) k_panel<<<94, kThreads, 0, s>>>(Big, 6008, 0, 64, 64, 6000, blk, flag, 0);
       }
       (void)hipEventRecord(e1, s);
       (void)hipEventSynchronize(e1);
