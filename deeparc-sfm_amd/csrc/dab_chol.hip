@@ -56,6 +56,8 @@ struct CholCtx {
   unsigned* ready = nullptr;  // per block: y_b published (k_trsv_back_flow; zeroed per solve)
   bool back_flow = true;      // DAB_CHOL_BACK_FLOW=0: the grid-barrier back substitution
   bool prefactor = true;      // DAB_CHOL_PREFACTOR=0: every panel work-group factors the diagonal block
+  bool nograph = false;       // DAB_CHOL_NOGRAPH=1: launch directly instead of the captured graph (traces)
+  bool serial = false;        // DAB_CHOL_SERIAL=1: the bulk updates on the chain stream (debugging)
   bool fuse_panel = true;     // DAB_CHOL_FUSE_PANEL=0: the panel step as its own launch after the column update
   unsigned* pready = nullptr; // per block: L_kk published by the fused column update (zeroed per factorisation)
   bool v1 = false;          // DAB_CHOL_V1=1: the per-step schedule (one bulk update per panel, one
@@ -80,6 +82,8 @@ CholCtx* chol_create() {
   if (const char* e = getenv("DAB_CHOL_BACK_FLOW")) c->back_flow = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_PREFACTOR")) c->prefactor = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_FUSE_PANEL")) c->fuse_panel = atoi(e) != 0;
+  c->nograph = getenv("DAB_CHOL_NOGRAPH") != nullptr;
+  c->serial = getenv("DAB_CHOL_SERIAL") != nullptr;
   if (const char* e = getenv("DAB_CHOL_BULK_PAD")) c->bulk_pad = (size_t)atoi(e) * 1024;
   if (const char* e = getenv("DAB_CHOL_BULK_KC")) c->bulk_kc = atoi(e);
   if (const char* e = getenv("DAB_CHOL_BULK_OCC")) c->bulk_occ = atoi(e);
@@ -1016,7 +1020,7 @@ int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
     c->ev_panel.push_back(a);
     c->ev_bulk.push_back(b);
   }
-  if (getenv("DAB_CHOL_NOGRAPH")) {  // debugging aid: launch directly on the two streams
+  if (c->nograph) {  // debugging aid: launch directly on the two streams
     enqueue_factor_solve(c, s, n, A, lda, y, d_flag);
     return 0;
   }
@@ -1057,7 +1061,7 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
     return;
   }
   const int nblk = (n + NB - 1) / NB;
-  hipStream_t s2 = getenv("DAB_CHOL_SERIAL") ? s : c->side;  // serial: debugging aid
+  hipStream_t s2 = c->serial ? s : c->side;  // serial: debugging aid
   auto kb_of = [&](int b) { return std::min(NB, n - b * NB); };
   // every panel after the first follows the column update of its block, which factors the
   // diagonal block (DAB_CHOL_PREFACTOR=0: each panel work-group factors it itself)
@@ -1125,7 +1129,7 @@ static void enqueue_factor_solve_v1(CholCtx* c, hipStream_t s, int n, double* A,
   // [wait bulk(b-1)] col-update(b) -> P(b+1); bulk stream s2: bulk(b) after P(b). The
   // bulk trailing update of step b overlaps the next panel step.
   const int nblk = (n + NB - 1) / NB;
-  hipStream_t s2 = getenv("DAB_CHOL_SERIAL") ? s : c->side;  // serial: debugging aid
+  hipStream_t s2 = c->serial ? s : c->side;  // serial: debugging aid
   auto panel = [&](int b) {
     const int k = b * NB, kb = (n - k < NB) ? n - k : NB;
     const int r0 = k + kb, r1 = n + 1;  // includes the rhs row n
