@@ -161,11 +161,9 @@ __device__ __noinline__ void factor16(double (*L)[LS], double (*D)[DS], int o, b
     rd[j] = y;  // 1 / L[j][j]
     const double lmj = (r == j) ? d * y : a[j] * y;
     a[j] = lmj;
+    // lanes r < l update entries above the diagonal that are never read: no mask
 #pragma unroll
-    for (int l = j + 1; l < 16; ++l) {
-      const double llj = ROWB(lmj, l);
-      if (r >= l) a[l] -= lmj * llj;
-    }
+    for (int l = j + 1; l < 16; ++l) a[l] = fma(-lmj, ROWB(lmj, l), a[l]);
   }
   // lane c: column c of the inverse, x[i] = (delta_ic - sum_{c<=m<i} L[i][m] x[m]) / L[i][i]
   const int cc = r;
