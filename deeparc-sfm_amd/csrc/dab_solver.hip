@@ -1527,14 +1527,17 @@ static int build_schur_tables(dab_handle* h) {
   }
   if (h->schur_tiles) {
     CHECK_RC(build_schur_tiles(h));
+    t_ph = now_s();
     h->nblk = 0;
     h->npairs = 0;
     CHECK_RC(h->dev.alloc(&h->d_spack, h->spack_count()));  // ybc only
+    phase("tiles: spack alloc");
     const int n = 6 * NC;
     h->lds = ((n + 1 + 7) / 8) * 8;
     if (h->lds % 512 == 0) h->lds += 8;
     CHECK_RC(h->dev.alloc(&h->d_S, (size_t)(n + 1) * h->lds));
     h->mf_grid_n = mf_grid(h->NP, h->ncu);
+    phase("tiles: S alloc");
     h->schur_built = true;
     return 0;
   }
