@@ -4,19 +4,20 @@
 // S is stored row-major, lower triangle, with the right-hand side appended as row n
 // (the augmented matrix [[S, b], [b^T, *]]). Factoring the first n pivots of the
 // augmented matrix leaves L in rows 0..n-1 and z = L^-1 b in row n, so the forward
-// substitution rides along with the factorisation. Blocked right-looking, NB = 64, with a
-// one-block-column lookahead:
-//   k_panel      one launch per block column: every work-group factors the 64x64 diagonal
-//                block (16x16 sub-blocks in registers, rank-16 updates and the panel
-//                solve on fp64 MFMA) and solves its own 64 rows below it with the 16x16
-//                inverses; work-group 0 stores L_kk and the inverses
-//   k_syrk_mfma  trailing update C -= P P^T on lower 64x64 tiles with fp64 MFMA
-//                (v_mfma_f64_16x16x4_f64, 4 waves x 32x32 quadrants, P tiles in LDS), split
-//                into the next block column (on the panel chain) and the bulk (on a second
-//                stream, overlapping the next panel step)
-// Back substitution L^T y = z: one launch per block, y_k = L_kk^-T z_k from the stored
-// 16x16 inverses followed by the block-column update of z[0:k].
-// The whole sequence is captured once into a hipGraph (two streams) and replayed.
+// substitution rides along with the factorisation. Blocked right-looking, NB = 64, panels
+// in pairs (the chain on one stream, the rank-128 bulk update of each pair on a second):
+//   k_panel      the first panel step: every work-group factors the 64x64 diagonal block
+//                (16x16 sub-blocks in registers, rank-16 updates and the panel solve on
+//                fp64 MFMA) and solves its own 64 rows below it with the 16x16 inverses
+//   k_syrk_mfma  the column update in front of each later panel (fp64 MFMA, 4 waves x 32x32
+//                quadrants): its diagonal-tile work-group factors the block and publishes
+//                L_kk and the inverses (ready flag); the other work-groups wait for it and
+//                solve their tile's panel rows, so one launch per block carries the chain
+//   k_syrk_big   the bulk trailing update of a panel pair on 128x128 super-tiles
+//   k_trsv_back_flow  L^T y = z as a dataflow over the blocks (owners keep z in LDS,
+//                per-block ready flags, no grid barrier)
+// The whole sequence is captured once into a hipGraph (two streams) and replayed;
+// DAB_CHOL_V1=1 keeps the round-1 per-step schedule.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
