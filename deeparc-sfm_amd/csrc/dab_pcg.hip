@@ -591,11 +591,11 @@ __global__ __launch_bounds__(kOneWG) void k_pcg_update(int NC, int mode, const d
 // global dot product is finished by the last work-group to arrive (partials stored
 // write-through and drained before one atomic count, read back with atomic loads, summed
 // in work-group order: deterministic, no fences), so the scalar recurrences stay on the
-// device. Three launches per CG iteration:
+// device. Two launches per CG iteration:
 //   k_cg_q      q = S p (Y part w + diagonal + cross terms), pq -> alpha (mode 0/1);
 //               mode 2: r = b - S x
-//   k_cg_xr     x += alpha p, r -= alpha q (mode 0), Q-test, z = M^-1 r, rho -> beta, iter
-//   k_cg_p      p = z + beta p
+//   k_cg_xr     x += alpha p, r -= alpha q (mode 0), Q-test, z = M^-1 r, rho -> beta, iter;
+//               the last work-group then p = z + beta p (z written with agent-scope stores)
 constexpr int kCgBlock = 64;
 
 // sum of v over the grid, valid in the last-arriving work-group (returns true there)
@@ -671,7 +671,7 @@ __global__ __launch_bounds__(kCgBlock) void k_cg_q(int NC, int mode, int L, cons
 
 // mode 0: x, r update + Q-test + direction scalars; 1: x update only; 2: Q-test + direction
 __global__ __launch_bounds__(kCgBlock) void k_cg_xr(int NC, int mode, const double* __restrict__ bvec,
-                                                    const double* __restrict__ p, const double* __restrict__ q,
+                                                    double* __restrict__ p, const double* __restrict__ q,
                                                     double* __restrict__ x, double* __restrict__ r,
                                                     const double* __restrict__ Minv, double* __restrict__ z,
                                                     PcgState* st, double* __restrict__ partial,
@@ -707,7 +707,8 @@ __global__ __launch_bounds__(kCgBlock) void k_cg_xr(int NC, int mode, const doub
         double t = 0.0;
 #pragma unroll
         for (int b = 0; b < 6; ++b) t += mi[6 * a + b] * rc[b];
-        z[6 * c + a] = t;
+        // agent scope: the last-arriving work-group reads every z for p = z + beta p
+        __hip_atomic_store(z + 6 * c + a, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         acc[1] += rc[a] * t;
       }
     }
@@ -715,7 +716,10 @@ __global__ __launch_bounds__(kCgBlock) void k_cg_xr(int NC, int mode, const doub
   if (mode == 1) return;
   double sums[2];
   if (!grid_sum_last<2>(acc, partial, cnt, sums)) return;
+  __shared__ double beta_s;
+  __shared__ int run_s;
   if (threadIdx.x == 63) {
+    run_s = 0;
     const double Q1 = -sums[0];
     const int iter = st->iter;
     int status = kPcgRunning;
@@ -730,17 +734,18 @@ __global__ __launch_bounds__(kCgBlock) void k_cg_xr(int NC, int mode, const doub
       st->pad[0] = beta;
       st->rho = rho;
       st->iter = iter + 1;
+      beta_s = beta;
     }
     st->status = status;
+    run_s = status == kPcgRunning;
   }
+  __syncthreads();
+  // p = z + beta p (k_cg_p) by the last work-group, every z of this launch now written
+  if (run_s)
+    for (int i = threadIdx.x; i < 6 * NC; i += blockDim.x)
+      p[i] = __hip_atomic_load(z + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + beta_s * p[i];
 }
 
-__global__ __launch_bounds__(256) void k_cg_p(int n, const double* __restrict__ z, double* __restrict__ p,
-                                              const PcgState* st) {
-  if (st->status != kPcgRunning) return;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) p[i] = z[i] + st->pad[0] * p[i];
-}
 
 // ---- launchers -------------------------------------------------------------------------
 
@@ -810,8 +815,7 @@ void launch_cg_update(hipStream_t s, int NC, int mode, const double* Ad, const d
     k_cg_q<<<gq, kCgBlock, 0, s>>>(NC, mode, L, Ad, w, xptr, xlist, xcam, X, scale_c, bvec, p, q, x, r, st, partial, cnt);
   else
     k_cg_q<<<gq, kCgBlock, 0, s>>>(NC, 2, L, Ad, w, xptr, xlist, xcam, X, scale_c, bvec, p, q, x, r, st, partial, cnt);
-  k_cg_xr<<<gx, kCgBlock, 0, s>>>(NC, mode, bvec, p, q, x, r, Minv, z, st, partial, cnt);
-  if (mode != 1) k_cg_p<<<(6 * NC + 255) / 256, 256, 0, s>>>(6 * NC, z, p, st);
+  k_cg_xr<<<gx, kCgBlock, 0, s>>>(NC, mode, bvec, p, q, x, r, Minv, z, st, partial, cnt);  // also p = z + beta p
 }
 int cg_partial_size(int NC) { return 2 * ((NC + 3) / 4) + 2 * ((NC + kCgBlock - 1) / kCgBlock); }
 
