@@ -281,7 +281,10 @@ void launch_pcg_matvec_passes(hipStream_t s, const DevView& v, int nchunk, const
 void launch_cg_update(hipStream_t s, int NC, int mode, const double* Ad, const double* w, const int* xptr,
                       const int* xlist, const int2* xcam, const double* X, const double* scale_c,
                       const double* bvec, double* p, double* q, double* x, double* r, PcgState* st,
-                      const double* Minv, double* z, double* partial, unsigned* cnt);
+                      const double* Minv, double* z, double* partial, unsigned* cnt,
+                      const double* wpart = nullptr, int wpart_g = 0);
+// wpart: the matrix-free product's [wpart_g][6 NC] work-group partials, summed inside the
+// update (one work-group per camera when there are cross blocks) instead of into w first
 int cg_partial_size(int NC);
 void launch_pcg_update(hipStream_t s, int NC, int mode, const double* Ad, const double* w, const int* xptr,
                        const int* xlist, const int2* xcam, const double* X, const double* scale_c,
@@ -292,7 +295,8 @@ void launch_pcg_update(hipStream_t s, int NC, int mode, const double* Ad, const 
 // Y_e is never stored: rows are re-evaluated per pass (tables and s_c staged in LDS).
 bool mf_schur_fits(int NC, int E, int NI);
 int mf_grid(int NP, int ncu);
-// Y part of S vec: partial[grid][6 NC] scratch -> w[NC][6] (fixed order)
+// Y part of S vec: partial[grid][6 NC] scratch -> w[NC][6] (fixed order; w = nullptr: the
+// partials are left for launch_cg_update's wpart)
 void launch_mf_product(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                        const double* scale_c, const double* PU, const double* vec, double* partial, double* w,
                        int grid, const PcgState* st);

@@ -4121,14 +4121,14 @@ void launch_mf_product(hipStream_t s, const DevView& v, const double* points, co
     k_mf_frame<0><<<grid, kMfBlock, mf2_lds_bytes(v.E, v.NI, v.NC, true), s>>>(v, points, camtab, scale_c, PU, vec,
                                                                               nullptr, partial, st);
   }
-  launch_pcg_fused_final(s, grid, 6 * v.NC, partial, w, st);
+  if (w) launch_pcg_fused_final(s, grid, 6 * v.NC, partial, w, st);
 }
 void launch_mf_product32(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                          const double* scale_c, const double* PU, const double* vec, double* partial, double* w,
                          int grid, const PcgState* st) {
   k_mf_frame32<<<grid, kMfBlock, mf32_lds_bytes(v.E, v.NI, v.NC), s>>>(v, points, camtab, scale_c, PU, vec, partial,
                                                                       st);
-  launch_pcg_fused_final(s, grid, 6 * v.NC, partial, w, st);
+  if (w) launch_pcg_fused_final(s, grid, 6 * v.NC, partial, w, st);
 }
 void launch_mf_backsub(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                        const double* scale_c, const double* PU, const double* q, const double* yc, double* dp,

@@ -449,8 +449,9 @@ __global__ __launch_bounds__(256) void k_pcg_cam_pass(DevView v, const int* __re
 // diagonal goes to lane 0, and the L partials are combined by a fixed xor tree (every lane
 // of the group ends with the same sum). Cameras with ~60 cross blocks (rig arc cameras) no
 // longer serialise one lane.
+// wc: camera c's 6 values of the Y part (w + 6 c, or a work-group's own sum of the partials)
 __device__ __forceinline__ void apply_cam8(int c, int s, int L, const double* __restrict__ Ad,
-                                           const double* __restrict__ vec, const double* __restrict__ w,
+                                           const double* __restrict__ vec, const double* wc,
                                            const int* __restrict__ xptr, const int* __restrict__ xlist,
                                            const int2* __restrict__ xcam, const double* __restrict__ X,
                                            const double* __restrict__ scc, double (&out)[6]) {
@@ -464,7 +465,7 @@ __device__ __forceinline__ void apply_cam8(int c, int s, int L, const double* __
       for (int b = 0; b < 6; ++b) vc[b] = vec[6 * c + b];
 #pragma unroll
       for (int a = 0; a < 6; ++a) {
-        double t = w[6 * c + a];
+        double t = wc[a];
 #pragma unroll
         for (int b = 0; b < 6; ++b) t += ad[6 * a + b] * vc[b];
         out[a] = t;
@@ -522,7 +523,7 @@ __global__ __launch_bounds__(kOneWG) void k_pcg_update(int NC, int mode, const d
     for (int rr = 0; rr < cam_rounds; ++rr) {
       const int c = rr * cpp + threadIdx.x / L;
       double o[6];
-      apply_cam8(c < NC ? c : -1, s8, L, Ad, p, w, xptr, xlist, xcam, X, scc, o);
+      apply_cam8(c < NC ? c : -1, s8, L, Ad, p, c < NC ? w + 6 * c : nullptr, xptr, xlist, xcam, X, scc, o);
       if (c < NC && s8 == 0) {
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
@@ -555,7 +556,7 @@ __global__ __launch_bounds__(kOneWG) void k_pcg_update(int NC, int mode, const d
     for (int rr = 0; rr < cam_rounds; ++rr) {
       const int c = rr * cpp + threadIdx.x / L;
       double o[6];
-      apply_cam8(c < NC ? c : -1, s8, L, Ad, x, w, xptr, xlist, xcam, X, scc, o);
+      apply_cam8(c < NC ? c : -1, s8, L, Ad, x, c < NC ? w + 6 * c : nullptr, xptr, xlist, xcam, X, scc, o);
       if (c < NC && s8 == 0) {
 #pragma unroll
         for (int a = 0; a < 6; ++a) r[6 * c + a] = bvec[6 * c + a] - o[a];
@@ -635,13 +636,27 @@ __global__ __launch_bounds__(kCgBlock) void k_cg_q(int NC, int mode, int L, cons
                                                    const double* __restrict__ bvec, const double* __restrict__ p,
                                                    double* __restrict__ q, const double* __restrict__ x,
                                                    double* __restrict__ r, PcgState* st, double* __restrict__ partial,
-                                                   unsigned* __restrict__ cnt) {
+                                                   unsigned* __restrict__ cnt, const double* __restrict__ wpart,
+                                                   int G) {
   if (st->status != kPcgRunning) return;
   const int s8 = threadIdx.x & (L - 1);
   const int c0 = blockIdx.x * (kCgBlock / L) + threadIdx.x / L;
   const int c = c0 < NC ? c0 : -1;
+  // wpart (L = 64, one camera per work-group): the product's G work-group partials summed
+  // here in a fixed order instead of by a launch of their own
+  __shared__ double wsh[6];
+  if (wpart) {
+    double a6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    if (c >= 0)
+      for (int g = threadIdx.x; g < G; g += kCgBlock)
+#pragma unroll
+        for (int a = 0; a < 6; ++a) a6[a] += wpart[(size_t)g * 6 * NC + 6 * c + a];
+    wave_sums_transposed<6>(a6, wsh);
+    __syncthreads();
+  }
   double o[6];
-  apply_cam8(c, s8, L, Ad, mode == 2 ? x : p, w, xptr, xlist, xcam, X, scc, o);
+  apply_cam8(c, s8, L, Ad, mode == 2 ? x : p, wpart ? wsh : (c >= 0 ? w + 6 * c : nullptr), xptr, xlist, xcam, X,
+             scc, o);
   double acc[1] = {0.0};
   if (c >= 0 && s8 == 0) {
     if (mode == 2) {
@@ -805,16 +820,19 @@ void launch_pcg_matvec_passes(hipStream_t s, const DevView& v, int nchunk, const
 void launch_cg_update(hipStream_t s, int NC, int mode, const double* Ad, const double* w, const int* xptr,
                       const int* xlist, const int2* xcam, const double* X, const double* scale_c,
                       const double* bvec, double* p, double* q, double* x, double* r, PcgState* st,
-                      const double* Minv, double* z, double* partial, unsigned* cnt) {
+                      const double* Minv, double* z, double* partial, unsigned* cnt, const double* wpart,
+                      int wpart_g) {
   if (NC <= 0) return;
   // with cross blocks a wave per camera: its cross blocks' loads all in flight at once (the
   // rig: 63 per arc camera; 16 lanes per camera walked them in 4 dependent rounds)
   const int L = xptr ? 64 : 1;
   const int gq = (NC + kCgBlock / L - 1) / (kCgBlock / L), gx = (NC + kCgBlock - 1) / kCgBlock;
   if (mode != 2)
-    k_cg_q<<<gq, kCgBlock, 0, s>>>(NC, mode, L, Ad, w, xptr, xlist, xcam, X, scale_c, bvec, p, q, x, r, st, partial, cnt);
+    k_cg_q<<<gq, kCgBlock, 0, s>>>(NC, mode, L, Ad, w, xptr, xlist, xcam, X, scale_c, bvec, p, q, x, r, st, partial, cnt,
+                                   L == 64 ? wpart : nullptr, wpart_g);
   else
-    k_cg_q<<<gq, kCgBlock, 0, s>>>(NC, 2, L, Ad, w, xptr, xlist, xcam, X, scale_c, bvec, p, q, x, r, st, partial, cnt);
+    k_cg_q<<<gq, kCgBlock, 0, s>>>(NC, 2, L, Ad, w, xptr, xlist, xcam, X, scale_c, bvec, p, q, x, r, st, partial, cnt,
+                                   L == 64 ? wpart : nullptr, wpart_g);
   k_cg_xr<<<gx, kCgBlock, 0, s>>>(NC, mode, bvec, p, q, x, r, Minv, z, st, partial, cnt);  // also p = z + beta p
 }
 int cg_partial_size(int NC) { return 2 * ((NC + 3) / 4) + 2 * ((NC + kCgBlock - 1) / kCgBlock); }

@@ -365,6 +365,7 @@ struct dab_handle {
   bool mf32 = false;   // this solve's matrix-free products in fp32 arithmetic (pcg_fp32)
   int mf_grid_n = 0;
   double* d_mf_partial = nullptr;
+  const double* cg_wpart = nullptr;  // set by pcg_matvec: the partials the next CG update sums
   int pcg_hint = 2;    // CG iterations of the previous solve (first batch size)
   double* d_cg_partial = nullptr;  // multi-work-group CG update: grid partials + counter
   unsigned* d_cg_cnt = nullptr;
@@ -1705,13 +1706,18 @@ static int build_pcg_buffers(dab_handle* h) {
 static int pcg_matvec(dab_handle* h, YBufs yb, const double* vec, bool exact = false) {
   hipStream_t s = h->stream;
   if (h->mf) {
+    // one rank with cross blocks (the rig): the product's partials are summed inside the CG
+    // update (no all-reduce in between), one launch fewer per iteration
+    const bool fuse = h->world == 1 && h->nxlist > 0 && h->knobs.cg_onewg == 0;
+    h->cg_wpart = fuse ? h->d_mf_partial : nullptr;
+    double* w = fuse ? nullptr : h->d_pcg_w;
     if (h->mf32 && !exact)
-      launch_mf_product32(s, h->view, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, vec, h->d_mf_partial,
-                          h->d_pcg_w, h->mf_grid_n, h->d_pcg_state);
+      launch_mf_product32(s, h->view, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, vec, h->d_mf_partial, w,
+                          h->mf_grid_n, h->d_pcg_state);
     else
-      launch_mf_product(s, h->view, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, vec, h->d_mf_partial,
-                        h->d_pcg_w, h->mf_grid_n, h->d_pcg_state);
-    CHECK_RC(h->allreduce(h->d_pcg_w, (size_t)6 * h->NC, ncclSum));
+      launch_mf_product(s, h->view, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, vec, h->d_mf_partial, w,
+                        h->mf_grid_n, h->d_pcg_state);
+    if (!fuse) CHECK_RC(h->allreduce(h->d_pcg_w, (size_t)6 * h->NC, ncclSum));
     return 0;
   }
   if (h->fused_grid > 0) {
@@ -1759,7 +1765,7 @@ static int pcg_solve(dab_handle* h, const dab_options& opt, StepScalars sc, YBuf
     else
       launch_cg_update(s, NC, mode, h->d_pcg_Ad, h->d_pcg_w, xptr, h->d_xlist, h->d_cross_cam, h->Ux(),
                        h->d_scale_c, h->d_pcg_b, h->d_pcg_p, h->d_pcg_q, h->d_yc, h->d_pcg_r, h->d_pcg_state,
-                       h->d_pcg_Minv, h->d_pcg_z, h->d_cg_partial, h->d_cg_cnt);
+                       h->d_pcg_Minv, h->d_pcg_z, h->d_cg_partial, h->d_cg_cnt, h->cg_wpart, h->mf_grid_n);
   };
   // CG iterations are enqueued in batches between reads of the device-side state. The
   // first batch is the previous solve's count + 2 (counts change slowly between LM
