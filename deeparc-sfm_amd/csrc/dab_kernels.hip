@@ -2762,33 +2762,55 @@ __global__ __launch_bounds__(256) void k_y_records(int NE, const double* __restr
   Yr[t] = Y[j * (size_t)NE + i];
 }
 
+// one wave per S block, three pairs per step: lane l < 54 is (group l / 18, row a, column
+// pair (c, c + 3)) and sums the terms of the pairs i = group, group + 3, ...; the three
+// groups are added in group order at the end (fixed order, deterministic). The old form
+// used 36 lanes on one pair per step.
 __global__ __launch_bounds__(256) void k_s_blocks(int nblk, const int* __restrict__ blk_pair_beg,
                                                   const int2* __restrict__ pairs,
                                                   const double* __restrict__ Yr,
                                                   double* __restrict__ packed) {
   const int blk = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (blk >= nblk || lane >= 36) return;
-  const int a = lane / 6, b = lane - 6 * (lane / 6);
-  double acc = 0.0;
-  auto term = [&](const int2 pr) {
+  if (blk >= nblk) return;  // wave-uniform
+  const int grp = lane < 54 ? lane / 18 : 3, k = lane - 18 * (lane / 18);
+  const int a = k / 3, c = k - 3 * (k / 3);
+  double acc0 = 0.0, acc1 = 0.0;
+  auto term = [&](const int2 pr, double& t0, double& t1) {
     const double* x = Yr + (size_t)kYRec * pr.x + 3 * a;
-    const double* y = Yr + (size_t)kYRec * pr.y + 3 * b;
-    return x[0] * y[0] + x[1] * y[1] + x[2] * y[2];
+    const double* y = Yr + (size_t)kYRec * pr.y + 3 * c;
+    const double x0 = x[0], x1 = x[1], x2 = x[2];
+    t0 = x0 * y[0] + x1 * y[1] + x2 * y[2];
+    t1 = x0 * y[9] + x1 * y[10] + x2 * y[11];
   };
-  // eight pairs' gathers in flight per step (the loop is latency bound); the sum keeps the
-  // pair order, so the result is bitwise that of the one-pair loop
   const int e = blk_pair_beg[blk + 1];
-  int i = blk_pair_beg[blk];
-  for (; i + 7 < e; i += 8) {
-    double t[8];
+  int i = blk_pair_beg[blk] + grp;
+  if (grp < 3) {
+    // four of the group's pairs in flight per step (twelve per wave)
+    for (; i + 9 < e; i += 12) {
+      double t0[4], t1[4];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) t[u] = term(pairs[i + u]);
+      for (int u = 0; u < 4; ++u) term(pairs[i + 3 * u], t0[u], t1[u]);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc += t[u];
+      for (int u = 0; u < 4; ++u) {
+        acc0 += t0[u];
+        acc1 += t1[u];
+      }
+    }
+    for (; i < e; i += 3) {
+      double t0, t1;
+      term(pairs[i], t0, t1);
+      acc0 += t0;
+      acc1 += t1;
+    }
   }
-  for (; i < e; ++i) acc += term(pairs[i]);
-  packed[36 * (size_t)blk + lane] = -acc;
+  // groups 0 + 1 + 2 in order, in the lanes of group 0
+  const double g1a = __shfl(acc0, lane + 18), g1b = __shfl(acc1, lane + 18);
+  const double g2a = __shfl(acc0, lane + 36), g2b = __shfl(acc1, lane + 36);
+  if (lane < 18) {
+    packed[36 * (size_t)blk + 6 * a + c] = -((acc0 + g1a) + g2a);
+    packed[36 * (size_t)blk + 6 * a + c + 3] = -((acc1 + g1b) + g2b);
+  }
 }
 
 void launch_s_blocks(hipStream_t s, int nblk, const int* blk_pair_beg, const int2* pairs,
