@@ -596,7 +596,8 @@ __global__ __launch_bounds__(kOneWG) void k_pcg_update(int NC, int mode, const d
 //   k_cg_q      q = S p (Y part w + diagonal + cross terms), pq -> alpha (mode 0/1);
 //               mode 2: r = b - S x
 //   k_cg_xr     x += alpha p, r -= alpha q (mode 0), Q-test, z = M^-1 r, rho -> beta, iter;
-//               the last work-group then p = z + beta p (z written with agent-scope stores)
+//               for small camera sets the last work-group then p = z + beta p (z written
+//               with agent-scope stores); otherwise a third launch, k_cg_p
 constexpr int kCgBlock = 64;
 
 // sum of v over the grid, valid in the last-arriving work-group (returns true there)
@@ -690,7 +691,7 @@ __global__ __launch_bounds__(kCgBlock) void k_cg_xr(int NC, int mode, const doub
                                                     double* __restrict__ x, double* __restrict__ r,
                                                     const double* __restrict__ Minv, double* __restrict__ z,
                                                     PcgState* st, double* __restrict__ partial,
-                                                    unsigned* __restrict__ cnt) {
+                                                    unsigned* __restrict__ cnt, int fold_p) {
   if (st->status != kPcgRunning) return;
   const int c = blockIdx.x * kCgBlock + threadIdx.x;
   double acc[2] = {0.0, 0.0};  // x.(b + r), r.z
@@ -755,12 +756,20 @@ __global__ __launch_bounds__(kCgBlock) void k_cg_xr(int NC, int mode, const doub
     run_s = status == kPcgRunning;
   }
   __syncthreads();
-  // p = z + beta p (k_cg_p) by the last work-group, every z of this launch now written
-  if (run_s)
+  // p = z + beta p by the last work-group, every z of this launch now written (small
+  // camera sets; otherwise k_cg_p spreads it)
+  if (fold_p && run_s)
     for (int i = threadIdx.x; i < 6 * NC; i += blockDim.x)
       p[i] = __hip_atomic_load(z + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + beta_s * p[i];
 }
 
+
+__global__ __launch_bounds__(256) void k_cg_p(int n, const double* __restrict__ z, double* __restrict__ p,
+                                              const PcgState* st) {
+  if (st->status != kPcgRunning) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = z[i] + st->pad[0] * p[i];
+}
 
 // ---- launchers -------------------------------------------------------------------------
 
@@ -833,7 +842,9 @@ void launch_cg_update(hipStream_t s, int NC, int mode, const double* Ad, const d
   else
     k_cg_q<<<gq, kCgBlock, 0, s>>>(NC, 2, L, Ad, w, xptr, xlist, xcam, X, scale_c, bvec, p, q, x, r, st, partial, cnt,
                                    L == 64 ? wpart : nullptr, wpart_g);
-  k_cg_xr<<<gx, kCgBlock, 0, s>>>(NC, mode, bvec, p, q, x, r, Minv, z, st, partial, cnt);  // also p = z + beta p
+  const int fold_p = 6 * NC <= 2048;  // one work-group does p = z + beta p in <= 32 passes
+  k_cg_xr<<<gx, kCgBlock, 0, s>>>(NC, mode, bvec, p, q, x, r, Minv, z, st, partial, cnt, fold_p);
+  if (mode != 1 && !fold_p) k_cg_p<<<(6 * NC + 255) / 256, 256, 0, s>>>(6 * NC, z, p, st);
 }
 int cg_partial_size(int NC) { return 2 * ((NC + 3) / 4) + 2 * ((NC + kCgBlock - 1) / kCgBlock); }
 
