@@ -163,10 +163,12 @@ void launch_point_factor(hipStream_t s, const DevView& v, const double* V, const
                          const double* scale_p, StepScalars sc, double* PU, double* q, int* fail);
 // entry Y = (s_c ∘ Jc^T Jp) PU_p (re-evaluated) -> Y.cm (camera-major pass) and Y.pm
 // (slot pass; with_pm = false skips it)
+// rec (fp64 Y only): the camera-major pass writes [NE][18] records there instead of Y.cm
 void launch_entry_y(hipStream_t s, const DevView& v, const double* points, const double* camtab,
-                    const double* scale_c, const double* PU, YBufs Y, bool with_pm);
+                    const double* scale_c, const double* PU, YBufs Y, bool with_pm, double* rec = nullptr);
 // S blocks (Y part): packed[blk][36] = - sum_pairs Y_row Y_col^T (pairs hold positions;
-// Y = the fp64 camera-major planes, stride NE; Yr = scratch [NE][18] for the records)
+// Y = the fp64 camera-major planes, stride NE; Yr = scratch [NE][18] for the records, or
+// Y = nullptr when Yr already holds them)
 void launch_s_blocks(hipStream_t s, int nblk, const int* blk_pair_beg, const int2* pairs,
                      const double* Y, int NE, double* packed, double* Yr);
 // Explicit S for small camera sets without pair tables (k_schur_y + k_schur_tiles): every
@@ -218,8 +220,9 @@ void launch_schur_unpack(hipStream_t s, int NC, const double* sblk, const unsign
 void launch_s_add_u(hipStream_t s, int NC, const double* ug, int ncross, const int2* cross_cam, const double* Ucross,
                     const double* scale_c, StepScalars sc, const double* ybc, double* S, int lds);
 // camera rhs partial: per position -Y q_p -> partial[chunk][6]
+// (Y planes, or rec = true: [NE][18] records)
 void launch_cam_rhs_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
-                            const double* Y, const double* q, double* partial);
+                            const double* Y, const double* q, double* partial, bool rec = false);
 // dense S (row-major, lower, ld = lds, n = 6 NC, n+1 rows): zero, scatter packed blocks,
 // add the U part + D^2, write rhs b = s_c g_c + ybc into row n.
 // ug: [NC][27] = (U upper-packed 21 | g_c 6) per camera

@@ -2671,7 +2671,7 @@ __device__ __forceinline__ void make_y(const double (&ja)[6], const double (&jb)
 }
 
 // SMALL: the camera tables are staged in LDS (small_tabs_fit) and the grid strides
-template <class YT, bool SMALL>
+template <class YT, bool SMALL, bool REC = false>  // REC: [NE][18] records instead of planes
 __global__ __launch_bounds__(256) void k_entry_y(DevView v, const double* __restrict__ points,
                                                  const double* __restrict__ camtab,
                                                  const double* __restrict__ scc,
@@ -2696,7 +2696,13 @@ __global__ __launch_bounds__(256) void k_entry_y(DevView v, const double* __rest
     }
     double y[18];
     make_y(ja, jb, jx0, jx1, scc + 6 * c, PU + 6 * (size_t)id.x, y);
-    store_yplane(Ycm, (size_t)v.NE, (size_t)i, y);
+    if constexpr (REC) {
+      double2* dst = reinterpret_cast<double2*>(Ycm + (size_t)kYRec * i);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) dst[k] = make_double2(y[2 * k], y[2 * k + 1]);
+    } else {
+      store_yplane(Ycm, (size_t)v.NE, (size_t)i, y);
+    }
   }
 }
 
@@ -2746,8 +2752,18 @@ static void launch_entry_y_t(hipStream_t s, const DevView& v, const double* poin
 }
 
 void launch_entry_y(hipStream_t s, const DevView& v, const double* points, const double* camtab,
-                    const double* scale_c, const double* PU, YBufs Y, bool with_pm) {
+                    const double* scale_c, const double* PU, YBufs Y, bool with_pm, double* rec) {
   if (v.NE <= 0) return;
+  if (rec && !Y.f32) {  // records for the explicit S blocks; the slot planes as usual
+    const int g = grid_for(v.NE, 256, 1 << 20);
+    if (small_tabs_fit(v.E, v.NI))
+      k_entry_y<double, true, true><<<std::min(g, kSmallGrid), 256, small_tabs_bytes(v.E, v.NI), s>>>(
+          v, points, camtab, scale_c, PU, rec);
+    else
+      k_entry_y<double, false, true><<<g, 256, 0, s>>>(v, points, camtab, scale_c, PU, rec);
+    if (with_pm) launch_entry_y_t<double>(s, v, points, camtab, scale_c, PU, nullptr, (double*)Y.pm);
+    return;
+  }
   if (Y.f32) launch_entry_y_t<float>(s, v, points, camtab, scale_c, PU, (float*)Y.cm, with_pm ? (float*)Y.pm : nullptr);
   else launch_entry_y_t<double>(s, v, points, camtab, scale_c, PU, (double*)Y.cm, with_pm ? (double*)Y.pm : nullptr);
 }
@@ -2816,10 +2832,11 @@ __global__ __launch_bounds__(256) void k_s_blocks(int nblk, const int* __restric
 void launch_s_blocks(hipStream_t s, int nblk, const int* blk_pair_beg, const int2* pairs,
                      const double* Y, int NE, double* packed, double* Yr) {
   if (nblk <= 0) return;
-  k_y_records<<<(unsigned)(((size_t)kYRec * NE + 255) / 256), 256, 0, s>>>(NE, Y, Yr);
+  if (Y) k_y_records<<<(unsigned)(((size_t)kYRec * NE + 255) / 256), 256, 0, s>>>(NE, Y, Yr);
   k_s_blocks<<<(nblk + 3) / 4, 256, 0, s>>>(nblk, blk_pair_beg, pairs, Yr, packed);
 }
 
+template <bool REC>
 __global__ __launch_bounds__(256) void k_cam_rhs_partial(DevView v, const int* __restrict__ chunk_beg,
                                                          const double* __restrict__ Y,
                                                          const double* __restrict__ q,
@@ -2832,7 +2849,17 @@ __global__ __launch_bounds__(256) void k_cam_rhs_partial(DevView v, const int* _
     const double2 qa = reinterpret_cast<const double2*>(q)[2 * (size_t)p];
     const double q2 = q[4 * (size_t)p + 2];
     double y[18];
-    load_yplane(Y, (size_t)v.NE, (size_t)i, y);
+    if constexpr (REC) {
+      const double2* src = reinterpret_cast<const double2*>(Y + (size_t)kYRec * i);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const double2 u = src[k];
+        y[2 * k] = u.x;
+        y[2 * k + 1] = u.y;
+      }
+    } else {
+      load_yplane(Y, (size_t)v.NE, (size_t)i, y);
+    }
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[a] -= y[3 * a] * qa.x + y[3 * a + 1] * qa.y + y[3 * a + 2] * q2;
   }
@@ -2840,9 +2867,10 @@ __global__ __launch_bounds__(256) void k_cam_rhs_partial(DevView v, const int* _
 }
 
 void launch_cam_rhs_partial(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg,
-                            const double* Y, const double* q, double* partial) {
+                            const double* Y, const double* q, double* partial, bool rec) {
   if (nchunk <= 0) return;
-  k_cam_rhs_partial<<<nchunk, 256, 0, s>>>(v, chunk_beg, Y, q, partial);
+  if (rec) k_cam_rhs_partial<true><<<nchunk, 256, 0, s>>>(v, chunk_beg, Y, q, partial);
+  else k_cam_rhs_partial<false><<<nchunk, 256, 0, s>>>(v, chunk_beg, Y, q, partial);
 }
 
 // --- dense reduced camera system ------------------------------------------------------

@@ -2187,9 +2187,13 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
       if (chol_factor_solve(h->chol, s, n, h->d_S, h->lds, h->d_yc, h->d_flags + 1) != 0)
         return set_error(DAB_E_DEVICE, "dense Cholesky launch failed");
     } else if (NC > 0) {
-      launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, yb, true);
-      launch_s_blocks(s, h->nblk, h->d_blk_pair_beg, h->d_pairs, h->d_Y, h->NE, h->packed(), h->d_Yrec);
-      launch_cam_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, h->d_Y, h->d_q, h->d_partial);
+      // fp64 Y: the camera-major pass writes the [NE][18] records the S blocks gather (no
+      // plane-to-record copy); the slot planes as before (back substitution)
+      const bool rec = !yb.f32;
+      launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, yb, true, rec ? h->d_Yrec : nullptr);
+      launch_s_blocks(s, h->nblk, h->d_blk_pair_beg, h->d_pairs, rec ? nullptr : h->d_Y, h->NE, h->packed(),
+                      h->d_Yrec);
+      launch_cam_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, rec ? h->d_Yrec : h->d_Y, h->d_q, h->d_partial, rec);
       launch_seg_final(s, NC, 6, h->d_seg_chunk, h->d_partial, h->ybc(), h->max_seg_chunks);
       CHECK_RC(h->allreduce(h->d_spack, h->spack_count(), ncclSum));
       launch_s_unpack(s, NC, h->nblk, h->d_blk_cam, h->packed(), h->ug(), h->ncross, h->d_cross_cam, h->Ux(),
