@@ -1,7 +1,9 @@
 """Benchmark of the BA hot path on MI355X (contract: one JSON line on rank 0).
 
 metric (BASELINE.json): "M observations/sec residual+Jacobian; wall-clock/LM-iter".
-  step  = one evaluation pass over the rank's shard with inputs resident in HBM:
+  step  = one evaluation pass over the rank's shard with inputs resident in HBM, at a NEW
+          linearization point (as after every accepted LM step, sfm.cc:66-73: anything the
+          pass derives from the points is rebuilt inside the timed step):
           residual + analytic Jacobian of every observation, reduced on chip into the
           J^T J / J^T r blocks (matrix-free; BAL-shaped problems on one GPU: one fused
           launch k_eval_fused with camera-side and point-side waves side by side; else point
@@ -20,8 +22,11 @@ metric (BASELINE.json): "M observations/sec residual+Jacobian; wall-clock/LM-ite
           kernel's time and HBM roofline fraction on rank 0's shard) and the mixed-precision
           PCG LM iteration (wall-clock, median).
   roofline: the evaluation kernel (k_eval_fused, or k_eval_points for the two-kernel
-          pass), algorithmic bytes (observations read once, parameters, outputs) / HIP-event
-          time.
+          pass), algorithmic bytes / HIP-event time. Bytes follow SURVEY §8(d)'s minimal
+          convention: per observation the 16-B pixel + its index words once per traversal
+          order (point-major; camera-major for the fused pass's camera side), per point 24 B
+          in + 72 B of V, g out, 48 B per extrinsic / intrinsic, 216 B of U | g_c per free
+          camera; no denormalised copies, no re-gathers.
   cpu_baseline: the C oracle (Ceres-semantics restatement, OpenMP) on the box's host
           cores, rank 0 at N=1 only, bounded sample.
 """
@@ -235,12 +240,20 @@ def main():
         barrier()
         ev_dt = max_over_ranks(time.perf_counter() - t_ev) / 40
         r_jac_ms, _ = rsolver.bench_kernel_ms()
+        r_pair_ms, r_pair_bytes = rsolver.bench_pair_ms()
         r_jac_ms = max_over_ranks(r_jac_ms)
+        r_pair_ms = max_over_ranks(r_pair_ms)
         r_bytes = rsolver.jacobian_bytes()
         r_gbs = r_bytes / (r_jac_ms * 1e-3) / 1e9
         rig_eval = {"rig_eval_ms_per_step": 1e3 * ev_dt, "rig_eval_mobs_per_s": gprob.num_obs / ev_dt / 1e6,
                     "rig_point_kernel_ms": r_jac_ms, "rig_point_kernel_bytes_per_launch_rank0": r_bytes,
-                    "rig_point_kernel_roofline_frac": r_gbs / HBM_PEAK_GBS}
+                    "rig_point_kernel_roofline_frac": r_gbs / HBM_PEAK_GBS,
+                    # the rig pass's dominant kernel: composed observations pair-major
+                    # (both cameras' blocks and the cross block from one projection)
+                    "rig_pair_kernel": "k_eval_pair", "rig_pair_kernel_ms": r_pair_ms,
+                    "rig_pair_kernel_bytes_per_launch_rank0": r_pair_bytes,
+                    "rig_pair_kernel_roofline_frac": (r_pair_bytes / (r_pair_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                                      if r_pair_ms > 0 else None)}
         opts = pkg.options(max_num_iterations=args.lm_iters, function_tolerance=0.0, gradient_tolerance=0.0,
                            parameter_tolerance=0.0, linear_solver_type=pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG,
                            pcg_fp32=1)

@@ -114,6 +114,7 @@ SIGNATURES = {
     "dab_sync": (C.c_int, [C.c_void_p]),
     "dab_bench_kernel_ms": (C.c_int, [C.c_void_p, _dp, _dp]),
     "dab_jacobian_bytes": (C.c_int, [C.c_void_p, _dp]),
+    "dab_bench_pair_ms": (C.c_int, [C.c_void_p, _dp, _dp]),
     "dab_eval_schedule": (C.c_int, [C.c_void_p, _ip]),
     "dab_pcg_schedule": (C.c_int, [C.c_void_p, _ip]),
     "dab_comm_schedule": (C.c_int, [C.c_void_p, _ip]),

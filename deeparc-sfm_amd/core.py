@@ -289,6 +289,13 @@ class Solver:
         check(self.lib.dab_jacobian_bytes(self.h, C.byref(b)), self.lib)
         return b.value
 
+    def bench_pair_ms(self):
+        """(ms per launch, algorithmic bytes per launch) of the rig's pair-major camera kernel
+        over the batches read by the last bench_kernel_ms() call"""
+        a, b = C.c_double(), C.c_double()
+        check(self.lib.dab_bench_pair_ms(self.h, C.byref(a), C.byref(b)), self.lib)
+        return a.value, b.value
+
     def comm_p2p(self):
         """1 when the one-shot xGMI peer-to-peer all-reduce carries the sums over ranks"""
         f = C.c_int32()

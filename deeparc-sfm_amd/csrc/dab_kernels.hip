@@ -1655,6 +1655,52 @@ __device__ __forceinline__ void eval_cams_stream(const double* __restrict__ cmx,
   }
 }
 
+// The fused pass's camera loop gathering the points itself (no camera-major copy to
+// refresh when the points move). Three register slots per ring; per 64-entry step the
+// point index is loaded four steps ahead and the point (with the pixel) gathered two
+// steps ahead, so the index -> gather -> compute chain has two steps of arithmetic to hide
+// each hop. Every load is unconditional (clamped to the last entry; the step count is
+// wave-uniform), so the waits the compiler places count exactly: the gather of step
+// st + 2 waits only for its index (vmcnt(5)), the compute of step st only for its point.
+__device__ __forceinline__ void eval_cams_gather(const int* __restrict__ cm_pt, const double2* __restrict__ cmxy,
+                                                 const double* __restrict__ points, int i0, int e, int ext_i,
+                                                 int intr_i, const double* __restrict__ ext,
+                                                 const double* __restrict__ intr, double (&acc)[27], double* jl) {
+  constexpr int DG = 2, DI = 4, R = 3;
+  const int lo = i0 - (int)(threadIdx.x & 63);
+  const int n = (e - lo + 63) >> 6;  // steps of 64 entries
+  int pid[R];
+  double2 xy[R];
+  double X[R][3];
+  auto load_idx = [&](int slot, int step) { pid[slot] = cm_pt[min(i0 + 64 * step, e - 1)]; };
+  auto gather = [&](int islot, int slot, int step) {
+    const int p = pid[islot];
+    xy[slot] = cmxy[min(i0 + 64 * step, e - 1)];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) X[slot][q] = points[3 * (size_t)p + q];
+  };
+  if (n > 0) {
+    // prologue: indices of steps 0 .. DI-1 ... in the order the loop body issues them
+#pragma unroll
+    for (int st = 0; st < DG; ++st) load_idx(st % R, st);
+#pragma unroll
+    for (int st = 0; st < DG; ++st) gather(st % R, st % R, st);
+#pragma unroll
+    for (int st = DG; st < DI; ++st) load_idx(st % R, st);
+  }
+  const UniFrame f(ext, intr, ext_i, intr_i, jl);  // built while the first loads fly
+  DAB_STAMP_ANY(1);
+  for (int st0 = 0; st0 < n; st0 += R) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int st = st0 + u;
+      gather((st + DG) % R, (st + DG) % R, st + DG);  // index of step st + DG -> its point
+      load_idx((st + DI) % R, st + DI);                // slot of step st + DI - R = st + 1: consumed
+      if (i0 + 64 * st < e) frame_rows_acc(xy[u], X[u], f, acc);
+    }
+  }
+}
+
 // entry k (< 27) of the camera's [U upper-packed | g_c] from the point-frame sums s
 // (same packing): U_rr = J^T U~_rr J, U_rt = J^T U~_rt, U_tt = U~_tt, g_r = J^T g~_r
 __device__ __forceinline__ int upk6(int a, int b) {  // packed index of (a, b), a <= b
@@ -1863,7 +1909,9 @@ constexpr int kFusedCW = 16 - kFusedPW;   // camera waves (kFusedCW / 2 cameras 
 // ST: the streamed form — camera waves read the camera-major point copy cmx (eval_cams_stream,
 // NS slots) and point waves the packed 4-B slot records v.obs_e (ext | intr << 16, a D-deep
 // queue at 5 VGPRs per row) instead of the 16-B obs_idx records.
-template <int D, int ABL = 0, int NS = 3, bool ST = false, bool TAB = false>  // ABL: 1 camera waves exit at once (point side
+// CG (with ST): the camera waves gather the points themselves (eval_cams_gather), no cmx.
+template <int D, int ABL = 0, int NS = 3, bool ST = false, bool TAB = false, bool CG = false>
+                                          // ABL: 1 camera waves exit at once (point side
                                           // only), 2 point waves do (camera side only) — the multi-rank split
                                           // schedule; timing ablations: 3 no trig in the staging, 21 / 22
                                           // point / camera waves at raised priority; NS: camera-entry slots
@@ -1909,6 +1957,8 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
       eval_cams_uni_pipe<NS>(v, lo + lane, hi, 64, points, [&]() { return UniTabs(ext, v.intr, u.x, u.y); },
                              acc);
       if (lane < 9) cjl[cw][lane] = (lane % 4 == 0) ? 1.0 : 0.0;
+    } else if constexpr (ST && CG) {
+      eval_cams_gather(v.cm_pt, v.cm_xy, points, lo + lane, hi, u.x, u.y, ext, v.intr, acc, cjl[cw]);
     } else if constexpr (ST) {
       eval_cams_stream<NS, TAB>(cmx, (size_t)v.NE, v.cm_xy, lo + lane, hi, u.x, u.y, ext, v.intr, acc, cjl[cw],
                                 camtab);
@@ -2209,6 +2259,14 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
     if (side == 1) k_eval_fused<3, 1, 2, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
     else if (side == 2) k_eval_fused<3, 2, 2, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
     else k_eval_fused<3, 0, 2, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+    return;
+  }
+  if (v.obs_e) {
+    // packed point-side records, camera waves gathering the points (nothing to refresh
+    // when the points move)
+    if (side == 1) k_eval_fused<3, 1, 3, true, false, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+    else if (side == 2) k_eval_fused<3, 2, 3, true, false, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+    else k_eval_fused<3, 0, 3, true, false, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
     return;
   }
   // one side only (the multi-rank split schedule): the same kernel with the other side's

@@ -25,7 +25,11 @@ size_t p2p_capacity(const P2pComm* c);
 // in-place sum over the ranks, enqueued on s (every rank calls in the same order)
 int p2p_allreduce_sum(P2pComm* c, hipStream_t s, double* buf, size_t n);
 int p2p_allreduce_sum_u64(P2pComm* c, hipStream_t s, unsigned long long* buf, size_t n);
-// DAB_E_COMM when a call gave up waiting for a peer (after the stream has drained)
+// in-place max over the ranks
+int p2p_allreduce_max(P2pComm* c, hipStream_t s, double* buf, size_t n);
+int p2p_allreduce_max_i32(P2pComm* c, hipStream_t s, int* buf, size_t n);
+// DAB_E_COMM when a call gave up waiting for a peer: a host read of the pinned error word,
+// no device synchronisation (call it after the stream has drained to cover every call)
 int p2p_check(P2pComm* c);
 
 }  // namespace dab

@@ -17,8 +17,11 @@
 //      output — the same order on every rank, so every rank gets bitwise the same result.
 // A slot is rewritten two calls later; by then every peer has signalled the call in
 // between, which it does only after its kernel of this call (same stream) has finished
-// reading. The waits are bounded: a peer that never arrives sets the region's error word
-// instead of hanging the GPU (p2p_check reports it).
+// reading. The waits are bounded (s_memrealtime deadline): a peer that never arrives sets
+// the context's error word (host-pinned) instead of hanging the GPU, the call writes
+// poison (NaN / all-ones / set flags) instead of a sum, and every later call of the
+// context fails at once without publishing, so the peers give up too. The solver polls the
+// word at every host synchronisation (p2p_check) and returns DAB_E_COMM.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,14 +36,15 @@ namespace dab {
 
 namespace {
 constexpr int kP2pBlock = 256;
-constexpr size_t kSpinLimit = size_t(1) << 26;  // ~1 s of polling before giving up
+// default bound of a wait for a peer: 60 s of the 100-MHz s_memrealtime clock (a peer may
+// legitimately be late by its own host-side set-up; DAB_P2P_TIMEOUT_MS overrides)
+constexpr long long kDefaultTimeoutMs = 60000;
 
 struct Layout {
   size_t cap;  // 8-byte words per slot
   __host__ __device__ size_t slot_off(int s) const { return (size_t)s * cap; }
   __host__ __device__ size_t flag_off() const { return 2 * cap; }  // [2][kP2pMaxWg][kP2pMaxRanks] words
-  __host__ __device__ size_t err_off() const { return flag_off() + 2 * (size_t)kP2pMaxWg * kP2pMaxRanks; }
-  __host__ __device__ size_t words() const { return err_off() + 16; }
+  __host__ __device__ size_t words() const { return flag_off() + 2 * (size_t)kP2pMaxWg * kP2pMaxRanks; }
 };
 
 struct PeerPtrs {
@@ -50,48 +54,83 @@ struct PeerPtrs {
 // Slot stores and loads are relaxed system-scope atomics (8-byte words): they bypass every
 // non-coherent cache on both sides, whatever memory type the importing process's mapping of
 // a peer region got, so a slot reused two calls later is never read from a stale line.
+// 4-byte values (the flag max) travel widened to one word.
 template <class T>
-__device__ __forceinline__ void sys_store(T* p, T v) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ unsigned long long to_word(T v) {
+  if constexpr (sizeof(T) == 8) return __builtin_bit_cast(unsigned long long, v);
+  else return (unsigned long long)__builtin_bit_cast(unsigned, v);
 }
 template <class T>
-__device__ __forceinline__ T sys_load(const T* p) {
-  return __builtin_bit_cast(T, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_SYSTEM));
+__device__ __forceinline__ T from_word(unsigned long long w) {
+  if constexpr (sizeof(T) == 8) return __builtin_bit_cast(T, w);
+  else return __builtin_bit_cast(T, (unsigned)w);
+}
+template <class T>
+__device__ __forceinline__ void sys_store(unsigned long long* p, T v) {
+  __hip_atomic_store(p, to_word(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <class T>
+__device__ __forceinline__ T sys_load(const unsigned long long* p) {
+  return from_word<T>(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+// what a failed call leaves in the output: non-finite sums, all-ones cost words, set flags,
+// so nothing downstream mistakes it for a result (the host sees the error word first)
+template <class T>
+__device__ __forceinline__ T poison() {
+  if constexpr (sizeof(T) == 8 && (T)0.5 != (T)0) return __builtin_nan("");
+  else return ~(T)0 > 0 ? ~(T)0 : (T)0x7fffffff;
 }
 
-template <class T>
+// OP: 0 sum, 1 max. err: this context's error word (host-pinned, coherent): nonzero after
+// a call gave up waiting; every later call then fails at once (no wait, no flag published,
+// so the peers give up too) and poisons its output.
+template <class T, int OP>
 __global__ __launch_bounds__(kP2pBlock) void k_p2p_allreduce(T* __restrict__ buf, size_t n, size_t chunk,
                                                              PeerPtrs peers, int rank, int world, size_t cap,
-                                                             unsigned long long seq) {
+                                                             unsigned long long seq, unsigned long long* err,
+                                                             long long timeout_ticks) {
   const Layout L{cap};
   const int j = blockIdx.x, s = (int)(seq & 1);
   const size_t b = (size_t)j * chunk, e = b + chunk < n ? b + chunk : n;
-  unsigned long long* mine = peers.p[rank];
-  T* my_slot = reinterpret_cast<T*>(mine + L.slot_off(s));
-  for (size_t i = b + threadIdx.x; i < e; i += kP2pBlock) sys_store(my_slot + i, buf[i]);
-  __threadfence_system();  // the slice is visible to every device before its flag
+  __shared__ int failed;
+  if (threadIdx.x == 0)
+    failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0ull ? 1 : 0;
   __syncthreads();
-  if ((int)threadIdx.x < world) {
-    unsigned long long* f = peers.p[threadIdx.x] + L.flag_off() + ((size_t)s * kP2pMaxWg + j) * kP2pMaxRanks + rank;
-    __hip_atomic_store(f, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  if ((int)threadIdx.x < world) {
-    unsigned long long* f = mine + L.flag_off() + ((size_t)s * kP2pMaxWg + j) * kP2pMaxRanks + threadIdx.x;
-    size_t spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
-      if (++spins > kSpinLimit) {
-        __hip_atomic_store(mine + L.err_off(), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
+  if (!failed) {
+    unsigned long long* mine = peers.p[rank];
+    unsigned long long* my_slot = mine + L.slot_off(s);
+    for (size_t i = b + threadIdx.x; i < e; i += kP2pBlock) sys_store(my_slot + i, buf[i]);
+    __threadfence_system();  // the slice is visible to every device before its flag
+    __syncthreads();
+    if ((int)threadIdx.x < world) {
+      unsigned long long* f = peers.p[threadIdx.x] + L.flag_off() + ((size_t)s * kP2pMaxWg + j) * kP2pMaxRanks + rank;
+      __hip_atomic_store(f, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    if ((int)threadIdx.x < world) {
+      unsigned long long* f = mine + L.flag_off() + ((size_t)s * kP2pMaxWg + j) * kP2pMaxRanks + threadIdx.x;
+      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+          // give up: record the call, and publish nothing more from this context
+          __hip_atomic_store(err, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          failed = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
+  if (failed) {  // never sum slots a peer may not have written
+    for (size_t i = b + threadIdx.x; i < e; i += kP2pBlock) buf[i] = poison<T>();
+    return;
+  }
   for (size_t i = b + threadIdx.x; i < e; i += kP2pBlock) {
-    T t = sys_load(reinterpret_cast<const T*>(peers.p[0] + L.slot_off(s)) + i);
-    for (int r = 1; r < world; ++r) t += sys_load(reinterpret_cast<const T*>(peers.p[r] + L.slot_off(s)) + i);
+    T t = sys_load<T>(peers.p[0] + L.slot_off(s) + i);
+    for (int r = 1; r < world; ++r) {
+      const T x = sys_load<T>(peers.p[r] + L.slot_off(s) + i);
+      t = OP == 0 ? t + x : (x > t ? x : t);
+    }
     buf[i] = t;
   }
 }
@@ -112,6 +151,9 @@ struct P2pComm {
   unsigned long long* peer[kP2pMaxRanks] = {};
   unsigned long long seq = 0;
   P2pShared* shared = nullptr;
+  unsigned long long* err = nullptr;  // host-pinned, coherent: the device writes, the host polls
+  long long timeout_ticks = 0;        // s_memrealtime ticks (100 MHz)
+  long long skip_call = 0;            // DAB_P2P_SKIP_CALL (failure-path test): this call is not launched
 };
 
 static void shared_release(P2pShared* sh) {
@@ -189,6 +231,9 @@ int p2p_create_group(int rank, int world, size_t cap_words, int nctx, const P2pA
     peer_base[r] = static_cast<char*>(q) + poff;
   }
   sh->refs = nctx;
+  long long tmo_ms = kDefaultTimeoutMs, skip = 0;
+  if (const char* e = getenv("DAB_P2P_TIMEOUT_MS")) tmo_ms = std::max(1LL, atoll(e));
+  if (const char* e = getenv("DAB_P2P_SKIP_CALL")) skip = atoll(e);
   for (int k = 0; k < nctx; ++k) {
     P2pComm* c = new P2pComm();
     c->rank = rank;
@@ -198,6 +243,16 @@ int p2p_create_group(int rank, int world, size_t cap_words, int nctx, const P2pA
     for (int r = 0; r < world; ++r)
       c->peer[r] = reinterpret_cast<unsigned long long*>(peer_base[r]) + (size_t)k * region;
     c->mine = c->peer[rank];
+    c->timeout_ticks = tmo_ms * 100000LL;
+    c->skip_call = k == 0 ? skip : 0;
+    void* e = nullptr;
+    if (hipHostMalloc(&e, 64, hipHostMallocCoherent) != hipSuccess) {
+      for (int q = 0; q <= k; ++q) p2p_destroy(q < k ? out[q] : c);
+      for (int q = 0; q < nctx; ++q) out[q] = nullptr;
+      return set_error(DAB_E_NOMEM, "p2p: pinned error word allocation failed");
+    }
+    c->err = static_cast<unsigned long long*>(e);
+    *c->err = 0;
     out[k] = c;
   }
   return 0;
@@ -206,13 +261,14 @@ int p2p_create_group(int rank, int world, size_t cap_words, int nctx, const P2pA
 void p2p_destroy(P2pComm* c) {
   if (!c) return;
   shared_release(c->shared);
+  if (c->err) (void)hipHostFree(c->err);
   delete c;
 }
 
 size_t p2p_capacity(const P2pComm* c) { return c ? c->cap : 0; }
 
-template <class T>
-static int p2p_sum(P2pComm* c, hipStream_t s, T* buf, size_t n) {
+template <class T, int OP>
+static int p2p_reduce(P2pComm* c, hipStream_t s, T* buf, size_t n) {
   if (n > c->cap) return set_error(DAB_E_INVALID, "p2p: vector larger than the slot");
   if (n == 0) return 0;
   // slices of >= 2048 words; at most kP2pMaxWg work-groups, each reading its slice from
@@ -222,20 +278,21 @@ static int p2p_sum(P2pComm* c, hipStream_t s, T* buf, size_t n) {
   PeerPtrs pp{};
   for (int r = 0; r < c->world; ++r) pp.p[r] = c->peer[r];
   ++c->seq;
-  k_p2p_allreduce<T><<<grid, kP2pBlock, 0, s>>>(buf, n, chunk, pp, c->rank, c->world, c->cap, c->seq);
+  if ((long long)c->seq == c->skip_call) return 0;  // failure-path test: this rank misses one call
+  k_p2p_allreduce<T, OP><<<grid, kP2pBlock, 0, s>>>(buf, n, chunk, pp, c->rank, c->world, c->cap, c->seq, c->err,
+                                                    c->timeout_ticks);
   return hipGetLastError() == hipSuccess ? 0 : set_error(DAB_E_DEVICE, "p2p: launch failed");
 }
-int p2p_allreduce_sum(P2pComm* c, hipStream_t s, double* buf, size_t n) { return p2p_sum(c, s, buf, n); }
+int p2p_allreduce_sum(P2pComm* c, hipStream_t s, double* buf, size_t n) { return p2p_reduce<double, 0>(c, s, buf, n); }
 int p2p_allreduce_sum_u64(P2pComm* c, hipStream_t s, unsigned long long* buf, size_t n) {
-  return p2p_sum(c, s, buf, n);
+  return p2p_reduce<unsigned long long, 0>(c, s, buf, n);
 }
+int p2p_allreduce_max(P2pComm* c, hipStream_t s, double* buf, size_t n) { return p2p_reduce<double, 1>(c, s, buf, n); }
+int p2p_allreduce_max_i32(P2pComm* c, hipStream_t s, int* buf, size_t n) { return p2p_reduce<int, 1>(c, s, buf, n); }
 
 int p2p_check(P2pComm* c) {
-  if (!c) return 0;
-  unsigned long long e = 0;
-  const Layout L{c->cap};
-  if (hipMemcpy(&e, c->mine + L.err_off(), 8, hipMemcpyDeviceToHost) != hipSuccess)
-    return set_error(DAB_E_DEVICE, "p2p: error word read failed");
+  if (!c || !c->err) return 0;
+  const unsigned long long e = __atomic_load_n(c->err, __ATOMIC_ACQUIRE);
   if (e != 0) return set_error(DAB_E_COMM, "p2p all-reduce: a peer did not arrive (call " + std::to_string(e) + ")");
   return 0;
 }

@@ -220,7 +220,9 @@ struct Knobs {
   int schur_tiles = 1;      // DAB_SCHUR_TILES=0: explicit S from the pair tables even for small NC
   int p2p = -1;             // DAB_P2P: one-shot xGMI all-reduce of small sums (-1 auto: RCCL handles
                             // only; 1 also on host-staged handles, the one-GPU rehearsal; 0 off)
-  int fused_stream = 1;     // DAB_FUSED_STREAM=0: the fused pass without the streamed camera-major point copy
+  int fused_stream = 2;     // DAB_FUSED_STREAM: fused pass records — 2 packed point-side records, camera
+                            // waves gather the points; 1 the same with the camera-major point copy
+                            // (refreshed after every point change); 0 the 16-B records
   int fused_variant = 0;    // DAB_FUSED_V: pipeline depths of the streamed fused pass (DAB_ABLATIONS builds)
   int fused_tab = 0;        // DAB_FUSED_TAB=1 (DAB_ABLATIONS builds): the streamed fused pass reads the
                             // k_cam_tables output instead of building its tables (kernel -0.9 us at C3,
@@ -262,9 +264,12 @@ struct dab_handle {
   hipStream_t comm_stream = nullptr;
   hipEvent_t ev_cam = nullptr, ev_comm = nullptr;
   // bench bookkeeping
-  double bench_jac_ms = 0, bench_asm_ms = 0;
-  int bench_count = 0, bench_pending = 0;
-  std::vector<std::array<hipEvent_t, 4>> bench_ev;  // per-step events (dab_bench_eval_pass)
+  double bench_jac_ms = 0, bench_asm_ms = 0, bench_pair_ms = 0;
+  int bench_count = 0, bench_pending = 0, bench_pair_count = 0;
+  // per-step events (dab_bench_eval_pass): start, point kernel start / end, end, and the
+  // rig's pair-major camera kernel (k_eval_pair) start / end
+  std::vector<std::array<hipEvent_t, 6>> bench_ev;
+  std::vector<char> bench_pair_rec;  // per pending step: the pair events were recorded
 
   // ---- host-side problem structure ----
   bool have_problem = false;
@@ -325,6 +330,7 @@ struct dab_handle {
   // pair-major evaluation of the composed observations (launch_eval_pair): the other
   // entries' camera-major copy and chunks, and per camera its pair-chunk halves
   bool pair_eval = false;
+  double pair_bytes = 0.0, last_pair_ms = 0.0;  // k_eval_pair: algorithmic bytes per launch, bench time
   int nchunk2 = 0;
   int4* d_cm2_idx = nullptr;
   double2* d_cm2_xy = nullptr;
@@ -481,7 +487,8 @@ struct dab_handle {
 
   int allreduce(double* buf, size_t n, ncclRedOp_t op) {
     if (world <= 1 || n == 0) return 0;
-    if (p2p_main && op == ncclSum && n <= kP2pWords) return p2p_allreduce_sum(p2p_main, stream, buf, n);
+    if (p2p_main && n <= kP2pWords && (op == ncclSum || op == ncclMax))
+      return op == ncclSum ? p2p_allreduce_sum(p2p_main, stream, buf, n) : p2p_allreduce_max(p2p_main, stream, buf, n);
     if (host_cb) return host_allreduce(buf, n, op == ncclMax ? 1 : 0);
     NCCL_OK(ncclAllReduce(buf, buf, n, ncclDouble, op, comm, stream));
     return 0;
@@ -489,6 +496,7 @@ struct dab_handle {
   // max over ranks of small int flag arrays
   int allreduce_max_i32(int* buf, int n) {
     if (world <= 1 || n == 0) return 0;
+    if (p2p_main) return p2p_allreduce_max_i32(p2p_main, stream, buf, (size_t)n);
     if (!host_cb) {
       NCCL_OK(ncclAllReduce(buf, buf, n, ncclInt32, ncclMax, comm, stream));
       return 0;
@@ -966,19 +974,27 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   // slots in increasing order (linear; the comparison sort of 9M keys took ~1 s at C5)
   big_vec<long long> xkeys;
   if (h->any_compose && NC > 0) {
-    auto pair_of = [&](long long s2) -> int {
+    // the two free cameras of a composed slot (-1: not a cross observation)
+    auto cams_of = [&](long long s2) -> int2 {
       const int e1 = obs_idx[s2].z;
-      if (e1 < 0 || obs_idx[s2].x < 0) return -1;
+      if (e1 < 0 || obs_idx[s2].x < 0) return make_int2(-1, -1);
       const int c0 = h->ext_col[obs_idx[s2].y], c1 = h->ext_col[e1];
-      if (c0 < 0 || c1 < 0) return -1;
-      return c0 * NC + c1;
+      if (c0 < 0 || c1 < 0) return make_int2(-1, -1);
+      return make_int2(c0, c1);
     };
-    big_vec<int> xs;
-    std::vector<long long> st;
-    bucket_sort(NS, NC * NC, pair_of, xs, st);
-    xkeys.resize(xs.size());
-    par_for((long long)xs.size(), [&](long long b, long long e, int) {
-      for (long long i = b; i < e; ++i) xkeys[i] = (long long)pair_of(xs[i]) * (long long)NS + xs[i];
+    // (c0, c1, slot) order by two stable NC-bucket passes (by c1, then by c0): counters of
+    // NC per thread, not NC^2, and the 64-bit key below does not overflow
+    big_vec<int> o1, o2;
+    std::vector<long long> st1, st2;
+    bucket_sort(NS, NC, [&](long long s2) { return cams_of(s2).y; }, o1, st1);
+    bucket_sort((long long)o1.size(), NC, [&](long long j) { return cams_of(o1[j]).x; }, o2, st2);
+    xkeys.resize(o2.size());
+    par_for((long long)o2.size(), [&](long long b, long long e, int) {
+      for (long long i = b; i < e; ++i) {
+        const int s2 = o1[o2[i]];
+        const int2 c = cams_of(s2);
+        xkeys[i] = ((long long)c.x * NC + c.y) * (long long)NS + s2;
+      }
     });
   }
   std::vector<long long> pairkeys;  // unique (c0*NC+c1)
@@ -1053,6 +1069,18 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   std::vector<int> chunk2_beg, seg2_chunk(NC + 1, 0), xcam_ptr(NC + 1, 0), xcam_list;
   h->pair_eval = h->nxchunk > 0 && pair_eval_fits(h->E, h->NI) && h->knobs.pair_eval != 0;
   if (h->pair_eval) {
+    {  // algorithmic bytes of one k_eval_pair launch (dab_bench_pair_ms)
+      std::vector<char> touched(NP, 0);
+      long long npt = 0;
+      for (long long k : xkeys) {
+        const int p = obs_idx[(int)(k % NS)].x;
+        if (p >= 0 && !touched[p]) {
+          touched[p] = 1;
+          ++npt;
+        }
+      }
+      h->pair_bytes = (16.0 + 12.0) * (double)xkeys.size() + 24.0 * (double)npt + 90.0 * 8.0 * h->nxchunk;
+    }
     // the entries that are not paired, per camera (counted, then filled in parallel)
     auto unpaired = [&](int i) {
       const int4 id = cm_idx[i];
@@ -1105,6 +1133,8 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   h->schur_built = false;
   h->schur_tiles = false;
   h->pcg_built = false;
+  h->mf = h->mf32 = false;
+  h->cg_wpart = nullptr;  // its buffer went with the previous problem's allocations
   h->nblk = 0;
   h->npairs = 0;
 
@@ -1269,12 +1299,14 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   h->d_cmx = nullptr;
   h->cmx_version = -1;
   if (h->fused && h->knobs.fused_stream != 0 && h->E < 0x8000 && h->NI < 0x8000) {
-    // streamed fused pass: 4-B slot records and the camera-major point copy
+    // packed 4-B slot records for the point waves; fused_stream = 1 also the camera-major
+    // point copy (re-gathered whenever the points move), 2 (default) camera waves that
+    // gather the points themselves
     std::vector<int> obs_e(NS, -1);
     for (int i = 0; i < NS; ++i)
       if (obs_idx[i].x >= 0) obs_e[i] = obs_idx[i].y | (obs_idx[i].w << 16);
     CHECK_RC(upload(&h->d_obs_e, d, obs_e, s));
-    CHECK_RC(d.alloc(&h->d_cmx, (size_t)3 * std::max(1, NE)));
+    if (h->knobs.fused_stream == 1) CHECK_RC(d.alloc(&h->d_cmx, (size_t)3 * std::max(1, NE)));
     HIP_OK(hipStreamSynchronize(s));
     v.obs_e = h->d_obs_e;
   }
@@ -1705,6 +1737,9 @@ static int build_pcg_buffers(dab_handle* h) {
 // exact: the fp64 product even in a mixed-precision solve (the true residual r = b - S x)
 static int pcg_matvec(dab_handle* h, YBufs yb, const double* vec, bool exact = false) {
   hipStream_t s = h->stream;
+  // the stored-Y products all-reduce into d_pcg_w; only the one-rank matrix-free product
+  // hands its work-group partials to the CG update (never left over from an earlier problem)
+  h->cg_wpart = nullptr;
   if (h->mf) {
     // one rank with cross blocks (the rig): the product's partials are summed inside the CG
     // update (no all-reduce in between), one launch fewer per iteration
@@ -1841,7 +1876,8 @@ extern "C" int dab_get_parameters(dab_handle* h, double* points, double* ext) {
 // the current x in d_camtab. ev_mid / ev_end (nullable) bracket the point kernel.
 // camtab_ready: the caller has just built the camera tables (the LM step needs them for
 // later passes); otherwise they are built here only if a pass of this problem reads them.
-static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullptr, hipEvent_t ev_end = nullptr) {
+static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullptr, hipEvent_t ev_end = nullptr,
+                     hipEvent_t ev_pair0 = nullptr, hipEvent_t ev_pair1 = nullptr, bool* pair_rec = nullptr) {
   hipStream_t s = h->stream;
   const DevView& v = h->view;
   bool overlapped = false;
@@ -1858,13 +1894,15 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
   const bool fx = h->fused || eval_points_fx(h->eval_wps);
   if (fx) h->fx_last ^= 1;  // this pass adds into set fx_last and zeroes the other
   h->cost_fx_pending = fx;
+  // the timed region of the single fused launch includes the refresh of the camera-major
+  // point copy (fused_stream = 1) that an evaluation at a new point needs
+  if (h->fused && !h->fused_split && ev_mid) HIP_OK(hipEventRecord(ev_mid, s));
   if (h->d_cmx && h->cmx_version != h->pts_version) {
     // the points changed since the camera-major copy was taken (set-up, accepted step)
     launch_cmx_gather(s, v, h->d_points, h->d_cmx);
     h->cmx_version = h->pts_version;
   }
   if (h->fused && !h->fused_split) {  // both halves of the pass in one launch (launch_eval_fused)
-    if (ev_mid) HIP_OK(hipEventRecord(ev_mid, s));
     launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
                       h->cost_fx(h->fx_last ^ 1), h->ncu, 0, h->d_cmx, h->knobs.fused_variant,
                       fused_tab ? h->d_camtab : nullptr);
@@ -1902,8 +1940,11 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
     v2.cm_idx = h->d_cm2_idx;
     v2.cm_xy = h->d_cm2_xy;
     launch_eval_cams_gen(s, v2, h->nchunk2, h->d_chunk2_beg, h->d_points, h->d_ext, h->d_camtab, h->d_partial2);
+    if (ev_pair0) HIP_OK(hipEventRecord(ev_pair0, s));
     launch_eval_pair(s, v, h->nxchunk, h->d_xchunk_beg, h->d_x_idx, h->d_x_xy, h->d_points, h->d_camtab,
                      h->d_xpartial, h->d_xcpart);
+    if (ev_pair1) HIP_OK(hipEventRecord(ev_pair1, s));
+    if (pair_rec) *pair_rec = ev_pair0 && ev_pair1 && h->nxchunk > 0;
     launch_cam_final(s, h->NC, h->d_seg2_chunk, h->d_partial2, h->d_xcam_ptr, h->d_xcam_list, h->d_xcpart, h->ug());
     launch_seg_final(s, h->ncross, 36, h->d_xseg_chunk, h->d_xpartial, h->Ux(), h->max_xseg_chunks);
   } else if (h->NC > 0) {
@@ -1967,6 +2008,10 @@ static int read_scalars(dab_handle* h) {
   HIP_OK(hipMemcpyAsync(h->h_scal, h->d_scal, sizeof(double) * S_NSLOTS, hipMemcpyDeviceToHost, h->stream));
   HIP_OK(hipMemcpyAsync(h->h_flags, h->d_flags, sizeof(int) * 4, hipMemcpyDeviceToHost, h->stream));
   HIP_OK(hipStreamSynchronize(h->stream));
+  // a one-shot all-reduce that gave up waiting for a peer poisons its output: stop here,
+  // before any decision is taken on it (every rank's next call fails the same way)
+  CHECK_RC(p2p_check(h->p2p_main));
+  CHECK_RC(p2p_check(h->p2p_comm));
   if (h->cost_fx_pending) {
     // the last evaluation pass left its cost in fixed point (cost_fx_commit): exact
     // integer limb sums, converted once here
@@ -2218,6 +2263,11 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
     CHECK_RC(h->allreduce(h->d_scal + S_MODEL, 5, ncclSum));
     CHECK_RC(h->allreduce_max_i32(h->d_flags, 4));
     CHECK_RC(read_scalars(h));
+    // bit 2 of the Cholesky flag: a bounded wait inside the factorisation gave up (a
+    // scheduling / residency fault, not a property of the matrix): an error, not a
+    // rejected step (bit 1 = not positive definite)
+    if (!use_pcg && NC > 0 && (h->h_flags[1] & 2))
+      return set_error(DAB_E_DEVICE, "dense Cholesky: a bounded wait between work-groups timed out");
     const double tdone = now_s();
     sum->linear_solver_time_in_seconds += tre - tls;
     sum->residual_evaluation_time_in_seconds += tdone - tre;
@@ -2299,9 +2349,10 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
   (void)minimum_cost;
   // the accepted iterate is always the lowest-cost one (steps are monotone), so the
   // device-resident x is Ceres' parameters_; write it back (sfm.cc:47-48 semantics)
-  CHECK_RC(dab_get_parameters(h, h->prob.points, h->prob.ext));
-  CHECK_RC(p2p_check(h->p2p_main));  // a one-shot all-reduce that gave up waiting for a peer
+  HIP_OK(hipStreamSynchronize(s));
+  CHECK_RC(p2p_check(h->p2p_main));  // fail closed: the caller's arrays stay untouched
   CHECK_RC(p2p_check(h->p2p_comm));
+  CHECK_RC(dab_get_parameters(h, h->prob.points, h->prob.ext));
   sum->total_time_in_seconds = now_s() - t_start;
   return 0;
 }
@@ -2453,6 +2504,12 @@ static int collect_bench_events(dab_handle* h) {
     h->bench_jac_ms += b;
     h->bench_asm_ms += a + c;
     h->bench_count++;
+    if (h->bench_pair_rec[i]) {
+      float d = 0.f;
+      HIP_OK(hipEventElapsedTime(&d, ev[4], ev[5]));  // pair-major camera kernel
+      h->bench_pair_ms += d;
+      h->bench_pair_count++;
+    }
   }
   h->bench_pending = 0;
   return 0;
@@ -2469,6 +2526,11 @@ extern "C" int dab_bench_eval_pass(dab_handle* h, int with_assembly, int count) 
   // would distort the throughput it measures. DAB_BENCH_SAMPLE overrides (0 = no events).
   const int sample = h->knobs.bench_sample;
   for (int step = 0; step < count; ++step) {
+    // every bench pass is an evaluation at a NEW linearization point, as in the LM loop
+    // after an accepted step (sfm.cc:66-73, Ceres re-linearises each iteration): whatever
+    // the pass derives from the points (the camera-major copy of fused_stream = 1) is
+    // rebuilt inside the pass
+    ++h->pts_version;
     if (sample <= 0 || step % sample != 0) {
       CHECK_RC(eval_pass(h, false));
       CHECK_RC(h->allreduce_cost());
@@ -2479,16 +2541,21 @@ extern "C" int dab_bench_eval_pass(dab_handle* h, int with_assembly, int count) 
     if (h->bench_pending >= (int)h->bench_ev.size()) {
       if (h->bench_pending >= 4096) CHECK_RC(collect_bench_events(h));
       while ((int)h->bench_ev.size() <= h->bench_pending) {
-        std::array<hipEvent_t, 4> e{};
+        std::array<hipEvent_t, 6> e{};
         // timing-only events: no system-scope fence (it costs several us per record)
         for (auto& x : e) HIP_OK(hipEventCreateWithFlags(&x, hipEventDisableSystemFence));
         h->bench_ev.push_back(e);
       }
     }
-    const auto& ev = h->bench_ev[h->bench_pending++];
+    h->bench_pair_rec.resize(h->bench_ev.size());
+    const int slot = h->bench_pending++;
+    const auto& ev = h->bench_ev[slot];
+    h->bench_pair_rec[slot] = 0;
     HIP_OK(hipEventRecord(ev[0], s));
     if (with_assembly) {
-      CHECK_RC(eval_pass(h, false, ev[1], ev[2]));
+      bool prec = false;
+      CHECK_RC(eval_pass(h, false, ev[1], ev[2], ev[4], ev[5], &prec));
+      h->bench_pair_rec[slot] = prec;
       CHECK_RC(h->allreduce_cost());
     } else {
       if (eval_points_needs_camtab(h->eval_wps)) launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
@@ -2520,8 +2587,22 @@ extern "C" int dab_bench_kernel_ms(dab_handle* h, double* jac_ms, double* assemb
   const double n = h->bench_count > 0 ? h->bench_count : 1;
   if (jac_ms) *jac_ms = h->bench_jac_ms / n;
   if (assembly_ms) *assembly_ms = h->bench_asm_ms / n;
-  h->bench_jac_ms = h->bench_asm_ms = 0;
-  h->bench_count = 0;
+  h->last_pair_ms = h->bench_pair_count > 0 ? h->bench_pair_ms / h->bench_pair_count : 0.0;
+  h->bench_jac_ms = h->bench_asm_ms = h->bench_pair_ms = 0;
+  h->bench_count = h->bench_pair_count = 0;
+  return 0;
+}
+
+extern "C" int dab_bench_pair_ms(dab_handle* h, double* ms, double* bytes) {
+  clear_error();
+  if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
+  // Algorithmic bytes of one k_eval_pair launch (the rig's composed observations whose two
+  // cameras are free, pair-major): per observation the 16-B pixel and three index words
+  // (point, arc, ring; the intrinsic is the arc's), the 24-B point once per distinct point
+  // the pass touches, and per chunk its 90 sums out (two camera halves + the cross block).
+  // The point array is read, in this order, by random gathers.
+  if (ms) *ms = h->last_pair_ms;
+  if (bytes) *bytes = h->pair_eval ? h->pair_bytes : 0.0;
   return 0;
 }
 
@@ -2540,17 +2621,12 @@ extern "C" int dab_jacobian_bytes(dab_handle* h, double* bytes) {
   // point index + pixel; the chunk's camera and intrinsic are per block). A deterministic
   // matrix-free pass needs both traversal orders (point-major for V, g; camera-major for
   // U, g_c: no atomics, no per-observation partials), so both reads are algorithmic.
-  // The streamed fused form reads, per observation, a packed 4-B record (ext | intr) + the
-  // 16-B pixel on the point side and, per entry, the camera-major point copy (24 B) + the
-  // pixel on the camera side (no index, no gather).
-  const double ext_b = eval_points_needs_camtab(h->eval_wps) ? 96.0 : 48.0;
-  double b = (24.0 + 72.0) * h->NP + ext_b * h->E + 48.0 * h->NI;
-  if (h->fused && h->d_cmx) {
-    b += 216.0 * h->NC + 40.0 * h->NE + 20.0 * h->N;
-  } else {
-    if (h->fused) b += 216.0 * h->NC + 20.0 * h->NE;
-    for (int o = 0; o < h->N; ++o) b += 16.0 + 4.0 * (h->prob.obs_ext1[o] >= 0 ? 3 : 2);
-  }
+  // This is the minimal count whatever the implementation reads: no denormalised copies
+  // (the camera-major point copy of fused_stream = 1 is not counted), no re-gathers of a
+  // point, each traversal's index words once.
+  double b = (24.0 + 72.0) * h->NP + 48.0 * h->E + 48.0 * h->NI;
+  if (h->fused) b += 216.0 * h->NC + 20.0 * h->NE;
+  for (int o = 0; o < h->N; ++o) b += 16.0 + 4.0 * (h->prob.obs_ext1[o] >= 0 ? 3 : 2);
   *bytes = b;
   return 0;
 }

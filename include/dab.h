@@ -247,6 +247,11 @@ int dab_sync(dab_handle* h);
 int dab_bench_kernel_ms(dab_handle* h, double* jac_ms, double* assembly_ms);
 /* Algorithmic HBM bytes of one residual+Jacobian launch on the resident problem. */
 int dab_jacobian_bytes(dab_handle* h, double* bytes);
+/* The rig's pair-major camera kernel (k_eval_pair; composed observations with both
+ * cameras free): its average device time (ms) over the sampled passes of the batches read
+ * by the last dab_bench_kernel_ms call, and its algorithmic bytes per launch (0 when the
+ * resident problem has no pair-major pass). */
+int dab_bench_pair_ms(dab_handle* h, double* ms, double* bytes);
 /* Which evaluation schedule the resident problem uses: *fused = 1 when the pass is the
  * single fused launch (k_eval_fused: camera and point side together), 2 when it is the
  * same kernel as a camera-side then a point-side launch (several ranks: the camera blocks'

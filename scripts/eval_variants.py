@@ -15,7 +15,7 @@ import _pkgload  # noqa: E402
 
 pkg = _pkgload.load()
 cfg = sys.argv[1]
-variants = sys.argv[2:]  # DAB_EVAL_WPS values (two-kernel pass), "fused[ABL]", "stream[V]" or "split"
+variants = sys.argv[2:]  # DAB_EVAL_WPS values (two-kernel pass), "fused[ABL]", "gather", "stream[V]" or "split"
 base = pkg.synth(**pkg.CONFIGS[cfg])
 ref = None
 for wps in variants:
@@ -30,6 +30,12 @@ for wps in variants:
         os.environ["DAB_FUSED_STREAM"] = "0"
         os.environ["DAB_FUSED_TAB"] = "0"
         os.environ["DAB_FUSED_ABL"] = wps[5:] or "0"
+        os.environ.pop("DAB_EVAL_WPS", None)
+    elif wps == "gather":  # packed point-side records, camera waves gathering the points (default)
+        os.environ["DAB_EVAL_FUSED"] = "1"
+        os.environ["DAB_FUSED_STREAM"] = "2"
+        os.environ["DAB_FUSED_TAB"] = "0"
+        os.environ.pop("DAB_FUSED_ABL", None)
         os.environ.pop("DAB_EVAL_WPS", None)
     elif wps.startswith(("stream", "tab")):  # streamed fused form, stream<DAB_FUSED_V> / tab<V> (tables read)
         os.environ["DAB_EVAL_FUSED"] = "1"

@@ -61,3 +61,20 @@ def test_rccl_one_rank_per_gpu(gpu):
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     assert "DIST_CHECK OK" in p.stdout, p.stdout[-3000:]
+
+
+def test_p2p_missed_call_fails_closed(gpu):
+    """A peer that misses one peer-to-peer all-reduce (DAB_P2P_SKIP_CALL on rank 1) must not
+    leave the other rank summing stale slots: the waiting call times out (3 s here), writes
+    poison instead of a sum, every later call fails at once, and BOTH ranks' dab_solve
+    return DAB_E_COMM with the caller's parameter arrays untouched (scripts/p2p_fail_check.py)."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "scripts", "p2p_fail_check.py")]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "P2P_FAIL_CHECK OK" in p.stdout, p.stdout[-3000:] + p.stderr[-3000:]

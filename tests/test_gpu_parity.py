@@ -384,6 +384,8 @@ def test_fused_camera_frame_small_angles(pkg, gpu, monkeypatch):
     assert sched == [1, 0]
     a, b = res
     assert [it["success"] for it in a["iterations"]] == [it["success"] for it in b["iterations"]]
+    assert [it["linear_solver_iterations"] for it in a["iterations"]] == \
+        [it["linear_solver_iterations"] for it in b["iterations"]]
     # accepted costs to 1e-10; the rejected candidates here are wild steps (costs ~1e23 from
     # ~1e7) whose cost amplifies the regrouped U, g_c rounding, so they get 1e-8
     for x, y in zip(a["iterations"], b["iterations"]):
