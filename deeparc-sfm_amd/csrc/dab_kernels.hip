@@ -1923,7 +1923,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
                                                      unsigned long long* __restrict__ fx_next,
                                                      const double* __restrict__ cmx,
                                                      const double* __restrict__ camtab, int wpc, int wps,
-                                                     int wxor) {
+                                                     int wxor, int side = 0) {
   __shared__ double rt_s[kLdsCams * 12];
   __shared__ double k_s[kLdsCams * 6];
   __shared__ double csum[kFusedCW][27];     // camera waves' sums: [camera slot * wpc + part][component]
@@ -1946,7 +1946,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
     if constexpr (ABL == 22) __builtin_amdgcn_s_setprio(2);
     const int cw = wave - kFusedPW, slot = cw / wpc, part = cw - slot * wpc;
     const int c = slot * gridDim.x + blockIdx.x;  // one round (fused_eval_fits / fused_wpc)
-    if (c >= v.NC || ABL == 1 || ABL == 15) return;
+    if (c >= v.NC || ABL == 1 || ABL == 15 || side == 1) return;
     const int b = chunk_beg[c], e = chunk_beg[c + 1];
     const int lo = b + (int)(((long long)(e - b) * part) / wpc), hi = b + (int)(((long long)(e - b) * (part + 1)) / wpc);
     const int2 u = v.chunk_uni[c];
@@ -1994,6 +1994,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
 
   // ---------------- point side ----------------
   if constexpr (ABL == 2 || ABL == 25) return;
+  if (side == 2) return;
   if constexpr (ABL == 21) __builtin_amdgcn_s_setprio(2);
   const size_t NPs = (size_t)v.NP;
   // wps point waves per slice (1 at C3; more for small problems, whose slices would
@@ -2263,10 +2264,10 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
   }
   if (v.obs_e) {
     // packed point-side records, camera waves gathering the points (nothing to refresh
-    // when the points move)
-    if (side == 1) k_eval_fused<3, 1, 3, true, false, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-    else if (side == 2) k_eval_fused<3, 2, 3, true, false, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-    else k_eval_fused<3, 0, 3, true, false, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
+    // when the points move). The multi-rank split schedule runs THIS instantiation with a
+    // run-time side, so both schedules execute the same machine code (the same fp
+    // contraction, hence bitwise the same sums).
+    k_eval_fused<3, 0, 3, true, false, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS, side);
     return;
   }
   // one side only (the multi-rank split schedule): the same kernel with the other side's
