@@ -94,6 +94,40 @@ void DabScene::build(DeepArcManager& m, bool freeze_camera) {
   problem.freeze_camera = freeze_camera ? 1 : 0;
 }
 
+void DabScene::refresh_values(DeepArcManager& m) {
+  std::vector<Point3d*>& pts = *m.point3ds();
+  std::vector<Extrinsic*>& exts = *m.extrinsics();
+  for (size_t i = 0; i < pts.size(); ++i)
+    for (int k = 0; k < 3; ++k) points[3 * i + k] = pts[i]->position()[k];
+  for (size_t i = 0; i < exts.size(); ++i)
+    for (int k = 0; k < 3; ++k) {
+      ext[6 * i + k] = exts[i]->rotation()[k];
+      ext[6 * i + 3 + k] = exts[i]->translation()[k];
+    }
+}
+
+int DabSession::ensure(DeepArcManager& m, int want_freeze) {
+  const bool same = resident && version == m.structureVersion() && n_blocks == m.parameters()->size() &&
+                    n_points == m.point3ds()->size() && n_ext == m.extrinsics()->size() &&
+                    n_intr == m.intrinsics()->size() && (want_freeze < 0 || (want_freeze != 0) == freeze);
+  if (same) {  // structure resident: the values may have changed on the host
+    scene.refresh_values(m);
+    return dab_update_parameters(handle.h, scene.points.data(), scene.ext.data());
+  }
+  resident = false;
+  freeze = want_freeze > 0;
+  scene.build(m, freeze);  // throws const char* on a block that references a foreign parameter
+  const int rc = dab_set_problem(handle.h, &scene.problem);
+  if (rc) return rc;
+  resident = true;
+  version = m.structureVersion();
+  n_blocks = m.parameters()->size();
+  n_points = m.point3ds()->size();
+  n_ext = m.extrinsics()->size();
+  n_intr = m.intrinsics()->size();
+  return 0;
+}
+
 void DabScene::write_back(DeepArcManager& m) {
   std::vector<Point3d*>& pts = *m.point3ds();
   std::vector<Extrinsic*>& exts = *m.extrinsics();

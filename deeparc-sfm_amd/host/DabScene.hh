@@ -20,6 +20,8 @@ struct DabScene {
   void build(DeepArcManager& m, bool freeze_camera);
   // parameter values back into the manager's Point3d / Extrinsic storage
   void write_back(DeepArcManager& m);
+  // the manager's current parameter values into points / ext (same structure as build)
+  void refresh_values(DeepArcManager& m);
 };
 
 // RAII device handle on the device named by $DAB_DEVICE (default 0).
@@ -29,6 +31,22 @@ struct DabHandle {
   ~DabHandle();
   DabHandle(const DabHandle&) = delete;
   DabHandle& operator=(const DabHandle&) = delete;
+};
+
+// The manager's resident problem: one handle for the manager's lifetime; the problem set
+// on it is valid while (version, freeze, sizes) match the manager (DeepArcManager::
+// dabSession). ensure() re-marshals and re-sets the problem when they do not, and only
+// uploads the parameter values when they do.
+struct DabSession {
+  DabHandle handle;
+  DabScene scene;
+  bool resident = false;
+  bool freeze = false;
+  unsigned long long version = 0;
+  size_t n_blocks = 0, n_points = 0, n_ext = 0, n_intr = 0;
+  // freeze < 0: any constancy will do (the filter's residual pass). Returns 0 or a DAB_E_*
+  // code; throws const char* when a block references a parameter the manager does not own.
+  int ensure(DeepArcManager& m, int freeze);
 };
 
 // throws the library's message as const char* (the reference throws const char*,

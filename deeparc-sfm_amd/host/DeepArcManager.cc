@@ -31,6 +31,11 @@ void Extrinsic::rotationMatrix(double R[9]) { dab::AngleAxisToRotationMatrix(rot
 
 DeepArcManager::~DeepArcManager() { clear(); }
 
+DabSession& DeepArcManager::dabSession() {
+  if (!session_) session_.reset(new DabSession());
+  return *session_;
+}
+
 void DeepArcManager::clear() {
   for (ParameterBlock* b : params_) delete b;
   for (Point3d* p : point3d_) delete p;
@@ -54,6 +59,7 @@ bool DeepArcManager::read(std::string filename) {
     throw "Cannot read input file";
   }
   clear();
+  ++structure_version_;
   (void)take<double>(f);  // version
   const int n_blocks = take<int>(f), n_intr = take<int>(f), n_arc = take<int>(f), n_ring = take<int>(f),
             n_points = take<int>(f);
@@ -287,11 +293,11 @@ void DeepArcManager::filterPoint3d(double error_boundary, double* hemisphere_cen
   // device: residual per observation, the mse test, the empty-point and hemisphere tests
   std::vector<uint8_t> keep_obs(params_.size(), 1), keep_pt(point3d_.size(), 1);
   if (!params_.empty()) {
-    DabScene scene;
-    scene.build(*this, false);
-    DabHandle dh;
-    dab_check(dab_set_problem(dh.h, &scene.problem));
-    dab_check(dab_filter(dh.h, error_boundary, hemisphere_center, hemisphere_radius, keep_obs.data(),
+    // on the resident problem of the last solve when the structure is unchanged (the
+    // residual pass does not depend on the constancy): no set-up, values refreshed only
+    DabSession& S = dabSession();
+    dab_check(S.ensure(*this, -1));
+    dab_check(dab_filter(S.handle.h, error_boundary, hemisphere_center, hemisphere_radius, keep_obs.data(),
                          keep_pt.data(), nullptr, nullptr));
   } else {
     std::fill(keep_pt.begin(), keep_pt.end(), 0);  // no observations: every point is empty
@@ -312,5 +318,7 @@ void DeepArcManager::filterPoint3d(double error_boundary, double* hemisphere_cen
       delete point3d_[i];
     }
   }
+  const bool changed = w != point3d_.size() || params_.size() != keep_obs.size();
   point3d_.resize(w);
+  if (changed) ++structure_version_;  // the resident problem no longer matches
 }

@@ -5,11 +5,14 @@
 // the reference's order, so the surviving blocks and points are the reference's.
 #pragma once
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "Geometry.hh"
 #include "ParameterBlock.hh"
+
+struct DabSession;  // DabScene.hh: the manager's resident libdab problem (handle reuse)
 
 class DeepArcManager {
  public:
@@ -37,8 +40,17 @@ class DeepArcManager {
   std::vector<Extrinsic*>* extrinsics() { return &extrinsics_; }
   int arcSize() const { return arc_size_; }
   int ringSize() const { return ring_size_; }
+  // One libdab handle per manager, kept across solve() / filterPoint3d() (the sfm.cc loop,
+  // sfm.cc:104-129): the problem stays resident on the device while the manager's
+  // structure is unchanged, so a filter after a solve, or a solve of unchanged structure,
+  // only refreshes the parameter values. structureVersion() changes whenever read() or
+  // filterPoint3d() change the blocks or points.
+  DabSession& dabSession();
+  unsigned long long structureVersion() const { return structure_version_; }
 
  private:
+  std::unique_ptr<DabSession> session_;
+  unsigned long long structure_version_ = 0;
   int arc_size_ = 0, ring_size_ = 0;
   bool share_extrinsic_ = false;
   std::map<int, std::map<int, Camera*> > hemisphere_;

@@ -172,4 +172,26 @@ int dam_run_pipeline(const char* input, const char* output, const char* ply_pref
   });
 }
 
+int dam_run_pipeline_report(const char* input, const char* output, const char* ply_prefix, int32_t max_iteration,
+                            int32_t max_second, double error_boundary, int32_t quiet, dam_pipeline_report* out) {
+  return guarded([&] {
+    PipelineReport r = runPipeline(input, output ? output : "", ply_prefix ? ply_prefix : "", max_iteration,
+                                   max_second, error_boundary, quiet == 0);
+    if (out) {
+      for (int k = 0; k < 3; ++k) out->hemisphere_center[k] = r.hemisphere_center[k];
+      out->hemisphere_radius = r.hemisphere_radius;
+      out->rounds = r.rounds;
+      out->final_blocks = r.final_blocks;
+      out->final_points = r.final_points;
+      out->solves = r.solves;
+      out->lm_iterations = r.lm_iterations;
+      out->reserved = 0;
+      out->final_cost = r.final_cost;
+      out->solve_seconds = r.solve_seconds;
+      out->filter_seconds = r.filter_seconds;
+      out->total_seconds = r.total_seconds;
+    }
+  });
+}
+
 }  // extern "C"

@@ -2,6 +2,7 @@
 #include "sfm.hh"
 
 #include <cfloat>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <functional>
@@ -10,11 +11,13 @@
 #include "DabScene.hh"
 
 int solveWith(DeepArcManager& m, const dab_options& options, bool freeze_camera, dab_summary* summary) {
-  DabScene scene;
-  scene.build(m, freeze_camera);
-  DabHandle dh;
-  int rc = dab_set_problem(dh.h, &scene.problem);
+  // the manager's resident problem (handle reused across the sfm.cc loop's solves and
+  // filters; re-set only when the structure or the constancy changed)
+  DabSession& S = m.dabSession();
+  int rc = S.ensure(m, freeze_camera ? 1 : 0);
   if (rc) return rc;
+  DabHandle& dh = S.handle;
+  DabScene& scene = S.scene;
   dab_summary local{};
   dab_summary* s = summary ? summary : &local;
   rc = dab_solve(dh.h, &options, s);
@@ -29,24 +32,39 @@ int solveWith(DeepArcManager& m, const dab_options& options, bool freeze_camera,
     o.linear_solver_type = DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG;
     rc = dab_solve(dh.h, &o, s);
   }
-  if (rc) return rc;
+  if (rc) {
+    S.resident = false;  // a failed solve leaves the device state unspecified
+    return rc;
+  }
   scene.write_back(m);  // dab_solve wrote the optimised values into scene.points / ext
   return 0;
 }
 
-void solve(DeepArcManager& deeparcManager, int max_iteration, int max_second, bool freeze_camera) {
+namespace {
+// solve() of sfm.cc:31-75 with the reference's options; verbose: its progress and summary
+dab_summary solve_opts(DeepArcManager& m, int max_iteration, int max_second, bool freeze_camera, bool verbose) {
   dab_options o;
   dab_options_init(&o);
   o.linear_solver_type = DAB_LINEAR_SOLVER_EXPLICIT_SCHUR;  // sfm.cc:67 DENSE_SCHUR
-  o.minimizer_progress_to_stdout = 1;                       // sfm.cc:68
+  o.minimizer_progress_to_stdout = verbose ? 1 : 0;         // sfm.cc:68
   o.max_num_iterations = max_iteration;                     // sfm.cc:69
   o.num_threads = 16;                                       // sfm.cc:70 (unused on the GPU)
   o.max_solver_time_in_seconds = max_second;                // sfm.cc:71
   dab_summary s{};
-  dab_check(solveWith(deeparcManager, o, freeze_camera, &s));
-  std::printf("Solver Summary: %s, initial cost %.6e, final cost %.6e, %d iterations (%d successful), %s\n",
-              s.linear_solver_type_used == DAB_LINEAR_SOLVER_EXPLICIT_SCHUR ? "DENSE_SCHUR" : "ITERATIVE_SCHUR (PCG)",
-              s.initial_cost, s.final_cost, s.num_iterations, s.num_successful_steps, s.message);
+  dab_check(solveWith(m, o, freeze_camera, &s));
+  if (verbose)
+    std::printf("Solver Summary: %s, initial cost %.6e, final cost %.6e, %d iterations (%d successful), %s\n",
+                s.linear_solver_type_used == DAB_LINEAR_SOLVER_EXPLICIT_SCHUR ? "DENSE_SCHUR" : "ITERATIVE_SCHUR (PCG)",
+                s.initial_cost, s.final_cost, s.num_iterations, s.num_successful_steps, s.message);
+  return s;
+}
+double now_seconds() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+}  // namespace
+
+void solve(DeepArcManager& deeparcManager, int max_iteration, int max_second, bool freeze_camera) {
+  (void)solve_opts(deeparcManager, max_iteration, max_second, freeze_camera, true);
 }
 
 // ---- small dense trust-region LM with Ceres semantics ---------------------
@@ -206,23 +224,39 @@ void fitHemisphere(const std::vector<std::vector<double> >& centers, double cent
 }
 
 PipelineReport runPipeline(const std::string& input, const std::string& output, const std::string& ply_prefix,
-                           int max_iteration, int max_second, double error_boundary) {
+                           int max_iteration, int max_second, double error_boundary, bool verbose) {
+  const double t_start = now_seconds();
   DeepArcManager m;
   m.read(input);
   PipelineReport rep{};
   double center[3] = {0, 0, 0}, radius = 1.0;  // sfm.cc:87-88
   fitHemisphere(m.getCameraCenter(), center, &radius);
   if (!ply_prefix.empty()) m.writePly(ply_prefix + "init.ply");
-  solve(m, max_iteration, max_second, true);  // sfm.cc:111: points only
-  m.filterPoint3d(error_boundary, center, radius);
+  // the manager keeps one libdab handle: each filter runs on the problem its solve left
+  // resident, and each solve after a filter re-sets the compacted problem on that handle
+  auto do_solve = [&](bool freeze) {
+    const double t = now_seconds();
+    const dab_summary s = solve_opts(m, max_iteration, max_second, freeze, verbose);
+    rep.solve_seconds += now_seconds() - t;
+    rep.solves++;
+    rep.lm_iterations += s.num_iterations;
+    rep.final_cost = s.final_cost;
+  };
+  auto do_filter = [&]() {
+    const double t = now_seconds();
+    m.filterPoint3d(error_boundary, center, radius);
+    rep.filter_seconds += now_seconds() - t;
+  };
+  do_solve(true);  // sfm.cc:111: points only
+  do_filter();
   int step = 0;
   if (!ply_prefix.empty()) m.writePly(ply_prefix + std::to_string(step) + ".ply");
   int old_points = 1, cur_points = 10000000;  // sfm.cc:106
   while (cur_points != old_points) {
     ++step;
     old_points = cur_points;
-    solve(m, max_iteration, max_second);
-    m.filterPoint3d(error_boundary, center, radius);
+    do_solve(false);
+    do_filter();
     cur_points = (int)m.point3ds()->size();
     if (!ply_prefix.empty()) m.writePly(ply_prefix + std::to_string(step) + ".ply");
   }
@@ -233,5 +267,6 @@ PipelineReport runPipeline(const std::string& input, const std::string& output, 
   rep.rounds = step;
   rep.final_blocks = (int)m.parameters()->size();
   rep.final_points = (int)m.point3ds()->size();
+  rep.total_seconds = now_seconds() - t_start;
   return rep;
 }

@@ -29,8 +29,13 @@ void fitHemisphere(const std::vector<std::vector<double> >& centers, double cent
 struct PipelineReport {
   double hemisphere_center[3], hemisphere_radius;
   int rounds, final_blocks, final_points;
+  int solves = 0, lm_iterations = 0;  // solve() calls, LM iterations summed over them
+  double final_cost = 0.0;            // the last solve's final cost
+  double solve_seconds = 0.0, filter_seconds = 0.0, total_seconds = 0.0;
 };
 // sfm.cc main() without the hard-coded paths: reads `input`, writes the outputs whose
-// names are non-empty (PLY snapshots are skipped when ply_prefix is empty).
+// names are non-empty (PLY snapshots are skipped when ply_prefix is empty). verbose: the
+// per-iteration progress and the per-solve summary line the reference prints.
 PipelineReport runPipeline(const std::string& input, const std::string& output, const std::string& ply_prefix,
-                           int max_iteration = 100, int max_second = 3600, double error_boundary = 5.0);
+                           int max_iteration = 100, int max_second = 3600, double error_boundary = 5.0,
+                           bool verbose = true);

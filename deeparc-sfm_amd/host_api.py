@@ -18,6 +18,14 @@ HOST_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdee
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int32)
 
+class PipelineReport(C.Structure):  # dam_pipeline_report
+    _fields_ = [("hemisphere_center", C.c_double * 3), ("hemisphere_radius", C.c_double),
+                ("rounds", C.c_int32), ("final_blocks", C.c_int32), ("final_points", C.c_int32),
+                ("solves", C.c_int32), ("lm_iterations", C.c_int32), ("reserved", C.c_int32),
+                ("final_cost", C.c_double), ("solve_seconds", C.c_double), ("filter_seconds", C.c_double),
+                ("total_seconds", C.c_double)]
+
+
 SIGNATURES = {
     "dam_last_error": (C.c_char_p, []),
     "dam_create": (C.c_int, [C.POINTER(C.c_void_p)]),
@@ -36,6 +44,8 @@ SIGNATURES = {
     "dam_fit_hemisphere": (C.c_int, [_dp, C.c_int32, _dp, _dp, C.c_int32]),
     "dam_run_pipeline": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int32, C.c_int32, C.c_double,
                                    _dp, _ip]),
+    "dam_run_pipeline_report": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int32, C.c_int32, C.c_double,
+                                          C.c_int32, C.POINTER(PipelineReport)]),
 }
 
 _LIB = None
@@ -161,3 +171,17 @@ def run_pipeline(input_path, output_path="", ply_prefix="", max_iteration=100, m
                                 _p(counts, C.c_int32)))
     return dict(hemisphere_center=hemi[:3].copy(), hemisphere_radius=float(hemi[3]), rounds=int(counts[0]),
                 blocks=int(counts[1]), points=int(counts[2]))
+
+
+def run_pipeline_report(input_path, output_path="", ply_prefix="", max_iteration=100, max_second=3600,
+                        error_boundary=5.0, quiet=True):
+    """run_pipeline with the full report (solves, LM iterations, last cost, host timings);
+    quiet suppresses the reference's per-iteration progress lines."""
+    lib = load_host_library()
+    r = PipelineReport()
+    _check(lib.dam_run_pipeline_report(os.fsencode(input_path), os.fsencode(output_path), os.fsencode(ply_prefix),
+                                       max_iteration, max_second, error_boundary, 1 if quiet else 0, C.byref(r)))
+    return dict(hemisphere_center=np.array(r.hemisphere_center[:]), hemisphere_radius=r.hemisphere_radius,
+                rounds=r.rounds, blocks=r.final_blocks, points=r.final_points, solves=r.solves,
+                lm_iterations=r.lm_iterations, final_cost=r.final_cost, solve_seconds=r.solve_seconds,
+                filter_seconds=r.filter_seconds, total_seconds=r.total_seconds)

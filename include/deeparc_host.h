@@ -58,6 +58,17 @@ int dam_fit_hemisphere(const double* centers, int32_t n, double center[3], doubl
  * may be empty strings */
 int dam_run_pipeline(const char* input, const char* output, const char* ply_prefix, int32_t max_iteration,
                      int32_t max_second, double error_boundary, double hemi_out[4], int32_t counts_out[3]);
+/* the same loop with a full report; quiet != 0 suppresses the per-iteration progress and
+ * the per-solve summary lines the reference prints */
+typedef struct dam_pipeline_report {
+  double hemisphere_center[3], hemisphere_radius;
+  int32_t rounds, final_blocks, final_points, solves;
+  int32_t lm_iterations, reserved;  /* LM iterations summed over the solves */
+  double final_cost;                /* the last solve's final cost */
+  double solve_seconds, filter_seconds, total_seconds;
+} dam_pipeline_report;
+int dam_run_pipeline_report(const char* input, const char* output, const char* ply_prefix, int32_t max_iteration,
+                            int32_t max_second, double error_boundary, int32_t quiet, dam_pipeline_report* out);
 
 #ifdef __cplusplus
 }

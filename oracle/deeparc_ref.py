@@ -338,18 +338,20 @@ def solve_scene(pkg, s, max_iteration=1000, max_second=3600, freeze_camera=False
     return summ
 
 
-def run_pipeline(pkg, path, max_iteration=100, error_boundary=5.0):
+def run_pipeline(pkg, path, max_iteration=100, error_boundary=5.0, num_threads=8):
     """sfm.cc main() (lines 79-129) without the PLY snapshots; returns (scene, report)."""
     s = read_deeparc(path)
     c, R = hemisphere_fit(camera_centers(s))
-    solve_scene(pkg, s, max_iteration, freeze_camera=True)
+    summ = solve_scene(pkg, s, max_iteration, freeze_camera=True, num_threads=num_threads)
+    solves, its = 1, summ["num_iterations"]
     filter_point3d(pkg, s, error_boundary, c, R)
     old, cur, step = 1, 10000000, 0
     while cur != old:
         step += 1
         old = cur
-        solve_scene(pkg, s, max_iteration)
+        summ = solve_scene(pkg, s, max_iteration, num_threads=num_threads)
+        solves, its = solves + 1, its + summ["num_iterations"]
         filter_point3d(pkg, s, error_boundary, c, R)
         cur = len(s["points"])
     return s, dict(hemisphere_center=c, hemisphere_radius=R, rounds=step, blocks=len(s["blocks"]),
-                   points=len(s["points"]))
+                   points=len(s["points"]), solves=solves, lm_iterations=its, final_cost=summ["final_cost"])

@@ -92,10 +92,14 @@ def test_pipeline_matches_oracle(pkg, host, ref, gpu, tmp_path):
     path = tmp_path / "rig.deeparc"
     path.write_text(gen.problem_to_deeparc(prob, True, 4, 8, [3], np.random.default_rng(0)))
     out = tmp_path / "out.deeparc"
-    rep = host.run_pipeline(str(path), str(out), max_iteration=50)
+    rep = host.run_pipeline_report(str(path), str(out), max_iteration=50)
     s, orep = ref.run_pipeline(pkg, str(path), max_iteration=50)
     assert rep["rounds"] == orep["rounds"]
     assert (rep["blocks"], rep["points"]) == (orep["blocks"], orep["points"])
+    # one handle for the whole loop (filters on the solves' resident problems): the same
+    # solves, LM iterations and last cost as the oracle's fresh problem per call
+    assert (rep["solves"], rep["lm_iterations"]) == (orep["solves"], orep["lm_iterations"])
+    assert rep["final_cost"] == pytest.approx(orep["final_cost"], rel=1e-9, abs=1e-9)
     np.testing.assert_allclose(rep["hemisphere_center"], orep["hemisphere_center"], rtol=1e-9, atol=1e-12)
     m = host.DeepArcManager()
     m.read(str(out))
