@@ -379,8 +379,34 @@ struct dab_handle {
   int eval_wps = 0;   // 0: LDS tables; else waves per slice (DAB_EVAL_WPS tuning knob)
   bool fused = false;  // evaluation pass as one launch (launch_eval_fused; DAB_EVAL_FUSED=0 disables)
 
+  // Buffers kept across dab_set_problem while the new problem's size fits: the dense S, the
+  // camera step and the flags. The Cholesky's captured graph is keyed on their addresses, so
+  // a problem re-set with the same camera count (the sfm.cc loop after every filter round)
+  // replays the graph instead of capturing a new one.
+  struct Sticky {
+    void* p = nullptr;
+    size_t cap = 0;
+  };
+  Sticky st_S, st_yc, st_flags;
+  template <class T>
+  int sticky(Sticky& st, T** out, size_t n) {
+    const size_t bytes = std::max<size_t>(1, n) * sizeof(T);
+    if (bytes > st.cap) {
+      if (st.p) (void)hipFree(st.p);
+      st.p = nullptr;
+      st.cap = 0;
+      if (hipMalloc(&st.p, bytes) != hipSuccess)
+        return set_error(DAB_E_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
+      st.cap = bytes;
+    }
+    *out = static_cast<T*>(st.p);
+    return 0;
+  }
+
   ~dab_handle() {
     dev.release();
+    for (Sticky* st : {&st_S, &st_yc, &st_flags})
+      if (st->p) (void)hipFree(st->p);
     if (h_scal) (void)hipHostFree(h_scal);
     if (h_flags) (void)hipHostFree(h_flags);
     if (h_pcg_state) (void)hipHostFree(h_pcg_state);
@@ -1235,7 +1261,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   const size_t npart = std::max<size_t>({(size_t)h->nchunk * 27, (size_t)h->nxchunk * 36, (size_t)h->nchunk * 6, 16});
   CHECK_RC(d.alloc(&h->d_partial, npart));
   CHECK_RC(d.alloc(&h->d_xpartial, (size_t)std::max(1, h->nxchunk) * 36));
-  CHECK_RC(d.alloc(&h->d_yc, (size_t)6 * NC));
+  CHECK_RC(h->sticky(h->st_yc, &h->d_yc, (size_t)6 * NC));
   CHECK_RC(d.alloc(&h->d_dp, (size_t)3 * NP));
   CHECK_RC(d.alloc(&h->d_dc, (size_t)6 * NC));
   h->red_grid = grid_for(std::max(h->NS, 3 * NP), 256, 1024);
@@ -1262,7 +1288,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   }
   CHECK_RC(d.alloc(&h->d_gpart, (size_t)std::max(h->red_grid, h->eval_grid) * 4));
   CHECK_RC(d.alloc(&h->d_scal, S_NSLOTS));
-  CHECK_RC(d.alloc(&h->d_flags, 4));
+  CHECK_RC(h->sticky(h->st_flags, &h->d_flags, 4));
   HIP_OK(hipMemsetAsync(h->d_scal, 0, sizeof(double) * S_NSLOTS, s));  // both fixed-point cost sets start zeroed
   h->fx_last = 1;
   h->cost_fx_pending = false;
@@ -1568,7 +1594,7 @@ static int build_schur_tables(dab_handle* h) {
     const int n = 6 * NC;
     h->lds = ((n + 1 + 7) / 8) * 8;
     if (h->lds % 512 == 0) h->lds += 8;
-    CHECK_RC(h->dev.alloc(&h->d_S, (size_t)(n + 1) * h->lds));
+    CHECK_RC(h->sticky(h->st_S, &h->d_S, (size_t)(n + 1) * h->lds));
     h->mf_grid_n = mf_grid(h->NP, h->ncu);
     phase("tiles: S alloc");
     h->schur_built = true;
@@ -1691,7 +1717,7 @@ static int build_schur_tables(dab_handle* h) {
   const int n = 6 * NC;
   h->lds = ((n + 1 + 7) / 8) * 8;
   if (h->lds % 512 == 0) h->lds += 8;  // avoid power-of-two row strides
-  CHECK_RC(d.alloc(&h->d_S, NC > 0 ? (size_t)(n + 1) * h->lds : 1));
+  CHECK_RC(h->sticky(h->st_S, &h->d_S, NC > 0 ? (size_t)(n + 1) * h->lds : 1));
   // Y as [NE][18] records for k_s_blocks (allocated here so that an OOM surfaces before
   // iteration 0, not mid-solve)
   if (NC > 0) CHECK_RC(d.alloc(&h->d_Yrec, (size_t)kYRec * std::max(1, h->NE)));
