@@ -1175,4 +1175,11 @@ static void enqueue_factor_solve_v1(CholCtx* c, hipStream_t s, int n, double* A,
   }
 }
 
+// Loads this translation unit's code object on the current device now: otherwise the first
+// launch of any of its kernels pays for it (10-40 ms, inside a process's first LM iteration).
+void warm_chol() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k_panel));
+}
+
 }  // namespace dab

@@ -330,4 +330,10 @@ int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
 
 int grid_for(int n, int block, int cap);
 
+// code-object warm-up, one per translation unit (called at handle creation)
+void warm_chol();
+void warm_kernels();
+void warm_pcg();
+void warm_p2p();
+
 }  // namespace dab

@@ -4596,6 +4596,13 @@ void launch_grad_points(hipStream_t s, int NP, const double* x, const double* g,
   k_grad_points<<<grid, 256, 0, s>>>(NP, x, g, partial);
 }
 
+// Loads this translation unit's code object on the current device now: otherwise the first
+// launch of any of its kernels pays for it (10-40 ms, inside a process's first LM iteration).
+void warm_kernels() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k_cam_tables));
+}
+
 }  // namespace dab
 
 #ifdef DAB_TRACE

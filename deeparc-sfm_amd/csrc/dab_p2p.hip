@@ -297,4 +297,11 @@ int p2p_check(P2pComm* c) {
   return 0;
 }
 
+// Loads this translation unit's code object on the current device now: otherwise the first
+// launch of any of its kernels pays for it (10-40 ms, inside a process's first LM iteration).
+void warm_p2p() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k_p2p_allreduce<double, 0>));
+}
+
 }  // namespace dab

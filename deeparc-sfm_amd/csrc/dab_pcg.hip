@@ -855,4 +855,11 @@ void launch_pcg_update(hipStream_t s, int NC, int mode, const double* Ad, const 
   k_pcg_update<<<1, kOneWG, 0, s>>>(NC, mode, Ad, w, xptr, xlist, xcam, X, scale_c, bvec, p, q, x, r, st, Minv, z);
 }
 
+// Loads this translation unit's code object on the current device now: otherwise the first
+// launch of any of its kernels pays for it (10-40 ms, inside a process's first LM iteration).
+void warm_pcg() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k_pcg_setup));
+}
+
 }  // namespace dab

@@ -544,6 +544,7 @@ struct dab_handle {
 // ------------------------------------------------------------------------------------
 // lifecycle
 // ------------------------------------------------------------------------------------
+__global__ void k_scale_points(int NP, const double* __restrict__ V, double* __restrict__ sp, int on);
 static int create_common(int device, dab_handle** out) {
   if (!out) return set_error(DAB_E_INVALID, "null handle pointer");
   int ndev = 0;
@@ -575,6 +576,18 @@ static int create_common(int device, dab_handle** out) {
       hipHostMalloc(reinterpret_cast<void**>(&h->h_flags), sizeof(int) * 4) != hipSuccess) {
     delete h;
     return set_error(DAB_E_NOMEM, "hipHostMalloc failed");
+  }
+  // every code object of the library loaded on this device now, once per process (the first
+  // kernel launch of a translation unit would otherwise pay for it mid-solve)
+  static bool warmed[64] = {};
+  if (device < 64 && !warmed[device]) {
+    warm_kernels();
+    warm_chol();
+    warm_pcg();
+    warm_p2p();
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k_scale_points));
+    warmed[device] = true;
   }
   *out = h;
   return 0;

@@ -25,14 +25,18 @@ import _pkgload  # noqa: E402
 import oracle  # noqa: E402
 
 OUT = os.path.join(ROOT, "tests", "golden", "trajectories.json")
+# final parameters of every record: extrinsics in full, points in full or every k-th point
+# (POINT_STRIDE; the fixture stays a few MB), float64, in tests/golden/trajectory_params.npz
+PARAMS = os.path.join(ROOT, "tests", "golden", "trajectory_params.npz")
+POINT_STRIDE = {"c2_explicit": 1, "c2_pcg": 1, "c3_explicit": 1, "c3_pcg": 8, "c5_explicit": 64, "c5_pcg": 64}
 
 # (record name, config, linear solver, LM iterations). Tolerances are zeroed so that every
 # iteration runs, as in bench.py.
 CASES = [
     ("c2_explicit", "c2_100cam", "explicit", 4),
     ("c2_pcg", "c2_100cam", "pcg", 4),
-    ("c3_explicit", "c3_1kcam", "explicit", 3),
-    ("c3_pcg", "c3_1kcam", "pcg", 3),
+    ("c3_explicit", "c3_1kcam", "explicit", 5),
+    ("c3_pcg", "c3_1kcam", "pcg", 5),
     ("c5_explicit", "c5_rig_16x64", "explicit", 2),
     ("c5_pcg", "c5_rig_16x64", "pcg", 2),
 ]
@@ -59,10 +63,23 @@ def sample_rows(a, n):
     return a[:: max(1, a.shape[0] // n)][:n]
 
 
+def gauge_normalised(points, ext):
+    """The reference's gauge fixes one extrinsic only: the scene's scale
+    stays free, so two correct solvers may drift apart along it by rounding. Points and
+    translations divided by the RMS spread of the points about their centroid; rotations
+    unchanged."""
+    c = points.mean(axis=0)
+    sigma = float(np.sqrt(((points - c) ** 2).sum(axis=1).mean()))
+    e = ext.copy()
+    e[:, 3:] /= sigma
+    return points / sigma, e, sigma
+
+
 def main(names):
     pkg = _pkgload.load()
     threads = min(16, os.cpu_count() or 1)
     out = json.load(open(OUT)) if os.path.exists(OUT) else {}
+    params = dict(np.load(PARAMS)) if os.path.exists(PARAMS) else {}
     probs = {}
     for name, cfg, solver, iters in CASES:
         if names and name not in names:
@@ -81,12 +98,17 @@ def main(names):
             success=[bool(it["success"]) for it in o["iterations"]],
             linear_iterations=[it["linear_solver_iterations"] for it in o["iterations"]],
             final_cost=o["final_cost"],
-            points_sample=sample_rows(prob.points, 64).tolist(), ext_sample=prob.ext[:16].tolist(),
-            oracle_wall_s=wall, oracle_threads=threads)
+            gradient_max_norms=[it["gradient_max_norm"] for it in o["iterations"]],
+            step_norms=[it["step_norm"] for it in o["iterations"]],
+            trust_region_radii=[it["trust_region_radius"] for it in o["iterations"]],
+            point_stride=POINT_STRIDE[name], oracle_wall_s=wall, oracle_threads=threads)
+        params[name + "_points"] = np.ascontiguousarray(prob.points[:: POINT_STRIDE[name]])
+        params[name + "_ext"] = np.ascontiguousarray(prob.ext)
         print(f"{name}: {o['num_iterations']} its, costs {out[name]['costs']}, "
               f"cg {out[name]['linear_iterations']}, {wall:.1f} s", flush=True)
         with open(OUT, "w") as f:
             json.dump(out, f, indent=1)
+        np.savez_compressed(PARAMS, **params)
 
 
 if __name__ == "__main__":
