@@ -255,6 +255,16 @@ class Solver:
               self.lib)
         return r, J
 
+    def filter(self, error_boundary, center, radius):
+        """filterPoint3d's masks on the resident problem (dab_filter): (observation keep,
+        point keep) in the caller's order, uint8."""
+        ok = np.zeros(self.problem.num_obs, np.uint8)
+        pk = np.zeros(self.problem.points.shape[0], np.uint8)
+        c = np.ascontiguousarray(center, np.float64)
+        check(self.lib.dab_filter(self.h, float(error_boundary), _ptr(c, C.c_double), float(radius),
+                                  _ptr(ok, C.c_uint8), _ptr(pk, C.c_uint8), None, None), self.lib)
+        return ok, pk
+
     def get_parameters(self, points, ext):
         check(self.lib.dab_get_parameters(self.h, _ptr(points, C.c_double), _ptr(ext, C.c_double)),
               self.lib)

@@ -92,6 +92,25 @@ CholCtx* chol_create() {
     const int v = atoi(e);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chol_prio), &v, sizeof(int));
   }
+  // the side stream, the barrier word and the graph machinery set up now (each costs
+  // milliseconds the first time; inside a solve they would land in its first LM iteration)
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess || hipMalloc(&c->bar, sizeof(unsigned)) != hipSuccess) {
+    chol_destroy(c);
+    return nullptr;
+  }
+  hipGraph_t g = nullptr;
+  hipGraphExec_t x = nullptr;
+  if (hipStreamBeginCapture(c->side, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+    (void)hipMemsetAsync(c->bar, 0, sizeof(unsigned), c->side);
+    if (hipStreamEndCapture(c->side, &g) == hipSuccess && g) {
+      if (hipGraphInstantiate(&x, g, nullptr, nullptr, 0) == hipSuccess && x) {
+        (void)hipGraphLaunch(x, c->side);
+        (void)hipStreamSynchronize(c->side);
+        (void)hipGraphExecDestroy(x);
+      }
+      (void)hipGraphDestroy(g);
+    }
+  }
   return c;
 }
 void chol_destroy(CholCtx* c) {

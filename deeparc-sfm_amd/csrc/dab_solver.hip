@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <numeric>
 #include <string>
 #include <thread>
@@ -34,6 +35,7 @@
 #include "dab_internal.h"
 #include "dab_kernels.h"
 #include "dab_p2p.h"
+#include "dab_setup.h"
 
 using namespace dab;
 
@@ -224,6 +226,7 @@ struct Knobs {
                             // waves gather the points; 1 the same with the camera-major point copy
                             // (refreshed after every point change); 0 the 16-B records
   int fused_variant = 0;    // DAB_FUSED_V: pipeline depths of the streamed fused pass (DAB_ABLATIONS builds)
+  int setup_host = 0;       // DAB_SETUP_HOST=1: dab_set_problem's host passes instead of the device ones
   int fused_tab = 0;        // DAB_FUSED_TAB=1 (DAB_ABLATIONS builds): the streamed fused pass reads the
                             // k_cam_tables output instead of building its tables (kernel -0.9 us at C3,
                             // but the extra launch in front costs more)
@@ -246,6 +249,7 @@ struct Knobs {
     get("DAB_FUSED_STREAM", fused_stream);
     get("DAB_FUSED_V", fused_variant);
     get("DAB_FUSED_TAB", fused_tab);
+    get("DAB_SETUP_HOST", setup_host);
   }
 };
 
@@ -273,6 +277,8 @@ struct dab_handle {
 
   // ---- host-side problem structure ----
   bool have_problem = false;
+  bool local_compose = false;       // some observation of this rank is composed (arc∘ring)
+  bool host_entries = false;        // h_pt_ent_ptr / h_ent_* hold the entry lists (else fetched on use)
   dab_problem prob{};               // caller's arrays (pointers valid until next set_problem)
   int N = 0, NP = 0, E = 0, NI = 0, NC = 0, NE = 0, nplanes = 18;
   bool any_compose = false;
@@ -562,7 +568,7 @@ static int create_common(int device, dab_handle** out) {
   h->chol = chol_create();
   if (!h->chol) {
     delete h;
-    return set_error(DAB_E_DEVICE, "rocblas handle creation failed");
+    return set_error(DAB_E_DEVICE, "Cholesky context creation failed");
   }
   if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
       hipEventCreate(&h->ev2) != hipSuccess || hipEventCreate(&h->ev3) != hipSuccess ||
@@ -585,6 +591,7 @@ static int create_common(int device, dab_handle** out) {
     warm_chol();
     warm_pcg();
     warm_p2p();
+    warm_setup();
     hipFuncAttributes a;
     (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k_scale_points));
     warmed[device] = true;
@@ -758,6 +765,10 @@ static int validate(const dab_problem* p) {
     if (p->intr_nf[i] < 1 || p->intr_nf[i] > 2) return set_error(DAB_E_INVALID, "intr_nf must be 1 or 2");
     if (p->intr_nk[i] < 0 || p->intr_nk[i] > 2) return set_error(DAB_E_INVALID, "intr_nk must be 0, 1 or 2");
   }
+  return 0;
+}
+// per-observation index ranges (the host path; the device path checks them in su_count)
+static int validate_obs(const dab_problem* p) {
   for (int o = 0; o < p->num_obs; ++o) {
     const int pt = p->obs_point[o], e0 = p->obs_ext0[o], e1 = p->obs_ext1[o], ii = p->obs_intr[o];
     if (pt < 0 || pt >= p->num_points || e0 < 0 || e0 >= p->num_ext || e1 < -1 || e1 >= p->num_ext ||
@@ -767,31 +778,13 @@ static int validate(const dab_problem* p) {
   return 0;
 }
 
-extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
-  clear_error();
-  if (!h) return set_error(DAB_E_INVALID, "null handle");
-  CHECK_RC(validate(p));
-  HIP_OK(hipSetDevice(h->device));
-  HIP_OK(hipStreamSynchronize(h->stream));
-  h->dev.release();
-  h->d_Yrec = nullptr;  // lazily allocated: reallocated by the next explicit step
-  h->have_problem = false;
-  h->prob = *p;
-  // DAB_SETUP_TIMING=1: phase times of the host preprocessing on stderr
-  static const bool timing = getenv("DAB_SETUP_TIMING") != nullptr;
-  double t_ph = now_s();
-  auto phase = [&](const char* name) {
-    if (!timing) return;
-    const double t = now_s();
-    fprintf(stderr, "set_problem %-22s %8.1f ms\n", name, 1e3 * (t - t_ph));
-    t_ph = t;
-  };
+// The host reference path of the set-up (DAB_SETUP_HOST=1; multi-rank problems and sizes
+// setup_device_fits refuses): stable counting sorts and gathers on host threads, then the
+// uploads. setup_device builds the same arrays on the GPU.
+static int setup_host(dab_handle* h, const dab_problem* p, const std::function<void(const char*)>& phase) {
+  CHECK_RC(validate_obs(p));
   const int N = p->num_obs;
-  h->N = N;
-  h->E = p->num_ext;
-  h->NI = p->num_intr;
   hipStream_t s = h->stream;
-
   // referenced points (local compact ids, in id order) and extrinsics
   std::vector<int> pt_local(p->num_points, -1);
   std::vector<char> pref(p->num_points, 0);
@@ -1254,6 +1247,21 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   CHECK_RC(upload(&h->d_points, d, points, s));
   ++h->pts_version;
   CHECK_RC(upload(&h->d_ext, d, ext, s));
+  h->local_compose = false;
+  for (int o = 0; o < N && !h->local_compose; ++o) h->local_compose = p->obs_ext1[o] >= 0;
+  h->h_pt_ent_ptr = std::move(pt_ent_ptr);
+  h->h_ent_cam = std::move(ent_cam);
+  h->h_ent_pos = std::move(ent_pos);
+  h->h_ent_os = std::move(ent_os);
+  h->host_entries = true;
+  return 0;
+}
+
+// Work buffers, launch geometry and the device view, common to both set-up paths.
+static int setup_buffers(dab_handle* h, const std::function<void(const char*)>& phase) {
+  hipStream_t s = h->stream;
+  Dev& d = h->dev;
+  const int NP = h->NP, NC = h->NC, NS = h->NS, NE = h->NE;
   CHECK_RC(d.alloc(&h->d_points_c, (size_t)3 * NP));
   CHECK_RC(d.alloc(&h->d_ext_c, (size_t)6 * h->E));
   CHECK_RC(d.alloc(&h->d_camtab, (size_t)kCamTab * h->E));
@@ -1316,8 +1324,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   v.NI = h->NI;
   v.NE = NE;
   v.nslice = h->nslice;
-  v.any_comp = 0;
-  for (int o = 0; o < h->N && !v.any_comp; ++o) v.any_comp = h->prob.obs_ext1[o] >= 0;
+  v.any_comp = h->local_compose ? 1 : 0;
   v.obs_idx = h->d_obs_idx;
   v.obs_xy = h->d_obs_xy;
   v.cm_idx = h->d_cm_idx;
@@ -1341,22 +1348,456 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
     // packed 4-B slot records for the point waves; fused_stream = 1 also the camera-major
     // point copy (re-gathered whenever the points move), 2 (default) camera waves that
     // gather the points themselves
-    std::vector<int> obs_e(NS, -1);
-    for (int i = 0; i < NS; ++i)
-      if (obs_idx[i].x >= 0) obs_e[i] = obs_idx[i].y | (obs_idx[i].w << 16);
-    CHECK_RC(upload(&h->d_obs_e, d, obs_e, s));
+    CHECK_RC(d.alloc(&h->d_obs_e, (size_t)std::max(1, NS)));
+    su_obs_e(s, NS, h->d_obs_idx, h->d_obs_e);
     if (h->knobs.fused_stream == 1) CHECK_RC(d.alloc(&h->d_cmx, (size_t)3 * std::max(1, NE)));
     HIP_OK(hipStreamSynchronize(s));
     v.obs_e = h->d_obs_e;
   }
   HIP_OK(hipStreamSynchronize(s));
   phase("upload");
-  h->h_pt_ent_ptr = std::move(pt_ent_ptr);
-  h->h_ent_cam = std::move(ent_cam);
-  h->h_ent_pos = std::move(ent_pos);
-  h->h_ent_os = std::move(ent_os);
   h->have_problem = true;
   return 0;
+}
+// ---- set-up on the device (dab_setup.hip) ------------------------------------------------
+// The same arrays as setup_host, built by rocPRIM radix sorts (stable: ties keep input
+// order, exactly as the host's counting sorts) and gather / scatter kernels; only the
+// camera-sized tables (chunks, cross pairs) are finished on the host. Multi-rank handles
+// keep the host path: their free-camera and pair sets are unions over the ranks.
+static int bits_for(long long maxval) {  // radix-sort end bit for keys in [0, maxval]
+  int b = 1;
+  while (b < 31 && (1LL << b) <= maxval) ++b;
+  return b;
+}
+static bool setup_device_fits(dab_handle* h, const dab_problem* p) {
+  if (h->world > 1) return false;
+  const long long ncam = p->num_ext;  // NC <= num_ext; the pair key c0 NC + c1 must fit an int
+  return ncam * ncam + 1 < (1LL << 30) && (long long)p->num_obs * 2 < (1LL << 30);
+}
+static int setup_device(dab_handle* h, const dab_problem* p, const std::function<void(const char*)>& phase) {
+  hipStream_t s = h->stream;
+  Dev& d = h->dev;
+  Dev tmp;  // set-up scratch, released on return
+  const int N = p->num_obs, NPT = p->num_points, E = p->num_ext;
+  // scratch for rocPRIM: sized by the largest query
+  void* rtmp = nullptr;
+  size_t rtmp_cap = 0;
+  auto rp = [&](auto call) -> int {  // query the bytes, grow the scratch, run
+    size_t bytes = 0;
+    if (call(nullptr, &bytes) != 0) return set_error(DAB_E_DEVICE, "rocPRIM size query failed");
+    if (bytes > rtmp_cap) {
+      void* q = nullptr;
+      CHECK_RC(tmp.alloc(reinterpret_cast<unsigned char**>(&q), bytes));
+      rtmp = q;
+      rtmp_cap = bytes;
+    }
+    if (call(rtmp, &bytes) != 0) return set_error(DAB_E_DEVICE, "rocPRIM pass failed");
+    return 0;
+  };
+  auto d2h = [&](void* dst, const void* src, size_t bytes) -> int {
+    if (bytes) HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+    return 0;
+  };
+  auto h2d = [&](void* dst, const void* src, size_t bytes) -> int {
+    if (bytes) HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+    return 0;
+  };
+
+  // ---- the caller's observation arrays ----
+  int *r_pt = nullptr, *r_e0 = nullptr, *r_e1 = nullptr, *r_in = nullptr;
+  double *r_xy = nullptr, *r_points = nullptr;
+  CHECK_RC(tmp.alloc(&r_pt, N));
+  CHECK_RC(tmp.alloc(&r_e0, N));
+  CHECK_RC(tmp.alloc(&r_e1, N));
+  CHECK_RC(tmp.alloc(&r_in, N));
+  CHECK_RC(tmp.alloc(&r_xy, (size_t)2 * N));
+  CHECK_RC(tmp.alloc(&r_points, (size_t)3 * std::max(1, NPT)));
+  CHECK_RC(h2d(r_pt, p->obs_point, sizeof(int) * (size_t)N));
+  CHECK_RC(h2d(r_e0, p->obs_ext0, sizeof(int) * (size_t)N));
+  CHECK_RC(h2d(r_e1, p->obs_ext1, sizeof(int) * (size_t)N));
+  CHECK_RC(h2d(r_in, p->obs_intr, sizeof(int) * (size_t)N));
+  CHECK_RC(h2d(r_xy, p->obs_xy, sizeof(double) * 2 * (size_t)N));
+  CHECK_RC(h2d(r_points, p->points, sizeof(double) * 3 * (size_t)NPT));
+  phase("device: upload");
+
+  // ---- counts, validation, referenced extrinsics ----
+  int *pcount = nullptr, *eref_d = nullptr, *small = nullptr;  // small: [flags, maxcount, nref, nvalid, count, ...]
+  CHECK_RC(tmp.alloc(&pcount, std::max(1, NPT)));
+  CHECK_RC(tmp.alloc(&eref_d, std::max(1, E)));
+  CHECK_RC(tmp.alloc(&small, 16));
+  HIP_OK(hipMemsetAsync(pcount, 0, sizeof(int) * std::max(1, NPT), s));
+  HIP_OK(hipMemsetAsync(eref_d, 0, sizeof(int) * std::max(1, E), s));
+  HIP_OK(hipMemsetAsync(small, 0, sizeof(int) * 16, s));
+  su_count(s, N, r_pt, r_e0, r_e1, r_in, NPT, E, p->num_intr, pcount, eref_d, small);
+  if (NPT > 0)
+    CHECK_RC(rp([&](void* t, size_t* b) { return su_max(t, b, pcount, small + 1, NPT, s); }));
+  int hs[4] = {0, 0, 0, 0};
+  std::vector<int> eref(std::max(1, E), 0);
+  CHECK_RC(d2h(hs, small, sizeof(int) * 2));
+  CHECK_RC(d2h(eref.data(), eref_d, sizeof(int) * (size_t)E));
+  HIP_OK(hipStreamSynchronize(s));
+  if (hs[0] & 1) {
+    // the host check names the first offending observation
+    CHECK_RC(validate_obs(p));
+    return set_error(DAB_E_INVALID, "an observation has an out-of-range index");
+  }
+  h->local_compose = h->any_compose = (hs[0] & 2) != 0;
+  const int maxcount = hs[1];
+
+  // ---- device point order (count descending, stable by id) ----
+  int *pk = nullptr, *pv = nullptr, *pk2 = nullptr, *pv2 = nullptr;
+  CHECK_RC(tmp.alloc(&pk, std::max(1, NPT)));
+  CHECK_RC(tmp.alloc(&pv, std::max(1, NPT)));
+  CHECK_RC(tmp.alloc(&pk2, std::max(1, NPT)));
+  CHECK_RC(tmp.alloc(&pv2, std::max(1, NPT)));
+  su_point_keys(s, NPT, pcount, small + 1, pk, pv, small + 2);
+  if (NPT > 0)
+    CHECK_RC(rp([&](void* t, size_t* b) { return su_sort_pairs(t, b, pk, pk2, pv, pv2, NPT, bits_for(maxcount + 1), s); }));
+  CHECK_RC(d2h(hs + 2, small + 2, sizeof(int)));
+  HIP_OK(hipStreamSynchronize(s));
+  const int NP = hs[2];
+  h->NP = NP;
+  h->pt_of.resize(NP);
+  const int* pt_of_d = pv2;  // first NP sorted ids
+  CHECK_RC(d2h(h->pt_of.data(), pt_of_d, sizeof(int) * (size_t)NP));
+  int *pt_local = nullptr, *lcount = nullptr;
+  CHECK_RC(tmp.alloc(&pt_local, std::max(1, NPT)));
+  CHECK_RC(tmp.alloc(&lcount, NP + 1));
+  su_point_local(s, NP, pt_of_d, pcount, pt_local, lcount);
+
+  // ---- free cameras (host: E is small) ----
+  h->ext_col.assign(E, -1);
+  h->NC = 0;
+  for (int e = 0; e < E; ++e) {
+    const bool is_const = p->freeze_camera || (p->ext_const && p->ext_const[e]);
+    if (eref[e] != 0 && !is_const) h->ext_col[e] = h->NC++;
+  }
+  const int NC = h->NC;
+  h->nplanes = h->any_compose ? 30 : 18;
+  CHECK_RC(upload(&h->d_ext_col, d, h->ext_col, s));
+  phase("device: points, cameras");
+
+  // ---- observations by point (stable), SELL-64 slots ----
+  int *ok = nullptr, *ov = nullptr, *ok2 = nullptr, *by_pt = nullptr, *cnt = nullptr;
+  CHECK_RC(tmp.alloc(&ok, std::max(1, N)));
+  CHECK_RC(tmp.alloc(&ov, std::max(1, N)));
+  CHECK_RC(tmp.alloc(&ok2, std::max(1, N)));
+  CHECK_RC(tmp.alloc(&by_pt, std::max(1, N)));
+  CHECK_RC(tmp.alloc(&cnt, NP + 1));
+  su_obs_keys(s, N, r_pt, pt_local, ok, ov);
+  if (N > 0)
+    CHECK_RC(rp([&](void* t, size_t* b) { return su_sort_pairs(t, b, ok, ok2, ov, by_pt, N, bits_for(NP), s); }));
+  CHECK_RC(rp([&](void* t, size_t* b) { return su_exclusive_scan(t, b, lcount, cnt, NP + 1, s); }));
+  h->nslice = (NP + 63) / 64;
+  const int nslice = h->nslice;
+  int* slen = nullptr;
+  CHECK_RC(tmp.alloc(&slen, nslice + 1));
+  CHECK_RC(d.alloc(&h->d_slice_off, nslice + 1));
+  su_slice_len(s, nslice, NP, lcount, slen);
+  CHECK_RC(rp([&](void* t, size_t* b) { return su_exclusive_scan(t, b, slen, h->d_slice_off, nslice + 1, s); }));
+  int NS = 0;
+  CHECK_RC(d2h(&NS, h->d_slice_off + nslice, sizeof(int)));
+  HIP_OK(hipStreamSynchronize(s));
+  h->NS = NS;
+  int *perm_d = nullptr, *ne = nullptr;
+  CHECK_RC(d.alloc(&h->d_obs_idx, (size_t)std::max(1, NS)));
+  CHECK_RC(d.alloc(&h->d_obs_xy, (size_t)std::max(1, NS)));
+  CHECK_RC(tmp.alloc(&perm_d, std::max(1, NS)));
+  CHECK_RC(tmp.alloc(&ne, NP + 1));
+  su_slots(s, NP, nslice, h->d_slice_off, cnt, lcount, by_pt, r_e0, r_e1, r_in, r_xy, h->d_ext_col, h->d_obs_idx,
+           h->d_obs_xy, perm_d, ne);
+  h->perm.resize(NS);
+  CHECK_RC(d2h(h->perm.data(), perm_d, sizeof(int) * (size_t)NS));
+  // entries (free-camera slots), point-major
+  CHECK_RC(d.alloc(&h->d_pt_ent_ptr, NP + 1));
+  CHECK_RC(rp([&](void* t, size_t* b) { return su_exclusive_scan(t, b, ne, h->d_pt_ent_ptr, NP + 1, s); }));
+  int NE = 0;
+  CHECK_RC(d2h(&NE, h->d_pt_ent_ptr + NP, sizeof(int)));
+  HIP_OK(hipStreamSynchronize(s));
+  h->NE = NE;
+  CHECK_RC(d.alloc(&h->d_ent_os, std::max(1, NE)));
+  CHECK_RC(d.alloc(&h->d_ent_cam, std::max(1, NE)));
+  CHECK_RC(d.alloc(&h->d_ent_pt, std::max(1, NE)));
+  su_entries(s, NP, h->d_slice_off, lcount, h->d_obs_idx, h->d_ext_col, h->d_pt_ent_ptr, h->d_ent_os, h->d_ent_cam,
+             h->d_ent_pt);
+  phase("device: slots, entries");
+
+  // ---- camera-major order (entries by camera, stable) ----
+  int *ek = nullptr, *ev = nullptr, *pos_cam = nullptr, *cam_ent = nullptr, *cam_cnt_d = nullptr;
+  CHECK_RC(tmp.alloc(&ev, std::max(1, NE)));
+  CHECK_RC(tmp.alloc(&pos_cam, std::max(1, NE)));
+  CHECK_RC(tmp.alloc(&cam_ent, std::max(1, NE)));
+  CHECK_RC(tmp.alloc(&cam_cnt_d, NC + 1));
+  ek = h->d_ent_cam;
+  su_iota(s, NE, ev);
+  if (NE > 0)
+    CHECK_RC(rp([&](void* t, size_t* b) { return su_sort_pairs(t, b, ek, pos_cam, ev, cam_ent, NE, bits_for(NC), s); }));
+  HIP_OK(hipMemsetAsync(cam_cnt_d, 0, sizeof(int) * (NC + 1), s));
+  su_bounds(s, NE, pos_cam, NC, cam_cnt_d);
+  std::vector<int> cam_cnt(NC + 1, 0);
+  CHECK_RC(d2h(cam_cnt.data(), cam_cnt_d, sizeof(int) * (NC + 1)));
+  HIP_OK(hipStreamSynchronize(s));
+  // chunks (host: NC is small)
+  const int chunk = std::max(64, h->knobs.chunk > 0 ? h->knobs.chunk : kChunk);
+  std::vector<int> chunk_beg, seg_chunk(NC + 1, 0);
+  for (int c = 0; c < NC; ++c) {
+    seg_chunk[c] = (int)chunk_beg.size();
+    for (int b = cam_cnt[c]; b < cam_cnt[c + 1]; b += chunk) chunk_beg.push_back(b);
+  }
+  seg_chunk[NC] = (int)chunk_beg.size();
+  h->nchunk = (int)chunk_beg.size();
+  h->max_seg_chunks = 1;
+  for (int c = 0; c < NC; ++c) h->max_seg_chunks = std::max(h->max_seg_chunks, seg_chunk[c + 1] - seg_chunk[c]);
+  chunk_beg.push_back(NE);
+  const int nchunk = h->nchunk;
+  CHECK_RC(upload(&h->d_chunk_beg, d, chunk_beg, s));
+  CHECK_RC(upload(&h->d_seg_chunk, d, seg_chunk, s));
+  CHECK_RC(d.alloc(&h->d_ent_pos, std::max(1, NE)));
+  CHECK_RC(d.alloc(&h->d_cm_pt, std::max(1, NE)));
+  CHECK_RC(d.alloc(&h->d_cm_idx, (size_t)std::max(1, NE)));
+  CHECK_RC(d.alloc(&h->d_cm_xy, (size_t)std::max(1, NE)));
+  su_camera_major(s, NE, cam_ent, h->d_ent_pt, h->d_ent_os, h->d_obs_idx, h->d_obs_xy, h->d_ent_pos, h->d_cm_pt,
+                  h->d_cm_idx, h->d_cm_xy);
+  CHECK_RC(d.alloc(&h->d_run, std::max(1, NE)));
+  su_runs(s, NE, pos_cam, h->d_cm_pt, h->d_run);
+  int* run_cnt = nullptr;
+  CHECK_RC(tmp.alloc(&run_cnt, nchunk + 1));
+  CHECK_RC(d.alloc(&h->d_run_beg, nchunk + 1));
+  HIP_OK(hipMemsetAsync(run_cnt, 0, sizeof(int) * (nchunk + 1), s));
+  su_chunk_runs(s, nchunk, h->d_chunk_beg, h->d_run, run_cnt);
+  CHECK_RC(rp([&](void* t, size_t* b) { return su_exclusive_scan(t, b, run_cnt, h->d_run_beg, nchunk + 1, s); }));
+  int nrun = 0;
+  CHECK_RC(d2h(&nrun, h->d_run_beg + nchunk, sizeof(int)));
+  HIP_OK(hipStreamSynchronize(s));
+  CHECK_RC(d.alloc(&h->d_run_rec, (size_t)std::max(1, nrun)));
+  su_chunk_run_rec(s, nchunk, h->d_chunk_beg, h->d_run, h->d_cm_pt, pos_cam, h->d_run_beg, h->d_run_rec);
+  CHECK_RC(d.alloc(&h->d_chunk_uni, (size_t)std::max(1, nchunk)));
+  su_chunk_uni(s, nchunk, h->d_chunk_beg, h->d_cm_idx, kSlotBit, h->d_chunk_uni);
+  std::vector<int2> chunk_uni(nchunk);
+  CHECK_RC(d2h(chunk_uni.data(), h->d_chunk_uni, sizeof(int2) * (size_t)nchunk));
+  HIP_OK(hipStreamSynchronize(s));
+  phase("device: camera-major");
+
+  // ---- pair-major copy of the composed observations (rig) ----
+  std::vector<long long> pairkeys;
+  std::vector<int> pair_cnt;
+  int nx = 0;
+  int* xslots = nullptr;
+  if (h->any_compose && NC > 0) {
+    int *xk = nullptr, *xv = nullptr, *xk2 = nullptr;
+    CHECK_RC(tmp.alloc(&xk, std::max(1, NS)));
+    CHECK_RC(tmp.alloc(&xv, std::max(1, NS)));
+    CHECK_RC(tmp.alloc(&xk2, std::max(1, NS)));
+    CHECK_RC(tmp.alloc(&xslots, std::max(1, NS)));
+    su_cross_keys(s, NS, h->d_obs_idx, h->d_ext_col, NC, xk, xv, small + 3);
+    CHECK_RC(rp([&](void* t, size_t* b) { return su_sort_pairs(t, b, xk, xk2, xv, xslots, NS, bits_for((long long)NC * NC), s); }));
+    CHECK_RC(d2h(hs + 3, small + 3, sizeof(int)));
+    HIP_OK(hipStreamSynchronize(s));
+    nx = hs[3];
+    if (nx > 0) {
+      int *uk = nullptr, *uc = nullptr;
+      CHECK_RC(tmp.alloc(&uk, nx));
+      CHECK_RC(tmp.alloc(&uc, nx));
+      CHECK_RC(rp([&](void* t, size_t* b) { return su_rle(t, b, xk2, uk, uc, small + 4, nx, s); }));
+      int nr = 0;
+      CHECK_RC(d2h(&nr, small + 4, sizeof(int)));
+      HIP_OK(hipStreamSynchronize(s));
+      std::vector<int> ukh(nr), uch(nr);
+      CHECK_RC(d2h(ukh.data(), uk, sizeof(int) * (size_t)nr));
+      CHECK_RC(d2h(uch.data(), uc, sizeof(int) * (size_t)nr));
+      HIP_OK(hipStreamSynchronize(s));
+      for (int k = 0; k < nr; ++k) {
+        pairkeys.push_back(ukh[k]);
+        pair_cnt.push_back(uch[k]);
+      }
+    }
+  }
+  h->ncross = (int)pairkeys.size();
+  std::vector<int2> cross_cam(h->ncross);
+  for (int k = 0; k < h->ncross; ++k) cross_cam[k] = make_int2((int)(pairkeys[k] / NC), (int)(pairkeys[k] % NC));
+  std::vector<int> xchunk_beg, xseg_chunk(h->ncross + 1, 0);
+  {
+    int b = 0;
+    for (int k = 0; k < h->ncross; ++k) {
+      xseg_chunk[k] = (int)xchunk_beg.size();
+      for (int q = b; q < b + pair_cnt[k]; q += chunk) xchunk_beg.push_back(q);
+      b += pair_cnt[k];
+    }
+    xseg_chunk[h->ncross] = (int)xchunk_beg.size();
+    h->nxchunk = (int)xchunk_beg.size();
+    h->max_xseg_chunks = 1;
+    for (int k = 0; k < h->ncross; ++k)
+      h->max_xseg_chunks = std::max(h->max_xseg_chunks, xseg_chunk[k + 1] - xseg_chunk[k]);
+    xchunk_beg.push_back(nx);
+  }
+  CHECK_RC(d.alloc(&h->d_x_idx, (size_t)std::max(1, nx)));
+  CHECK_RC(d.alloc(&h->d_x_xy, (size_t)std::max(1, nx)));
+  h->pair_eval = h->nxchunk > 0 && pair_eval_fits(h->E, h->NI) && h->knobs.pair_eval != 0;
+  unsigned char* touched = nullptr;
+  if (h->pair_eval) {
+    CHECK_RC(tmp.alloc(&touched, std::max(1, NP)));
+    HIP_OK(hipMemsetAsync(touched, 0, (size_t)std::max(1, NP), s));
+  }
+  su_cross_copy(s, nx, xslots, h->d_obs_idx, h->d_obs_xy, h->d_x_idx, h->d_x_xy, touched);
+  // per-camera CSR of cross blocks for the implicit operator: code = 2 k + (camera is c1)
+  std::vector<int> xptr(NC + 1, 0), xlist;
+  {
+    std::vector<std::vector<int>> per(NC);
+    for (int k = 0; k < h->ncross; ++k) {
+      per[cross_cam[k].x].push_back(2 * k);
+      per[cross_cam[k].y].push_back(2 * k + 1);
+    }
+    for (int c = 0; c < NC; ++c) {
+      xptr[c] = (int)xlist.size();
+      xlist.insert(xlist.end(), per[c].begin(), per[c].end());
+    }
+    if (NC > 0) xptr[NC] = (int)xlist.size();
+    h->nxlist = (int)xlist.size();
+  }
+  std::vector<int> chunk2_beg, seg2_chunk(NC + 1, 0), xcam_ptr(NC + 1, 0), xcam_list;
+  int n2 = 0;
+  int* sel2 = nullptr;
+  if (h->pair_eval) {
+    HIP_OK(hipMemsetAsync(small + 5, 0, sizeof(int) * 2, s));
+    su_count_flags(s, NP, touched, small + 5);
+    // the entries that are not paired, per camera, in camera-major order
+    unsigned char* uf = nullptr;
+    int *ufi = nullptr, *uscan = nullptr, *iota = nullptr, *c2cnt_d = nullptr;
+    CHECK_RC(tmp.alloc(&uf, std::max(1, NE)));
+    CHECK_RC(tmp.alloc(&ufi, NE + 1));
+    CHECK_RC(tmp.alloc(&uscan, NE + 1));
+    CHECK_RC(tmp.alloc(&iota, std::max(1, NE)));
+    CHECK_RC(tmp.alloc(&sel2, std::max(1, NE)));
+    CHECK_RC(tmp.alloc(&c2cnt_d, NC + 1));
+    su_unpaired_flags(s, NE, h->d_cm_idx, h->d_ext_col, uf, ufi);
+    CHECK_RC(rp([&](void* t, size_t* b) { return su_exclusive_scan(t, b, ufi, uscan, NE + 1, s); }));
+    su_gather_at(s, NC + 1, cam_cnt_d, uscan, c2cnt_d);
+    su_iota(s, NE, iota);
+    if (NE > 0)
+      CHECK_RC(rp([&](void* t, size_t* b) { return su_select_flagged_i(t, b, iota, uf, sel2, small + 6, NE, s); }));
+    std::vector<int> c2cnt(NC + 1, 0);
+    CHECK_RC(d2h(c2cnt.data(), c2cnt_d, sizeof(int) * (NC + 1)));
+    int pb[2] = {0, 0};
+    CHECK_RC(d2h(pb, small + 5, sizeof(int) * 2));
+    HIP_OK(hipStreamSynchronize(s));
+    h->pair_bytes = (16.0 + 12.0) * (double)nx + 24.0 * (double)pb[0] + 90.0 * 8.0 * h->nxchunk;
+    n2 = pb[1];
+    for (int c = 0; c < NC; ++c) {
+      seg2_chunk[c] = (int)chunk2_beg.size();
+      for (int q = c2cnt[c]; q < c2cnt[c + 1]; q += chunk) chunk2_beg.push_back(q);
+    }
+    seg2_chunk[NC] = (int)chunk2_beg.size();
+    h->nchunk2 = (int)chunk2_beg.size();
+    chunk2_beg.push_back(n2);
+    std::vector<std::vector<int>> per(NC);
+    for (int k = 0; k < h->ncross; ++k)
+      for (int q = xseg_chunk[k]; q < xseg_chunk[k + 1]; ++q) {
+        per[cross_cam[k].x].push_back(2 * q);
+        per[cross_cam[k].y].push_back(2 * q + 1);
+      }
+    for (int c = 0; c < NC; ++c) {
+      std::sort(per[c].begin(), per[c].end());
+      xcam_ptr[c] = (int)xcam_list.size();
+      xcam_list.insert(xcam_list.end(), per[c].begin(), per[c].end());
+    }
+    xcam_ptr[NC] = (int)xcam_list.size();
+  }
+  phase("device: pair-major");
+  h->schur_built = false;
+  h->schur_tiles = false;
+  h->pcg_built = false;
+  h->mf = h->mf32 = false;
+  h->cg_wpart = nullptr;
+  h->nblk = 0;
+  h->npairs = 0;
+
+  // intrinsics: (cx, cy, fx, fy', k0, k1) with unused distortion terms zeroed
+  std::vector<double> intr((size_t)kIntr * std::max(1, h->NI), 0.0);
+  for (int i = 0; i < h->NI; ++i) {
+    const double* K = p->intr + 6 * (size_t)i;
+    double* o = &intr[(size_t)kIntr * i];
+    o[0] = K[0];
+    o[1] = K[1];
+    o[2] = K[2];
+    o[3] = p->intr_nf[i] == 2 ? K[3] : K[2];
+    o[4] = p->intr_nk[i] >= 1 ? K[4] : 0.0;
+    o[5] = p->intr_nk[i] >= 2 ? K[5] : 0.0;
+  }
+  std::vector<double> ext(p->ext, p->ext + 6 * (size_t)h->E);
+  CHECK_RC(d.alloc(&h->d_arrivals, 1));
+  HIP_OK(hipMemsetAsync(h->d_arrivals, 0, sizeof(unsigned), s));
+  {
+    std::vector<int> lists;
+    for (int q = 0; q < nchunk; ++q)
+      if (chunk_uni[q].x >= 0) lists.push_back(q);
+    const int nuni = (int)lists.size();
+    for (int q = 0; q < nchunk; ++q)
+      if (chunk_uni[q].x < 0) lists.push_back(q);
+    CHECK_RC(upload(&h->d_chunk_lists, d, lists, s));
+    h->chunks.nchunk = nchunk;
+    h->chunks.nuni = nuni;
+    h->chunks.ngen = nchunk - nuni;
+    h->chunks.uni = h->d_chunk_lists;
+    h->chunks.gen = h->d_chunk_lists + nuni;
+  }
+  CHECK_RC(upload(&h->d_xchunk_beg, d, xchunk_beg, s));
+  CHECK_RC(upload(&h->d_xseg_chunk, d, xseg_chunk, s));
+  CHECK_RC(upload(&h->d_cross_cam, d, cross_cam, s));
+  CHECK_RC(upload(&h->d_xptr, d, xptr, s));
+  CHECK_RC(upload(&h->d_xlist, d, xlist, s));
+  if (h->pair_eval) {
+    if (n2 > 0) {
+      CHECK_RC(d.alloc(&h->d_cm2_idx, (size_t)n2));
+      CHECK_RC(d.alloc(&h->d_cm2_xy, (size_t)n2));
+      su_gather_cm(s, n2, sel2, h->d_cm_idx, h->d_cm_xy, h->d_cm2_idx, h->d_cm2_xy);
+    }
+    CHECK_RC(upload(&h->d_chunk2_beg, d, chunk2_beg, s));
+    CHECK_RC(upload(&h->d_seg2_chunk, d, seg2_chunk, s));
+    CHECK_RC(upload(&h->d_xcam_ptr, d, xcam_ptr, s));
+    if (!xcam_list.empty()) CHECK_RC(upload(&h->d_xcam_list, d, xcam_list, s));
+    CHECK_RC(d.alloc(&h->d_partial2, (size_t)std::max(1, h->nchunk2) * 27));
+    CHECK_RC(d.alloc(&h->d_xcpart, (size_t)h->nxchunk * 54));
+  }
+  CHECK_RC(upload(&h->d_intr, d, intr, s));
+  CHECK_RC(d.alloc(&h->d_points, (size_t)3 * NP));
+  su_points(s, NP, pt_of_d, r_points, h->d_points);
+  ++h->pts_version;
+  CHECK_RC(upload(&h->d_ext, d, ext, s));
+  h->host_entries = false;  // build_schur_* fetch the entry lists from the device on first use
+  HIP_OK(hipStreamSynchronize(s));
+  HIP_OK(hipGetLastError());
+  phase("device: tables");
+  return 0;
+}
+
+extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
+  clear_error();
+  if (!h) return set_error(DAB_E_INVALID, "null handle");
+  CHECK_RC(validate(p));
+  HIP_OK(hipSetDevice(h->device));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  h->dev.release();
+  h->d_Yrec = nullptr;  // lazily allocated: reallocated by the next explicit step
+  h->have_problem = false;
+  h->prob = *p;
+  // DAB_SETUP_TIMING=1: phase times of the host preprocessing on stderr
+  static const bool timing = getenv("DAB_SETUP_TIMING") != nullptr;
+  double t_ph = now_s();
+  auto phase = [&](const char* name) {
+    if (!timing) return;
+    const double t = now_s();
+    fprintf(stderr, "set_problem %-22s %8.1f ms\n", name, 1e3 * (t - t_ph));
+    t_ph = t;
+  };
+  const int N = p->num_obs;
+  h->N = N;
+  h->E = p->num_ext;
+  h->NI = p->num_intr;
+
+  const bool on_device = h->knobs.setup_host == 0 && setup_device_fits(h, p);
+  if (on_device) CHECK_RC(setup_device(h, p, phase));
+  else CHECK_RC(setup_host(h, p, phase));
+  return setup_buffers(h, phase);
 }
 
 
@@ -1383,6 +1824,27 @@ static int max_all_ranks(dab_handle* h, double& x) {  // max over ranks of one h
 // free cameras. Tables: each point's entries sorted by camera, records (distinct point-camera
 // pairs), batches of whole points (<= 640 records, <= 64 points), tiles of <= 1024 blocks.
 static constexpr int kBatchPts = 64, kTileBlocks = 1024;
+// the entry lists on the host (the explicit-step table builders read them); the device
+// set-up leaves them on the device until a builder asks
+static int fetch_host_entries(dab_handle* h) {
+  if (h->host_entries) return 0;
+  hipStream_t s = h->stream;
+  h->h_pt_ent_ptr.resize((size_t)h->NP + 1);
+  h->h_ent_cam.resize(h->NE);
+  h->h_ent_pos.resize(h->NE);
+  h->h_ent_os.resize(h->NE);
+  HIP_OK(hipMemcpyAsync(h->h_pt_ent_ptr.data(), h->d_pt_ent_ptr, sizeof(int) * ((size_t)h->NP + 1),
+                        hipMemcpyDeviceToHost, s));
+  if (h->NE > 0) {
+    HIP_OK(hipMemcpyAsync(h->h_ent_cam.data(), h->d_ent_cam, sizeof(int) * (size_t)h->NE, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(h->h_ent_pos.data(), h->d_ent_pos, sizeof(int) * (size_t)h->NE, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(h->h_ent_os.data(), h->d_ent_os, sizeof(int) * (size_t)h->NE, hipMemcpyDeviceToHost, s));
+  }
+  HIP_OK(hipStreamSynchronize(s));
+  h->host_entries = true;
+  return 0;
+}
+
 static int build_schur_tiles(dab_handle* h) {
   hipStream_t s = h->stream;
   static const bool timing = getenv("DAB_SETUP_TIMING") != nullptr;
@@ -1553,6 +2015,7 @@ static int build_schur_tiles(dab_handle* h) {
 }
 
 static int build_schur_tables(dab_handle* h) {
+  if (!h->schur_built) CHECK_RC(fetch_host_entries(h));
   if (h->schur_built) return 0;
   static const bool timing = getenv("DAB_SETUP_TIMING") != nullptr;
   const double t_b = now_s();

@@ -13,7 +13,9 @@ pkg = _pkgload.load()
 prob = pkg.synth(**pkg.CONFIGS["c1_rig_8x36"])
 p0, e0 = prob.points.copy(), prob.ext.copy()
 o = pkg.options(max_num_iterations=10)
+t = time.perf_counter()
 s = pkg.Solver(0)
+print(f"handle creation {1e3 * (time.perf_counter() - t):.2f} ms", flush=True)
 for tag in ("cold", "reset", "warm"):
     t = time.perf_counter()
     if tag != "warm":

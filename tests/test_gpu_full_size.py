@@ -9,7 +9,8 @@
   the test first checks that it regenerated the identical problem (sha256 of the arrays).
   Tolerances: per-iteration cost 1e-9 relative for the exact step (DENSE_SCHUR), 1e-8 for
   PCG with identical CG iteration counts; per-iteration gradient max norm 1e-7 relative
-  (exact) / 1e-6 (PCG); final parameters, gauge-normalised (the free scale removed:
+  (exact) / 1e-6 (PCG) plus 1e-13 / 1e-12 of the initial gradient (the cancellation floor
+  near convergence); final parameters, gauge-normalised (the free scale removed:
   gen_trajectories.gauge_normalised), 1e-7 absolute (exact) / 1e-6 (PCG) on every extrinsic
   and on every point (C2, C3 exact), every 8th (C3 PCG) or every 64th (C5) point.
 * C4 shape: the C3 global problem point-sharded over two ranks (collectives staged through
@@ -72,9 +73,12 @@ def test_full_size_trajectory_matches_oracle(pkg, gpu, name):
         assert [it["linear_solver_iterations"] for it in g["iterations"]] == rec["linear_iterations"]
     else:
         assert g["schur_assembly"] == (1 if rec["config"] != "c3_1kcam" else 0)
-    gtol = 1e-7 if exact else 1e-6
+    # near convergence the gradient is a cancellation of terms of the initial gradient's size,
+    # so its rounding floor is relative to that size (1e-13 / 1e-12 of it), not to itself
+    gtol, g0 = (1e-7, 1e-13) if exact else (1e-6, 1e-12)
+    gn0 = rec["gradient_max_norms"][0]
     for a, b in zip([it["gradient_max_norm"] for it in g["iterations"]], rec["gradient_max_norms"]):
-        assert abs(a - b) <= gtol * abs(b), (name, "gradient max norm", a, b)
+        assert abs(a - b) <= gtol * abs(b) + g0 * gn0, (name, "gradient max norm", a, b)
     # every extrinsic and the recorded points (stride), with the free scale removed
     k = rec["point_stride"]
     gp, ge, gs = gt.gauge_normalised(prob.points[::k], prob.ext)
