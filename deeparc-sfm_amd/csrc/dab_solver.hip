@@ -298,6 +298,7 @@ struct dab_handle {
 
   // ---- device buffers ----
   Dev dev;
+  Dev setup_tmp;  // the device set-up's scratch (released by the next set-up)
   DevView view{};
   int4* d_obs_idx = nullptr;
   double2* d_obs_xy = nullptr;
@@ -558,6 +559,12 @@ static int create_common(int device, dab_handle** out) {
     return set_error(DAB_E_DEVICE, "no HIP device available");
   if (device < 0 || device >= ndev) return set_error(DAB_E_INVALID, "device ordinal out of range");
   HIP_OK(hipSetDevice(device));
+  // Host waits spin (the solver's host round trips are latency-critical: read_scalars every
+  // LM iteration). With the runtime's default the waits after a burst of short kernels
+  // (the device set-up) fell back to blocking, and the first synchronisation of the
+  // following solve took 10-25 ms for 10 us of device work. DAB_SCHEDULE_BLOCKING=1 keeps
+  // the default.
+  if (!getenv("DAB_SCHEDULE_BLOCKING")) (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
   dab_handle* h = new dab_handle();
   h->device = device;
   h->knobs.read();
@@ -1377,7 +1384,10 @@ static bool setup_device_fits(dab_handle* h, const dab_problem* p) {
 static int setup_device(dab_handle* h, const dab_problem* p, const std::function<void(const char*)>& phase) {
   hipStream_t s = h->stream;
   Dev& d = h->dev;
-  Dev tmp;  // set-up scratch, released on return
+  // set-up scratch: kept until the next set-up (freeing it here stalled the solve's first
+  // kernels by 10-25 ms)
+  Dev& tmp = h->setup_tmp;
+  tmp.release();
   const int N = p->num_obs, NPT = p->num_points, E = p->num_ext;
   // scratch for rocPRIM: sized by the largest query
   void* rtmp = nullptr;

@@ -23,6 +23,9 @@ for tag in ("cold", "reset", "warm"):
         s.set_problem(prob)
     else:
         s.update_parameters(p0, e0)
+    s.sync()
+    if os.environ.get("C1_SLEEP"):
+        time.sleep(float(os.environ["C1_SLEEP"]))
     ts = time.perf_counter()
     g = s.solve(o)
     te = time.perf_counter()
