@@ -417,7 +417,10 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             t = json.load(open(args.traffic_json))
-            if (t.get("config") == args.config and t.get("n_obs") == n_obs
+            import hashlib
+            lib_sha = hashlib.sha256(open(os.path.join(ROOT, "deeparc-sfm_amd", "libdab.so"), "rb").read()).hexdigest()
+            # PMC traffic only from a profile of this exact binary (scripts/gpu_prof.sh)
+            if (t.get("config") == args.config and t.get("n_obs") == n_obs and t.get("libdab_sha256") == lib_sha
                     and str(t.get("kernel", "")).startswith(eval_kernel)):
                 traffic = t.get("bytes_per_launch")
                 valu = t.get("valu_insts_per_launch")

@@ -7,11 +7,11 @@ TAG=${TAG:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-SHORT="--steps 10 --warmup 3 --no-cpu --no-lm --no-c2 --no-c4"
+SHORT="--steps 10 --warmup 3 --no-cpu --no-lm --no-c2 --no-c4 --no-rig --no-c1"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 bench.py $SHORT ${PROF_ARGS} > $OUT/fetch.log 2>&1 || { echo "fetch pass failed"; tail -20 $OUT/fetch.log; exit 1; }
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 bench.py $SHORT ${PROF_ARGS} > $OUT/write.log 2>&1 || { echo "write pass failed"; tail -20 $OUT/write.log; exit 1; }
 timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU -d $OUT/valu -o run --output-format csv -- python3 bench.py $SHORT ${PROF_ARGS} > $OUT/valu.log 2>&1 || { echo "valu pass failed"; tail -20 $OUT/valu.log; exit 1; }
-python3 scripts/traffic.py $OUT/fetch $OUT/write profiles/traffic_latest.json --valu-dir $OUT/valu > $OUT/traffic.txt 2>&1 || { cat $OUT/traffic.txt; exit 1; }
+python3 scripts/traffic.py $OUT/fetch $OUT/write profiles/traffic_latest.json --valu-dir $OUT/valu --lib deeparc-sfm_amd/libdab.so > $OUT/traffic.txt 2>&1 || { cat $OUT/traffic.txt; exit 1; }
 cp profiles/traffic_latest.json $OUT/
 head -25 $OUT/traffic.txt
 timeout -k 10 600 python3 bench.py ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -20 $OUT/bench.err; exit 1; }

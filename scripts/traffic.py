@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--config", default="c3_1kcam")
     ap.add_argument("--n-obs", type=int, default=1000000)
     ap.add_argument("--valu-dir", default="", help="a third PMC pass with SQ_INSTS_VALU (wave-instructions)")
+    ap.add_argument("--lib", default="", help="the libdab.so profiled (its sha256 goes into the record; "
+                    "bench.py reports the traffic only for that exact binary)")
     ap.add_argument("--kernel", default="auto", help="kernel name prefix (auto: k_eval_fused if it ran, "
                     "else k_eval_points)")
     a = ap.parse_args()
@@ -58,7 +60,11 @@ def main():
         a.kernel = "k_eval_fused" if any(k.startswith("k_eval_fused") for k in table) else "k_eval_points"
     # the evaluation-kernel variant the bench ran (most launches among the matching names)
     main_k = sorted((k for k in table if k.startswith(a.kernel)), key=lambda k: -table[k]["launches"])
-    out = dict(config=a.config, n_obs=a.n_obs, kernel=main_k[0] if main_k else None,
+    lib_sha = None
+    if a.lib:
+        import hashlib
+        lib_sha = hashlib.sha256(open(a.lib, "rb").read()).hexdigest()
+    out = dict(config=a.config, n_obs=a.n_obs, kernel=main_k[0] if main_k else None, libdab_sha256=lib_sha,
                bytes_per_launch=table[main_k[0]]["bytes_per_launch"] if main_k else None,
                valu_insts_per_launch=table[main_k[0]]["valu_insts"] if main_k else None,
                correction="FETCH_SIZE x2 (gfx950 wide-load tally), WRITE_SIZE x1, KiB->B",
