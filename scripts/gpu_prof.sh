@@ -12,7 +12,7 @@ timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-forma
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 bench.py $SHORT ${PROF_ARGS} > $OUT/write.log 2>&1 || { echo "write pass failed"; tail -20 $OUT/write.log; exit 1; }
 timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU -d $OUT/valu -o run --output-format csv -- python3 bench.py $SHORT ${PROF_ARGS} > $OUT/valu.log 2>&1 || { echo "valu pass failed"; tail -20 $OUT/valu.log; exit 1; }
 python3 scripts/traffic.py $OUT/fetch $OUT/write profiles/traffic_latest.json --valu-dir $OUT/valu --lib deeparc-sfm_amd/libdab.so > $OUT/traffic.txt 2>&1 || { cat $OUT/traffic.txt; exit 1; }
-cp profiles/traffic_latest.json $OUT/
+cp profiles/traffic_latest.json $OUT/  # copy it back into profiles/ here (only gpurun_out/ returns)
 head -25 $OUT/traffic.txt
 timeout -k 10 600 python3 bench.py ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
