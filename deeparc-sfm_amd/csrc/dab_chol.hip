@@ -1012,7 +1012,16 @@ __global__ __launch_bounds__(kThreads) void k_trsv_back_flow(const double* __res
 static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y,
                                  int* d_flag);
 
+static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag, bool launch);
 int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag) {
+  return chol_build(c, s, n, A, lda, y, d_flag, true);
+}
+// the scratch and the captured graph of a factorisation of this shape and these buffers,
+// without running it (the solve's set-up, so its first LM iteration does not capture)
+int chol_prepare(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag) {
+  return chol_build(c, s, n, A, lda, y, d_flag, false);
+}
+static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag, bool launch) {
   if (n <= 0) return 0;
   const int nblk = (n + NB - 1) / NB;
   if ((size_t)nblk > c->nblk_alloc) {
@@ -1039,7 +1048,7 @@ int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
     c->ev_bulk.push_back(b);
   }
   if (c->nograph) {  // debugging aid: launch directly on the two streams
-    enqueue_factor_solve(c, s, n, A, lda, y, d_flag);
+    if (launch) enqueue_factor_solve(c, s, n, A, lda, y, d_flag);
     return 0;
   }
   const bool same = c->exec && c->g_n == n && c->g_lda == lda && c->g_A == A && c->g_y == y && c->g_flag == d_flag;
@@ -1062,6 +1071,7 @@ int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
     c->g_y = y;
     c->g_flag = d_flag;
   }
+  if (!launch) return 0;
   return hipGraphLaunch(c->exec, s) == hipSuccess ? 0 : -3;
 }
 

@@ -327,6 +327,7 @@ struct CholCtx;
 CholCtx* chol_create();
 void chol_destroy(CholCtx*);
 int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag);
+int chol_prepare(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag);
 
 int grid_for(int n, int block, int cap);
 

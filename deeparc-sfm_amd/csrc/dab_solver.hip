@@ -2592,6 +2592,11 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
   const bool use_pcg = opt.linear_solver_type == DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG;
   HIP_OK(hipSetDevice(h->device));
   CHECK_RC(use_pcg ? build_pcg_buffers(h) : build_schur_tables(h));
+  // the dense factorisation's scratch and captured graph belong to the set-up, not to the
+  // first LM iteration (kept while the camera count and the buffers stay the same)
+  if (!use_pcg && h->NC > 0 &&
+      chol_prepare(h->chol, h->stream, 6 * h->NC, h->d_S, h->lds, h->d_yc, h->d_flags + 1) != 0)
+    return set_error(DAB_E_DEVICE, "dense Cholesky set-up failed");
   // Y records of each step: fp64 (both layouts), or fp32 for the mixed-precision PCG
   // (Jacobians, residuals, V/U/g, the CG vectors and scalars stay fp64)
   // (the matrix-free PCG of small camera sets stores no Y and is all fp64)
