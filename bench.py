@@ -201,7 +201,8 @@ def main():
             if not args.no_lm:
                 p40, e40 = sprob.points.copy(), sprob.ext.copy()
                 for tag, lst in (("c4_lm", pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR),
-                                 ("c4_lm_pcg", pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)):
+                                 ("c4_lm_pcg", pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG),
+                                 ("c4_lm_auto", pkg.DAB_LINEAR_SOLVER_AUTO)):
                     csolver.update_parameters(p40, e40)
                     barrier()
                     summ4 = csolver.solve(pkg.options(max_num_iterations=args.lm_iters, function_tolerance=0.0,
@@ -210,6 +211,8 @@ def main():
                     its4 = [it["time"] for it in summ4["iterations"][1:]]
                     c4[f"{tag}_iter_ms_median"] = max_over_ranks(1e3 * float(np.median(its4))) if its4 else None
                     c4[f"{tag}_final_cost"] = summ4["final_cost"]
+                    c4[f"{tag}_solver_used"] = {0: "explicit Schur (DENSE_SCHUR)",
+                                                1: "implicit Schur PCG"}[summ4["linear_solver_type_used"]]
             csolver.close()
             del gprob, sprob
         c4["c4_config"] = f"{args.config} global problem point-sharded over {world} rank(s) (strong scaling)"

@@ -13,6 +13,7 @@ LIB_PATH = os.path.join(HERE, "libdab.so")
 DAB_OK = 0
 DAB_LINEAR_SOLVER_EXPLICIT_SCHUR = 0
 DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG = 1
+DAB_LINEAR_SOLVER_AUTO = 2
 DAB_CONVERGENCE = 0
 DAB_NO_CONVERGENCE = 1
 DAB_FAILURE = 2

@@ -2587,8 +2587,13 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
   if (opt_in) opt = *opt_in;
   else dab_options_init(&opt);
   if (opt.linear_solver_type != DAB_LINEAR_SOLVER_EXPLICIT_SCHUR &&
-      opt.linear_solver_type != DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)
+      opt.linear_solver_type != DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG &&
+      opt.linear_solver_type != DAB_LINEAR_SOLVER_AUTO)
     return set_error(DAB_E_INVALID, "unknown linear_solver_type");
+  if (opt.linear_solver_type == DAB_LINEAR_SOLVER_AUTO)  // the same choice on every rank (NC is the union's)
+    opt.linear_solver_type = h->world <= 1 || h->NC == 0 || mf_schur_fits(h->NC, h->E, h->NI)
+                                 ? DAB_LINEAR_SOLVER_EXPLICIT_SCHUR
+                                 : DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG;
   const bool use_pcg = opt.linear_solver_type == DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG;
   HIP_OK(hipSetDevice(h->device));
   CHECK_RC(use_pcg ? build_pcg_buffers(h) : build_schur_tables(h));

@@ -91,6 +91,13 @@ typedef struct dab_problem {
  * Ceres trust-region defaults it relies on implicitly) ------------- */
 #define DAB_LINEAR_SOLVER_EXPLICIT_SCHUR 0  /* exact: DENSE_SCHUR equivalent (sfm.cc:67) */
 #define DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG 1 /* inexact: ITERATIVE_SCHUR + SCHUR_JACOBI */
+/* the exact step where it scales over the ranks, PCG where it does not: EXPLICIT_SCHUR on
+ * one rank and, on several, for small camera systems (<= 160 free cameras: the rig; S is a
+ * few MB to all-reduce and its factorisation takes microseconds); IMPLICIT_SCHUR_PCG for
+ * large camera systems on several ranks (BASELINE config 4: the 288-MB S all-reduce and the
+ * serial 5.5-ms factorisation on every rank would cap the speed-up near 1.2x). The summary's
+ * linear_solver_type_used says which ran. */
+#define DAB_LINEAR_SOLVER_AUTO 2
 
 typedef struct dab_options {
   int32_t max_num_iterations;            /* sfm.cc:69 (call sites pass 100) */
@@ -155,7 +162,8 @@ typedef struct dab_summary {
   dab_iteration* iterations;       /* optional caller buffer (may be NULL) */
   int32_t iterations_capacity;     /* entries available in `iterations` */
   int32_t iterations_written;      /* entries filled */
-  int32_t linear_solver_type_used; /* the DAB_LINEAR_SOLVER_* that ran (the requested one) */
+  int32_t linear_solver_type_used; /* the DAB_LINEAR_SOLVER_* that ran (the requested one, or
+                                      what DAB_LINEAR_SOLVER_AUTO chose) */
   int32_t schur_assembly;          /* EXPLICIT_SCHUR: DAB_SCHUR_* (how S was assembled);
                                       IMPLICIT_SCHUR_PCG: DAB_PCG_* (the Schur products) */
 } dab_summary;

@@ -57,14 +57,22 @@ def main():
         else:
             glob = pkg.synth(**pkg.CONFIGS[kind])
         owner = glob.point_owner(world)
-        for lst in (pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR, pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG):
+        for lst in (pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR, pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG,
+                    pkg.DAB_LINEAR_SOLVER_AUTO):
             opts = pkg.options(max_num_iterations=a.iters, linear_solver_type=lst)
             ref = None
             if rank == 0:
                 g1 = glob.copy()
                 s1 = pkg.Solver(dev)
                 s1.set_problem(g1)
-                ref = (s1.solve(opts), g1.points.copy(), g1.ext.copy())
+                ropts = opts
+                if lst == pkg.DAB_LINEAR_SOLVER_AUTO:
+                    # what AUTO must pick on several ranks: the exact step for small camera
+                    # systems (the rig), PCG for large ones (BAL / config 4)
+                    want = (pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR if glob.ext.shape[0] <= 160
+                            else pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)
+                    ropts = pkg.options(max_num_iterations=a.iters, linear_solver_type=want)
+                ref = (s1.solve(ropts), g1.points.copy(), g1.ext.copy())
                 s1.close()
             dist.barrier()
             mine = glob.copy().shard(rank, world)
@@ -93,14 +101,16 @@ def main():
                     dpts=float(np.abs(pts.numpy() - rp).max()),
                     dext=float(np.abs(ext.numpy() - re).max()),
                     ext_ranks_equal=bool(torch.equal(ext, ext_min)),
-                    eval_schedule=sched, p2p=p2p)
+                    eval_schedule=sched, p2p=p2p,
+                    solver_used=(summ["linear_solver_type_used"], rs["linear_solver_type_used"]))
     if rank == 0:
         print(json.dumps(out, indent=1))
         bad = [k for k, v in out.items()
                if v["iters"][0] != v["iters"][1] or v["max_rel_cost"] > 1e-8 or v["dpts"] > 1e-6
                or v["dext"] > 1e-6 or not v["ext_ranks_equal"]
                or (not k.startswith("rig") and v["eval_schedule"] != 2)  # BAL shards: the split fused pass
-               or (a.expect_p2p and v["p2p"] != 1)]
+               or (a.expect_p2p and v["p2p"] != 1)
+               or v["solver_used"][0] != v["solver_used"][1]]
         print("DIST_CHECK", "FAIL " + ",".join(bad) if bad else "OK")
     dist.destroy_process_group()
 
