@@ -80,6 +80,15 @@ void su_points(hipStream_t s, int NP, const int* pt_of, const double* raw_points
 // (17) iota; out[c] = in[idx[c]] (small tables read back to the host)
 void su_iota(hipStream_t s, int n, int* out);
 void su_gather_at(hipStream_t s, int n, const int* idx, const int* in, int* out);
+// (18) explicit-Schur pair tables: per point the count of ordered entry pairs (e, f) with
+// cam(e) >= cam(f) (and their 64-bit total, added into *total); the pairs in (point, e, f)
+// order as key cam(e) NC + cam(f), value = position, ef = (e, f); after the stable sort by
+// key, pairs[i] = (ent_pos[e], ent_pos[f]) of the i-th sorted position
+void su_pair_count(hipStream_t s, int NP, const int* pt_ent_ptr, const int* ent_cam, int* cnt,
+                   unsigned long long* total);
+void su_pair_gen(hipStream_t s, int NP, const int* pt_ent_ptr, const int* ent_cam, const int* poff, int NC, int* keys,
+                 int* vals, int2* ef);
+void su_pair_gather(hipStream_t s, int n, const int* idx, const int2* ef, const int* ent_pos, int2* pairs);
 // code-object warm-up (handle creation)
 void warm_setup();
 

@@ -496,4 +496,62 @@ void warm_setup() {
   (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k_su_count));
 }
 
+// ---- (18) explicit-Schur pair tables (build_schur_tables, large camera sets) ----
+// ordered entry pairs (e, f) of one point with cam(e) >= cam(f), generated per point in
+// (e, f) order: the host path's order before its stable sort by block key
+__global__ __launch_bounds__(kSuBlock) void k_su_pair_count(int NP, const int* __restrict__ ptr,
+                                                            const int* __restrict__ cam, int* __restrict__ cnt,
+                                                            unsigned long long* __restrict__ total) {
+  __shared__ int red[kSuBlock / 64];
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  int c = 0;
+  if (p < NP) {
+    const int b = ptr[p], e = ptr[p + 1];
+    for (int i = b; i < e; ++i) {
+      const int ci = cam[i];
+      for (int j = b; j < e; ++j) c += ci >= cam[j];
+    }
+    cnt[p] = c;
+  }
+  const int t = block_sum(c, red);
+  if (threadIdx.x == 0 && t) atomicAdd(total, (unsigned long long)t);  // integer: order-free
+}
+void su_pair_count(hipStream_t s, int NP, const int* pt_ent_ptr, const int* ent_cam, int* cnt,
+                   unsigned long long* total) {
+  if (NP > 0) k_su_pair_count<<<su_grid(NP), kSuBlock, 0, s>>>(NP, pt_ent_ptr, ent_cam, cnt, total);
+}
+__global__ void k_su_pair_gen(int NP, const int* __restrict__ ptr, const int* __restrict__ cam,
+                              const int* __restrict__ poff, int NC, int* __restrict__ keys, int* __restrict__ vals,
+                              int2* __restrict__ ef) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= NP) return;
+  const int b = ptr[p], e = ptr[p + 1];
+  int o = poff[p];
+  for (int i = b; i < e; ++i) {
+    const int ci = cam[i];
+    for (int j = b; j < e; ++j) {
+      const int cj = cam[j];
+      if (ci < cj) continue;
+      keys[o] = ci * NC + cj;
+      vals[o] = o;
+      ef[o] = make_int2(i, j);
+      ++o;
+    }
+  }
+}
+void su_pair_gen(hipStream_t s, int NP, const int* pt_ent_ptr, const int* ent_cam, const int* poff, int NC, int* keys,
+                 int* vals, int2* ef) {
+  if (NP > 0) k_su_pair_gen<<<su_grid(NP), kSuBlock, 0, s>>>(NP, pt_ent_ptr, ent_cam, poff, NC, keys, vals, ef);
+}
+__global__ void k_su_pair_gather(int n, const int* __restrict__ idx, const int2* __restrict__ ef,
+                                 const int* __restrict__ ent_pos, int2* __restrict__ pairs) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int2 q = ef[idx[i]];
+  pairs[i] = make_int2(ent_pos[q.x], ent_pos[q.y]);  // Y records are camera-major
+}
+void su_pair_gather(hipStream_t s, int n, const int* idx, const int2* ef, const int* ent_pos, int2* pairs) {
+  if (n > 0) k_su_pair_gather<<<su_grid(n), kSuBlock, 0, s>>>(n, idx, ef, ent_pos, pairs);
+}
+
 }  // namespace dab

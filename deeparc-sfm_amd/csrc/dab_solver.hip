@@ -2024,8 +2024,105 @@ static int build_schur_tiles(dab_handle* h) {
   return 0;
 }
 
+// present block keys: the union over ranks (every rank must all-reduce the same S layout)
+static int union_block_keys(dab_handle* h, std::vector<long long>& keys) {
+  if (h->world <= 1) return 0;
+  const int NC = h->NC;
+  hipStream_t s = h->stream;
+  std::vector<double> bm((size_t)NC * NC, 0.0);
+  for (long long k : keys) bm[(size_t)k] = 1.0;
+  double* d_bm = nullptr;
+  CHECK_RC(h->dev.alloc(&d_bm, bm.size()));
+  HIP_OK(hipMemcpyAsync(d_bm, bm.data(), bm.size() * sizeof(double), hipMemcpyHostToDevice, s));
+  CHECK_RC(h->allreduce(d_bm, bm.size(), ncclMax));
+  HIP_OK(hipMemcpyAsync(bm.data(), d_bm, bm.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  keys.clear();
+  for (size_t i = 0; i < bm.size(); ++i)
+    if (bm[i] != 0.0) keys.push_back((long long)i);
+  return 0;
+}
+
+// Pair tables on the device (dab_setup.hip, 18): h->d_pairs in sorted (key, e, f) order;
+// pk / pbeg: the present keys (increasing) and their first pair; np2 pairs
+static int build_schur_pairs_device(dab_handle* h, std::vector<long long>& pk, std::vector<int>& pbeg,
+                                    long long& np2) {
+  hipStream_t s = h->stream;
+  const int NP = h->NP, NC = h->NC;
+  Dev& tmp = h->setup_tmp;  // released at the next set-up
+  void* rtmp = nullptr;
+  size_t rtmp_cap = 0;
+  auto rp = [&](auto call) -> int {
+    size_t bytes = 0;
+    if (call(nullptr, &bytes) != 0) return set_error(DAB_E_DEVICE, "rocPRIM size query failed");
+    if (bytes > rtmp_cap) {
+      void* q = nullptr;
+      CHECK_RC(tmp.alloc(reinterpret_cast<unsigned char**>(&q), bytes));
+      rtmp = q;
+      rtmp_cap = bytes;
+    }
+    if (call(rtmp, &bytes) != 0) return set_error(DAB_E_DEVICE, "rocPRIM pass failed");
+    return 0;
+  };
+  int* cnt = nullptr;
+  unsigned long long* tot = nullptr;
+  CHECK_RC(tmp.alloc(&cnt, (size_t)NP + 1));
+  CHECK_RC(tmp.alloc(&tot, 1));
+  HIP_OK(hipMemsetAsync(tot, 0, sizeof(unsigned long long), s));
+  HIP_OK(hipMemsetAsync(cnt + NP, 0, sizeof(int), s));
+  su_pair_count(s, NP, h->d_pt_ent_ptr, h->d_ent_cam, cnt, tot);
+  unsigned long long total = 0;
+  HIP_OK(hipMemcpyAsync(&total, tot, sizeof(total), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  double flag = NC > 0 && (long long)total > kMaxExplicitPairs ? 1.0 : 0.0;
+  CHECK_RC(max_all_ranks(h, flag));  // every rank must take the same branch
+  if (flag != 0.0)
+    return set_error(DAB_E_UNSUPPORTED,
+                     "reduced camera system too large for explicit Schur pair tables (" + std::to_string(total) +
+                         " pairs); use DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG");
+  np2 = NC > 0 ? (long long)total : 0;
+  const int n = (int)np2;
+  pk.clear();
+  pbeg.clear();
+  CHECK_RC(h->dev.alloc(&h->d_pairs, (size_t)std::max(1, n)));
+  if (n == 0) return 0;
+  int *poff = nullptr, *k1 = nullptr, *v1 = nullptr, *k2 = nullptr, *v2 = nullptr, *uk = nullptr, *uc = nullptr,
+      *nr = nullptr;
+  int2* ef = nullptr;
+  CHECK_RC(tmp.alloc(&poff, (size_t)NP + 1));
+  CHECK_RC(tmp.alloc(&k1, (size_t)n));
+  CHECK_RC(tmp.alloc(&v1, (size_t)n));
+  CHECK_RC(tmp.alloc(&k2, (size_t)n));
+  CHECK_RC(tmp.alloc(&v2, (size_t)n));
+  CHECK_RC(tmp.alloc(&ef, (size_t)n));
+  CHECK_RC(rp([&](void* t, size_t* b) { return su_exclusive_scan(t, b, cnt, poff, NP + 1, s); }));
+  su_pair_gen(s, NP, h->d_pt_ent_ptr, h->d_ent_cam, poff, NC, k1, v1, ef);
+  CHECK_RC(rp([&](void* t, size_t* b) { return su_sort_pairs(t, b, k1, k2, v1, v2, n, bits_for(NC * NC), s); }));
+  su_pair_gather(s, n, v2, ef, h->d_ent_pos, h->d_pairs);
+  // present keys and their run lengths
+  uk = k1;  // the unsorted keys are no longer needed
+  uc = v1;
+  CHECK_RC(tmp.alloc(&nr, 1));
+  CHECK_RC(rp([&](void* t, size_t* b) { return su_rle(t, b, k2, uk, uc, nr, n, s); }));
+  int nruns = 0;
+  HIP_OK(hipMemcpyAsync(&nruns, nr, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  std::vector<int> ukh(nruns), uch(nruns);
+  HIP_OK(hipMemcpyAsync(ukh.data(), uk, sizeof(int) * (size_t)nruns, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(uch.data(), uc, sizeof(int) * (size_t)nruns, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  pk.resize(nruns);
+  pbeg.resize(nruns);
+  int acc = 0;
+  for (int i = 0; i < nruns; ++i) {
+    pk[i] = ukh[i];
+    pbeg[i] = acc;
+    acc += uch[i];
+  }
+  return 0;
+}
+
 static int build_schur_tables(dab_handle* h) {
-  if (!h->schur_built) CHECK_RC(fetch_host_entries(h));
   if (h->schur_built) return 0;
   static const bool timing = getenv("DAB_SETUP_TIMING") != nullptr;
   const double t_b = now_s();
@@ -2049,9 +2146,13 @@ static int build_schur_tables(dab_handle* h) {
   const big_vec<int>& ent_cam = h->h_ent_cam;
   const big_vec<int>& ent_pos = h->h_ent_pos;
   {
-    // tile mode: every rank must take the same branch (the all-reduced S layouts differ)
+    // tile mode: every rank must take the same branch (the all-reduced S layouts differ).
+    // The host entry lists are needed by the tile tables (and by the host reference path of
+    // the pair tables); large camera sets with device set-up never fetch them.
+    const bool tiles_possible = h->knobs.schur_tiles != 0 && NC > 0 && mf_schur_fits(NC, h->E, h->NI);
+    if (tiles_possible) CHECK_RC(fetch_host_entries(h));
     std::vector<int> tmax(setup_threads(), 0);  // distinct free cameras of one point
-    par_for(NP, [&](long long pb, long long pe, int t) {
+    if (tiles_possible) par_for(NP, [&](long long pb, long long pe, int t) {
       std::vector<int> seen(std::max(1, NC), -1);
       for (int pt = (int)pb; pt < (int)pe; ++pt) {
         int m = 0;
@@ -2065,8 +2166,7 @@ static int build_schur_tables(dab_handle* h) {
     });
     const int maxm = *std::max_element(tmax.begin(), tmax.end());
     phase("camera counts");
-    double no_tiles = (h->knobs.schur_tiles != 0 && NC > 0 && mf_schur_fits(NC, h->E, h->NI) && maxm <= kTileMaxRec)
-                          ? 0.0 : 1.0;
+    double no_tiles = (tiles_possible && maxm <= kTileMaxRec) ? 0.0 : 1.0;
     CHECK_RC(max_all_ranks(h, no_tiles));
     h->schur_tiles = no_tiles == 0.0;
   }
@@ -2086,23 +2186,51 @@ static int build_schur_tables(dab_handle* h) {
     h->schur_built = true;
     return 0;
   }
-  long long total = 0;
-  for (int pt = 0; pt < NP; ++pt) {
-    const long long m = pt_ent_ptr[pt + 1] - pt_ent_ptr[pt];
-    total += m * (m + 1) / 2 + m;  // upper bound
-  }
-  double flag = total > kMaxExplicitPairs ? 1.0 : 0.0;
-  CHECK_RC(max_all_ranks(h, flag));  // every rank must take the same branch
-  if (flag != 0.0)
-    return set_error(DAB_E_UNSUPPORTED,
-                     "reduced camera system too large for explicit Schur pair tables (" +
-                         std::to_string(total) + " pairs); use DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG");
   // reduced-camera-system blocks: ordered entry pairs (e, f) of one point with
   // cam(e) >= cam(f); block (cam(e), cam(f)) of the lower triangle of S.
   std::vector<long long> blkkeys;
   std::vector<int2> pairs;
   std::vector<int> blk_pair_beg;
-  if (NC > 0) {
+  const bool on_device = !h->host_entries;
+  if (on_device) {
+    // device: count, scan, generate, stable radix sort by block key, gather (bitwise the
+    // host path's tables; the pairs stay on the device)
+    std::vector<long long> pk;
+    std::vector<int> pbeg;
+    long long np2 = 0;
+    CHECK_RC(build_schur_pairs_device(h, pk, pbeg, np2));
+    phase("pairs on device");
+    std::vector<long long> diag((size_t)NC), keys;
+    for (int c = 0; c < NC; ++c) diag[c] = (long long)c * NC + c;
+    keys.reserve(pk.size() + diag.size());
+    std::merge(pk.begin(), pk.end(), diag.begin(), diag.end(), std::back_inserter(keys));
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    CHECK_RC(union_block_keys(h, keys));
+    blkkeys = keys;
+    blk_pair_beg.assign(blkkeys.size() + 1, 0);
+    size_t j = 0;
+    for (size_t b2 = 0; b2 < blkkeys.size(); ++b2) {
+      while (j < pk.size() && pk[j] < blkkeys[b2]) ++j;
+      blk_pair_beg[b2] = j < pk.size() ? pbeg[j] : (int)np2;
+    }
+    blk_pair_beg[blkkeys.size()] = (int)np2;
+    h->npairs = np2;
+  }
+  long long total = 0;
+  if (!on_device) {
+    for (int pt = 0; pt < NP; ++pt) {
+      const long long m = pt_ent_ptr[pt + 1] - pt_ent_ptr[pt];
+      total += m * (m + 1) / 2 + m;  // upper bound
+    }
+    double flag = total > kMaxExplicitPairs ? 1.0 : 0.0;
+    CHECK_RC(max_all_ranks(h, flag));  // every rank must take the same branch
+    if (flag != 0.0)
+      return set_error(DAB_E_UNSUPPORTED,
+                       "reduced camera system too large for explicit Schur pair tables (" +
+                           std::to_string(total) + " pairs); use DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG");
+  }
+  if (on_device) {
+  } else if (NC > 0) {
     // pairs generated per point in parallel, in (e, f) order (entries are point-major, so
     // that is the global (e, f) order), then a stable counting sort by block key: the
     // (key, e, f) order of the former comparison sort (~0.4 s at C3), bitwise the same tables
@@ -2165,19 +2293,7 @@ static int build_schur_tables(dab_handle* h) {
     keys.reserve(pk.size() + diag.size());
     std::merge(pk.begin(), pk.end(), diag.begin(), diag.end(), std::back_inserter(keys));  // both sorted
     keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
-    if (h->world > 1) {
-      std::vector<double> bm((size_t)NC * NC, 0.0);
-      for (long long k : keys) bm[(size_t)k] = 1.0;
-      double* d_bm = nullptr;
-      CHECK_RC(h->dev.alloc(&d_bm, bm.size()));
-      HIP_OK(hipMemcpyAsync(d_bm, bm.data(), bm.size() * sizeof(double), hipMemcpyHostToDevice, s));
-      CHECK_RC(h->allreduce(d_bm, bm.size(), ncclMax));
-      HIP_OK(hipMemcpyAsync(bm.data(), d_bm, bm.size() * sizeof(double), hipMemcpyDeviceToHost, s));
-      HIP_OK(hipStreamSynchronize(s));
-      keys.clear();
-      for (size_t i = 0; i < bm.size(); ++i)
-        if (bm[i] != 0.0) keys.push_back((long long)i);
-    }
+    CHECK_RC(union_block_keys(h, keys));
     blkkeys = keys;
     blk_pair_beg.assign(blkkeys.size() + 1, 0);
     size_t j = 0;  // blocks without local pairs start where the next present key does
@@ -2191,12 +2307,12 @@ static int build_schur_tables(dab_handle* h) {
   }
   phase("block keys");
   h->nblk = (int)blkkeys.size();
-  h->npairs = (long long)pairs.size();
+  if (!on_device) h->npairs = (long long)pairs.size();
   std::vector<int2> blk_cam(h->nblk);
   for (int b = 0; b < h->nblk; ++b) blk_cam[b] = make_int2((int)(blkkeys[b] / NC), (int)(blkkeys[b] % NC));
 
   Dev& d = h->dev;
-  CHECK_RC(upload(&h->d_pairs, d, pairs, s));
+  if (!on_device) CHECK_RC(upload(&h->d_pairs, d, pairs, s));
   CHECK_RC(upload(&h->d_blk_cam, d, blk_cam, s));
   CHECK_RC(upload(&h->d_blk_pair_beg, d, blk_pair_beg, s));
   CHECK_RC(d.alloc(&h->d_spack, h->spack_count()));
