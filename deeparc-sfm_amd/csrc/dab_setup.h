@@ -89,6 +89,15 @@ void su_pair_count(hipStream_t s, int NP, const int* pt_ent_ptr, const int* ent_
 void su_pair_gen(hipStream_t s, int NP, const int* pt_ent_ptr, const int* ent_cam, const int* poff, int NC, int* keys,
                  int* vals, int2* ef);
 void su_pair_gather(hipStream_t s, int n, const int* idx, const int2* ef, const int* ent_pos, int2* pairs);
+// (19) explicit-S block tiles: per point its entries as (slot, camera) sorted by (camera,
+// slot) and its count of distinct cameras; per batch (64-thread block) the header and the
+// records ordered (camera, point); sampled block hit counts (every 4th point, added into
+// hits[nb])
+void su_tile_sort(hipStream_t s, int NP, const int* pt_ent_ptr, const int* ent_cam, const int* ent_os, int2* sch,
+                  int* m);
+void su_tile_batch(hipStream_t s, int nbatch, int NC, const int* batch_pt, const int* batch_rec, const int* pt_ent_ptr,
+                   const int2* sch, const int4* obs_idx, int hdr_bytes, unsigned char* hdr, int4* rec, int4* robs);
+void su_tile_hits(hipStream_t s, int NP, int nb, const int* pt_ent_ptr, const int2* sch, int* hits);
 // code-object warm-up (handle creation)
 void warm_setup();
 

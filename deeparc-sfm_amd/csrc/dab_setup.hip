@@ -554,4 +554,111 @@ void su_pair_gather(hipStream_t s, int n, const int* idx, const int2* ef, const 
   if (n > 0) k_su_pair_gather<<<su_grid(n), kSuBlock, 0, s>>>(n, idx, ef, ent_pos, pairs);
 }
 
+// ---- (19) explicit-S block tiles (build_schur_tiles, small camera sets) ----
+// per point: its entries as (slot, camera) sorted by (camera, slot); distinct cameras m[p]
+__global__ void k_su_tile_sort(int NP, const int* __restrict__ ptr, const int* __restrict__ cam,
+                               const int* __restrict__ os, int2* __restrict__ sch, int* __restrict__ m) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= NP) return;
+  const int b = ptr[p], e = ptr[p + 1];
+  for (int i = b; i < e; ++i) {  // insertion sort in place (short lists; keys are unique)
+    const int2 v = make_int2(os[i], cam[i]);
+    int j = i;
+    while (j > b) {
+      const int2 u = sch[j - 1];
+      if (u.y < v.y || (u.y == v.y && u.x < v.x)) break;
+      sch[j] = u;
+      --j;
+    }
+    sch[j] = v;
+  }
+  int c = 0;
+  for (int i = b; i < e; ++i) c += (i == b || sch[i].y != sch[i - 1].y);
+  m[p] = c;
+}
+void su_tile_sort(hipStream_t s, int NP, const int* pt_ent_ptr, const int* ent_cam, const int* ent_os, int2* sch,
+                  int* m) {
+  if (NP > 0) k_su_tile_sort<<<su_grid(NP), kSuBlock, 0, s>>>(NP, pt_ent_ptr, ent_cam, ent_os, sch, m);
+}
+// one 64-thread block per batch, thread = point of the batch: the header (mask per camera,
+// records before each camera) and the records ordered (camera, point) inside the batch
+__global__ __launch_bounds__(64) void k_su_tile_batch(int NC, const int* __restrict__ batch_pt,
+                                                      const int* __restrict__ batch_rec, const int* __restrict__ ptr,
+                                                      const int2* __restrict__ sch, const int4* __restrict__ obs_idx,
+                                                      int hdr_bytes, unsigned char* __restrict__ hdr,
+                                                      int4* __restrict__ rec, int4* __restrict__ robs) {
+  extern __shared__ unsigned long long tb_lds[];
+  unsigned long long* mask = tb_lds;                       // [NC]
+  int* off = reinterpret_cast<int*>(tb_lds + NC);          // [NC + 1]
+  const int b = blockIdx.x, t = threadIdx.x;
+  for (int c = t; c < NC; c += 64) mask[c] = 0ull;
+  for (int c = t; c <= NC; c += 64) off[c] = 0;
+  __syncthreads();
+  const int p = batch_pt[b] + t;
+  const bool live = p < batch_pt[b + 1];
+  if (live)
+    for (int i = ptr[p]; i < ptr[p + 1]; ++i)
+      if (i == ptr[p] || sch[i].y != sch[i - 1].y) {
+        __hip_atomic_fetch_or(mask + sch[i].y, 1ull << t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(off + sch[i].y + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+  __syncthreads();
+  if (t == 0)
+    for (int c = 0; c < NC; ++c) off[c + 1] += off[c];
+  __syncthreads();
+  unsigned long long* hm = reinterpret_cast<unsigned long long*>(hdr + (size_t)b * hdr_bytes);
+  int* ho = reinterpret_cast<int*>(hdr + (size_t)b * hdr_bytes + 8 * (size_t)NC);
+  for (int c = t; c < NC; c += 64) hm[c] = mask[c];
+  for (int c = t; c <= NC; c += 64) ho[c] = off[c];
+  if (!live) return;
+  const unsigned long long below = (1ull << t) - 1ull;
+  int r = -1;
+  for (int i = ptr[p]; i < ptr[p + 1]; ++i) {
+    const int c = sch[i].y;
+    if (i > ptr[p] && c == sch[i - 1].y) {
+      rec[r].y++;
+      continue;
+    }
+    r = batch_rec[b] + off[c] + __popcll(mask[c] & below);
+    rec[r] = make_int4(i, 1, p, c);
+    const int4 oi = obs_idx[sch[i].x >> 1];  // the slot's observation: (point, ext0, ext1, intr)
+    robs[r] = make_int4(sch[i].x, oi.y, oi.z, oi.w);
+  }
+}
+void su_tile_batch(hipStream_t s, int nbatch, int NC, const int* batch_pt, const int* batch_rec, const int* pt_ent_ptr,
+                   const int2* sch, const int4* obs_idx, int hdr_bytes, unsigned char* hdr, int4* rec, int4* robs) {
+  if (nbatch <= 0) return;
+  const size_t lds = sizeof(unsigned long long) * (size_t)NC + sizeof(int) * ((size_t)NC + 1);
+  k_su_tile_batch<<<nbatch, 64, lds, s>>>(NC, batch_pt, batch_rec, pt_ent_ptr, sch, obs_idx, hdr_bytes, hdr, rec,
+                                          robs);
+}
+// block hit counts from every 4th point: the points that see both cameras of the block
+// (integer counts: the order of the adds does not matter)
+__global__ __launch_bounds__(kSuBlock) void k_su_tile_hits(int NP, int nb, const int* __restrict__ ptr,
+                                                           const int2* __restrict__ sch, int* __restrict__ hits) {
+  extern __shared__ int th_lds[];  // [nb]
+  for (int k = threadIdx.x; k < nb; k += blockDim.x) th_lds[k] = 0;
+  __syncthreads();
+  const int p = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
+  if (p < NP) {
+    const int b = ptr[p], e = ptr[p + 1];
+    for (int x = b; x < e; ++x) {
+      if (x > b && sch[x].y == sch[x - 1].y) continue;
+      const int cx = sch[x].y;
+      const int base = (cx * (cx + 1)) >> 1;
+      for (int y = b; y <= x; ++y) {
+        if (y > b && sch[y].y == sch[y - 1].y) continue;
+        atomicAdd(th_lds + base + sch[y].y, 1);
+      }
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < nb; k += blockDim.x)
+    if (th_lds[k]) atomicAdd(hits + k, th_lds[k]);
+}
+void su_tile_hits(hipStream_t s, int NP, int nb, const int* pt_ent_ptr, const int2* sch, int* hits) {
+  const long long ns = (NP + 3) / 4;
+  if (ns > 0) k_su_tile_hits<<<su_grid(ns), kSuBlock, sizeof(int) * (size_t)nb, s>>>(NP, nb, pt_ent_ptr, sch, hits);
+}
+
 }  // namespace dab

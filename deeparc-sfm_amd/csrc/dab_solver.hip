@@ -278,7 +278,7 @@ struct dab_handle {
   // ---- host-side problem structure ----
   bool have_problem = false;
   bool local_compose = false;       // some observation of this rank is composed (arc∘ring)
-  bool host_entries = false;        // h_pt_ent_ptr / h_ent_* hold the entry lists (else fetched on use)
+  bool host_entries = false;        // h_pt_ent_ptr / h_ent_* hold the entry lists (host set-up path)
   dab_problem prob{};               // caller's arrays (pointers valid until next set_problem)
   int N = 0, NP = 0, E = 0, NI = 0, NC = 0, NE = 0, nplanes = 18;
   bool any_compose = false;
@@ -1836,26 +1836,12 @@ static int max_all_ranks(dab_handle* h, double& x) {  // max over ranks of one h
 static constexpr int kBatchPts = 64, kTileBlocks = 1024;
 // the entry lists on the host (the explicit-step table builders read them); the device
 // set-up leaves them on the device until a builder asks
-static int fetch_host_entries(dab_handle* h) {
-  if (h->host_entries) return 0;
-  hipStream_t s = h->stream;
-  h->h_pt_ent_ptr.resize((size_t)h->NP + 1);
-  h->h_ent_cam.resize(h->NE);
-  h->h_ent_pos.resize(h->NE);
-  h->h_ent_os.resize(h->NE);
-  HIP_OK(hipMemcpyAsync(h->h_pt_ent_ptr.data(), h->d_pt_ent_ptr, sizeof(int) * ((size_t)h->NP + 1),
-                        hipMemcpyDeviceToHost, s));
-  if (h->NE > 0) {
-    HIP_OK(hipMemcpyAsync(h->h_ent_cam.data(), h->d_ent_cam, sizeof(int) * (size_t)h->NE, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipMemcpyAsync(h->h_ent_pos.data(), h->d_ent_pos, sizeof(int) * (size_t)h->NE, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipMemcpyAsync(h->h_ent_os.data(), h->d_ent_os, sizeof(int) * (size_t)h->NE, hipMemcpyDeviceToHost, s));
-  }
-  HIP_OK(hipStreamSynchronize(s));
-  h->host_entries = true;
-  return 0;
-}
-
-static int build_schur_tiles(dab_handle* h) {
+// The tile tables (k_schur_y / k_schur_tiles): per point its entries sorted by (camera,
+// slot) (sch), one record per distinct (point, camera) ordered (batch, camera, point), batch
+// headers, and the blocks' owners. On the device (dab_setup.hip, 19) unless the host entry
+// lists are resident (DAB_SETUP_HOST=1: the host reference path); bitwise the same tables.
+// d_sch / d_m: the device per-point sort (su_tile_sort) when on the device.
+static int build_schur_tiles(dab_handle* h, int2* d_sch, const int* d_m) {
   hipStream_t s = h->stream;
   static const bool timing = getenv("DAB_SETUP_TIMING") != nullptr;
   double t_ph = now_s();
@@ -1866,31 +1852,15 @@ static int build_schur_tiles(dab_handle* h) {
     t_ph = t;
   };
   const int NP = h->NP, NC = h->NC;
-  const std::vector<int>& pt_ent_ptr = h->h_pt_ent_ptr;
-  const big_vec<int>& ent_cam = h->h_ent_cam;
-  const big_vec<int>& ent_os = h->h_ent_os;
-  big_vec<int2> sch(h->NE);
-  std::vector<int> rec_ptr(NP + 1, 0);
-  // per point (threads): entries sorted by (camera, slot), distinct cameras counted
-  par_for(NP, [&](long long pb, long long pe, int) {
-    for (int p = (int)pb; p < (int)pe; ++p) {
-      const int b = pt_ent_ptr[p], e = pt_ent_ptr[p + 1];
-      for (int i = b; i < e; ++i) sch[i] = make_int2(ent_os[i], ent_cam[i]);
-      std::sort(sch.begin() + b, sch.begin() + e, [](const int2& x, const int2& y) {
-        return x.y != y.y ? x.y < y.y : x.x < y.x;
-      });
-      int m = 0;
-      for (int i = b; i < e; ++i) m += (i == b || sch[i].y != sch[i - 1].y);
-      rec_ptr[p + 1] = m;
-    }
-  }, 2048);
-  for (int p = 0; p < NP; ++p) rec_ptr[p + 1] += rec_ptr[p];
-  const int nrec = rec_ptr[NP];
-  phase("sort entries");
-  // batches of whole points: <= kBatchPts points (one mask word) and <= cap records
-  std::vector<int> batch_rec{0}, batch_pt{0};
+  const bool on_device = d_sch != nullptr;
+  Dev& d = h->dev;
   const int cap = schur_tile_batch_cap(NC);
-  {
+  const int hdr_bytes = schur_tile_hdr_bytes(NC);
+  const int nb = (int)tri_n(NC);
+  std::vector<int> rec_ptr(NP + 1, 0);
+  std::vector<int> batch_rec{0}, batch_pt{0};
+  // batches of whole points: <= kBatchPts points (one mask word) and <= cap records
+  auto cut_batches = [&]() {
     int cur = 0, curp = 0;
     for (int p = 0; p < NP; ++p) {
       const int m = rec_ptr[p + 1] - rec_ptr[p];
@@ -1902,52 +1872,98 @@ static int build_schur_tiles(dab_handle* h) {
       cur += m;
       curp += 1;
     }
-    batch_rec.push_back(nrec);
+    batch_rec.push_back(rec_ptr[NP]);
     batch_pt.push_back(NP);
-  }
-  const int nbatch = (int)batch_rec.size() - 1;
-  // records ordered (batch, camera, point) and the batch headers: mask[NC] | off[NC + 1]
-  const int hdr_bytes = schur_tile_hdr_bytes(NC);
-  big_vec<int4> rec(nrec), robs(nrec);
-  std::vector<unsigned char> hdr((size_t)nbatch * hdr_bytes, 0);
-  par_for(nbatch, [&](long long bb, long long be, int) {
-    std::vector<int> pos(NC + 1);
-    for (int b = (int)bb; b < (int)be; ++b) {
-      unsigned long long* mask = reinterpret_cast<unsigned long long*>(&hdr[(size_t)b * hdr_bytes]);
-      int* off = reinterpret_cast<int*>(&hdr[(size_t)b * hdr_bytes + 8 * (size_t)NC]);
-      for (int p = batch_pt[b]; p < batch_pt[b + 1]; ++p)
-        for (int i = pt_ent_ptr[p]; i < pt_ent_ptr[p + 1]; ++i)
-          if (i == pt_ent_ptr[p] || sch[i].y != sch[i - 1].y) {
-            off[sch[i].y + 1]++;
-            mask[sch[i].y] |= 1ull << (p - batch_pt[b]);
+  };
+  std::vector<long long> hits(std::max(1, nb), 0);
+  int nbatch = 0, nrec = 0;
+  int *d_br = nullptr, *d_bp = nullptr;
+  unsigned char* d_hdr = nullptr;
+  int4 *d_rec = nullptr, *d_robs = nullptr;
+  if (on_device) {
+    {
+      std::vector<int> m(NP);
+      if (NP > 0) HIP_OK(hipMemcpyAsync(m.data(), d_m, sizeof(int) * (size_t)NP, hipMemcpyDeviceToHost, s));
+      HIP_OK(hipStreamSynchronize(s));
+      for (int p = 0; p < NP; ++p) rec_ptr[p + 1] = rec_ptr[p] + m[p];
+    }
+    cut_batches();
+    nbatch = (int)batch_rec.size() - 1;
+    nrec = rec_ptr[NP];
+    phase("device sort, batches");
+    CHECK_RC(upload(&d_br, d, batch_rec, s));
+    CHECK_RC(upload(&d_bp, d, batch_pt, s));
+    CHECK_RC(d.alloc(&d_hdr, (size_t)std::max(1, nbatch) * hdr_bytes));
+    CHECK_RC(d.alloc(&d_rec, (size_t)std::max(1, nrec)));
+    CHECK_RC(d.alloc(&d_robs, (size_t)std::max(1, nrec)));
+    HIP_OK(hipMemsetAsync(d_hdr, 0, (size_t)std::max(1, nbatch) * hdr_bytes, s));
+    su_tile_batch(s, nbatch, NC, d_bp, d_br, h->d_pt_ent_ptr, d_sch, h->d_obs_idx, hdr_bytes, d_hdr, d_rec, d_robs);
+    int* d_hits = nullptr;
+    CHECK_RC(h->setup_tmp.alloc(&d_hits, (size_t)std::max(1, nb)));
+    HIP_OK(hipMemsetAsync(d_hits, 0, sizeof(int) * (size_t)std::max(1, nb), s));
+    su_tile_hits(s, NP, nb, h->d_pt_ent_ptr, d_sch, d_hits);
+    std::vector<int> hi(std::max(1, nb));
+    HIP_OK(hipMemcpyAsync(hi.data(), d_hits, sizeof(int) * (size_t)std::max(1, nb), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    for (int k = 0; k < nb; ++k) hits[k] = hi[k];
+    phase("device records, hits");
+  } else {
+    const std::vector<int>& pt_ent_ptr = h->h_pt_ent_ptr;
+    const big_vec<int>& ent_cam = h->h_ent_cam;
+    const big_vec<int>& ent_os = h->h_ent_os;
+    big_vec<int2> sch(h->NE);
+    // per point (threads): entries sorted by (camera, slot), distinct cameras counted
+    par_for(NP, [&](long long pb, long long pe, int) {
+      for (int p = (int)pb; p < (int)pe; ++p) {
+        const int b = pt_ent_ptr[p], e = pt_ent_ptr[p + 1];
+        for (int i = b; i < e; ++i) sch[i] = make_int2(ent_os[i], ent_cam[i]);
+        std::sort(sch.begin() + b, sch.begin() + e, [](const int2& x, const int2& y) {
+          return x.y != y.y ? x.y < y.y : x.x < y.x;
+        });
+        int m = 0;
+        for (int i = b; i < e; ++i) m += (i == b || sch[i].y != sch[i - 1].y);
+        rec_ptr[p + 1] = m;
+      }
+    }, 2048);
+    for (int p = 0; p < NP; ++p) rec_ptr[p + 1] += rec_ptr[p];
+    nrec = rec_ptr[NP];
+    phase("sort entries");
+    cut_batches();
+    nbatch = (int)batch_rec.size() - 1;
+    // records ordered (batch, camera, point) and the batch headers: mask[NC] | off[NC + 1]
+    big_vec<int4> rec(nrec), robs(nrec);
+    std::vector<unsigned char> hdr((size_t)nbatch * hdr_bytes, 0);
+    par_for(nbatch, [&](long long bb, long long be, int) {
+      std::vector<int> pos(NC + 1);
+      for (int b = (int)bb; b < (int)be; ++b) {
+        unsigned long long* mask = reinterpret_cast<unsigned long long*>(&hdr[(size_t)b * hdr_bytes]);
+        int* off = reinterpret_cast<int*>(&hdr[(size_t)b * hdr_bytes + 8 * (size_t)NC]);
+        for (int p = batch_pt[b]; p < batch_pt[b + 1]; ++p)
+          for (int i = pt_ent_ptr[p]; i < pt_ent_ptr[p + 1]; ++i)
+            if (i == pt_ent_ptr[p] || sch[i].y != sch[i - 1].y) {
+              off[sch[i].y + 1]++;
+              mask[sch[i].y] |= 1ull << (p - batch_pt[b]);
+            }
+        for (int c = 0; c < NC; ++c) off[c + 1] += off[c];
+        for (int c = 0; c <= NC; ++c) pos[c] = off[c];
+        for (int p = batch_pt[b]; p < batch_pt[b + 1]; ++p) {
+          int r = -1;
+          for (int i = pt_ent_ptr[p]; i < pt_ent_ptr[p + 1]; ++i) {
+            if (i > pt_ent_ptr[p] && sch[i].y == sch[i - 1].y) {
+              rec[r].y++;
+              continue;
+            }
+            r = batch_rec[b] + pos[sch[i].y]++;
+            rec[r] = make_int4(i, 1, p, sch[i].y);
+            const int o = h->perm[sch[i].x >> 1];  // the caller's observation of the slot
+            robs[r] = make_int4(sch[i].x, h->prob.obs_ext0[o], h->prob.obs_ext1[o], h->prob.obs_intr[o]);
           }
-      for (int c = 0; c < NC; ++c) off[c + 1] += off[c];
-      for (int c = 0; c <= NC; ++c) pos[c] = off[c];
-      for (int p = batch_pt[b]; p < batch_pt[b + 1]; ++p) {
-        int r = -1;
-        for (int i = pt_ent_ptr[p]; i < pt_ent_ptr[p + 1]; ++i) {
-          if (i > pt_ent_ptr[p] && sch[i].y == sch[i - 1].y) {
-            rec[r].y++;
-            continue;
-          }
-          r = batch_rec[b] + pos[sch[i].y]++;
-          rec[r] = make_int4(i, 1, p, sch[i].y);
-          const int o = h->perm[sch[i].x >> 1];  // the caller's observation of the slot
-          robs[r] = make_int4(sch[i].x, h->prob.obs_ext0[o], h->prob.obs_ext1[o], h->prob.obs_intr[o]);
         }
       }
-    }
-  }, 16);
-  phase("records, headers");
-  // tiles: equal block ranges of <= kTileBlocks (rows up to the tile's last camera)
-  const int nb = (int)tri_n(NC);
-  const int ntile = std::max(1, (nb + kTileBlocks - 1) / kTileBlocks);
-  std::vector<int> tb(ntile + 1), clast(ntile);
-  for (int t = 0; t <= ntile; ++t) tb[t] = (int)((long long)nb * t / ntile);
-  // hit counts of every block from a sample of the points (every 4th): the points that see
-  // both of its cameras
-  std::vector<long long> hits(std::max(1, nb), 0);
-  {
+    }, 16);
+    phase("records, headers");
+    // hit counts of every block from a sample of the points (every 4th): the points that see
+    // both of its cameras
     std::vector<std::vector<long long>> th(setup_threads(), std::vector<long long>(std::max(1, nb), 0));
     par_for(NP, [&](long long pb, long long pe, int t) {
       std::vector<int> cams;
@@ -1962,7 +1978,17 @@ static int build_schur_tiles(dab_handle* h) {
     });
     for (auto& v : th)
       for (int k = 0; k < nb; ++k) hits[k] += v[k];
+    CHECK_RC(upload(&d_br, d, batch_rec, s));
+    CHECK_RC(upload(&d_hdr, d, hdr, s));
+    CHECK_RC(upload(&d_sch, d, sch, s));
+    CHECK_RC(upload(&d_rec, d, rec, s));
+    CHECK_RC(upload(&d_robs, d, robs, s));
+    phase("hits, upload");
   }
+  // tiles: equal block ranges of <= kTileBlocks (rows up to the tile's last camera)
+  const int ntile = std::max(1, (nb + kTileBlocks - 1) / kTileBlocks);
+  std::vector<int> tb(ntile + 1), clast(ntile);
+  for (int t = 0; t <= ntile; ++t) tb[t] = (int)((long long)nb * t / ntile);
   // slots: per tile, blocks by hit count (descending); thread i owns the i-th heaviest and
   // the (1023 - i)-th, so the pairs' sums are even and a wave's threads have similar work
   std::vector<int> slot((size_t)ntile * 2 * kTileThreads, -1);
@@ -1978,7 +2004,7 @@ static int build_schur_tiles(dab_handle* h) {
     while (tri_n(c + 1) <= tb[t + 1] - 1) ++c;
     clast[t] = c;
   }
-  phase("hits, slots");
+  phase("slots");
   SchurTiles& a = h->tiles;
   a.ntile = ntile;
   a.nbatch = nbatch;
@@ -1993,19 +2019,9 @@ static int build_schur_tiles(dab_handle* h) {
   a.kq = 0;
   a.batch_cap = cap;
   a.hdr_bytes = hdr_bytes;
-  Dev& d = h->dev;
-  int *d_br = nullptr, *d_cl = nullptr, *d_slot = nullptr;
-  unsigned char* d_hdr = nullptr;
-  int2* d_sch = nullptr;
-  int4* d_rec = nullptr;
-  CHECK_RC(upload(&d_br, d, batch_rec, s));
+  int *d_cl = nullptr, *d_slot = nullptr;
   CHECK_RC(upload(&d_cl, d, clast, s));
   CHECK_RC(upload(&d_slot, d, slot, s));
-  CHECK_RC(upload(&d_hdr, d, hdr, s));
-  CHECK_RC(upload(&d_sch, d, sch, s));
-  CHECK_RC(upload(&d_rec, d, rec, s));
-  int4* d_robs = nullptr;
-  CHECK_RC(upload(&d_robs, d, robs, s));
   a.rec_obs = d_robs;
   a.batch_rec = d_br;
   a.tile_clast = d_cl;
@@ -2145,14 +2161,33 @@ static int build_schur_tables(dab_handle* h) {
   const std::vector<int>& pt_ent_ptr = h->h_pt_ent_ptr;
   const big_vec<int>& ent_cam = h->h_ent_cam;
   const big_vec<int>& ent_pos = h->h_ent_pos;
+  int2* tile_sch = nullptr;
+  int* tile_m = nullptr;
+  int dev_maxm = 0;
   {
     // tile mode: every rank must take the same branch (the all-reduced S layouts differ).
     // The host entry lists are needed by the tile tables (and by the host reference path of
     // the pair tables); large camera sets with device set-up never fetch them.
     const bool tiles_possible = h->knobs.schur_tiles != 0 && NC > 0 && mf_schur_fits(NC, h->E, h->NI);
-    if (tiles_possible) CHECK_RC(fetch_host_entries(h));
+    if (tiles_possible && !h->host_entries) {
+      // device: per point entries sorted by (camera, slot), distinct cameras counted
+      CHECK_RC(h->dev.alloc(&tile_sch, (size_t)std::max(1, h->NE)));
+      CHECK_RC(h->setup_tmp.alloc(&tile_m, (size_t)std::max(1, NP)));
+      su_tile_sort(s, NP, h->d_pt_ent_ptr, h->d_ent_cam, h->d_ent_os, tile_sch, tile_m);
+      if (NP > 0) {
+        int* d_max = nullptr;
+        CHECK_RC(h->setup_tmp.alloc(&d_max, 1));
+        size_t bytes = 0;
+        if (su_max(nullptr, &bytes, tile_m, d_max, NP, s) != 0) return set_error(DAB_E_DEVICE, "rocPRIM size query failed");
+        unsigned char* t = nullptr;
+        CHECK_RC(h->setup_tmp.alloc(&t, std::max<size_t>(1, bytes)));
+        if (su_max(t, &bytes, tile_m, d_max, NP, s) != 0) return set_error(DAB_E_DEVICE, "rocPRIM pass failed");
+        HIP_OK(hipMemcpyAsync(&dev_maxm, d_max, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIP_OK(hipStreamSynchronize(s));
+      }
+    }
     std::vector<int> tmax(setup_threads(), 0);  // distinct free cameras of one point
-    if (tiles_possible) par_for(NP, [&](long long pb, long long pe, int t) {
+    if (tiles_possible && h->host_entries) par_for(NP, [&](long long pb, long long pe, int t) {
       std::vector<int> seen(std::max(1, NC), -1);
       for (int pt = (int)pb; pt < (int)pe; ++pt) {
         int m = 0;
@@ -2164,14 +2199,14 @@ static int build_schur_tables(dab_handle* h) {
         tmax[t] = std::max(tmax[t], m);
       }
     });
-    const int maxm = *std::max_element(tmax.begin(), tmax.end());
+    const int maxm = std::max(dev_maxm, *std::max_element(tmax.begin(), tmax.end()));
     phase("camera counts");
     double no_tiles = (tiles_possible && maxm <= kTileMaxRec) ? 0.0 : 1.0;
     CHECK_RC(max_all_ranks(h, no_tiles));
     h->schur_tiles = no_tiles == 0.0;
   }
   if (h->schur_tiles) {
-    CHECK_RC(build_schur_tiles(h));
+    CHECK_RC(build_schur_tiles(h, tile_sch, tile_m));
     t_ph = now_s();
     h->nblk = 0;
     h->npairs = 0;
