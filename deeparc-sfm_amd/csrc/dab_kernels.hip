@@ -3919,6 +3919,10 @@ static size_t mf32_lds_bytes(int E, int NI, int NC) {
   return sizeof(double) * (9 * (size_t)NC + (kMfBlock / 64) * 6 * (size_t)(NC | 1)) +
          sizeof(float) * (12 * (size_t)E + 4 * (size_t)NI + 6 * (size_t)NC) + 2 * sizeof(int) * (size_t)E;
 }
+// ACC: 0 = fp64 per-wave LDS sums; 2 = no camera sums (ablation, wrong result: DAB_MF32_ACC=2
+// measures what the LDS atomics cost). Measured and dropped: fp32 LDS sums (3x slower) and a
+// copy of the sums per half wave (no gain: the atomics are not bank-conflict bound)
+template <int ACC>
 __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame32(DevView v, const double* __restrict__ points,
                                                          const double* __restrict__ camtab,
                                                          const double* __restrict__ scc,
@@ -3970,7 +3974,10 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame32(DevView v, const dou
   for (int i = threadIdx.x; i < (kMfBlock / 64) * 6 * NCP; i += blockDim.x) accs[i] = 0.0;
   __syncthreads();
   double* acc = accs + (threadIdx.x >> 6) * 6 * NCP;
-  auto add = [&](int c, int a, float x) { atomicAdd(acc + a * NCP + c, (double)x); };  // fp64 per-wave sums
+  auto add = [&](int c, int a, float x) {
+    if constexpr (ACC == 0) atomicAdd(acc + a * NCP + c, (double)x);  // fp64 per-wave sums
+    else if (x == 1234.5f) acc[0] = x;  // keep the arithmetic alive
+  };
   auto sum_of = [&](int c, int a) {  // fixed order over the waves
     double t = accs[a * NCP + c];
 #pragma unroll
@@ -4235,8 +4242,13 @@ void launch_mf_product(hipStream_t s, const DevView& v, const double* points, co
 void launch_mf_product32(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                          const double* scale_c, const double* PU, const double* vec, double* partial, double* w,
                          int grid, const PcgState* st) {
-  k_mf_frame32<<<grid, kMfBlock, mf32_lds_bytes(v.E, v.NI, v.NC), s>>>(v, points, camtab, scale_c, PU, vec, partial,
-                                                                      st);
+  static const int acc = getenv("DAB_MF32_ACC") ? atoi(getenv("DAB_MF32_ACC")) : 0;
+  if (acc == 2)
+    k_mf_frame32<2><<<grid, kMfBlock, mf32_lds_bytes(v.E, v.NI, v.NC), s>>>(v, points, camtab, scale_c, PU, vec,
+                                                                           partial, st);
+  else
+    k_mf_frame32<0><<<grid, kMfBlock, mf32_lds_bytes(v.E, v.NI, v.NC), s>>>(v, points, camtab, scale_c, PU, vec,
+                                                                           partial, st);
   if (w) launch_pcg_fused_final(s, grid, 6 * v.NC, partial, w, st);
 }
 void launch_mf_backsub(hipStream_t s, const DevView& v, const double* points, const double* camtab,
