@@ -1174,6 +1174,8 @@ static int setup_host(dab_handle* h, const dab_problem* p, const std::function<v
   h->pcg_built = false;
   h->mf = h->mf32 = false;
   h->cg_wpart = nullptr;  // its buffer went with the previous problem's allocations
+  h->fused_grid = 0;      // so did the single-pass product's partials
+  h->mf_grid_n = 0;
   h->nblk = 0;
   h->npairs = 0;
 
@@ -1718,6 +1720,8 @@ static int setup_device(dab_handle* h, const dab_problem* p, const std::function
   h->pcg_built = false;
   h->mf = h->mf32 = false;
   h->cg_wpart = nullptr;
+  h->fused_grid = 0;
+  h->mf_grid_n = 0;
   h->nblk = 0;
   h->npairs = 0;
 
@@ -1787,7 +1791,11 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
   HIP_OK(hipSetDevice(h->device));
   HIP_OK(hipStreamSynchronize(h->stream));
   h->dev.release();
-  h->d_Yrec = nullptr;  // lazily allocated: reallocated by the next explicit step
+  // lazily allocated buffers went with the release: clear their pointers so that the next
+  // use allocates again (a stale pointer would be written after its memory was freed)
+  h->d_Yrec = nullptr;
+  h->d_Y32c = h->d_Y32p = nullptr;
+  h->d_Jfull = nullptr;
   h->have_problem = false;
   h->prob = *p;
   // DAB_SETUP_TIMING=1: phase times of the host preprocessing on stderr
@@ -2385,6 +2393,7 @@ static int build_pcg_buffers(dab_handle* h) {
     h->mf_grid_n = mf_grid(h->NP, h->ncu);
     CHECK_RC(d.alloc(&h->d_mf_partial, (size_t)h->mf_grid_n * 6 * h->NC));
   }
+  h->fused_grid = 0;
   if (pcg_fused_fits(h->NC) && h->NP > 0 && h->knobs.pcg_fused != 0) {
     h->fused_grid = pcg_fused_grid(h->NP, h->ncu);
     CHECK_RC(d.alloc(&h->d_fused_partial, (size_t)h->fused_grid * 6 * h->NC));

@@ -1,18 +1,20 @@
 """One handle across problems of different shapes (the host adapter keeps one libdab handle
 for a whole sfm.cc pipeline): solving problem B after problem A on the same handle must give
 bitwise the trajectory of a fresh handle on B. Covers the round-2 advisor finding that a
-matrix-free rig solve left the CG update pointed at its freed work-group partials, which a
-following large-camera rig (stored-Y PCG, cross blocks) would have summed."""
+matrix-free rig solve left the CG update pointed at its freed work-group partials, and two
+found by these tests: the single-pass product's grid size outlived its problem (a small rig
+followed by a large-camera rig ran the single-pass product on freed partials, results off
+in the last bits), and the lazily allocated fp32 Y records kept a freed pointer."""
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 
-def _solve(pkg, s, prob, lst, iters=4):
+def _solve(pkg, s, prob, lst, iters=4, **kw):
     p = prob.copy()
     s.set_problem(p)
-    summ = s.solve(pkg.options(max_num_iterations=iters, linear_solver_type=lst))
+    summ = s.solve(pkg.options(max_num_iterations=iters, linear_solver_type=lst, **kw))
     return [it["cost"] for it in summ["iterations"]], \
         [it["linear_solver_iterations"] for it in summ["iterations"]], p.points.copy(), p.ext.copy()
 
@@ -63,3 +65,26 @@ def test_handle_reuse_large_then_small(pkg, gpu):
         assert got[1] == ref[1]
         np.testing.assert_array_equal(got[2], ref[2])
         np.testing.assert_array_equal(got[3], ref[3])
+
+
+def test_handle_reuse_fp32_stored_y(pkg, gpu):
+    """Mixed-precision stored-Y PCG (fp32 Y records, allocated on first use) on a handle
+    that already ran it on another problem: the records are allocated again, not reused
+    from the freed set."""
+    a = pkg.synth(kind=0, num_cameras=220, num_points=5000, obs_per_point=6, seed=85)
+    b = pkg.synth(kind=0, num_cameras=240, num_points=7000, obs_per_point=7, seed=86)
+    pcg = pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG
+    fresh = pkg.Solver(0)
+    try:
+        ref = _solve(pkg, fresh, b, pcg, pcg_fp32=1)
+    finally:
+        fresh.close()
+    s = pkg.Solver(0)
+    try:
+        _solve(pkg, s, a, pcg, pcg_fp32=1)
+        got = _solve(pkg, s, b, pcg, pcg_fp32=1)
+    finally:
+        s.close()
+    assert got[0] == ref[0]
+    assert got[1] == ref[1]
+    np.testing.assert_array_equal(got[2], ref[2])
