@@ -88,3 +88,70 @@ def test_handle_reuse_fp32_stored_y(pkg, gpu):
     assert got[0] == ref[0]
     assert got[1] == ref[1]
     np.testing.assert_array_equal(got[2], ref[2])
+
+
+def test_solve_continues_on_same_problem(pkg, gpu):
+    """Two solves of 3 iterations on one handle and problem (the second starts from the
+    first's result, as sfm.cc's repeated solve() calls) against one fresh solve each: the
+    second solve of the reused handle equals a fresh handle started from the same
+    parameters, for the exact step (sticky dense S, captured Cholesky graph) and PCG."""
+    prob = pkg.synth(kind=0, num_cameras=60, num_points=3000, obs_per_point=6, seed=87)
+    for lst in (pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR, pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG,
+                pkg.DAB_LINEAR_SOLVER_AUTO):
+        p = prob.copy()
+        s = pkg.Solver(0)
+        try:
+            s.set_problem(p)
+            s.solve(pkg.options(max_num_iterations=3, linear_solver_type=lst))
+            mid_pts, mid_ext = p.points.copy(), p.ext.copy()
+            s.set_problem(p)  # the re-set of the same shape keeps S and the graph
+            b = s.solve(pkg.options(max_num_iterations=3, linear_solver_type=lst))
+        finally:
+            s.close()
+        q = prob.copy()
+        q.points[:] = mid_pts
+        q.ext[:] = mid_ext
+        f = pkg.Solver(0)
+        try:
+            f.set_problem(q)
+            c = f.solve(pkg.options(max_num_iterations=3, linear_solver_type=lst))
+        finally:
+            f.close()
+        assert [it["cost"] for it in b["iterations"]] == [it["cost"] for it in c["iterations"]]
+        np.testing.assert_array_equal(p.points, q.points)
+        np.testing.assert_array_equal(p.ext, q.ext)
+        if lst == pkg.DAB_LINEAR_SOLVER_AUTO:  # one rank: AUTO is the exact step
+            assert b["linear_solver_type_used"] == pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR
+
+
+def test_filter_then_resolve_matches_fresh(pkg, gpu):
+    """dab_filter on the solve's resident problem, then the caller drops the filtered
+    observations and re-sets the same handle (the sfm.cc loop): same trajectory as a
+    fresh handle on the filtered problem."""
+    prob = pkg.synth(kind=1, num_arcs=5, num_rings=14, num_points=4000, obs_per_point=7, seed=88)
+    lst = pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR
+    s = pkg.Solver(0)
+    try:
+        p = prob.copy()
+        s.set_problem(p)
+        s.solve(pkg.options(max_num_iterations=3, linear_solver_type=lst))
+        for bound in (4.0, 2.0, 1.0, 0.5, 0.25, 0.1):  # a boundary that drops some
+            obs_keep, _ = s.filter(bound, [0.0, 0.0, 0.0], 1e9)
+            keep = np.nonzero(np.asarray(obs_keep))[0]
+            if 0 < len(keep) < p.num_obs:
+                break
+        assert 0 < len(keep) < p.num_obs
+        q = p.subset(keep)
+        q_fresh = q.copy()
+        s.set_problem(q)
+        a = s.solve(pkg.options(max_num_iterations=3, linear_solver_type=lst))
+    finally:
+        s.close()
+    f = pkg.Solver(0)
+    try:
+        f.set_problem(q_fresh)
+        b = f.solve(pkg.options(max_num_iterations=3, linear_solver_type=lst))
+    finally:
+        f.close()
+    assert [it["cost"] for it in a["iterations"]] == [it["cost"] for it in b["iterations"]]
+    np.testing.assert_array_equal(q.points, q_fresh.points)
