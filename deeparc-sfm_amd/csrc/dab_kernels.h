@@ -135,10 +135,7 @@ void launch_eval_cross(hipStream_t s, const DevView& v, int nchunk, const int* c
 bool pair_eval_fits(int E, int NI);  // the tables fit LDS (small_tabs_fit)
 void launch_eval_pair(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
                       const double2* x_xy, const double* points, const double* camtab, double* xpart,
-                      double* cpart,
-                      const double* xpts = nullptr);
-// the pair-major copy's points in entry order (xpts [n][3]), for launch_eval_pair's xpts
-void launch_pair_gather(hipStream_t s, int n, const int4* x_idx, const double* points, double* xpts);
+                      double* cpart);
 void launch_cam_final(hipStream_t s, int NC, const int* seg_chunk, const double* partial, const int* xcam_ptr,
                       const int* xcam_list, const double* cpart, double* ug);
 void launch_eval_cams_gen(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const double* points,

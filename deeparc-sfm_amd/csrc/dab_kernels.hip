@@ -1793,7 +1793,7 @@ __device__ __forceinline__ void ext_frame(const double* __restrict__ camtab, int
 template <int NS, class Body>
 __device__ __forceinline__ void pipe_entries_ns(const int4* __restrict__ idx, const double2* __restrict__ xyv,
                                                 int i0, int e, int stride, const double* __restrict__ points,
-                                                Body body, const double* __restrict__ xpts = nullptr) {
+                                                Body body) {
   static_assert(NS >= 3, "at least three slots");
   int4 id[NS];
   double2 xy[NS];
@@ -1810,13 +1810,11 @@ __device__ __forceinline__ void pipe_entries_ns(const int4* __restrict__ idx, co
       id[s] = idx[i0 + s * stride];
       xy[s] = xyv[i0 + s * stride];
     }
-  // xpts: the points already gathered in entry order (k_pair_gather), read by position
 #pragma unroll
   for (int s = 0; s < NS - 2; ++s)
     if (id[s].x >= 0) {
-      const double* src = xpts ? xpts + 3 * (size_t)(i0 + s * stride) : points + 3 * (size_t)id[s].x;
 #pragma unroll
-      for (int q = 0; q < 3; ++q) X[s][q] = src[q];
+      for (int q = 0; q < 3; ++q) X[s][q] = points[3 * (size_t)id[s].x + q];
     }
   for (int i = i0; i < e; i += NS * stride) {
 #pragma unroll
@@ -1825,9 +1823,8 @@ __device__ __forceinline__ void pipe_entries_ns(const int4* __restrict__ idx, co
       if (ii >= e) break;
       const int sg = (u + NS - 2) % NS, sl = (u + NS - 1) % NS;
       if (id[sg].x >= 0 && ii + (NS - 2) * stride < e) {
-        const double* src = xpts ? xpts + 3 * (size_t)(ii + (NS - 2) * stride) : points + 3 * (size_t)id[sg].x;
 #pragma unroll
-        for (int q = 0; q < 3; ++q) X[sg][q] = src[q];
+        for (int q = 0; q < 3; ++q) X[sg][q] = points[3 * (size_t)id[sg].x + q];
       }
       if (ii + (NS - 1) * stride < e) {
         id[sl] = idx[ii + (NS - 1) * stride];
@@ -2469,7 +2466,7 @@ __global__ __launch_bounds__(256) void k_eval_pair(DevView v, const int* __restr
                                                    const double2* __restrict__ x_xy,
                                                    const double* __restrict__ points,
                                                    const double* __restrict__ camtab, double* __restrict__ xpart,
-                                                   double* __restrict__ cpart, const double* __restrict__ xpts) {
+                                                   double* __restrict__ cpart) {
   const int c = blockIdx.x;
   const int b = chunk_beg[c], e = chunk_beg[c + 1];
   extern __shared__ double tabs_lds[];
@@ -2541,7 +2538,7 @@ __global__ __launch_bounds__(256) void k_eval_pair(DevView v, const int* __restr
 #pragma unroll
                      for (int bb = 0; bb < 6; ++bb) acc[54 + 6 * a + bb] = fma(w0[a], w1[bb], acc[54 + 6 * a + bb]);
                  }
-               }, xpts);
+               });
   {
     double h0[30], h1[30], h2[30];
 #pragma unroll
@@ -2590,35 +2587,15 @@ __global__ __launch_bounds__(256) void k_eval_pair(DevView v, const int* __restr
 }
 
 bool pair_eval_fits(int E, int NI) { return small_tabs_fit(E, NI); }
-// the pair-major copy's points in entry order: one thread per observation, many gathers in
-// flight (the pair kernel runs at one wave per SIMD and keeps only two in flight)
-__global__ __launch_bounds__(256) void k_pair_gather(int n, const int4* __restrict__ x_idx,
-                                                     const double* __restrict__ points, double* __restrict__ xpts) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  const int p = x_idx[k].x;
-  double x0 = 0.0, x1 = 0.0, x2 = 0.0;
-  if (p >= 0) {
-    x0 = points[3 * (size_t)p];
-    x1 = points[3 * (size_t)p + 1];
-    x2 = points[3 * (size_t)p + 2];
-  }
-  xpts[3 * (size_t)k] = x0;
-  xpts[3 * (size_t)k + 1] = x1;
-  xpts[3 * (size_t)k + 2] = x2;
-}
-void launch_pair_gather(hipStream_t s, int n, const int4* x_idx, const double* points, double* xpts) {
-  if (n > 0) k_pair_gather<<<grid_for(n, 256, 1 << 20), 256, 0, s>>>(n, x_idx, points, xpts);
-}
 void launch_eval_pair(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
                       const double2* x_xy, const double* points, const double* camtab, double* xpart,
-                      double* cpart, const double* xpts) {
+                      double* cpart) {
   if (nchunk <= 0) return;
   // 90 sums per lane: ~300 VGPRs, one wave per SIMD (a 256-VGPR cap spills hundreds)
   // four register slots: measured 285 us at C5 against 295 (three) and 286 (five); one
   // wave per SIMD leaves the registers for it
   k_eval_pair<4><<<nchunk, 256, small_tabs_bytes(v.E, v.NI), s>>>(v, chunk_beg, x_idx, x_xy, points, camtab, xpart,
-                                                                  cpart, xpts);
+                                                                  cpart);
 }
 
 // ug[c] = its camera-major chunk partials (seg_chunk) + its halves of the pair chunks

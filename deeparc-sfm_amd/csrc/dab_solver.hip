@@ -222,7 +222,6 @@ struct Knobs {
   int schur_tiles = 1;      // DAB_SCHUR_TILES=0: explicit S from the pair tables even for small NC
   int p2p = -1;             // DAB_P2P: one-shot xGMI all-reduce of small sums (-1 auto: RCCL handles
                             // only; 1 also on host-staged handles, the one-GPU rehearsal; 0 off)
-  int pair_gather = 0;      // DAB_PAIR_GATHER=1: the pair kernel reads points pre-gathered in entry order
   int fused_stream = 2;     // DAB_FUSED_STREAM: fused pass records — 2 packed point-side records, camera
                             // waves gather the points; 1 the same with the camera-major point copy
                             // (refreshed after every point change); 0 the 16-B records
@@ -248,7 +247,6 @@ struct Knobs {
     get("DAB_SCHUR_TILES", schur_tiles);
     get("DAB_P2P", p2p);
     get("DAB_FUSED_STREAM", fused_stream);
-    get("DAB_PAIR_GATHER", pair_gather);
     get("DAB_FUSED_V", fused_variant);
     get("DAB_FUSED_TAB", fused_tab);
     get("DAB_SETUP_HOST", setup_host);
@@ -309,10 +307,6 @@ struct dab_handle {
   int* d_obs_e = nullptr;
   double* d_cmx = nullptr;
   long long pts_version = 0, cmx_version = -1;
-  // rig: the pair-major copy's points in entry order, re-gathered whenever the points moved
-  double* d_xpts = nullptr;
-  long long xpts_version = -1;
-  int nx_obs = 0;  // observations of the pair-major copy
   int4* d_cm_idx = nullptr;
   double2* d_cm_xy = nullptr;
   int4* d_x_idx = nullptr;
@@ -1067,7 +1061,6 @@ static int setup_host(dab_handle* h, const dab_problem* p, const std::function<v
   std::vector<int> xchunk_beg, xseg_chunk(h->ncross + 1, 0);
   big_vec<int4> x_idx(xkeys.size());
   big_vec<double2> x_xy(xkeys.size());
-  h->nx_obs = (int)xkeys.size();
   {
     par_for((long long)xkeys.size(), [&](long long b, long long e, int) {
       for (long long i = b; i < e; ++i) {
@@ -1360,10 +1353,6 @@ static int setup_buffers(dab_handle* h, const std::function<void(const char*)>& 
   h->d_obs_e = nullptr;
   h->d_cmx = nullptr;
   h->cmx_version = -1;
-  h->d_xpts = nullptr;
-  h->xpts_version = -1;
-  if (h->pair_eval && h->knobs.pair_gather != 0 && h->nx_obs > 0)
-    CHECK_RC(d.alloc(&h->d_xpts, (size_t)3 * h->nx_obs));
   if (h->fused && h->knobs.fused_stream != 0 && h->E < 0x8000 && h->NI < 0x8000) {
     // packed 4-B slot records for the point waves; fused_stream = 1 also the camera-major
     // point copy (re-gathered whenever the points move), 2 (default) camera waves that
@@ -1654,7 +1643,6 @@ static int setup_device(dab_handle* h, const dab_problem* p, const std::function
     xchunk_beg.push_back(nx);
   }
   CHECK_RC(d.alloc(&h->d_x_idx, (size_t)std::max(1, nx)));
-  h->nx_obs = nx;
   CHECK_RC(d.alloc(&h->d_x_xy, (size_t)std::max(1, nx)));
   h->pair_eval = h->nxchunk > 0 && pair_eval_fits(h->E, h->NI) && h->knobs.pair_eval != 0;
   unsigned char* touched = nullptr;
@@ -2625,14 +2613,8 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
     v2.cm_xy = h->d_cm2_xy;
     launch_eval_cams_gen(s, v2, h->nchunk2, h->d_chunk2_beg, h->d_points, h->d_ext, h->d_camtab, h->d_partial2);
     if (ev_pair0) HIP_OK(hipEventRecord(ev_pair0, s));
-    // the pair kernel's points in entry order (timed with it: an evaluation at a new point
-    // pays the gather)
-    if (h->d_xpts && h->xpts_version != h->pts_version) {
-      launch_pair_gather(s, h->nx_obs, h->d_x_idx, h->d_points, h->d_xpts);
-      h->xpts_version = h->pts_version;
-    }
     launch_eval_pair(s, v, h->nxchunk, h->d_xchunk_beg, h->d_x_idx, h->d_x_xy, h->d_points, h->d_camtab,
-                     h->d_xpartial, h->d_xcpart, h->d_xpts);
+                     h->d_xpartial, h->d_xcpart);
     if (ev_pair1) HIP_OK(hipEventRecord(ev_pair1, s));
     if (pair_rec) *pair_rec = ev_pair0 && ev_pair1 && h->nxchunk > 0;
     launch_cam_final(s, h->NC, h->d_seg2_chunk, h->d_partial2, h->d_xcam_ptr, h->d_xcam_list, h->d_xcpart, h->ug());
