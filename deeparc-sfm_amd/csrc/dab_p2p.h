@@ -31,5 +31,7 @@ int p2p_allreduce_max_i32(P2pComm* c, hipStream_t s, int* buf, size_t n);
 // DAB_E_COMM when a call gave up waiting for a peer: a host read of the pinned error word,
 // no device synchronisation (call it after the stream has drained to cover every call)
 int p2p_check(P2pComm* c);
+// two verified sums on the context (3-s timeout); 0 when the path delivers exact results
+int p2p_selftest(P2pComm* c, hipStream_t s);
 
 }  // namespace dab

@@ -290,6 +290,51 @@ int p2p_allreduce_sum_u64(P2pComm* c, hipStream_t s, unsigned long long* buf, si
 int p2p_allreduce_max(P2pComm* c, hipStream_t s, double* buf, size_t n) { return p2p_reduce<double, 1>(c, s, buf, n); }
 int p2p_allreduce_max_i32(P2pComm* c, hipStream_t s, int* buf, size_t n) { return p2p_reduce<int, 1>(c, s, buf, n); }
 
+// One verified exchange before the path is trusted: two sums (both slots of the context)
+// of known integer patterns, exact in fp64, under a short timeout. A peer mapping that
+// does not deliver (a platform where the IPC-mapped uncached region is not coherent across
+// devices, say) shows up here, at set-up, and the caller keeps RCCL instead.
+int p2p_selftest(P2pComm* c, hipStream_t s) {
+  const size_t n = std::min<size_t>(c->cap, 4096);  // two work-groups' slices
+  if (n == 0) return 0;
+  const long long keep = c->timeout_ticks;
+  c->timeout_ticks = std::min<long long>(keep, 3000LL * 100000LL);  // 3 s
+  double* d = nullptr;
+  if (hipMalloc(&d, n * sizeof(double)) != hipSuccess) {
+    c->timeout_ticks = keep;
+    return set_error(DAB_E_NOMEM, "p2p self-test: allocation failed");
+  }
+  std::vector<double> h(n);
+  int rc = 0;
+  const double w = (double)c->world, tri = w * (w + 1.0) / 2.0;
+  // DAB_P2P_SELFTEST_SKEW=r (test knob): rank r contributes a wrong word, so every rank's
+  // check fails and the set-up falls back
+  const char* sk = getenv("DAB_P2P_SELFTEST_SKEW");
+  const bool skew = sk && atoi(sk) == c->rank;
+  for (int call = 0; call < 2 && rc == 0; ++call) {
+    for (size_t k = 0; k < n; ++k) h[k] = (double)(c->rank + 1) * (double)(k + 1 + call);
+    if (skew) h[0] += 1.0;
+    if (hipMemcpy(d, h.data(), n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+        p2p_allreduce_sum(c, s, d, n) != 0 || hipStreamSynchronize(s) != hipSuccess ||
+        hipMemcpy(h.data(), d, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
+      rc = set_error(DAB_E_DEVICE, "p2p self-test: a call failed");
+      break;
+    }
+    if (p2p_check(c) != 0) {
+      rc = -1;
+      break;
+    }
+    for (size_t k = 0; k < n; ++k)
+      if (h[k] != tri * (double)(k + 1 + call)) {
+        rc = set_error(DAB_E_COMM, "p2p self-test: wrong sum at word " + std::to_string(k));
+        break;
+      }
+  }
+  (void)hipFree(d);
+  c->timeout_ticks = keep;
+  return rc;
+}
+
 int p2p_check(P2pComm* c) {
   if (!c || !c->err) return 0;
   const unsigned long long e = __atomic_load_n(c->err, __ATOMIC_ACQUIRE);

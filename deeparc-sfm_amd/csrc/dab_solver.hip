@@ -671,9 +671,12 @@ static int setup_p2p(dab_handle* h) {
     };
   }
   P2pComm* ctx[2] = {nullptr, nullptr};
-  const int rc = p2p_create_group(h->rank, h->world, dab_handle::kP2pWords, 2, gather, ctx);
-  // every rank must agree: if the contexts could not be set up anywhere, all ranks keep
-  // their sums on RCCL (or the host path) instead
+  int rc = p2p_create_group(h->rank, h->world, dab_handle::kP2pWords, 2, gather, ctx);
+  // a verified exchange on both contexts before the path is trusted (every rank runs it:
+  // the calls are collective)
+  for (int k = 0; k < 2 && rc == 0; ++k) rc = p2p_selftest(ctx[k], h->stream);
+  // every rank must agree: if the contexts could not be set up or did not verify anywhere,
+  // all ranks keep their sums on RCCL (or the host path) instead
   double bad = rc != 0 ? 1.0 : 0.0;
   if (h->host_cb) {
     CHECK_RC(h->stage(1));

@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--expect-p2p", action="store_true",
                     help="fail unless the one-shot peer-to-peer all-reduce carried the sums")
+    ap.add_argument("--expect-no-p2p", action="store_true",
+                    help="fail if the peer-to-peer path is in use (its set-up self-test must have "
+                    "failed over to the other collectives)")
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dev = a.device if a.device >= 0 else int(os.environ.get("LOCAL_RANK", "0"))
@@ -110,6 +113,7 @@ def main():
                or v["dext"] > 1e-6 or not v["ext_ranks_equal"]
                or (not k.startswith("rig") and v["eval_schedule"] != 2)  # BAL shards: the split fused pass
                or (a.expect_p2p and v["p2p"] != 1)
+               or (a.expect_no_p2p and v["p2p"] != 0)
                or v["solver_used"][0] != v["solver_used"][1]]
         print("DIST_CHECK", "FAIL " + ",".join(bad) if bad else "OK")
     dist.destroy_process_group()

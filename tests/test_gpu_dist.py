@@ -78,3 +78,22 @@ def test_p2p_missed_call_fails_closed(gpu):
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     assert "P2P_FAIL_CHECK OK" in p.stdout, p.stdout[-3000:] + p.stderr[-3000:]
+
+
+def test_p2p_selftest_failure_falls_back(gpu):
+    """The peer-to-peer path is trusted only after a verified exchange at set-up (two exact
+    integer sums per context). A rank that contributes a wrong word (DAB_P2P_SELFTEST_SKEW)
+    makes every rank's check fail; all ranks then agree to keep the other collectives
+    (here the host-staged ones), report p2p = 0, and the sharded trajectories still match
+    the single handle."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, DAB_P2P="1", DAB_P2P_SELFTEST_SKEW="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "scripts", "dist_check.py"), "--device", "0", "--host-collective", "--expect-no-p2p",
+           "--config", "c2_100cam", "--iters", "4"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "DIST_CHECK OK" in p.stdout, p.stdout[-3000:]
