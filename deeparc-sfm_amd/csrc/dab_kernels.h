@@ -199,8 +199,14 @@ struct SchurTiles {
                                      // ext0, ext1, intr): k_schur_y streams it instead of two gathers
   const int2* sch_ent;               // [NE] (ent_os, camera), sorted by camera inside each point
   const int* kx;                     // [6 NC] rhs row exponents (launch_schur_scale)
-  double* partial;                   // [ngroup][stride] per-group block sums
+  double* partial;                   // [nslot][stride] per-slot block sums
   size_t stride;                     // nelem
+  // load balance: tile t's batches are cut into ngroup * tile_sub[t] slots (a heavy tile
+  // gets more work-groups); the launch has ngroup * nsub work-groups, nsub = sum of tile_sub
+  int nsub;
+  const int* tile_sub;               // [ntile] work-groups per group of batches
+  const int* tile_subbeg;            // [ntile + 1] prefix of tile_sub
+  const int* blk_nslot;              // [nblocks] slots holding the block's partials (k_schur_sum)
 };
 constexpr int kTileThreads = 512;     // threads of a k_schur_tiles work-group (two blocks each)
 constexpr size_t kTileLdsMax = 163840;            // LDS of one k_schur_tiles work-group (at most)
@@ -212,6 +218,8 @@ void launch_schur_y(hipStream_t s, const DevView& v, const double* points, const
                     const double* q, const double* scale_c, const SchurTiles& a, double* yrec,
                     unsigned long long* rhs_out);
 void launch_schur_tiles(hipStream_t s, const double* yrec, const SchurTiles& a, int NC);
+// sblk[i] = sum of the slots' partials of element i in slot order (blk_nslot[i / 36] slots)
+void launch_schur_sum_tiles(hipStream_t s, const SchurTiles& a, double* out);
 void launch_schur_sum(hipStream_t s, int ngroup, size_t stride, size_t count, const double* partial, double* out);
 // S lower rows 0..n-1 = -Schur part, ybc = -rhs part (then launch_s_add_u)
 void launch_schur_unpack(hipStream_t s, int NC, const double* sblk, const unsigned long long* rfx, const int* kx,

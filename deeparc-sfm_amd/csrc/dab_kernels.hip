@@ -3169,15 +3169,21 @@ __global__ __launch_bounds__(kTileThreads) void k_schur_tiles(const double* __re
   extern __shared__ __align__(16) unsigned char tile_lds[];
   // XCD-aware placement: the tiles of one group of points run on one XCD (blocks b and b + 8
   // share one), so the group's records come from HBM once and from that L2 for the others
-  int t, g;
+  // work-group -> (tile t, part j of its group g): the nsub work-groups of one group of
+  // batches (every tile, a heavy tile in several parts) run on one XCD
+  int u, g;
   if (a.ngroup % 8 == 0) {
     const int x = blockIdx.x & 7, y = blockIdx.x >> 3;
-    t = y % a.ntile;
-    g = (y / a.ntile) * 8 + x;
+    u = y % a.nsub;
+    g = (y / a.nsub) * 8 + x;
   } else {
-    t = blockIdx.x % a.ntile;
-    g = blockIdx.x / a.ntile;
+    u = blockIdx.x % a.nsub;
+    g = blockIdx.x / a.nsub;
   }
+  int t = 0;
+  while (a.tile_subbeg[t + 1] <= u) ++t;
+  const int ns = a.tile_sub[t];
+  const int slot = g * ns + (u - a.tile_subbeg[t]), nslot = a.ngroup * ns;
   const int clast = a.tile_clast[t];
   const int blA = a.tile_slot[(size_t)t * 2 * kTileThreads + threadIdx.x];
   const int blB = a.tile_slot[(size_t)t * 2 * kTileThreads + kTileThreads + threadIdx.x];
@@ -3193,7 +3199,7 @@ __global__ __launch_bounds__(kTileThreads) void k_schur_tiles(const double* __re
   double accA[36], accB[36];
 #pragma unroll
   for (int k = 0; k < 36; ++k) accA[k] = accB[k] = 0.0;
-  const int b0 = (int)((long long)a.nbatch * g / a.ngroup), b1 = (int)((long long)a.nbatch * (g + 1) / a.ngroup);
+  const int b0 = (int)((long long)a.nbatch * slot / nslot), b1 = (int)((long long)a.nbatch * (slot + 1) / nslot);
   if (b0 < b1) tile_dma_batch(a, yrec, NC, clast, b0, tile_lds);
   __syncthreads();  // drains the DMA (vmcnt) and publishes buffer 0
   for (int b = b0; b < b1; ++b) {
@@ -3208,7 +3214,7 @@ __global__ __launch_bounds__(kTileThreads) void k_schur_tiles(const double* __re
     if (blB >= 0) tile_block_hits(ly, mask, off, cB, dB, accB);
     __syncthreads();  // batch b consumed, batch b + 1 landed
   }
-  double* out = a.partial + (size_t)g * a.stride;
+  double* out = a.partial + (size_t)slot * a.stride;
   if (blA >= 0) {
     double2* o = reinterpret_cast<double2*>(out + 36 * (size_t)blA);
 #pragma unroll
@@ -3236,6 +3242,22 @@ __global__ void k_schur_scale(int NC, const double* __restrict__ ug, const doubl
     k = (e + 1) >> 1;
   }
   kx[i] = k;
+}
+
+// the tiles' partials: element i of block i / 36 summed over that block's slots in order
+__global__ void k_schur_sum_tiles(const int* __restrict__ blk_nslot, size_t stride, size_t count,
+                                  const double* __restrict__ partial, double* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int ns = blk_nslot[i / 36];
+  double s = 0.0;
+  for (int g = 0; g < ns; ++g) s += partial[(size_t)g * stride + i];
+  out[i] = s;
+}
+void launch_schur_sum_tiles(hipStream_t s, const SchurTiles& a, double* out) {
+  const size_t count = (size_t)a.nelem;
+  if (count > 0)
+    k_schur_sum_tiles<<<(unsigned)((count + 255) / 256), 256, 0, s>>>(a.blk_nslot, a.stride, count, a.partial, out);
 }
 
 // sum over the groups' partials in group order (fixed: bitwise reproducible)
@@ -3285,7 +3307,7 @@ void launch_schur_tiles(hipStream_t s, const double* yrec, const SchurTiles& a, 
                               (int)kTileLdsMax);
     attr = true;
   }
-  k_schur_tiles<<<a.ntile * a.ngroup, kTileThreads, kTileLdsMax, s>>>(yrec, a, NC);
+  k_schur_tiles<<<a.nsub * a.ngroup, kTileThreads, kTileLdsMax, s>>>(yrec, a, NC);
 }
 void launch_schur_scale(hipStream_t s, int NC, const double* ug, const double* scale_c, int* kx) {
   if (NC > 0) k_schur_scale<<<grid_for(6 * NC, 256, 1 << 20), 256, 0, s>>>(NC, ug, scale_c, kx);

@@ -220,6 +220,7 @@ struct Knobs {
   int cg_onewg = 0;         // DAB_CG_ONEWG=1: single-work-group CG update
   int bench_sample = 8;     // DAB_BENCH_SAMPLE: timing-event stride of dab_bench_eval_pass
   int schur_tiles = 1;      // DAB_SCHUR_TILES=0: explicit S from the pair tables even for small NC
+  int tile_balance = 1;     // DAB_TILE_BALANCE=0: one work-group per tile and group of batches
   int p2p = -1;             // DAB_P2P: one-shot xGMI all-reduce of small sums (-1 auto: RCCL handles
                             // only; 1 also on host-staged handles, the one-GPU rehearsal; 0 off)
   int fused_stream = 2;     // DAB_FUSED_STREAM: fused pass records — 2 packed point-side records, camera
@@ -245,6 +246,7 @@ struct Knobs {
     get("DAB_CG_ONEWG", cg_onewg);
     get("DAB_BENCH_SAMPLE", bench_sample);
     get("DAB_SCHUR_TILES", schur_tiles);
+    get("DAB_TILE_BALANCE", tile_balance);
     get("DAB_P2P", p2p);
     get("DAB_FUSED_STREAM", fused_stream);
     get("DAB_FUSED_V", fused_variant);
@@ -2020,11 +2022,58 @@ static int build_schur_tiles(dab_handle* h, int2* d_sch, const int* d_m) {
   a.ntile = ntile;
   a.nbatch = nbatch;
   a.nrec = nrec;
-  // one work-group per CU; groups in multiples of 8 (one XCD per group)
-  int ng = std::max(1, h->ncu / a.ntile);
+  // load balance: a tile's time is its busiest wave's, summed over its batches, and the
+  // tiles differ (C5: the arc rows' tile ~2x the others), so a heavy tile's batches go to
+  // several work-groups per group. Parts per tile from the sampled hits (the tile's work):
+  // the split that minimises max_t(hits_t / sub_t) / groups, groups = CUs / sum(sub)
+  // (multiples of 8: one XCD per group). DAB_TILE_BALANCE=0 keeps one part per tile.
+  std::vector<int> sub(ntile, 1);
+  {
+    std::vector<double> w(ntile, 0.0);
+    for (int t = 0; t < ntile; ++t)
+      for (int k = tb[t]; k < tb[t + 1]; ++k) w[t] += (double)hits[k] + 1.0;
+    auto groups_for = [&](int nsub) {
+      int ng = std::max(1, h->ncu / nsub);
+      if (ng >= 8) ng -= ng % 8;
+      return ng;
+    };
+    auto cost = [&](const std::vector<int>& sb) {
+      int ns = 0;
+      double m = 0.0;
+      for (int t = 0; t < ntile; ++t) {
+        ns += sb[t];
+        m = std::max(m, w[t] / sb[t]);
+      }
+      return m / groups_for(ns);
+    };
+    if (h->knobs.tile_balance != 0 && ntile > 1 && ntile <= 6) {
+      std::vector<int> cur(ntile, 1), best = cur;
+      double bc = cost(cur);
+      for (;;) {  // odometer over sub_t in 1..4
+        int t = 0;
+        while (t < ntile && cur[t] == 4) cur[t++] = 1;
+        if (t == ntile) break;
+        ++cur[t];
+        const double c = cost(cur);
+        if (c < bc * (1.0 - 1e-12)) {
+          bc = c;
+          best = cur;
+        }
+      }
+      sub = best;
+    }
+  }
+  std::vector<int> subbeg(ntile + 1, 0);
+  for (int t = 0; t < ntile; ++t) subbeg[t + 1] = subbeg[t] + sub[t];
+  a.nsub = subbeg[ntile];
+  int ng = std::max(1, h->ncu / a.nsub);
   if (ng >= 8) ng -= ng % 8;
-  // at least 8 batches per group: small problems keep few partials for k_schur_sum
-  a.ngroup = std::max(1, std::min(ng, a.nbatch / 8));
+  // at least 8 batches per work-group: small problems keep few partials for the sum
+  const int smax = *std::max_element(sub.begin(), sub.end());
+  a.ngroup = std::max(1, std::min(ng, a.nbatch / (8 * smax)));
+  std::vector<int> blk_nslot(std::max(1, nb), a.ngroup);
+  for (int t = 0; t < ntile; ++t)
+    for (int k = tb[t]; k < tb[t + 1]; ++k) blk_nslot[k] = a.ngroup * sub[t];
   a.nelem = 36 * nb;
   a.stride = (size_t)a.nelem;
   a.kq = 0;
@@ -2042,7 +2091,14 @@ static int build_schur_tiles(dab_handle* h, int2* d_sch, const int* d_m) {
   a.rec_info = d_rec;
   CHECK_RC(d.alloc(&h->d_kx, (size_t)6 * NC));
   a.kx = h->d_kx;
-  CHECK_RC(d.alloc(&a.partial, (size_t)a.ngroup * a.stride));
+  CHECK_RC(d.alloc(&a.partial, (size_t)a.ngroup * smax * a.stride));
+  int *d_sub = nullptr, *d_subbeg = nullptr, *d_nslot = nullptr;
+  CHECK_RC(upload(&d_sub, d, sub, s));
+  CHECK_RC(upload(&d_subbeg, d, subbeg, s));
+  CHECK_RC(upload(&d_nslot, d, blk_nslot, s));
+  a.tile_sub = d_sub;
+  a.tile_subbeg = d_subbeg;
+  a.blk_nslot = d_nslot;
   CHECK_RC(d.alloc(&h->d_sblk, a.stride));
   CHECK_RC(d.alloc(&h->d_rfx, (size_t)6 * NC));
   CHECK_RC(d.alloc(&h->d_yrec, (size_t)18 * std::max(1, a.nrec)));
@@ -2908,7 +2964,7 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
       HIP_OK(hipMemsetAsync(h->d_rfx, 0, sizeof(unsigned long long) * 6 * (size_t)NC, s));
       launch_schur_y(s, v, h->d_points, h->d_camtab, h->d_L, h->d_q, h->d_scale_c, a, h->d_yrec, h->d_rfx);
       launch_schur_tiles(s, h->d_yrec, a, NC);
-      launch_schur_sum(s, a.ngroup, a.stride, (size_t)a.nelem, a.partial, h->d_sblk);
+      launch_schur_sum_tiles(s, a, h->d_sblk);
       CHECK_RC(h->allreduce(h->d_sblk, (size_t)a.nelem, ncclSum));
       CHECK_RC(h->allreduce_u64(reinterpret_cast<uint64_t*>(h->d_rfx), (size_t)6 * NC));
       HIP_OK(hipMemsetAsync(h->d_S, 0, sizeof(double) * (size_t)(n + 1) * h->lds, s));
