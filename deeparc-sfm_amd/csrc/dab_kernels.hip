@@ -3013,7 +3013,7 @@ int schur_tile_batch_cap(int NC) {
 
 // k_schur_y: thread per record; tables staged in LDS; rhs partials of the work-group in LDS
 // (fixed point, 2^(60 - kx[R] - kq) units), then one global integer atomic per rhs row.
-__global__ __launch_bounds__(256) void k_schur_y(DevView v, const double* __restrict__ points,
+__global__ __launch_bounds__(256, 3) void k_schur_y(DevView v, const double* __restrict__ points,
                                                  const double* __restrict__ camtab, const double* __restrict__ PU,
                                                  const double* __restrict__ q, const double* __restrict__ scc,
                                                  SchurTiles a, double* __restrict__ yrec,
@@ -3027,11 +3027,14 @@ __global__ __launch_bounds__(256) void k_schur_y(DevView v, const double* __rest
   // wave stores the 9 KB as lane-contiguous 16-B pieces (whole lines, instead of 64 lines
   // touched 16 B at a time by every store)
   const int lane = threadIdx.x & 63;
-  double* stage = reinterpret_cast<double*>(rhs + 6 * (size_t)v.NC) + (size_t)(threadIdx.x >> 6) * 64 * 18;
+  // half a wave's records at a time (32 x 144 B per wave): the smaller stage lets three
+  // work-groups share a CU (three waves per SIMD)
+  double* stage = reinterpret_cast<double*>(rhs + 6 * (size_t)v.NC) + (size_t)(threadIdx.x >> 6) * 32 * 18;
   for (int rb = blockIdx.x * blockDim.x + (threadIdx.x & ~63); rb < a.nrec; rb += gridDim.x * blockDim.x) {
     const int r = rb + lane;
     const int nvalid = min(64, a.nrec - rb);
     double rq[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // this record's rhs terms (Y q per row)
+    double yo[18];  // this record's Y (staged below)
     int rcam = -1;
     if (r < a.nrec) {
     const int4 ri = a.rec_info[r];  // (first sorted entry, count, point, camera)
@@ -3063,21 +3066,21 @@ __global__ __launch_bounds__(256) void k_schur_y(DevView v, const double* __rest
 #pragma unroll
         for (int k = 0; k < 3; ++k) w[3 * r + k] = fma(jb[r], jx1[k], fma(ja[r], jx0[k], w[3 * r + k]));
     }
-    double y[18];
+    double (&y)[18] = w;  // Y = s_c o (W PU) in place, row by row (W's registers are reused)
     {
       const double* pu = PU + 6 * (size_t)pt;
       const double u00 = pu[0], u01 = pu[1], u02 = pu[2], u11 = pu[3], u12 = pu[4], u22 = pu[5];
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
         const double sa = scc[6 * cam + r];
-        y[3 * r] = sa * (w[3 * r] * u00);
-        y[3 * r + 1] = sa * (w[3 * r] * u01 + w[3 * r + 1] * u11);
-        y[3 * r + 2] = sa * (w[3 * r] * u02 + w[3 * r + 1] * u12 + w[3 * r + 2] * u22);
+        const double w0 = w[3 * r], w1 = w[3 * r + 1], w2 = w[3 * r + 2];
+        y[3 * r] = sa * (w0 * u00);
+        y[3 * r + 1] = sa * (w0 * u01 + w1 * u11);
+        y[3 * r + 2] = sa * (w0 * u02 + w1 * u12 + w2 * u22);
       }
     }
-    double2* o = reinterpret_cast<double2*>(stage + 18 * lane);
 #pragma unroll
-    for (int k = 0; k < 9; ++k) o[k] = make_double2(y[2 * k], y[2 * k + 1]);
+    for (int k = 0; k < 18; ++k) yo[k] = y[k];
     const double q0 = q[4 * (size_t)pt], q1 = q[4 * (size_t)pt + 1], q2 = q[4 * (size_t)pt + 2];
 #pragma unroll
     for (int k = 0; k < 6; ++k) rq[k] = y[3 * k] * q0 + y[3 * k + 1] * q1 + y[3 * k + 2] * q2;
@@ -3090,19 +3093,29 @@ __global__ __launch_bounds__(256) void k_schur_y(DevView v, const double* __rest
                                (unsigned long long)__double2ll_rn(ldexp(rq[k], 60 - a.kx[6 * rcam + k] - a.kq)),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double2* dst = reinterpret_cast<double2*>(yrec + 18 * (size_t)rb);
-    const double2* src = reinterpret_cast<const double2*>(stage);
 #pragma unroll
-    for (int j = 0; j < 9; ++j) {
-      const int piece = 64 * j + lane;
-      if (piece < 9 * nvalid) dst[piece] = src[piece];
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int nv = min(32, nvalid - 32 * h2);
+      if (nv <= 0) break;
+      if ((lane >> 5) == h2 && rcam >= 0) {
+        double2* o = reinterpret_cast<double2*>(stage + 18 * (lane & 31));
+#pragma unroll
+        for (int k = 0; k < 9; ++k) o[k] = make_double2(yo[2 * k], yo[2 * k + 1]);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      double2* dst = reinterpret_cast<double2*>(yrec + 18 * ((size_t)rb + 32 * h2));
+      const double2* src = reinterpret_cast<const double2*>(stage);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const int piece = 64 * j + lane;
+        if (piece < 9 * nv) dst[piece] = src[piece];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 6 * v.NC; i += blockDim.x)
@@ -3296,7 +3309,7 @@ void launch_schur_y(hipStream_t s, const DevView& v, const double* points, const
                     unsigned long long* rhs_out) {
   if (a.nrec <= 0) return;
   const size_t lds = small_tabs_bytes(v.E, v.NI) + sizeof(unsigned long long) * 6 * (size_t)v.NC +
-                     sizeof(double) * 4 * 64 * 18;  // + a record stage per wave
+                     sizeof(double) * 4 * 32 * 18;  // + a half-wave record stage per wave
   k_schur_y<<<std::min(grid_for(a.nrec, 256, 1 << 20), kSmallGrid), 256, lds, s>>>(v, points, camtab, PU, q, scale_c,
                                                                                    a, yrec, rhs_out);
 }
