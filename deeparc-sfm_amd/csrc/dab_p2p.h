@@ -9,7 +9,7 @@ namespace dab {
 
 constexpr int kP2pMaxRanks = 8;    // one node
 constexpr int kP2pMaxWg = 32;      // work-groups (slices) per call
-constexpr int kP2pHandleBytes = 80;  // IPC handle (64) | offset of the region in its allocation (8)
+constexpr int kP2pHandleBytes = 96;  // IPC handle (64) | allocation offset (8) | arena slot offset (8) | valid
 
 struct P2pComm;
 // in-place gather of every rank's kP2pHandleBytes record: buf[world][kP2pHandleBytes], own

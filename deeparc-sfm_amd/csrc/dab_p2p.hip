@@ -26,7 +26,10 @@
 
 #include <algorithm>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "dab_internal.h"
@@ -136,13 +139,30 @@ __global__ __launch_bounds__(kP2pBlock) void k_p2p_allreduce(T* __restrict__ buf
 }
 }  // namespace
 
-// One allocation per rank holds the regions of every context of a group (each process
-// opens each peer's handle once: two handles of one peer opened in one process were seen
-// to resolve to the same mapping on the one-GPU rehearsal).
-struct P2pShared {
-  int rank = 0, world = 1, refs = 0;
+// The regions live in one process-wide arena per device, allocated and exported once and
+// never freed; each peer's arena is imported once per process and never closed. A group takes
+// a free slot of the arena and gives it back on destroy. Re-exporting fresh allocations per
+// group was unsafe on this runtime: an importer could get back its mapping of the peer's
+// earlier (freed) allocation for the new handle — two live handles of one peer were seen to
+// resolve to one mapping, and on the 4-rank one-GPU rehearsal the third and later groups read
+// stale slots and wrote flags into memory the peer had reused (wrong sums, then wrong
+// trajectories after the fallback). With one export per process the handle an importer
+// sees for a peer never changes.
+namespace {
+constexpr int kArenaSlots = 8;  // live groups per process and device
+struct Arena {
   void* alloc = nullptr;
-  void* opened[kP2pMaxRanks] = {};  // what hipIpcOpenMemHandle returned (closed on release)
+  size_t slot_bytes = 0;
+  unsigned char rec[kP2pHandleBytes] = {};  // IPC handle | offset of the allocation in its range
+  bool used[kArenaSlots] = {};
+};
+std::mutex g_p2p_mu;
+std::map<int, Arena> g_arena;                              // device -> arena
+std::map<std::pair<int, std::string>, char*> g_imported;  // (device, peer handle) -> mapping
+}  // namespace
+
+struct P2pShared {
+  int device = 0, slot = -1, refs = 0;
 };
 struct P2pComm {
   int rank = 0, world = 1;
@@ -158,10 +178,65 @@ struct P2pComm {
 
 static void shared_release(P2pShared* sh) {
   if (!sh || --sh->refs > 0) return;
-  for (int r = 0; r < sh->world; ++r)
-    if (r != sh->rank && sh->opened[r]) (void)hipIpcCloseMemHandle(sh->opened[r]);
-  if (sh->alloc) (void)hipFree(sh->alloc);
+  if (sh->slot >= 0) {
+    std::lock_guard<std::mutex> lk(g_p2p_mu);
+    g_arena[sh->device].used[sh->slot] = false;
+  }
   delete sh;
+}
+
+// a free slot of this device's arena (allocated and exported on first use), zeroed: the
+// previous group on the slot has finished with it (its last call completed on every rank
+// before any rank could join this group's collective handle exchange)
+static std::string arena_take(int device, size_t bytes, int* slot, char** base, unsigned long long* soff,
+                              unsigned char* rec) {
+  std::lock_guard<std::mutex> lk(g_p2p_mu);
+  Arena& a = g_arena[device];
+  if (!a.alloc) {
+    void* p = nullptr;
+    const size_t total = bytes * kArenaSlots;
+    if (hipExtMallocWithFlags(&p, total, hipDeviceMallocUncached) != hipSuccess) return "p2p: uncached arena allocation failed";
+    hipIpcMemHandle_t hd{};
+    hipDeviceptr_t rbase = nullptr;
+    size_t range = 0;
+    if (hipIpcGetMemHandle(&hd, p) != hipSuccess || hipMemGetAddressRange(&rbase, &range, p) != hipSuccess) {
+      (void)hipFree(p);
+      return "p2p: arena export failed";
+    }
+    const unsigned long long off = (unsigned long long)(static_cast<char*>(p) - static_cast<char*>(rbase));
+    a.alloc = p;
+    a.slot_bytes = bytes;
+    std::memcpy(a.rec, &hd, sizeof(hd));
+    std::memcpy(a.rec + sizeof(hd), &off, 8);
+  }
+  if (bytes > a.slot_bytes) return "p2p: group larger than the arena slot";
+  int k = 0;
+  while (k < kArenaSlots && a.used[k]) ++k;
+  if (k == kArenaSlots) return "p2p: every arena slot is in use";
+  char* b = static_cast<char*>(a.alloc) + (size_t)k * a.slot_bytes;
+  if (hipMemset(b, 0, a.slot_bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    return "p2p: arena slot initialisation failed";
+  a.used[k] = true;
+  *slot = k;
+  *base = b;
+  *soff = (unsigned long long)k * a.slot_bytes;
+  std::memcpy(rec, a.rec, kP2pHandleBytes);
+  return "";
+}
+
+// the mapping of a peer's arena, opened once per process
+static char* arena_import(int device, const unsigned char* rec) {
+  std::lock_guard<std::mutex> lk(g_p2p_mu);
+  const auto key = std::make_pair(device, std::string(reinterpret_cast<const char*>(rec), sizeof(hipIpcMemHandle_t)));
+  auto it = g_imported.find(key);
+  if (it != g_imported.end()) return it->second;
+  hipIpcMemHandle_t ph;
+  std::memcpy(&ph, rec, sizeof(ph));
+  void* q = nullptr;
+  if (hipIpcOpenMemHandle(&q, ph, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return nullptr;
+  char* m = static_cast<char*>(q);
+  g_imported[key] = m;
+  return m;
 }
 
 int p2p_create_group(int rank, int world, size_t cap_words, int nctx, const P2pAllgather& allgather,
@@ -170,44 +245,31 @@ int p2p_create_group(int rank, int world, size_t cap_words, int nctx, const P2pA
   if (world < 2 || world > kP2pMaxRanks) return set_error(DAB_E_INVALID, "p2p: world size out of range");
   const Layout L{cap_words};
   const size_t region = (L.words() + 511) / 512 * 512;  // words per context, 4-KB aligned
+  int device = 0;
+  (void)hipGetDevice(&device);
   P2pShared* sh = new P2pShared();
-  sh->rank = rank;
-  sh->world = world;
+  sh->device = device;
   // local failures still take part in the (collective) handle exchange, with a zero record
-  std::string err;
-  void* p = nullptr;
-  hipIpcMemHandle_t hd{};
-  unsigned long long off = 0;
-  if (hipExtMallocWithFlags(&p, region * nctx * 8, hipDeviceMallocUncached) != hipSuccess) {
-    p = nullptr;
-    err = "p2p: uncached region allocation failed";
-  } else {
-    sh->alloc = p;
-    hipDeviceptr_t base = nullptr;  // the handle names the whole allocation: send the offset too
-    size_t range = 0;
-    if (hipMemset(p, 0, region * nctx * 8) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
-      err = "p2p: region initialisation failed";
-    else if (hipIpcGetMemHandle(&hd, p) != hipSuccess)
-      err = "p2p: hipIpcGetMemHandle failed";
-    else if (hipMemGetAddressRange(&base, &range, p) != hipSuccess)
-      err = "p2p: hipMemGetAddressRange failed";
-    else
-      off = (unsigned long long)(static_cast<char*>(p) - static_cast<char*>(base));
-  }
+  char* mine = nullptr;
+  unsigned char rec[kP2pHandleBytes] = {};
+  unsigned long long soff = 0;
+  std::string err = arena_take(device, region * nctx * 8, &sh->slot, &mine, &soff, rec);
   sh->refs = 1;
-  static_assert(sizeof(hipIpcMemHandle_t) + 9 <= kP2pHandleBytes, "IPC handle size");
+  static_assert(sizeof(hipIpcMemHandle_t) + 17 <= kP2pHandleBytes, "IPC handle size");
+  // record: IPC handle | allocation offset in its range (8) | slot offset in the arena (8) | valid
   std::vector<unsigned char> all((size_t)world * kP2pHandleBytes, 0);
   if (err.empty()) {
-    std::memcpy(all.data() + (size_t)rank * kP2pHandleBytes, &hd, sizeof(hd));
-    std::memcpy(all.data() + (size_t)rank * kP2pHandleBytes + sizeof(hd), &off, 8);
-    all[(size_t)rank * kP2pHandleBytes + sizeof(hd) + 8] = 1;  // valid record
+    unsigned char* r = all.data() + (size_t)rank * kP2pHandleBytes;
+    std::memcpy(r, rec, sizeof(hipIpcMemHandle_t) + 8);
+    std::memcpy(r + sizeof(hipIpcMemHandle_t) + 8, &soff, 8);
+    r[sizeof(hipIpcMemHandle_t) + 16] = 1;  // valid record
   }
   if (allgather(all.data()) != 0) {
     shared_release(sh);
     return set_error(DAB_E_COMM, "p2p: handle exchange failed");
   }
   for (int r = 0; r < world && err.empty(); ++r)
-    if (all[(size_t)r * kP2pHandleBytes + sizeof(hd) + 8] != 1) err = "p2p: a peer could not export its region";
+    if (all[(size_t)r * kP2pHandleBytes + sizeof(hipIpcMemHandle_t) + 16] != 1) err = "p2p: a peer could not export its region";
   if (!err.empty()) {
     shared_release(sh);
     return set_error(DAB_E_DEVICE, err);
@@ -215,20 +277,19 @@ int p2p_create_group(int rank, int world, size_t cap_words, int nctx, const P2pA
   std::vector<char*> peer_base(world, nullptr);
   for (int r = 0; r < world; ++r) {
     if (r == rank) {
-      peer_base[r] = static_cast<char*>(p);
+      peer_base[r] = mine;
       continue;
     }
-    hipIpcMemHandle_t ph;
-    unsigned long long poff = 0;
-    std::memcpy(&ph, all.data() + (size_t)r * kP2pHandleBytes, sizeof(ph));
-    std::memcpy(&poff, all.data() + (size_t)r * kP2pHandleBytes + sizeof(ph), 8);
-    void* q = nullptr;
-    if (hipIpcOpenMemHandle(&q, ph, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+    const unsigned char* pr = all.data() + (size_t)r * kP2pHandleBytes;
+    unsigned long long poff = 0, psoff = 0;
+    std::memcpy(&poff, pr + sizeof(hipIpcMemHandle_t), 8);
+    std::memcpy(&psoff, pr + sizeof(hipIpcMemHandle_t) + 8, 8);
+    char* q = arena_import(device, pr);
+    if (!q) {
       shared_release(sh);
       return set_error(DAB_E_DEVICE, "p2p: hipIpcOpenMemHandle failed");
     }
-    sh->opened[r] = q;
-    peer_base[r] = static_cast<char*>(q) + poff;
+    peer_base[r] = q + poff + psoff;
   }
   sh->refs = nctx;
   long long tmo_ms = kDefaultTimeoutMs, skip = 0;

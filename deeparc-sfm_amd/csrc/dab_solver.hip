@@ -695,6 +695,9 @@ static int setup_p2p(dab_handle* h) {
     (void)hipFree(d_f);
   }
   if (bad != 0.0) {
+    // one line on stderr: a silent fallback would hide a platform whose peer mappings fail
+    fprintf(stderr, "dab: rank %d: peer-to-peer all-reduce not verified (%s); sums stay on %s\n", h->rank,
+            rc != 0 ? dab_last_error() : "a peer failed", h->host_cb ? "the host collective" : "RCCL");
     p2p_destroy(ctx[0]);
     p2p_destroy(ctx[1]);
     clear_error();
