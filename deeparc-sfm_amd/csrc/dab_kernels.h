@@ -42,6 +42,11 @@ inline void cost_fx_total(const unsigned long long* words, double& sum, double& 
   bad = (double)acc[kFxBad];
 }
 constexpr int kChunk = 4096;  // max entries per reduction chunk (C3: one chunk per camera)
+// max records per pair-major chunk (k_eval_pair; pairs are cut into equal pieces). C5
+// (945 pairs of 9.5-10 K records), k_eval_pair per piece count: 5 pieces 200 us, 4 pieces
+// 149-151, 3 pieces 190, 2 pieces 154-156 (the launch runs in rounds of two work-groups per
+// CU; the 4-piece cut fills its last round best)
+constexpr int kPairChunk = 2560;
 constexpr int kSlotBit = 1 << 30;  // cm_idx.w flag: the entry is the ring (slot 1) camera
 
 // Device-side problem view. Observations are point-major ("s" order). An "entry" is an
@@ -135,7 +140,7 @@ void launch_eval_cross(hipStream_t s, const DevView& v, int nchunk, const int* c
 bool pair_eval_fits(int E, int NI);  // the tables fit LDS (small_tabs_fit)
 void launch_eval_pair(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
                       const double2* x_xy, const double* points, const double* camtab, double* xpart,
-                      double* cpart);
+                      double* cpart, bool uni_intr);
 void launch_cam_final(hipStream_t s, int NC, const int* seg_chunk, const double* partial, const int* xcam_ptr,
                       const int* xcam_list, const double* cpart, double* ug);
 void launch_eval_cams_gen(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const double* points,

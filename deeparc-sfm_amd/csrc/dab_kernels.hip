@@ -1835,6 +1835,54 @@ __device__ __forceinline__ void pipe_entries_ns(const int4* __restrict__ idx, co
   }
 }
 
+// pipe_entries_ns with a uniform trip count: every lane of the block runs ceil((e - b) /
+// stride) iterations, a lane past the end on the clamped last entry with valid = false (its
+// body must add nothing). Every load is unconditional, so the memory counters the compiler
+// tracks stay exact across the unrolled slots and a body waits only for its own slot's
+// loads. With the guarded loads of pipe_entries_ns the compiler could not count what was
+// outstanding on every path and waited for all of it (vmcnt(0)) before each body: the
+// prefetch of the next slots never overlapped the arithmetic.
+// NS register slots: the record of entry k + NS - 1 is loaded, then the point of entry
+// k + GD gathered (its record loaded NS - 1 - GD iterations earlier), then entry k computed;
+// with GD <= NS - 3 each load has at least two bodies of arithmetic to arrive in.
+template <int NS, int GD, class Body>
+__device__ __forceinline__ void pipe_entries_uni(const int4* __restrict__ idx, const double2* __restrict__ xyv,
+                                                 int b, int e, int lane, int stride,
+                                                 const double* __restrict__ points, Body body) {
+  static_assert(NS >= 3 && GD >= 1 && GD <= NS - 2, "slot distances");
+  constexpr int RD = NS - 1;
+  const int niter = (e - b + stride - 1) / stride;
+  const int last = e - 1;
+  int4 id[NS];
+  double2 xy[NS];
+  double X[NS][3];
+#pragma unroll
+  for (int s = 0; s < RD; ++s) {
+    const int i = min(b + lane + s * stride, last);
+    id[s] = idx[i];
+    xy[s] = xyv[i];
+  }
+#pragma unroll
+  for (int s = 0; s < GD; ++s)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) X[s][q] = points[3 * (size_t)max(id[s].x, 0) + q];
+  for (int k = 0; k < niter; k += NS) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int kk = k + u;
+      const int sl = (u + RD) % NS, sg = (u + GD) % NS;
+      {
+        const int i = min(b + lane + (kk + RD) * stride, last);
+        id[sl] = idx[i];
+        xy[sl] = xyv[i];
+      }
+#pragma unroll
+      for (int q = 0; q < 3; ++q) X[sg][q] = points[3 * (size_t)max(id[sg].x, 0) + q];
+      if (kk < niter) body(id[u], xy[u], X[u], b + lane + kk * stride <= last);
+    }
+  }
+}
+
 // UNI: the chunks of `list` are uniform (chunk_uni), tables read once per block
 template <bool UNI>
 __global__ __launch_bounds__(256) void k_eval_cams(DevView v, const int* __restrict__ chunk_beg,
@@ -2460,7 +2508,7 @@ __global__ __launch_bounds__(256) void k_eval_cross(DevView v, const int* __rest
 // sums). It replaces, for these observations, both camera-major entries and the separate
 // cross pass: one 56-B input per observation instead of three. k_cam_final adds the
 // camera halves to the camera-major partials of the remaining entries.
-template <int PNS>
+template <int PNS, int PGD, bool UT = false>
 __global__ __launch_bounds__(256) void k_eval_pair(DevView v, const int* __restrict__ chunk_beg,
                                                    const int4* __restrict__ x_idx,
                                                    const double2* __restrict__ x_xy,
@@ -2470,7 +2518,8 @@ __global__ __launch_bounds__(256) void k_eval_pair(DevView v, const int* __restr
   const int c = blockIdx.x;
   const int b = chunk_beg[c], e = chunk_beg[c + 1];
   extern __shared__ double tabs_lds[];
-  const SmallTabs st = stage_small_tabs(tabs_lds, v.E, v.NI, camtab, v.intr);  // barrier inside
+  SmallTabs st{nullptr, nullptr};
+  if constexpr (!UT) st = stage_small_tabs(tabs_lds, v.E, v.NI, camtab, v.intr);  // barrier inside
   __shared__ double jl[2][9];
   __shared__ double ws[kRedBlock / 64][90];
   if (b >= e) {
@@ -2482,16 +2531,33 @@ __global__ __launch_bounds__(256) void k_eval_pair(DevView v, const int* __restr
   bool sa, sr;
   ext_frame(camtab, id0.y, jl[0], threadIdx.x, sa);
   ext_frame(camtab, id0.z, jl[1], threadIdx.x, sr);
+  double Tau[12], Tbu[12], Ku[6];  // UT: the chunk's one arc, ring and intrinsic
+  if constexpr (UT) {
+    const GlobalTabs g{camtab, v.intr};
+    g.rt(id0.y, Tau);
+    g.rt(id0.z, Tbu);
+    g.k(id0.w, Ku);
+  }
   // [0, 27) arc U | g, [27, 54) ring U | g, [54, 90) cross (arc row-major)
   double acc[90];
 #pragma unroll
   for (int i = 0; i < 90; ++i) acc[i] = 0.0;
-  pipe_entries_ns<PNS>(x_idx, x_xy, b + threadIdx.x, e, blockDim.x, points,
-               [&](const int4 id, const double2 xy, const double (&X)[3]) {
+  pipe_entries_uni<PNS, PGD>(x_idx, x_xy, b, e, threadIdx.x, blockDim.x, points,
+               [&](const int4 id, const double2 xy, const double (&X)[3], const bool valid) {
                  double Ta[12], Tb[12], Kr[6];
-                 st.rt(id.y, Ta);
-                 st.rt(id.z, Tb);
-                 st.k(id.w, Kr);
+                 if constexpr (UT) {
+#pragma unroll
+                   for (int k = 0; k < 12; ++k) {
+                     Ta[k] = Tau[k];
+                     Tb[k] = Tbu[k];
+                   }
+#pragma unroll
+                   for (int k = 0; k < 6; ++k) Kr[k] = Ku[k];
+                 } else {
+                   st.rt(id.y, Ta);
+                   st.rt(id.z, Tb);
+                   st.k(id.w, Kr);
+                 }
                  double Q[3], P[3], Z0[3], Z1[3];
                  matvec_add(Tb, X, Tb + 9, Q);
                  matvec_add(Ta, Q, Ta + 9, P);
@@ -2502,6 +2568,11 @@ __global__ __launch_bounds__(256) void k_eval_pair(DevView v, const int* __restr
                  }
                  Proj pr;
                  project(P, Kr, xy.x, xy.y, pr, true);
+                 if (!valid) {  // a lane past the chunk's end: zero rows add exactly nothing
+                   pr.ru = pr.rv = 0.0;
+#pragma unroll
+                   for (int k = 0; k < 3; ++k) pr.A0[k] = pr.A1[k] = 0.0;
+                 }
 #pragma unroll
                  for (int row = 0; row < 2; ++row) {
                    const double* A = row == 0 ? pr.A0 : pr.A1;
@@ -2589,13 +2660,18 @@ __global__ __launch_bounds__(256) void k_eval_pair(DevView v, const int* __restr
 bool pair_eval_fits(int E, int NI) { return small_tabs_fit(E, NI); }
 void launch_eval_pair(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
                       const double2* x_xy, const double* points, const double* camtab, double* xpart,
-                      double* cpart) {
+                      double* cpart, bool uni_intr) {
   if (nchunk <= 0) return;
-  // 90 sums per lane: ~300 VGPRs, one wave per SIMD (a 256-VGPR cap spills hundreds)
-  // four register slots: measured 285 us at C5 against 295 (three) and 286 (five); one
-  // wave per SIMD leaves the registers for it
-  k_eval_pair<4><<<nchunk, 256, small_tabs_bytes(v.E, v.NI), s>>>(v, chunk_beg, x_idx, x_xy, points, camtab, xpart,
-                                                                  cpart);
+  // four register slots, the point gathered one entry ahead: 256 VGPRs and no AGPRs, two
+  // waves per SIMD (deeper slots spilled into AGPRs and measured slower: 6 slots 249 us,
+  // 5 slots 212 against 198 at C5 before the chunk cut below). With one intrinsic per pair
+  // the chunk's arc, ring and intrinsic tables are uniform values (no LDS tables): 198
+  // against 244 us.
+  if (uni_intr)
+    k_eval_pair<4, 1, true><<<nchunk, 256, 0, s>>>(v, chunk_beg, x_idx, x_xy, points, camtab, xpart, cpart);
+  else
+    k_eval_pair<4, 1, false><<<nchunk, 256, small_tabs_bytes(v.E, v.NI), s>>>(v, chunk_beg, x_idx, x_xy, points,
+                                                                            camtab, xpart, cpart);
 }
 
 // ug[c] = its camera-major chunk partials (seg_chunk) + its halves of the pair chunks

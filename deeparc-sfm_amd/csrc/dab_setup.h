@@ -69,6 +69,8 @@ void su_cross_copy(hipStream_t s, int n, const int* slots, const int4* obs_idx, 
                    int4* x_idx, double2* x_xy, unsigned char* touched);
 // (14) count of set bytes
 void su_count_flags(hipStream_t s, int n, const unsigned char* flags, int* count);
+// neighbouring pair-major records of one (arc, ring) pair with different intrinsics, added to *count
+void su_pair_intr(hipStream_t s, int n, const int4* x_idx, int* count);
 // (15) entries not paired (camera-major flags) and the stable copy of their records
 void su_unpaired_flags(hipStream_t s, int NE, const int4* cm_idx, const int* ext_col, unsigned char* flags,
                        int* flags_i);

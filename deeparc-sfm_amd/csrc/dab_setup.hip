@@ -423,6 +423,25 @@ void su_count_flags(hipStream_t s, int n, const unsigned char* flags, int* count
   if (n > 0) k_su_count_flags<<<std::min(su_grid(n), 2048u), kSuBlock, 0, s>>>(n, flags, count);
 }
 
+// ---- (14b) one intrinsic per pair ----
+// k_eval_pair reads the arc, ring and intrinsic tables of a chunk once (uniform values)
+// when every pair-major record of one (arc, ring) pair names the same intrinsic; count the
+// neighbours in one pair that differ (0: the fast form applies)
+__global__ __launch_bounds__(kSuBlock) void k_su_pair_intr(int n, const int4* __restrict__ x_idx,
+                                                           int* __restrict__ count) {
+  __shared__ int red[kSuBlock / 64];
+  int c = 0;
+  for (long long i = 1 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int4 a = x_idx[i - 1], b = x_idx[i];
+    c += a.y == b.y && a.z == b.z && a.w != b.w;
+  }
+  const int t = block_sum(c, red);
+  if (threadIdx.x == 0 && t) atomicAdd(count, t);
+}
+void su_pair_intr(hipStream_t s, int n, const int4* x_idx, int* count) {
+  if (n > 1) k_su_pair_intr<<<std::min(su_grid(n), 2048u), kSuBlock, 0, s>>>(n, x_idx, count);
+}
+
 // ---- (15) unpaired entries ----
 __global__ void k_su_unpaired(int NE, const int4* __restrict__ cm_idx, const int* __restrict__ ext_col,
                               unsigned char* __restrict__ flags, int* __restrict__ flags_i) {

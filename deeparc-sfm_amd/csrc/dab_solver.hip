@@ -109,6 +109,14 @@ struct NoInit : std::allocator<T> {
 template <class T>
 using big_vec = std::vector<T, NoInit<T>>;
 
+// Pair-major chunks: a pair of n records is cut into ceil(n / most) equal pieces (the last
+// one shorter by less than one per piece), not into full chunks and a ragged remainder:
+// every chunk's work-group then runs about the same number of iterations per lane
+static size_t pair_piece(size_t n, int most) {
+  const size_t m = (size_t)std::max(1, most), parts = std::max<size_t>(1, (n + m - 1) / m);
+  return std::max<size_t>(1, (n + parts - 1) / parts);
+}
+
 // stable counting sort of [0, n) by key(i) in [0, nb): out[pos] = i; start[nb + 1] = bucket
 // offsets. key(i) < 0 drops i.
 template <class K, class V>
@@ -210,6 +218,7 @@ int upload(T** dptr, Dev& dev, const std::vector<T, A>& h, hipStream_t s) {
 // on a launch path). Unset = the production default.
 struct Knobs {
   int chunk = 0;            // DAB_CHUNK: entries per camera-side reduction chunk (0: kChunk)
+  int xchunk = 0;           // DAB_XCHUNK: most entries per pair-major chunk (0: kPairChunk)
   int pair_eval = -1;       // DAB_PAIR_EVAL=0: rig camera side camera-major + cross passes
   int eval_wps = INT_MIN;   // DAB_EVAL_WPS: point-kernel variant of the two-kernel pass
   int free_cus = 8;         // DAB_EVAL_FREE_CUS: CUs the multi-rank point kernel leaves free
@@ -236,6 +245,7 @@ struct Knobs {
       if (const char* e = getenv(name)) out = atoi(e);
     };
     get("DAB_CHUNK", chunk);
+    get("DAB_XCHUNK", xchunk);
     get("DAB_PAIR_EVAL", pair_eval);
     get("DAB_EVAL_WPS", eval_wps);
     get("DAB_EVAL_FREE_CUS", free_cus);
@@ -339,6 +349,7 @@ struct dab_handle {
   // pair-major evaluation of the composed observations (launch_eval_pair): the other
   // entries' camera-major copy and chunks, and per camera its pair-chunk halves
   bool pair_eval = false;
+  bool pair_uni_intr = false;  // one intrinsic per (arc, ring) pair: k_eval_pair's uniform tables
   double pair_bytes = 0.0, last_pair_ms = 0.0;  // k_eval_pair: algorithmic bytes per launch, bench time
   int nchunk2 = 0;
   int4* d_cm2_idx = nullptr;
@@ -1077,12 +1088,19 @@ static int setup_host(dab_handle* h, const dab_problem* p, const std::function<v
         x_xy[i] = obs_xy[s2];
       }
     });
+    std::vector<size_t> pbeg(h->ncross + 1, 0);
+    std::vector<long long> pcnt(h->ncross, 0);
     size_t i = 0;
     for (int k = 0; k < h->ncross; ++k) {
-      xseg_chunk[k] = (int)xchunk_beg.size();
-      const size_t b = i;
+      pbeg[k] = i;
       while (i < xkeys.size() && xkeys[i] / NS == pairkeys[k]) ++i;
-      for (size_t q = b; q < i; q += chunk) xchunk_beg.push_back((int)q);
+      pcnt[k] = (long long)(i - pbeg[k]);
+    }
+    const int xchunk = std::max(64, h->knobs.xchunk > 0 ? h->knobs.xchunk : kPairChunk);
+    for (int k = 0; k < h->ncross; ++k) {
+      xseg_chunk[k] = (int)xchunk_beg.size();
+      const size_t b = pbeg[k], piece = pair_piece((size_t)pcnt[k], xchunk);
+      for (size_t q = b; q < b + (size_t)pcnt[k]; q += piece) xchunk_beg.push_back((int)q);
     }
     xseg_chunk[h->ncross] = (int)xchunk_beg.size();
     h->nxchunk = (int)xchunk_beg.size();
@@ -1127,6 +1145,10 @@ static int setup_host(dab_handle* h, const dab_problem* p, const std::function<v
         }
       }
       h->pair_bytes = (16.0 + 12.0) * (double)xkeys.size() + 24.0 * (double)npt + 90.0 * 8.0 * h->nxchunk;
+      h->pair_uni_intr = true;
+      for (size_t i = 1; i < x_idx.size() && h->pair_uni_intr; ++i)
+        if (x_idx[i].y == x_idx[i - 1].y && x_idx[i].z == x_idx[i - 1].z && x_idx[i].w != x_idx[i - 1].w)
+          h->pair_uni_intr = false;
     }
     // the entries that are not paired, per camera (counted, then filled in parallel)
     auto unpaired = [&](int i) {
@@ -1638,9 +1660,16 @@ static int setup_device(dab_handle* h, const dab_problem* p, const std::function
   std::vector<int> xchunk_beg, xseg_chunk(h->ncross + 1, 0);
   {
     int b = 0;
+    const int xchunk = std::max(64, h->knobs.xchunk > 0 ? h->knobs.xchunk : kPairChunk);
+    if (getenv("DAB_SETUP_TIMING")) {  // the pair sizes the chunk plan saw
+      fprintf(stderr, "pair chunks: %d pairs, most %d records per chunk, counts", h->ncross, xchunk);
+      for (int k = 0; k < h->ncross; ++k) fprintf(stderr, " %d", pair_cnt[k]);
+      fprintf(stderr, "\n");
+    }
     for (int k = 0; k < h->ncross; ++k) {
       xseg_chunk[k] = (int)xchunk_beg.size();
-      for (int q = b; q < b + pair_cnt[k]; q += chunk) xchunk_beg.push_back(q);
+      const int piece = (int)pair_piece((size_t)pair_cnt[k], xchunk);
+      for (int q = b; q < b + pair_cnt[k]; q += piece) xchunk_beg.push_back(q);
       b += pair_cnt[k];
     }
     xseg_chunk[h->ncross] = (int)xchunk_beg.size();
@@ -1678,8 +1707,9 @@ static int setup_device(dab_handle* h, const dab_problem* p, const std::function
   int n2 = 0;
   int* sel2 = nullptr;
   if (h->pair_eval) {
-    HIP_OK(hipMemsetAsync(small + 5, 0, sizeof(int) * 2, s));
+    HIP_OK(hipMemsetAsync(small + 5, 0, sizeof(int) * 3, s));
     su_count_flags(s, NP, touched, small + 5);
+    su_pair_intr(s, nx, h->d_x_idx, small + 7);
     // the entries that are not paired, per camera, in camera-major order
     unsigned char* uf = nullptr;
     int *ufi = nullptr, *uscan = nullptr, *iota = nullptr, *c2cnt_d = nullptr;
@@ -1697,9 +1727,10 @@ static int setup_device(dab_handle* h, const dab_problem* p, const std::function
       CHECK_RC(rp([&](void* t, size_t* b) { return su_select_flagged_i(t, b, iota, uf, sel2, small + 6, NE, s); }));
     std::vector<int> c2cnt(NC + 1, 0);
     CHECK_RC(d2h(c2cnt.data(), c2cnt_d, sizeof(int) * (NC + 1)));
-    int pb[2] = {0, 0};
-    CHECK_RC(d2h(pb, small + 5, sizeof(int) * 2));
+    int pb[3] = {0, 0, 0};
+    CHECK_RC(d2h(pb, small + 5, sizeof(int) * 3));
     HIP_OK(hipStreamSynchronize(s));
+    h->pair_uni_intr = pb[2] == 0;
     h->pair_bytes = (16.0 + 12.0) * (double)nx + 24.0 * (double)pb[0] + 90.0 * 8.0 * h->nxchunk;
     n2 = pb[1];
     for (int c = 0; c < NC; ++c) {
@@ -2676,7 +2707,7 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
     launch_eval_cams_gen(s, v2, h->nchunk2, h->d_chunk2_beg, h->d_points, h->d_ext, h->d_camtab, h->d_partial2);
     if (ev_pair0) HIP_OK(hipEventRecord(ev_pair0, s));
     launch_eval_pair(s, v, h->nxchunk, h->d_xchunk_beg, h->d_x_idx, h->d_x_xy, h->d_points, h->d_camtab,
-                     h->d_xpartial, h->d_xcpart);
+                     h->d_xpartial, h->d_xcpart, h->pair_uni_intr);
     if (ev_pair1) HIP_OK(hipEventRecord(ev_pair1, s));
     if (pair_rec) *pair_rec = ev_pair0 && ev_pair1 && h->nxchunk > 0;
     launch_cam_final(s, h->NC, h->d_seg2_chunk, h->d_partial2, h->d_xcam_ptr, h->d_xcam_list, h->d_xcpart, h->ug());

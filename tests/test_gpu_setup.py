@@ -31,12 +31,13 @@ def _problems(pkg):
     return out
 
 
-def _run(pkg, prob, host, monkeypatch, lst, freeze=False, chunk=None):
+def _run(pkg, prob, host, monkeypatch, lst, freeze=False, chunk=None, xchunk=None):
     monkeypatch.setenv("DAB_SETUP_HOST", "1" if host else "0")
-    if chunk:
-        monkeypatch.setenv("DAB_CHUNK", str(chunk))
-    else:
-        monkeypatch.delenv("DAB_CHUNK", raising=False)
+    for name, val in (("DAB_CHUNK", chunk), ("DAB_XCHUNK", xchunk)):
+        if val:
+            monkeypatch.setenv(name, str(val))
+        else:
+            monkeypatch.delenv(name, raising=False)
     p = prob.copy()
     p.freeze_camera = 1 if freeze else 0
     s = pkg.Solver(0)
@@ -102,3 +103,45 @@ def test_device_setup_rejects_bad_index(pkg, gpu, monkeypatch):
             s.set_problem(p)
     finally:
         s.close()
+
+
+def test_pair_chunks_cut_into_pieces(pkg, gpu, monkeypatch):
+    """Pairs cut into several equal pieces (DAB_XCHUNK = 100: every pair of this rig spans
+    several k_eval_pair chunks): device and host set-up agree bitwise, and the trajectory
+    stays within rounding of the one-chunk-per-pair layout."""
+    prob = _problems(pkg)["rig"]
+    lst = pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR
+    a, pa, _ = _run(pkg, prob, False, monkeypatch, lst, xchunk=100)
+    b, pb, _ = _run(pkg, prob, True, monkeypatch, lst, xchunk=100)
+    c, pc, _ = _run(pkg, prob, False, monkeypatch, lst)
+    assert [it["cost"] for it in a["iterations"]] == [it["cost"] for it in b["iterations"]]
+    np.testing.assert_array_equal(pa.points, pb.points)
+    ca, cc = [it["cost"] for it in a["iterations"]], [it["cost"] for it in c["iterations"]]
+    assert len(ca) == len(cc)
+    np.testing.assert_allclose(ca, cc, rtol=1e-12)
+
+
+@pytest.mark.parametrize("host", [False, True])
+def test_pair_eval_mixed_intrinsics(pkg, gpu, monkeypatch, host):
+    """k_eval_pair reads a chunk's arc, ring and intrinsic tables once when every record of
+    an (arc, ring) pair names one intrinsic (the rig: intrinsic = arc). Here intrinsic 0 is
+    duplicated and every other observation of it re-pointed at the copy, so pairs mix two
+    intrinsics of equal values: the set-up must fall back to per-record tables, and the
+    trajectory must equal the unmodified problem's bitwise (same values, same sums)."""
+    prob = _problems(pkg)["rig"]
+    q = prob.copy()
+    ni = q.intr.shape[0]
+    q.intr = np.ascontiguousarray(np.vstack([q.intr, q.intr[:1]]))
+    q.intr_nf = np.ascontiguousarray(np.append(q.intr_nf, q.intr_nf[0]).astype(np.int32))
+    q.intr_nk = np.ascontiguousarray(np.append(q.intr_nk, q.intr_nk[0]).astype(np.int32))
+    sel = np.nonzero(q.obs_intr == 0)[0][::2]
+    assert len(sel) > 0
+    q.obs_intr[sel] = ni
+    for lst in (pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR, pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG):
+        a, pa, ra = _run(pkg, prob, host, monkeypatch, lst)
+        b, pb, rb = _run(pkg, q, host, monkeypatch, lst)
+        assert [it["cost"] for it in a["iterations"]] == [it["cost"] for it in b["iterations"]]
+        assert [it["linear_solver_iterations"] for it in a["iterations"]] == \
+            [it["linear_solver_iterations"] for it in b["iterations"]]
+        np.testing.assert_array_equal(pa.points, pb.points)
+        np.testing.assert_array_equal(pa.ext, pb.ext)
