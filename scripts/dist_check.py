@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--expect-p2p", action="store_true",
                     help="fail unless the one-shot peer-to-peer all-reduce carried the sums")
+    ap.add_argument("--live-together", action="store_true",
+                    help="keep the three sharded handles of a problem alive at once (bench.py holds two: "
+                    "each takes its own slot of the peer-to-peer arena)")
     ap.add_argument("--expect-no-p2p", action="store_true",
                     help="fail if the peer-to-peer path is in use (its set-up self-test must have "
                     "failed over to the other collectives)")
@@ -60,8 +63,13 @@ def main():
         else:
             glob = pkg.synth(**pkg.CONFIGS[kind])
         owner = glob.point_owner(world)
-        for lst in (pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR, pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG,
-                    pkg.DAB_LINEAR_SOLVER_AUTO):
+        live = []
+        if a.live_together:  # every handle of this problem created (and its arena slot taken) up front
+            for _ in range(3):
+                h = pkg.Solver(dev, rank, world, uid, host_allreduce=gloo_allreduce if a.host_collective else None)
+                live.append(h)
+        for li, lst in enumerate((pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR, pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG,
+                                  pkg.DAB_LINEAR_SOLVER_AUTO)):
             opts = pkg.options(max_num_iterations=a.iters, linear_solver_type=lst)
             ref = None
             if rank == 0:
@@ -79,12 +87,14 @@ def main():
                 s1.close()
             dist.barrier()
             mine = glob.copy().shard(rank, world)
-            s = pkg.Solver(dev, rank, world, uid, host_allreduce=gloo_allreduce if a.host_collective else None)
+            s = live[li] if live else pkg.Solver(dev, rank, world, uid,
+                                                 host_allreduce=gloo_allreduce if a.host_collective else None)
             s.set_problem(mine)
             sched = s.eval_fused()
             p2p = s.comm_p2p()
             summ = s.solve(opts)
-            s.close()
+            if not live:
+                s.close()
             pts = torch.from_numpy(np.where((owner == rank)[:, None], mine.points, 0.0))
             dist.all_reduce(pts)
             ext = torch.from_numpy(mine.ext.copy())
@@ -106,6 +116,8 @@ def main():
                     ext_ranks_equal=bool(torch.equal(ext, ext_min)),
                     eval_schedule=sched, p2p=p2p,
                     solver_used=(summ["linear_solver_type_used"], rs["linear_solver_type_used"]))
+        for h in live:
+            h.close()
     if rank == 0:
         print(json.dumps(out, indent=1))
         bad = [k for k, v in out.items()

@@ -44,9 +44,11 @@ def test_two_ranks_p2p_allreduce_match_single_handle(gpu):
     assert "DIST_CHECK OK" in p.stdout, p.stdout[-3000:]
 
 
-def test_four_ranks_p2p_six_groups(gpu):
-    """Four processes, six handles each in sequence (BAL and rig x three solver types), every
-    one with its own peer-to-peer group. Groups take slots of a per-process arena exported
+@pytest.mark.parametrize("live", [False, True])
+def test_four_ranks_p2p_six_groups(gpu, live):
+    """Four processes, six handles each (BAL and rig x three solver types), every one with
+    its own peer-to-peer group: in sequence, or three alive at once per problem (bench.py
+    holds two at once on several ranks). Groups take slots of a per-process arena exported
     once: re-exporting a fresh region per group let importers resolve the new handle to the
     peer's freed one (the self-test failed from the third group on and the freed memory was
     written). Every group must verify and match the single handle."""
@@ -57,7 +59,7 @@ def test_four_ranks_p2p_six_groups(gpu):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.join(ROOT, "scripts", "dist_check.py"), "--device", "0", "--host-collective", "--expect-p2p",
-           "--iters", "6"]
+           "--iters", "6"] + (["--live-together"] if live else [])
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     assert "DIST_CHECK OK" in p.stdout, p.stdout[-3000:]
