@@ -308,6 +308,7 @@ int p2p_create_group(int rank, int world, size_t cap_words, int nctx, const P2pA
     c->skip_call = k == 0 ? skip : 0;
     void* e = nullptr;
     if (hipHostMalloc(&e, 64, hipHostMallocCoherent) != hipSuccess) {
+      sh->refs = k + 1;  // the contexts made so far hold the slot: destroying them returns it
       for (int q = 0; q <= k; ++q) p2p_destroy(q < k ? out[q] : c);
       for (int q = 0; q < nctx; ++q) out[q] = nullptr;
       return set_error(DAB_E_NOMEM, "p2p: pinned error word allocation failed");
