@@ -1626,6 +1626,9 @@ static int setup_device(dab_handle* h, const dab_problem* p, const std::function
   int nx = 0;
   int* xslots = nullptr;
   if (h->any_compose && NC > 0) {
+    // the (c0, c1) sort key c0 * NC + c1 (and its sentinel NC * NC) is a 32-bit int
+    if ((long long)NC * NC > (long long)INT_MAX)
+      return set_error(DAB_E_UNSUPPORTED, "composed observations with more than 46340 free cameras");
     int *xk = nullptr, *xv = nullptr, *xk2 = nullptr;
     CHECK_RC(tmp.alloc(&xk, std::max(1, NS)));
     CHECK_RC(tmp.alloc(&xv, std::max(1, NS)));
@@ -2166,6 +2169,9 @@ static int build_schur_pairs_device(dab_handle* h, std::vector<long long>& pk, s
                                     long long& np2) {
   hipStream_t s = h->stream;
   const int NP = h->NP, NC = h->NC;
+  // block key c0 * NC + c1 is a 32-bit int (a dense S that large would not fit anyway)
+  if ((long long)NC * NC > (long long)INT_MAX)
+    return set_error(DAB_E_UNSUPPORTED, "explicit Schur pair tables for more than 46340 free cameras");
   Dev& tmp = h->setup_tmp;  // released at the next set-up
   void* rtmp = nullptr;
   size_t rtmp_cap = 0;
@@ -2381,7 +2387,7 @@ static int build_schur_tables(dab_handle* h) {
     }, 4096);
     for (int pt = 0; pt < NP; ++pt) poff[pt + 1] += poff[pt];
     const long long np2 = poff[NP];
-    big_vec<int> pkey((size_t)np2);
+    big_vec<long long> pkey((size_t)np2);  // c0 * NC + c1 in 64 bits
     big_vec<int2> pef((size_t)np2);
     par_for(NP, [&](long long pb, long long pe, int) {
       for (int pt = (int)pb; pt < (int)pe; ++pt) {
@@ -2390,7 +2396,7 @@ static int build_schur_tables(dab_handle* h) {
           for (int f = pt_ent_ptr[pt]; f < pt_ent_ptr[pt + 1]; ++f) {
             const int ce = ent_cam[e], cf = ent_cam[f];
             if (ce < cf) continue;
-            pkey[o] = ce * NC + cf;
+            pkey[o] = (long long)ce * NC + cf;
             pef[o] = make_int2(e, f);
             ++o;
           }
@@ -2400,10 +2406,10 @@ static int build_schur_tables(dab_handle* h) {
     phase("pairs generated");
     big_vec<int> o1, o2;
     std::vector<long long> st1, st2;
-    bucket_sort(np2, NC, [&](long long i) { return pkey[i] % NC; }, o1, st1);
-    bucket_sort(np2, NC, [&](long long j) { return pkey[o1[j]] / NC; }, o2, st2);
+    bucket_sort(np2, NC, [&](long long i) { return (int)(pkey[i] % NC); }, o1, st1);
+    bucket_sort(np2, NC, [&](long long j) { return (int)(pkey[o1[j]] / NC); }, o2, st2);
     pairs.resize((size_t)np2);
-    big_vec<int> skey((size_t)np2);
+    big_vec<long long> skey((size_t)np2);
     par_for(np2, [&](long long pb, long long pe, int) {
       for (long long i = pb; i < pe; ++i) {
         const int q = o1[o2[i]];
