@@ -1462,12 +1462,23 @@ struct UniFrame {
                                       int i, double* jl) {
     double F[30];
     cam_table(ext + 6 * (size_t)e, F);
+    init(F, intr + (size_t)kIntr * i, jl);
+  }
+  // the same from the extrinsic's 6 parameters and the intrinsic's 6 values already in
+  // registers (loaded at the top of the caller, so that the trigonometry can run while its
+  // first gathers are in flight instead of waiting behind them)
+  struct FromValues {};
+  __device__ __forceinline__ UniFrame(FromValues, const double (&x6)[6], const double (&k6)[6], double* jl) {
+    double F[30];
+    cam_table(x6, F);
+    init(F, k6, jl);
+  }
+  __device__ __forceinline__ void init(const double (&F)[30], const double* k, double* jl) {
     // cam_table's branch (its small-angle Rd is exactly I, R never is otherwise)
     small = F[12] == 1.0 && F[13] == 0.0 && F[14] == 0.0 && F[15] == 0.0 && F[16] == 1.0 && F[17] == 0.0 &&
             F[18] == 0.0 && F[19] == 0.0 && F[20] == 1.0 && F[21] == 1.0 && F[25] == 1.0 && F[29] == 1.0;
 #pragma unroll
     for (int q = 0; q < 12; ++q) T[q] = UniTabs::uniform(F[q]);
-    const double* k = intr + (size_t)kIntr * i;
 #pragma unroll
     for (int q = 0; q < 6; ++q) K[q] = UniTabs::uniform(k[q]);
     // J_l = Rd Jd (Rd = R, or I with Jd = I for the small-angle tables), wave-uniform,
@@ -1679,6 +1690,13 @@ __device__ __forceinline__ void eval_cams_gather(const int* __restrict__ cm_pt, 
 #pragma unroll
     for (int q = 0; q < 3; ++q) X[slot][q] = points[3 * (size_t)p + q];
   };
+  // the camera's parameters leave with the first indices (one round trip for both); its
+  // table is then built while the first points are gathered
+  double x6[6], k6[6];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)ext_i + q];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) k6[q] = intr[(size_t)kIntr * intr_i + q];
   if (n > 0) {
     // prologue: indices of steps 0 .. DI-1 ... in the order the loop body issues them
 #pragma unroll
@@ -1688,7 +1706,7 @@ __device__ __forceinline__ void eval_cams_gather(const int* __restrict__ cm_pt, 
 #pragma unroll
     for (int st = DG; st < DI; ++st) load_idx(st % R, st);
   }
-  const UniFrame f(ext, intr, ext_i, intr_i, jl);  // built while the first loads fly
+  const UniFrame f(UniFrame::FromValues{}, x6, k6, jl);  // built while the first gathers fly
   DAB_STAMP_ANY(1);
   for (int st0 = 0; st0 < n; st0 += R) {
 #pragma unroll
@@ -1954,6 +1972,10 @@ void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, con
 // uniform chunk per free camera, E, NI <= kLdsCams, NC <= (camera waves / 2) x grid.
 constexpr int kFusedPW = 8;               // point waves per work-group
 constexpr int kFusedCW = 16 - kFusedPW;   // camera waves (kFusedCW / 2 cameras per round)
+#ifndef DAB_CAM_SPLIT
+#define DAB_CAM_SPLIT 512
+#endif
+constexpr int kCamSplit = DAB_CAM_SPLIT;  // first part of a two-part camera chunk, in 1/1024
 // ST: the streamed form — camera waves read the camera-major point copy cmx (eval_cams_stream,
 // NS slots) and point waves the packed 4-B slot records v.obs_e (ext | intr << 16, a D-deep
 // queue at 5 VGPRs per row) instead of the 16-B obs_idx records.
@@ -1992,11 +2014,19 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
     // ------- camera side: wpc waves per camera (2 at C3; up to 8 for small camera sets),
     // each one contiguous part of the camera's uniform chunk -------
     if constexpr (ABL == 22) __builtin_amdgcn_s_setprio(2);
-    const int cw = wave - kFusedPW, slot = cw / wpc, part = cw - slot * wpc;
+    // parts are dealt across the slots (part = cw / slots): part 0 of every camera runs on
+    // the older hardware waves, which the issue arbiter serves first, so with two parts the
+    // first is the larger one (kCamSplit / 1024 of the chunk) and the younger waves, which
+    // start late beside the point waves, get the smaller rest
+    const int nsl = kFusedCW / wpc, cw = wave - kFusedPW, part = cw / nsl, slot = cw - part * nsl;
     const int c = slot * gridDim.x + blockIdx.x;  // one round (fused_eval_fits / fused_wpc)
     if (c >= v.NC || ABL == 1 || ABL == 15 || side == 1) return;
     const int b = chunk_beg[c], e = chunk_beg[c + 1];
-    const int lo = b + (int)(((long long)(e - b) * part) / wpc), hi = b + (int)(((long long)(e - b) * (part + 1)) / wpc);
+    auto cut = [&](int q) -> int {
+      if (wpc == 2 && q == 1) return b + (int)(((long long)(e - b) * kCamSplit) >> 10);
+      return b + (int)(((long long)(e - b) * q) / wpc);
+    };
+    const int lo = cut(part), hi = cut(part + 1);
     const int2 u = v.chunk_uni[c];
     double acc[27];
 #pragma unroll
@@ -2014,7 +2044,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
       eval_cams_uni_frame<NS>(v, lo + lane, hi, 64, points, u.x, u.y, ext, acc, cjl[cw]);
     }
     DAB_STAMP(2);
-    wave_sums_transposed<27>(acc, csum[cw]);
+    wave_sums_transposed<27>(acc, csum[slot * wpc + part]);
     unsigned old = 0;
     if (lane == 0) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -9,7 +9,7 @@ OUT=${OUT:-$HERE/trace}
 mkdir -p "$OUT"
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -DDAB_TRACE $EXTRA"
 pids=()
-for f in dab_kernels dab_chol dab_pcg dab_solver dab_p2p; do
+for f in dab_kernels dab_chol dab_pcg dab_solver dab_p2p dab_setup; do
   /opt/rocm/bin/hipcc $F -c "$SRC/$f.hip" -o "$OUT/$f.o" & pids+=($!)
 done
 for f in errors synth; do
