@@ -1973,7 +1973,7 @@ void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, con
 constexpr int kFusedPW = 8;               // point waves per work-group
 constexpr int kFusedCW = 16 - kFusedPW;   // camera waves (kFusedCW / 2 cameras per round)
 #ifndef DAB_CAM_SPLIT
-#define DAB_CAM_SPLIT 512
+#define DAB_CAM_SPLIT 688
 #endif
 constexpr int kCamSplit = DAB_CAM_SPLIT;  // first part of a two-part camera chunk, in 1/1024
 // ST: the streamed form — camera waves read the camera-major point copy cmx (eval_cams_stream,

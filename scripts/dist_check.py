@@ -127,7 +127,8 @@ def main():
                or (a.expect_p2p and v["p2p"] != 1)
                or (a.expect_no_p2p and v["p2p"] != 0)
                or v["solver_used"][0] != v["solver_used"][1]]
-        print("DIST_CHECK", "FAIL " + ",".join(bad) if bad else "OK")
+        sys.stdout.write("DIST_CHECK " + ("FAIL " + ",".join(bad) if bad else "OK") + "\n")  # one write
+        sys.stdout.flush()
     dist.destroy_process_group()
 
 

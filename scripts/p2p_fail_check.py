@@ -56,8 +56,11 @@ def main():
     dist.all_reduce(res, op=dist.ReduceOp.MIN)
     print(f"rank {rank}: {dt:.1f} s, error {err!r}, arrays unchanged "
           f"{np.array_equal(mine.points, p0) and np.array_equal(mine.ext, e0)}", flush=True)
+    dist.barrier()  # every rank's line is out before the verdict (torchrun merges the streams)
     if rank == 0:
-        print("P2P_FAIL_CHECK", "OK" if int(res.item()) == 1 else "FAIL", flush=True)
+        # one write: separate print arguments could interleave with the other rank's line
+        sys.stdout.write("P2P_FAIL_CHECK " + ("OK" if int(res.item()) == 1 else "FAIL") + "\n")
+        sys.stdout.flush()
     dist.destroy_process_group()
 
 
