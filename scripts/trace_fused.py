@@ -1,0 +1,66 @@
+"""Per-wave timeline of k_eval_fused from the timing build (scripts/trace_build.sh:
+s_memrealtime stamps, 100 MHz, at kernel entry / after staging / after the entry loop /
+at exit, per work-group and wave). Prints, relative to the earliest entry stamp, the
+distribution of each phase boundary over camera and point waves.
+
+usage: python scripts/trace_fused.py CONFIG [abl]   (DAB_FUSED_ABL: 0 fused, 1 point side, 2 camera side, ...)
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import _pkgload  # noqa: E402
+
+pkg = _pkgload.load()
+abi = sys.modules["deeparc_sfm_amd._abi"]
+lib = abi.load_library(os.environ.get("DAB_TRACE_LIB", os.path.join(ROOT, "scripts", "trace", "libdab.so")))
+abi._LIB = lib
+cfg = sys.argv[1]
+side = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+os.environ["DAB_FUSED_ABL"] = str(side)  # launch_eval_fused's ablation code (1 point side, 2 camera side)
+prob = pkg.synth(**pkg.CONFIGS[cfg])
+s = pkg.Solver(0)
+s.set_problem(prob)
+s.bench_eval_pass(True, 20)
+s.sync()
+s.bench_kernel_ms()
+s.bench_eval_pass(True, 50)
+s.sync()
+jk, _ = s.bench_kernel_ms()
+print(f"{cfg} abl={side} lib={os.path.basename(os.path.dirname(lib._name))}: kernel {jk * 1e3:.1f} us (50-pass average)")
+buf = np.zeros(256 * 16 * 4, dtype=np.uint64)
+runs = []
+for rep in range(5):
+    lib.dab_trace_clear()
+    s.bench_eval_pass(True, 1)
+    s.sync()
+    lib.dab_trace_fetch(buf.ctypes.data_as(C.POINTER(C.c_ulonglong)))
+    runs.append(buf.reshape(256, 16, 4).astype(np.int64).copy())
+s.close()
+for r, t in enumerate(runs):
+    have = t[:, :, 0] > 0
+    t0 = t[:, :, 0][have].min()
+    rel = np.where(t > 0, (t - t0) * 0.01, np.nan)  # us
+    print(f"{cfg} side={side} run {r}: work-groups with stamps {int(have.any(axis=1).sum())}")
+    for name, ws in (("point", slice(0, 8)), ("camera", slice(8, 16))):
+        x = rel[:, ws, :]
+        if np.isnan(x[:, :, 0]).all():
+            continue
+        q = lambda a: " ".join(f"{v:6.2f}" for v in np.nanpercentile(a, [0, 10, 50, 90, 100]))
+        print(f"  {name:6s} entry   {q(x[:, :, 0])}")
+        print(f"  {name:6s} staged  {q(x[:, :, 1])}")
+        print(f"  {name:6s} loopend {q(x[:, :, 2])}")
+        print(f"  {name:6s} exit    {q(x[:, :, 3])}")
+        print(f"  {name:6s} loop    {q(x[:, :, 2] - x[:, :, 1])}   (per wave, percentiles 0/10/50/90/100)")
+if os.environ.get("DAB_TRACE_PER_WAVE"):
+    t = runs[-1]
+    have = t[:, :, 0] > 0
+    t0 = t[:, :, 0][have].min()
+    rel = np.where(t > 0, (t - t0) * 0.01, np.nan)
+    print("per logical wave: median staged / loop end / exit (us)")
+    for w in range(16):
+        print(f"  wave {w:2d}: " + " ".join(f"{np.nanmedian(rel[:, w, k]):6.2f}" for k in (1, 2, 3)))
