@@ -410,6 +410,8 @@ def main():
                                   "to a stable point count; max_iteration 100",
             "c1_pipeline_gpu_s": tg, "c1_pipeline_cpu_s": tc, "c1_pipeline_speedup": tc / tg if tg > 0 else None,
             "c1_pipeline_gpu_solve_s": grep_["solve_seconds"], "c1_pipeline_gpu_filter_s": grep_["filter_seconds"],
+            # host-timed stages of the GPU pipeline, summed over the loop (dam_pipeline_report)
+            "c1_pipeline_gpu_breakdown_s": grep_["breakdown"],
             "c1_pipeline_rounds": [grep_["rounds"], crep["rounds"]],
             "c1_pipeline_solves": [grep_["solves"], crep["solves"]],
             "c1_pipeline_lm_iterations": [grep_["lm_iterations"], crep["lm_iterations"]],

@@ -195,7 +195,9 @@ class Solver:
             self._cb = _abi.HostAllreduceFn(_cb)
             check(self.lib.dab_create_dist_host(device, rank, world_size, self._cb, None, C.byref(h)),
                   self.lib)
-        elif world_size > 1:
+        elif world_size > 1 or unique_id is not None:
+            # world_size 1 with a unique id: a one-rank RCCL communicator, every collective
+            # executed (the multi-GPU transport rehearsed on one GPU)
             buf = (C.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
             check(self.lib.dab_create_dist(device, rank, world_size, buf, C.byref(h)), self.lib)
         else:

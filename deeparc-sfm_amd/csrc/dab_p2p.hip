@@ -185,11 +185,14 @@ static void shared_release(P2pShared* sh) {
   delete sh;
 }
 
-// a free slot of this device's arena (allocated and exported on first use), zeroed: the
-// previous group on the slot has finished with it (its last call completed on every rank
-// before any rank could join this group's collective handle exchange)
+// a free slot of this device's arena (allocated and exported on first use), NOT yet zeroed:
+// a peer's last call of the slot's previous group may still be reading it over its mapping.
+// The device is drained first, so this rank's own calls of earlier groups are complete
+// before it joins the new group's exchange; p2p_create_group zeroes the slot only after
+// that exchange (every member drained), then meets the members once more before any call.
 static std::string arena_take(int device, size_t bytes, int* slot, char** base, unsigned long long* soff,
                               unsigned char* rec) {
+  if (hipDeviceSynchronize() != hipSuccess) return "p2p: device synchronisation failed";
   std::lock_guard<std::mutex> lk(g_p2p_mu);
   Arena& a = g_arena[device];
   if (!a.alloc) {
@@ -213,12 +216,9 @@ static std::string arena_take(int device, size_t bytes, int* slot, char** base, 
   int k = 0;
   while (k < kArenaSlots && a.used[k]) ++k;
   if (k == kArenaSlots) return "p2p: every arena slot is in use";
-  char* b = static_cast<char*>(a.alloc) + (size_t)k * a.slot_bytes;
-  if (hipMemset(b, 0, a.slot_bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
-    return "p2p: arena slot initialisation failed";
   a.used[k] = true;
   *slot = k;
-  *base = b;
+  *base = static_cast<char*>(a.alloc) + (size_t)k * a.slot_bytes;
   *soff = (unsigned long long)k * a.slot_bytes;
   std::memcpy(rec, a.rec, kP2pHandleBytes);
   return "";
@@ -268,8 +268,22 @@ int p2p_create_group(int rank, int world, size_t cap_words, int nctx, const P2pA
     shared_release(sh);
     return set_error(DAB_E_COMM, "p2p: handle exchange failed");
   }
-  for (int r = 0; r < world && err.empty(); ++r)
+  // Every member drained its device before the exchange, so no call of an earlier group
+  // still reads this rank's slot: zero it now (stale flags and data), then meet once more
+  // (a second exchange of one status byte each) so that no member publishes into the slot
+  // before it is clear. Both exchanges run on every rank, whatever failed locally.
+  if (err.empty() && (hipMemset(mine, 0, region * nctx * 8) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
+    err = "p2p: arena slot initialisation failed";
+  std::vector<unsigned char> ok((size_t)world * kP2pHandleBytes, 0);
+  ok[(size_t)rank * kP2pHandleBytes] = err.empty() ? 1 : 0;
+  if (allgather(ok.data()) != 0) {
+    shared_release(sh);
+    return set_error(DAB_E_COMM, "p2p: handle exchange failed");
+  }
+  for (int r = 0; r < world && err.empty(); ++r) {
     if (all[(size_t)r * kP2pHandleBytes + sizeof(hipIpcMemHandle_t) + 16] != 1) err = "p2p: a peer could not export its region";
+    else if (ok[(size_t)r * kP2pHandleBytes] != 1) err = "p2p: a peer could not initialise its region";
+  }
   if (!err.empty()) {
     shared_release(sh);
     return set_error(DAB_E_DEVICE, err);

@@ -1,8 +1,12 @@
 // DabScene.cc — DeepArcManager <-> dab_problem marshalling (see DabScene.hh).
 #include "DabScene.hh"
 
+#include <chrono>
 #include <cstdlib>
-#include <unordered_map>
+
+double dab_now_seconds() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 void dab_check(int rc) {
   if (rc != 0) throw dab_last_error();
@@ -21,16 +25,17 @@ void DabScene::build(DeepArcManager& m, bool freeze_camera) {
   std::vector<Point3d*>& pts = *m.point3ds();
   std::vector<Extrinsic*>& exts = *m.extrinsics();
   std::vector<Intrinsic*>& ks = *m.intrinsics();
-  std::unordered_map<Point3d*, int> pid;
-  std::unordered_map<Extrinsic*, int> eid;
-  std::unordered_map<Intrinsic*, int> kid;
-  for (size_t i = 0; i < pts.size(); ++i) pid[pts[i]] = (int)i;
-  for (size_t i = 0; i < exts.size(); ++i) eid[exts[i]] = (int)i;
-  for (size_t i = 0; i < ks.size(); ++i) kid[ks[i]] = (int)i;
-  auto find = [](auto& map, auto* key) {
-    auto it = map.find(key);
-    if (it == map.end()) throw "Parameter block references a parameter outside the manager";
-    return it->second;
+  // index of every parameter in the manager's lists, kept on the objects themselves (one
+  // store each, no hashing); a block whose parameter is not at its recorded index in this
+  // manager references a foreign parameter
+  for (size_t i = 0; i < pts.size(); ++i) pts[i]->slot((int)i);
+  for (size_t i = 0; i < exts.size(); ++i) exts[i]->slot((int)i);
+  for (size_t i = 0; i < ks.size(); ++i) ks[i]->slot((int)i);
+  auto find = [](auto& list, auto* key) {
+    const int i = key ? key->slot() : -1;
+    if (i < 0 || (size_t)i >= list.size() || list[i] != key)
+      throw "Parameter block references a parameter outside the manager";
+    return i;
   };
   const size_t N = blocks.size();
   xy.resize(2 * N);
@@ -43,11 +48,11 @@ void DabScene::build(DeepArcManager& m, bool freeze_camera) {
     ParameterBlock* b = blocks[o];
     xy[2 * o] = b->point2d()->x();
     xy[2 * o + 1] = b->point2d()->y();
-    obs_point[o] = find(pid, b->point3d());
-    obs_intr[o] = find(kid, b->intrinsic());
-    obs_ext0[o] = find(eid, b->first_extrinsic());
+    obs_point[o] = find(pts, b->point3d());
+    obs_intr[o] = find(ks, b->intrinsic());
+    obs_ext0[o] = find(exts, b->first_extrinsic());
     Extrinsic* e1 = b->second_extrinsic();
-    obs_ext1[o] = e1 ? find(eid, e1) : -1;
+    obs_ext1[o] = e1 ? find(exts, e1) : -1;
     // gauge: the extrinsic of a (0,0) block is constant (sfm.cc:50-53)
     if (b->pos_arc() == 0 && b->pos_ring() == 0) ext_const[obs_ext0[o]] = 1;
   }
@@ -110,14 +115,21 @@ int DabSession::ensure(DeepArcManager& m, int want_freeze) {
   const bool same = resident && version == m.structureVersion() && n_blocks == m.parameters()->size() &&
                     n_points == m.point3ds()->size() && n_ext == m.extrinsics()->size() &&
                     n_intr == m.intrinsics()->size() && (want_freeze < 0 || (want_freeze != 0) == freeze);
+  double t0 = dab_now_seconds();
   if (same) {  // structure resident: the values may have changed on the host
     scene.refresh_values(m);
-    return dab_update_parameters(handle.h, scene.points.data(), scene.ext.data());
+    const int rc = dab_update_parameters(handle.h, scene.points.data(), scene.ext.data());
+    if (rc) resident = false;  // the handle's state is unknown: the next call re-sets the problem
+    t.update += dab_now_seconds() - t0;
+    return rc;
   }
   resident = false;
   freeze = want_freeze > 0;
   scene.build(m, freeze);  // throws const char* on a block that references a foreign parameter
+  const double t1 = dab_now_seconds();
+  t.marshal += t1 - t0;
   const int rc = dab_set_problem(handle.h, &scene.problem);
+  t.setup += dab_now_seconds() - t1;
   if (rc) return rc;
   resident = true;
   version = m.structureVersion();

@@ -37,7 +37,19 @@ struct DabHandle {
 // on it is valid while (version, freeze, sizes) match the manager (DeepArcManager::
 // dabSession). ensure() re-marshals and re-sets the problem when they do not, and only
 // uploads the parameter values when they do.
+// Host-side time of each stage of the sfm.cc loop on this manager, accumulated (seconds):
+// marshal = DabScene::build (pointer walk into the SoA arrays), setup = dab_set_problem,
+// update = values-only refresh, prep = a solve's table build / graph capture (dab_solve
+// wall minus its summary's total time), lm = the LM iterations (summary total time),
+// writeback = values back into the manager, filter_dev = dab_filter, filter_host = the
+// manager's compaction of blocks and points.
+struct DabTimers {
+  double marshal = 0, setup = 0, update = 0, prep = 0, lm = 0, writeback = 0, filter_dev = 0, filter_host = 0;
+};
+double dab_now_seconds();
+
 struct DabSession {
+  DabTimers t;
   DabHandle handle;
   DabScene scene;
   bool resident = false;

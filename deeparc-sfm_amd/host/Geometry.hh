@@ -5,6 +5,7 @@
 #pragma once
 #include <algorithm>
 #include <set>
+#include <vector>
 
 class ParameterBlock;
 
@@ -33,17 +34,32 @@ class Point3d {
   double* position() { return position_; }
   void require_remove(bool v) { require_remove_ = v; }
   bool require_remove() { return require_remove_; }
-  // observation links (ParameterBlock::point3d keeps them current)
-  void link(ParameterBlock* b) { blocks_.insert(b); }
-  void unlink(ParameterBlock* b) { blocks_.erase(b); }
-  std::set<ParameterBlock*> total_link() { return blocks_; }
+  // observation links (ParameterBlock::point3d keeps them current). Held as a small
+  // vector (a point has a handful of observations; the set's node allocations were most
+  // of the reader's time on 160k observations); total_link() still returns the
+  // reference's std::set.
+  void link(ParameterBlock* b) {
+    if (std::find(blocks_.begin(), blocks_.end(), b) == blocks_.end()) blocks_.push_back(b);
+  }
+  void unlink(ParameterBlock* b) {
+    auto it = std::find(blocks_.begin(), blocks_.end(), b);
+    if (it != blocks_.end()) {
+      *it = blocks_.back();
+      blocks_.pop_back();
+    }
+  }
+  std::set<ParameterBlock*> total_link() { return std::set<ParameterBlock*>(blocks_.begin(), blocks_.end()); }
   bool empty() { return blocks_.empty(); }
+  // the solver adapter's scratch: this point's index in the manager's list (DabScene::build)
+  int slot() { return slot_; }
+  void slot(int v) { slot_ = v; }
 
  private:
+  int slot_ = -1;
   bool require_remove_;
   int r_, g_, b_, id_;
   double position_[3];
-  std::set<ParameterBlock*> blocks_;
+  std::vector<ParameterBlock*> blocks_;
 };
 
 // Camera/Intrinsic.hh. center() takes ints: the principal point is truncated on load
@@ -69,8 +85,11 @@ class Intrinsic {
     center_[0] = cx;
     center_[1] = cy;
   }
+  int slot() { return slot_; }  // adapter scratch (DabScene::build)
+  void slot(int v) { slot_ = v; }
 
  private:
+  int slot_ = -1;
   double focal_[2] = {0, 0}, center_[2] = {0, 0}, distortion_[2] = {0, 0};
   int focal_size_ = 0, distortion_size_ = 0, id_ = -1;
 };
@@ -90,8 +109,11 @@ class Extrinsic {
   }
   // R(w) column-major (ceres::AngleAxisToRotationMatrix, Extrinsic.hh:12-17)
   void rotationMatrix(double R[9]);
+  int slot() { return slot_; }  // adapter scratch (DabScene::build)
+  void slot(int v) { slot_ = v; }
 
  private:
+  int slot_ = -1;
   double rotation_[3] = {0, 0, 0}, translation_[3] = {0, 0, 0};
   int id_ = -1;
 };

@@ -190,6 +190,17 @@ int dam_run_pipeline_report(const char* input, const char* output, const char* p
       out->solve_seconds = r.solve_seconds;
       out->filter_seconds = r.filter_seconds;
       out->total_seconds = r.total_seconds;
+      out->read_seconds = r.read_seconds;
+      out->fit_seconds = r.fit_seconds;
+      out->write_seconds = r.write_seconds;
+      out->marshal_seconds = r.marshal_seconds;
+      out->setup_seconds = r.setup_seconds;
+      out->update_seconds = r.update_seconds;
+      out->prep_seconds = r.prep_seconds;
+      out->lm_seconds = r.lm_seconds;
+      out->writeback_seconds = r.writeback_seconds;
+      out->filter_device_seconds = r.filter_device_seconds;
+      out->filter_host_seconds = r.filter_host_seconds;
     }
   });
 }

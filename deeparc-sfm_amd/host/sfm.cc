@@ -20,6 +20,7 @@ int solveWith(DeepArcManager& m, const dab_options& options, bool freeze_camera,
   DabScene& scene = S.scene;
   dab_summary local{};
   dab_summary* s = summary ? summary : &local;
+  const double t0 = dab_now_seconds();
   rc = dab_solve(dh.h, &options, s);
   if (rc == DAB_E_UNSUPPORTED && options.linear_solver_type == DAB_LINEAR_SOLVER_EXPLICIT_SCHUR) {
     // The explicit reduced system is refused only when it is both too large for the LDS
@@ -36,7 +37,11 @@ int solveWith(DeepArcManager& m, const dab_options& options, bool freeze_camera,
     S.resident = false;  // a failed solve leaves the device state unspecified
     return rc;
   }
+  const double t1 = dab_now_seconds();
+  S.t.lm += s->total_time_in_seconds;
+  S.t.prep += (t1 - t0) - s->total_time_in_seconds;
   scene.write_back(m);  // dab_solve wrote the optimised values into scene.points / ext
+  S.t.writeback += dab_now_seconds() - t1;
   return 0;
 }
 
@@ -58,9 +63,7 @@ dab_summary solve_opts(DeepArcManager& m, int max_iteration, int max_second, boo
                 s.initial_cost, s.final_cost, s.num_iterations, s.num_successful_steps, s.message);
   return s;
 }
-double now_seconds() {
-  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
+double now_seconds() { return dab_now_seconds(); }
 }  // namespace
 
 void solve(DeepArcManager& deeparcManager, int max_iteration, int max_second, bool freeze_camera) {
@@ -229,9 +232,14 @@ PipelineReport runPipeline(const std::string& input, const std::string& output, 
   DeepArcManager m;
   m.read(input);
   PipelineReport rep{};
+  const double t_read = now_seconds();
+  rep.read_seconds = t_read - t_start;
   double center[3] = {0, 0, 0}, radius = 1.0;  // sfm.cc:87-88
   fitHemisphere(m.getCameraCenter(), center, &radius);
+  rep.fit_seconds = now_seconds() - t_read;
+  double t_w = now_seconds();
   if (!ply_prefix.empty()) m.writePly(ply_prefix + "init.ply");
+  rep.write_seconds += now_seconds() - t_w;
   // the manager keeps one libdab handle: each filter runs on the problem its solve left
   // resident, and each solve after a filter re-sets the compacted problem on that handle
   auto do_solve = [&](bool freeze) {
@@ -250,7 +258,9 @@ PipelineReport runPipeline(const std::string& input, const std::string& output, 
   do_solve(true);  // sfm.cc:111: points only
   do_filter();
   int step = 0;
+  t_w = now_seconds();
   if (!ply_prefix.empty()) m.writePly(ply_prefix + std::to_string(step) + ".ply");
+  rep.write_seconds += now_seconds() - t_w;
   int old_points = 1, cur_points = 10000000;  // sfm.cc:106
   while (cur_points != old_points) {
     ++step;
@@ -258,10 +268,23 @@ PipelineReport runPipeline(const std::string& input, const std::string& output, 
     do_solve(false);
     do_filter();
     cur_points = (int)m.point3ds()->size();
+    t_w = now_seconds();
     if (!ply_prefix.empty()) m.writePly(ply_prefix + std::to_string(step) + ".ply");
+    rep.write_seconds += now_seconds() - t_w;
   }
+  t_w = now_seconds();
   if (!ply_prefix.empty()) m.writePly(ply_prefix + "clear.ply");
   if (!output.empty()) m.write(output);
+  rep.write_seconds += now_seconds() - t_w;
+  const DabTimers& T = m.dabSession().t;
+  rep.marshal_seconds = T.marshal;
+  rep.setup_seconds = T.setup;
+  rep.update_seconds = T.update;
+  rep.prep_seconds = T.prep;
+  rep.lm_seconds = T.lm;
+  rep.writeback_seconds = T.writeback;
+  rep.filter_device_seconds = T.filter_dev;
+  rep.filter_host_seconds = T.filter_host;
   for (int k = 0; k < 3; ++k) rep.hemisphere_center[k] = center[k];
   rep.hemisphere_radius = radius;
   rep.rounds = step;

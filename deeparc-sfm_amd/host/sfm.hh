@@ -32,6 +32,11 @@ struct PipelineReport {
   int solves = 0, lm_iterations = 0;  // solve() calls, LM iterations summed over them
   double final_cost = 0.0;            // the last solve's final cost
   double solve_seconds = 0.0, filter_seconds = 0.0, total_seconds = 0.0;
+  // breakdown (seconds, summed over the loop): read the .deeparc, hemisphere fit, PLY and
+  // output writes, and the DabTimers stages (DabScene.hh)
+  double read_seconds = 0.0, fit_seconds = 0.0, write_seconds = 0.0, marshal_seconds = 0.0, setup_seconds = 0.0,
+         update_seconds = 0.0, prep_seconds = 0.0, lm_seconds = 0.0, writeback_seconds = 0.0,
+         filter_device_seconds = 0.0, filter_host_seconds = 0.0;
 };
 // sfm.cc main() without the hard-coded paths: reads `input`, writes the outputs whose
 // names are non-empty (PLY snapshots are skipped when ply_prefix is empty). verbose: the

@@ -18,12 +18,17 @@ HOST_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdee
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int32)
 
+# dam_pipeline_report's breakdown fields, in order
+PIPELINE_STAGES = ("read", "fit", "write", "marshal", "setup", "update", "prep", "lm", "writeback", "filter_device",
+                   "filter_host")
+
+
 class PipelineReport(C.Structure):  # dam_pipeline_report
     _fields_ = [("hemisphere_center", C.c_double * 3), ("hemisphere_radius", C.c_double),
                 ("rounds", C.c_int32), ("final_blocks", C.c_int32), ("final_points", C.c_int32),
                 ("solves", C.c_int32), ("lm_iterations", C.c_int32), ("reserved", C.c_int32),
                 ("final_cost", C.c_double), ("solve_seconds", C.c_double), ("filter_seconds", C.c_double),
-                ("total_seconds", C.c_double)]
+                ("total_seconds", C.c_double)] + [(k + "_seconds", C.c_double) for k in PIPELINE_STAGES]
 
 
 SIGNATURES = {
@@ -184,4 +189,5 @@ def run_pipeline_report(input_path, output_path="", ply_prefix="", max_iteration
     return dict(hemisphere_center=np.array(r.hemisphere_center[:]), hemisphere_radius=r.hemisphere_radius,
                 rounds=r.rounds, blocks=r.final_blocks, points=r.final_points, solves=r.solves,
                 lm_iterations=r.lm_iterations, final_cost=r.final_cost, solve_seconds=r.solve_seconds,
-                filter_seconds=r.filter_seconds, total_seconds=r.total_seconds)
+                filter_seconds=r.filter_seconds, total_seconds=r.total_seconds,
+                breakdown={k: getattr(r, k + "_seconds") for k in PIPELINE_STAGES})

@@ -183,10 +183,18 @@ int dab_abi_version(void);
 const char* dab_last_error(void);
 void dab_options_init(dab_options* opt);
 
-/* device: HIP ordinal. Single-process handle (world_size 1). */
+/* device: HIP ordinal. Single-process handle (world_size 1).
+   Side effect, process-wide: every dab_create* sets hipSetDeviceFlags(hipDeviceScheduleSpin)
+   (the LM loop's host round trips are latency-critical), so every host wait of the
+   embedding process spins instead of blocking. DAB_SCHEDULE_BLOCKING=1 in the environment
+   keeps the runtime's default; a refused flag is reported once on stderr. */
 int dab_create(int device, dab_handle** out);
 /* Multi-GPU (one process per GPU, RCCL over xGMI). `unique_id` is the 128-byte
- * ncclUniqueId produced on rank 0 by dab_comm_unique_id and broadcast by the caller. */
+ * ncclUniqueId produced on rank 0 by dab_comm_unique_id and broadcast by the caller.
+ * world_size 1 with a non-null unique_id builds a one-rank RCCL communicator and runs
+ * every collective of the multi-rank path through it (the split evaluation schedule with
+ * its camera all-reduce on the communication stream included): the same results as
+ * dab_create, with the multi-GPU transport executed on one GPU. */
 int dab_comm_unique_id(uint8_t out_id[128]);
 int dab_create_dist(int device, int rank, int world_size, const uint8_t unique_id[128],
                     dab_handle** out);

@@ -66,6 +66,12 @@ typedef struct dam_pipeline_report {
   int32_t lm_iterations, reserved;  /* LM iterations summed over the solves */
   double final_cost;                /* the last solve's final cost */
   double solve_seconds, filter_seconds, total_seconds;
+  /* breakdown, seconds summed over the loop: .deeparc read, hemisphere fit, PLY/output
+   * writes; per libdab handle stage: marshal (manager -> SoA arrays), setup
+   * (dab_set_problem), update (values-only refresh), prep (a solve's table build and graph
+   * capture), lm (the LM iterations), writeback, filter device pass, filter host compaction */
+  double read_seconds, fit_seconds, write_seconds, marshal_seconds, setup_seconds, update_seconds, prep_seconds,
+      lm_seconds, writeback_seconds, filter_device_seconds, filter_host_seconds;
 } dam_pipeline_report;
 int dam_run_pipeline_report(const char* input, const char* output, const char* ply_prefix, int32_t max_iteration,
                             int32_t max_second, double error_boundary, int32_t quiet, dam_pipeline_report* out);

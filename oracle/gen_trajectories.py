@@ -25,20 +25,25 @@ import _pkgload  # noqa: E402
 import oracle  # noqa: E402
 
 OUT = os.path.join(ROOT, "tests", "golden", "trajectories.json")
-# final parameters of every record: extrinsics in full, points in full or every k-th point
-# (POINT_STRIDE; the fixture stays a few MB), float64, in tests/golden/trajectory_params.npz
+# final parameters of every record, in tests/golden/trajectory_params.npz: extrinsics in full
+# (float64); points in full, as float64 (`_points`) or — the 1M-point rig records — as the
+# float32 change from the generated initial points (`_dpoints32`: the change is < 0.1, so
+# float32 keeps it to ~1e-9, far inside the 1e-7 / 1e-6 tolerances, at half the size)
 PARAMS = os.path.join(ROOT, "tests", "golden", "trajectory_params.npz")
-POINT_STRIDE = {"c2_explicit": 1, "c2_pcg": 1, "c3_explicit": 1, "c3_pcg": 8, "c5_explicit": 64, "c5_pcg": 64}
+DELTA32 = {"c5_explicit", "c5_pcg"}
 
-# (record name, config, linear solver, LM iterations). Tolerances are zeroed so that every
-# iteration runs, as in bench.py.
+# (record name, config, linear solver, LM iterations, converge). Tolerances are zeroed so that
+# every iteration runs, as in bench.py — except for the `converge` records, which keep Ceres'
+# default tolerances and end by CONVERGENCE (function tolerance) at full size.
 CASES = [
-    ("c2_explicit", "c2_100cam", "explicit", 4),
-    ("c2_pcg", "c2_100cam", "pcg", 4),
-    ("c3_explicit", "c3_1kcam", "explicit", 5),
-    ("c3_pcg", "c3_1kcam", "pcg", 5),
-    ("c5_explicit", "c5_rig_16x64", "explicit", 2),
-    ("c5_pcg", "c5_rig_16x64", "pcg", 2),
+    ("c2_explicit", "c2_100cam", "explicit", 4, False),
+    ("c2_pcg", "c2_100cam", "pcg", 4, False),
+    ("c3_explicit", "c3_1kcam", "explicit", 5, False),
+    ("c3_pcg", "c3_1kcam", "pcg", 5, False),
+    ("c5_explicit", "c5_rig_16x64", "explicit", 5, False),
+    ("c5_pcg", "c5_rig_16x64", "pcg", 5, False),
+    ("c2_converge", "c2_100cam", "explicit", 100, True),
+    ("c3_converge", "c3_1kcam", "explicit", 100, True),
 ]
 
 
@@ -52,11 +57,24 @@ def problem_digest(prob):
     return h.hexdigest()
 
 
-def case_options(pkg, solver, iters, threads=8):
+def case_options(pkg, solver, iters, threads=8, converge=False):
     lst = (pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR if solver == "explicit"
            else pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)
+    if converge:  # Ceres' default tolerances
+        return pkg.options(max_num_iterations=iters, linear_solver_type=lst, num_threads=threads)
     return pkg.options(max_num_iterations=iters, function_tolerance=0.0, gradient_tolerance=0.0,
                        parameter_tolerance=0.0, linear_solver_type=lst, num_threads=threads)
+
+
+def record_options(pkg, rec, threads=8):
+    return case_options(pkg, rec["solver"], rec["max_num_iterations"], threads, rec.get("converge", False))
+
+
+def reference_points(params, name, initial_points):
+    """The oracle's final points of record `name` (every point), float64."""
+    if name + "_dpoints32" in params:
+        return initial_points + params[name + "_dpoints32"].astype(np.float64)
+    return params[name + "_points"]
 
 
 def sample_rows(a, n):
@@ -77,19 +95,20 @@ def gauge_normalised(points, ext):
 
 def main(names):
     pkg = _pkgload.load()
-    threads = min(16, os.cpu_count() or 1)
+    threads = int(os.environ.get("ORACLE_THREADS", min(16, os.cpu_count() or 1)))
     out = json.load(open(OUT)) if os.path.exists(OUT) else {}
     params = dict(np.load(PARAMS)) if os.path.exists(PARAMS) else {}
     probs = {}
-    for name, cfg, solver, iters in CASES:
+    for name, cfg, solver, iters, converge in CASES:
         if names and name not in names:
             continue
         if cfg not in probs:
             probs = {cfg: pkg.synth(**pkg.CONFIGS[cfg])}
         prob = probs[cfg].copy()
         digest = problem_digest(prob)
+        p_init = prob.points.copy()
         t = time.perf_counter()
-        o = oracle.solve(pkg, prob, case_options(pkg, solver, iters, threads))
+        o = oracle.solve(pkg, prob, case_options(pkg, solver, iters, threads, converge))
         wall = time.perf_counter() - t
         out[name] = dict(
             config=cfg, solver=solver, max_num_iterations=iters, digest=digest, num_obs=prob.num_obs,
@@ -101,8 +120,13 @@ def main(names):
             gradient_max_norms=[it["gradient_max_norm"] for it in o["iterations"]],
             step_norms=[it["step_norm"] for it in o["iterations"]],
             trust_region_radii=[it["trust_region_radius"] for it in o["iterations"]],
-            point_stride=POINT_STRIDE[name], oracle_wall_s=wall, oracle_threads=threads)
-        params[name + "_points"] = np.ascontiguousarray(prob.points[:: POINT_STRIDE[name]])
+            converge=converge, oracle_wall_s=wall, oracle_threads=threads)
+        for k in (name + "_points", name + "_dpoints32"):
+            params.pop(k, None)
+        if name in DELTA32:
+            params[name + "_dpoints32"] = np.ascontiguousarray((prob.points - p_init).astype(np.float32))
+        else:
+            params[name + "_points"] = np.ascontiguousarray(prob.points)
         params[name + "_ext"] = np.ascontiguousarray(prob.ext)
         print(f"{name}: {o['num_iterations']} its, costs {out[name]['costs']}, "
               f"cg {out[name]['linear_iterations']}, {wall:.1f} s", flush=True)

@@ -119,3 +119,57 @@ def test_p2p_selftest_failure_falls_back(gpu):
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     assert "DIST_CHECK OK" in p.stdout, p.stdout[-3000:]
+
+
+def test_eight_ranks_p2p_handles_live_together(gpu):
+    """BASELINE config 4's widest partition on the one-GPU rehearsal: eight processes (the
+    driver's 8-GPU node runs bench.py with eight ranks and kP2pMaxRanks = 8), small BAL and
+    rig problems, every solver type's sharded handle alive at once per process (bench.py
+    holds two), each with its own peer-to-peer group in the per-process arena. Every group
+    must pass its set-up self-test and every trajectory match the single handle. Unmeasured
+    on hardware: eight processes share one device here."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, DAB_P2P="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "scripts", "dist_check.py"), "--device", "0", "--host-collective", "--expect-p2p",
+           "--iters", "6", "--live-together"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "DIST_CHECK OK" in p.stdout, p.stdout[-3000:]
+    assert "not verified" not in p.stderr, p.stderr[-3000:]
+
+
+@pytest.mark.parametrize("cfg,solvers", [("c3_1kcam", ("explicit", "pcg")), ("c5_rig_16x64", ("pcg",))])
+def test_rccl_one_rank_bitwise_equals_single_handle(pkg, gpu, cfg, solvers):
+    """The RCCL transport executed on one GPU: dab_create_dist with world_size 1 and a
+    unique id builds a real one-rank RCCL communicator, and every collective of the
+    multi-rank path runs through ncclAllReduce instead of returning early — the camera
+    blocks on the communication stream beside the point side (the split evaluation
+    schedule), the Schur blocks / PCG vectors, the fixed-point cost words, the flags and the
+    solver-time max. A one-rank sum is the identity, so the LM trajectories must be
+    bitwise those of dab_create (unmeasured on hardware across GPUs: that needs the 8-GPU
+    node)."""
+    import gen_trajectories as gt
+    base = pkg.synth(**pkg.CONFIGS[cfg])
+    for solver in solvers:
+        opts = gt.case_options(pkg, solver, 3 if cfg == "c3_1kcam" else 2)
+        res = []
+        for uid in (None, pkg.Solver.unique_id()):
+            prob = base.copy()
+            s = pkg.Solver(0, 0, 1, uid)
+            try:
+                s.set_problem(prob)
+                if uid is not None:
+                    assert s.eval_fused() != 1  # not the single fused launch: the split schedule (or two kernels)
+                g = s.solve(opts)
+            finally:
+                s.close()
+            res.append((g, prob))
+        (g0, p0), (g1, p1) = res
+        assert [it["cost"] for it in g1["iterations"]] == [it["cost"] for it in g0["iterations"]], (cfg, solver)
+        assert [it["linear_solver_iterations"] for it in g1["iterations"]] == \
+            [it["linear_solver_iterations"] for it in g0["iterations"]]
+        assert (p1.points == p0.points).all() and (p1.ext == p0.ext).all(), (cfg, solver)

@@ -12,7 +12,9 @@
   (exact) / 1e-6 (PCG) plus 1e-13 / 1e-12 of the initial gradient (the cancellation floor
   near convergence); final parameters, gauge-normalised (the free scale removed:
   gen_trajectories.gauge_normalised), 1e-7 absolute (exact) / 1e-6 (PCG) on every extrinsic
-  and on every point (C2, C3 exact), every 8th (C3 PCG) or every 64th (C5) point.
+  and on every point. The C5 records run the 5 LM iterations bench.py times; c2_converge and
+  c3_converge keep Ceres' default tolerances and end by CONVERGENCE, so the function-
+  tolerance test is pinned at full size.
 * C4 shape: the C3 global problem point-sharded over two ranks (collectives staged through
   gloo, both ranks on this GPU) against the single-handle solve.
 * Near Ceres' first-order rotation branch: the analytic HIP Jacobian against the oracle's
@@ -57,10 +59,11 @@ def test_full_size_trajectory_matches_oracle(pkg, gpu, name):
     rec = TRAJ[name]
     prob = _problem(pkg, rec["config"])
     assert gt.problem_digest(prob) == rec["digest"], "the generator no longer gives the recorded problem"
+    p_init = prob.points.copy()
     s = pkg.Solver(0)
     try:
         s.set_problem(prob)
-        g = s.solve(gt.case_options(pkg, rec["solver"], rec["max_num_iterations"]))
+        g = s.solve(gt.record_options(pkg, rec))
     finally:
         s.close()
     exact = rec["solver"] == "explicit"
@@ -84,10 +87,11 @@ def test_full_size_trajectory_matches_oracle(pkg, gpu, name):
     gn0 = rec["gradient_max_norms"][0]
     for a, b in zip([it["gradient_max_norm"] for it in g["iterations"]][:n_dec], rec["gradient_max_norms"][:n_dec]):
         assert abs(a - b) <= gtol * abs(b) + g0 * gn0, (name, "gradient max norm", a, b)
-    # every extrinsic and the recorded points (stride), with the free scale removed
-    k = rec["point_stride"]
-    gp, ge, gs = gt.gauge_normalised(prob.points[::k], prob.ext)
-    op, oe, osig = gt.gauge_normalised(PARAMS[name + "_points"], PARAMS[name + "_ext"])
+    if rec.get("converge"):
+        assert g["termination"] == "CONVERGENCE"
+    # every extrinsic and every point, with the free scale removed
+    gp, ge, gs = gt.gauge_normalised(prob.points, prob.ext)
+    op, oe, osig = gt.gauge_normalised(gt.reference_points(PARAMS, name, p_init), PARAMS[name + "_ext"])
     assert abs(gs - osig) <= 1e-6 * osig, (name, "scale", gs, osig)
     ptol = 1e-7 if exact else 1e-6
     np.testing.assert_allclose(gp, op, rtol=0, atol=ptol)
@@ -102,8 +106,9 @@ def test_c5_mixed_precision_pcg_matches_oracle(pkg, gpu):
     rec = TRAJ["c5_pcg"]
     prob = _problem(pkg, rec["config"])
     assert gt.problem_digest(prob) == rec["digest"]
-    opts = gt.case_options(pkg, "pcg", rec["max_num_iterations"])
+    opts = gt.record_options(pkg, rec)
     opts.pcg_fp32 = 1
+    p_init = prob.points.copy()
     s = pkg.Solver(0)
     try:
         s.set_problem(prob)
@@ -115,9 +120,8 @@ def test_c5_mixed_precision_pcg_matches_oracle(pkg, gpu):
     assert [it["linear_solver_iterations"] for it in g["iterations"]] == rec["linear_iterations"]
     for a, b in zip([it["cost"] for it in g["iterations"]], rec["costs"]):
         assert abs(a - b) <= 1e-7 * abs(b), (a, b)
-    k = rec["point_stride"]
-    gp, ge, _ = gt.gauge_normalised(prob.points[::k], prob.ext)
-    op, oe, _ = gt.gauge_normalised(PARAMS["c5_pcg_points"], PARAMS["c5_pcg_ext"])
+    gp, ge, _ = gt.gauge_normalised(prob.points, prob.ext)
+    op, oe, _ = gt.gauge_normalised(gt.reference_points(PARAMS, "c5_pcg", p_init), PARAMS["c5_pcg_ext"])
     np.testing.assert_allclose(gp, op, rtol=0, atol=1e-5)
     np.testing.assert_allclose(ge, oe, rtol=0, atol=1e-5)
 
