@@ -128,7 +128,7 @@ bool fused_eval_fits(const DevView& v, int nchunk, int ngen, int ncross, int gri
 void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
                        double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
                        int grid, int side, const double* cmx = nullptr, int variant = 0,
-                       const double* camtab = nullptr);
+                       const double* camtab = nullptr, int gv = 0);
 void launch_cmx_gather(hipStream_t s, const DevView& v, const double* points, double* cmx);
 //  arc∘ring cross blocks Jc0^T Jc1 over composed observations (pair-major copy) -> partial[chunk][36]
 void launch_eval_cross(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,

@@ -1673,10 +1673,15 @@ __device__ __forceinline__ void eval_cams_stream(const double* __restrict__ cmx,
 // each hop. Every load is unconditional (clamped to the last entry; the step count is
 // wave-uniform), so the waits the compiler places count exactly: the gather of step
 // st + 2 waits only for its index (vmcnt(5)), the compute of step st only for its point.
+// AB (timing ablations, wrong results): 2 gathers confined to the first 1024 points (L1/L2
+// hits), 4 no per-entry arithmetic (one add per entry keeps the loads live).
+// camtab (TAB): the camera's frame from the precomputed table (scalar loads, no trigonometry)
+template <int AB = 0, bool TAB = false>
 __device__ __forceinline__ void eval_cams_gather(const int* __restrict__ cm_pt, const double2* __restrict__ cmxy,
                                                  const double* __restrict__ points, int i0, int e, int ext_i,
                                                  int intr_i, const double* __restrict__ ext,
-                                                 const double* __restrict__ intr, double (&acc)[27], double* jl) {
+                                                 const double* __restrict__ intr, double (&acc)[27], double* jl,
+                                                 const double* __restrict__ camtab = nullptr) {
   constexpr int DG = 2, DI = 4, R = 3;
   const int lo = i0 - (int)(threadIdx.x & 63);
   const int n = (e - lo + 63) >> 6;  // steps of 64 entries
@@ -1685,7 +1690,7 @@ __device__ __forceinline__ void eval_cams_gather(const int* __restrict__ cm_pt, 
   double X[R][3];
   auto load_idx = [&](int slot, int step) { pid[slot] = cm_pt[min(i0 + 64 * step, e - 1)]; };
   auto gather = [&](int islot, int slot, int step) {
-    const int p = pid[islot];
+    const int p = (AB & 2) ? (pid[islot] & 1023) : pid[islot];
     xy[slot] = cmxy[min(i0 + 64 * step, e - 1)];
 #pragma unroll
     for (int q = 0; q < 3; ++q) X[slot][q] = points[3 * (size_t)p + q];
@@ -1693,10 +1698,12 @@ __device__ __forceinline__ void eval_cams_gather(const int* __restrict__ cm_pt, 
   // the camera's parameters leave with the first indices (one round trip for both); its
   // table is then built while the first points are gathered
   double x6[6], k6[6];
+  if constexpr (!TAB) {
 #pragma unroll
-  for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)ext_i + q];
+    for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)ext_i + q];
 #pragma unroll
-  for (int q = 0; q < 6; ++q) k6[q] = intr[(size_t)kIntr * intr_i + q];
+    for (int q = 0; q < 6; ++q) k6[q] = intr[(size_t)kIntr * intr_i + q];
+  }
   if (n > 0) {
     // prologue: indices of steps 0 .. DI-1 ... in the order the loop body issues them
 #pragma unroll
@@ -1706,7 +1713,8 @@ __device__ __forceinline__ void eval_cams_gather(const int* __restrict__ cm_pt, 
 #pragma unroll
     for (int st = DG; st < DI; ++st) load_idx(st % R, st);
   }
-  const UniFrame f(UniFrame::FromValues{}, x6, k6, jl);  // built while the first gathers fly
+  const UniFrame f = TAB ? UniFrame(UniFrame::FromTable{}, camtab, intr, ext_i, intr_i, jl)
+                         : UniFrame(UniFrame::FromValues{}, x6, k6, jl);  // built while the first gathers fly
   DAB_STAMP_ANY(1);
   for (int st0 = 0; st0 < n; st0 += R) {
 #pragma unroll
@@ -1714,7 +1722,11 @@ __device__ __forceinline__ void eval_cams_gather(const int* __restrict__ cm_pt, 
       const int st = st0 + u;
       gather((st + DG) % R, (st + DG) % R, st + DG);  // index of step st + DG -> its point
       load_idx((st + DI) % R, st + DI);                // slot of step st + DI - R = st + 1: consumed
-      if (i0 + 64 * st < e) frame_rows_acc(xy[u], X[u], f, acc);
+      if constexpr ((AB & 4) != 0) {
+        if (i0 + 64 * st < e) acc[0] += xy[u].x + X[u][0] + X[u][1] + X[u][2];
+      } else if (i0 + 64 * st < e) {
+        frame_rows_acc(xy[u], X[u], f, acc);
+      }
     }
   }
 }
@@ -1980,7 +1992,9 @@ constexpr int kCamSplit = DAB_CAM_SPLIT;  // first part of a two-part camera chu
 // NS slots) and point waves the packed 4-B slot records v.obs_e (ext | intr << 16, a D-deep
 // queue at 5 VGPRs per row) instead of the 16-B obs_idx records.
 // CG (with ST): the camera waves gather the points themselves (eval_cams_gather), no cmx.
-template <int D, int ABL = 0, int NS = 3, bool ST = false, bool TAB = false, bool CG = false>
+template <int D, int ABL = 0, int NS = 3, bool ST = false, bool TAB = false, bool CG = false, int GV = 0>
+                                          // GV (with CG; DAB_ABLATIONS builds): camera-side timing ablations,
+                                          // eval_cams_gather's AB flags
                                           // ABL: 1 camera waves exit at once (point side
                                           // only), 2 point waves do (camera side only) — the multi-rank split
                                           // schedule; timing ablations: 3 no trig in the staging, 21 / 22
@@ -2036,7 +2050,8 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
                              acc);
       if (lane < 9) cjl[cw][lane] = (lane % 4 == 0) ? 1.0 : 0.0;
     } else if constexpr (ST && CG) {
-      eval_cams_gather(v.cm_pt, v.cm_xy, points, lo + lane, hi, u.x, u.y, ext, v.intr, acc, cjl[cw]);
+      eval_cams_gather<GV & 6, TAB>(v.cm_pt, v.cm_xy, points, lo + lane, hi, u.x, u.y, ext, v.intr, acc, cjl[cw],
+                                    camtab);
     } else if constexpr (ST) {
       eval_cams_stream<NS, TAB>(cmx, (size_t)v.NE, v.cm_xy, lo + lane, hi, u.x, u.y, ext, v.intr, acc, cjl[cw],
                                 camtab);
@@ -2309,7 +2324,7 @@ static int fused_wps(int nslice, int E, int grid) {
 }
 void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
                        double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
-                       int grid, int side, const double* cmx, int variant, const double* camtab) {
+                       int grid, int side, const double* cmx, int variant, const double* camtab, int gv) {
   const int wpc = fused_wpc(v.NC, grid), wps = fused_wps(v.nslice, v.E, grid);
   const int wxor = variant >= 1000 ? 8 : 0;  // camera side on the older hardware waves
   variant %= 1000;
@@ -2340,11 +2355,25 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
     else k_eval_fused<3, 0, 2, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
     return;
   }
+  if (v.obs_e && camtab) {
+    // the same with the camera tables of the current x read from k_cam_tables' output (built
+    // once per parameter state: the LM loop builds them for the whole iteration anyway)
+    k_eval_fused<3, 0, 3, true, true, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS, side);
+    return;
+  }
   if (v.obs_e) {
     // packed point-side records, camera waves gathering the points (nothing to refresh
     // when the points move). The multi-rank split schedule runs THIS instantiation with a
     // run-time side, so both schedules execute the same machine code (the same fp
     // contraction, hence bitwise the same sums).
+#ifdef DAB_ABLATIONS
+    // camera-side timing ablations (wrong results): 2 gathers confined to the first 1024
+    // points, 4 no per-entry arithmetic, 6 both (DAB_FUSED_GV)
+    if (gv == 2) k_eval_fused<3, 0, 3, true, false, true, 2><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS, side);
+    else if (gv == 4) k_eval_fused<3, 0, 3, true, false, true, 4><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS, side);
+    else if (gv == 6) k_eval_fused<3, 0, 3, true, false, true, 6><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS, side);
+    else
+#endif
     k_eval_fused<3, 0, 3, true, false, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS, side);
     return;
   }

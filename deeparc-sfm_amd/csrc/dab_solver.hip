@@ -188,20 +188,68 @@ enum Slot {
   S_NSLOTS = S_CFX + 2 * kFxWords
 };
 
+// Device buffers of one problem. dab_set_problem releases them all and the new problem
+// allocates its own; a release keeps the memory in a pool instead of freeing it, and an
+// allocation takes the smallest pooled block that holds it without wasting more than half
+// (or 1 MiB), so the sfm.cc loop's re-set-up after every filter round (the same problem,
+// a little smaller) finds its ~50 buffers there instead of paying a hipMalloc / hipFree pair
+// each (a few ms per set-up at 160k observations). A pooled block unused through one whole
+// set-up and solve cycle is freed at the next release. The stream is synchronised before a
+// release (dab_set_problem), so no queued kernel still reads a block that gets reused.
 struct Dev {
-  std::vector<void*> allocs;
-  ~Dev() { release(); }
+  struct Blk {
+    void* p;
+    size_t bytes;
+    int age;
+  };
+  std::vector<Blk> live, pool;
+  ~Dev() {
+    for (const Blk& b : live) (void)hipFree(b.p);
+    for (const Blk& b : pool) (void)hipFree(b.p);
+  }
+  void clear() {  // free everything now, pooled blocks included
+    for (const Blk& b : live) (void)hipFree(b.p);
+    for (const Blk& b : pool) (void)hipFree(b.p);
+    live.clear();
+    pool.clear();
+  }
   void release() {
-    for (void* p : allocs) (void)hipFree(p);
-    allocs.clear();
+    std::vector<Blk> keep;
+    for (Blk& b : pool) {
+      if (++b.age >= 2) (void)hipFree(b.p);
+      else keep.push_back(b);
+    }
+    for (Blk b : live) {
+      b.age = 0;
+      keep.push_back(b);
+    }
+    pool.swap(keep);
+    live.clear();
   }
   template <class T>
   int alloc(T** out, size_t n) {
-    void* p = nullptr;
     if (n == 0) n = 1;
-    if (hipMalloc(&p, n * sizeof(T)) != hipSuccess)
-      return set_error(DAB_E_NOMEM, "hipMalloc of " + std::to_string(n * sizeof(T)) + " bytes failed");
-    allocs.push_back(p);
+    const size_t bytes = (n * sizeof(T) + 255) & ~(size_t)255;
+    const size_t cap = std::max(2 * bytes, bytes + ((size_t)1 << 20));
+    size_t best = pool.size();
+    for (size_t i = 0; i < pool.size(); ++i)
+      if (pool[i].bytes >= bytes && pool[i].bytes <= cap && (best == pool.size() || pool[i].bytes < pool[best].bytes))
+        best = i;
+    void* p = nullptr;
+    size_t got = bytes;
+    if (best < pool.size()) {
+      p = pool[best].p;
+      got = pool[best].bytes;
+      pool[best] = pool.back();
+      pool.pop_back();
+    } else if (hipMalloc(&p, bytes) != hipSuccess) {
+      // the pool may hold what the device needs: give it back and try once more
+      for (const Blk& b : pool) (void)hipFree(b.p);
+      pool.clear();
+      if (hipMalloc(&p, bytes) != hipSuccess)
+        return set_error(DAB_E_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
+    }
+    live.push_back(Blk{p, got, 0});
     *out = static_cast<T*>(p);
     return 0;
   }
@@ -237,9 +285,11 @@ struct Knobs {
                             // (refreshed after every point change); 0 the 16-B records
   int fused_variant = 0;    // DAB_FUSED_V: pipeline depths of the streamed fused pass (DAB_ABLATIONS builds)
   int setup_host = 0;       // DAB_SETUP_HOST=1: dab_set_problem's host passes instead of the device ones
-  int fused_tab = 0;        // DAB_FUSED_TAB=1 (DAB_ABLATIONS builds): the streamed fused pass reads the
-                            // k_cam_tables output instead of building its tables (kernel -0.9 us at C3,
-                            // but the extra launch in front costs more)
+  int fused_gv = 0;         // DAB_FUSED_GV (DAB_ABLATIONS builds): fused-pass camera-side timing ablations
+  int fused_tab = -1;       // DAB_FUSED_TAB: the fused pass reads the camera tables of the current x
+                            // instead of building them in every work-group — -1 (default) when they
+                            // exist already (the LM loop: the accepted candidate's tables), 1 always
+                            // (building them first where they do not), 0 never
   void read() {
     auto get = [](const char* name, int& out) {
       if (const char* e = getenv(name)) out = atoi(e);
@@ -262,6 +312,7 @@ struct Knobs {
     get("DAB_FUSED_V", fused_variant);
     get("DAB_FUSED_TAB", fused_tab);
     get("DAB_SETUP_HOST", setup_host);
+    get("DAB_FUSED_GV", fused_gv);
   }
 };
 
@@ -460,7 +511,12 @@ struct dab_handle {
   P2pComm* p2p_comm = nullptr;
   static constexpr size_t kP2pWords = 65536;
   // an all-reduce on comm_stream can overlap the point-side kernel (RCCL or peer-to-peer)
-  bool can_overlap() const { return world > 1 && ((comm && !host_cb) || p2p_comm); }
+  // rccl1: a one-rank handle on a real one-rank RCCL communicator (dab_create_dist with
+  // world_size 1 and a unique id): every collective and the overlapped camera all-reduce run
+  // through RCCL although they sum one rank, so the multi-GPU transport executes on one GPU
+  bool rccl1 = false;
+  bool coll() const { return world > 1 || rccl1; }
+  bool can_overlap() const { return coll() && ((comm && !host_cb) || p2p_comm); }
   int allreduce_comm_stream(double* buf, size_t n) {
     if (p2p_comm && n <= kP2pWords) return p2p_allreduce_sum(p2p_comm, comm_stream, buf, n);
     if (!comm || host_cb) return set_error(DAB_E_STATE, "no collective for the communication stream");
@@ -498,7 +554,7 @@ struct dab_handle {
   // exact integer sum over ranks of n uint64 words (the fixed-point cost); the host path
   // moves each word as three 22-bit pieces, which gloo's double sum adds exactly
   int allreduce_u64(uint64_t* buf, size_t n) {
-    if (world <= 1 || n == 0) return 0;
+    if (!coll() || n == 0) return 0;
     if (p2p_main && n <= kP2pWords)
       return p2p_allreduce_sum_u64(p2p_main, stream, reinterpret_cast<unsigned long long*>(buf), n);
     if (!host_cb) {
@@ -532,7 +588,7 @@ struct dab_handle {
   }
 
   int allreduce(double* buf, size_t n, ncclRedOp_t op) {
-    if (world <= 1 || n == 0) return 0;
+    if (!coll() || n == 0) return 0;
     if (p2p_main && n <= kP2pWords && (op == ncclSum || op == ncclMax))
       return op == ncclSum ? p2p_allreduce_sum(p2p_main, stream, buf, n) : p2p_allreduce_max(p2p_main, stream, buf, n);
     if (host_cb) return host_allreduce(buf, n, op == ncclMax ? 1 : 0);
@@ -541,7 +597,7 @@ struct dab_handle {
   }
   // max over ranks of small int flag arrays
   int allreduce_max_i32(int* buf, int n) {
-    if (world <= 1 || n == 0) return 0;
+    if (!coll() || n == 0) return 0;
     if (p2p_main) return p2p_allreduce_max_i32(p2p_main, stream, buf, (size_t)n);
     if (!host_cb) {
       NCCL_OK(ncclAllReduce(buf, buf, n, ncclInt32, ncclMax, comm, stream));
@@ -577,7 +633,18 @@ static int create_common(int device, dab_handle** out) {
   // (the device set-up) fell back to blocking, and the first synchronisation of the
   // following solve took 10-25 ms for 10 us of device work. DAB_SCHEDULE_BLOCKING=1 keeps
   // the default.
-  if (!getenv("DAB_SCHEDULE_BLOCKING")) (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+  // The flag is process-wide (every host wait of the embedding process spins): dab.h says so.
+  // A runtime that refuses it (flags fixed once the device's context exists) keeps its
+  // default; that is reported once on stderr, not as an error.
+  if (!getenv("DAB_SCHEDULE_BLOCKING")) {
+    const hipError_t fe = hipSetDeviceFlags(hipDeviceScheduleSpin);
+    static bool warned = false;
+    if (fe != hipSuccess && !warned) {
+      warned = true;
+      fprintf(stderr, "dab: hipSetDeviceFlags(hipDeviceScheduleSpin) not applied (%s); host waits keep the "
+                      "runtime's scheduling\n", hipGetErrorString(fe));
+    }
+  }
   dab_handle* h = new dab_handle();
   h->device = device;
   h->knobs.read();
@@ -728,6 +795,19 @@ extern "C" int dab_create_dist(int device, int rank, int world_size, const uint8
   dab_handle* h = *out;
   h->rank = rank;
   h->world = world_size;
+  if (world_size == 1 && unique_id) {
+    // one-rank RCCL communicator: the collectives execute (on one GPU) instead of returning
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, 128);
+    ncclResult_t r = ncclCommInitRank(&h->comm, 1, id, 0);
+    if (r != ncclSuccess) {
+      std::string msg = std::string("ncclCommInitRank (one rank): ") + ncclGetErrorString(r);
+      delete h;
+      *out = nullptr;
+      return set_error(DAB_E_COMM, msg);
+    }
+    h->rccl1 = true;
+  }
   if (world_size > 1) {
     ncclUniqueId id;
     std::memcpy(&id, unique_id, 128);
@@ -809,6 +889,7 @@ static int validate_obs(const dab_problem* p) {
 // uploads. setup_device builds the same arrays on the GPU.
 static int setup_host(dab_handle* h, const dab_problem* p, const std::function<void(const char*)>& phase) {
   CHECK_RC(validate_obs(p));
+  h->setup_tmp.clear();  // a previous device set-up's scratch (the host path needs none)
   const int N = p->num_obs;
   hipStream_t s = h->stream;
   // referenced points (local compact ids, in id order) and extrinsics
@@ -1341,10 +1422,12 @@ static int setup_buffers(dab_handle* h, const std::function<void(const char*)>& 
     // free for them (DAB_EVAL_FREE_CUS overrides; its slices are dealt round robin over
     // whatever grid it gets).
     int pcus = ncu;
+    // (a one-rank RCCL handle keeps the full grid: the same work-group partition, hence
+    // bitwise the same sums, as dab_create)
     if (h->world > 1 && h->eval_wps <= 0) pcus = std::max(1, ncu - h->knobs.free_cus);
     h->eval_grid = h->eval_wps <= 0 ? std::max(1, std::min(pcus, h->nslice)) : std::max(1, h->nslice);
     h->fused = h->knobs.eval_fused != 0;
-    h->fused_split = h->world > 1 || h->knobs.eval_split != 0;  // the split schedule on one rank too (tests)
+    h->fused_split = h->coll() || h->knobs.eval_split != 0;  // the split schedule on one rank too (tests)
   }
   CHECK_RC(d.alloc(&h->d_gpart, (size_t)std::max(h->red_grid, h->eval_grid) * 4));
   CHECK_RC(d.alloc(&h->d_scal, S_NSLOTS));
@@ -1868,7 +1951,7 @@ extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
 // union over ranks so the all-reduced packed layout matches.
 static constexpr long long kMaxExplicitPairs = 200000000LL;
 static int max_all_ranks(dab_handle* h, double& x) {  // max over ranks of one host scalar
-  if (h->world <= 1) return 0;
+  if (!h->coll()) return 0;
   hipStream_t s = h->stream;
   double* d_f = nullptr;
   CHECK_RC(h->dev.alloc(&d_f, 1));
@@ -2146,7 +2229,7 @@ static int build_schur_tiles(dab_handle* h, int2* d_sch, const int* d_m) {
 
 // present block keys: the union over ranks (every rank must all-reduce the same S layout)
 static int union_block_keys(dab_handle* h, std::vector<long long>& keys) {
-  if (h->world <= 1) return 0;
+  if (!h->coll()) return 0;
   const int NC = h->NC;
   hipStream_t s = h->stream;
   std::vector<double> bm((size_t)NC * NC, 0.0);
@@ -2654,11 +2737,11 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
   bool overlapped = false;
   // the streamed fused pass reads R, t (point side) and R, t, Rd, Jd (camera side) from the
   // tables of the current x instead of building them in every work-group
-#ifdef DAB_ABLATIONS
-  const bool fused_tab = h->fused && h->d_cmx && h->knobs.fused_tab != 0;
-#else
-  const bool fused_tab = false;
-#endif
+  // the fused pass reads the tables when the caller has them (the LM loop) — C3: 21.3
+  // against 23.2 us per launch — but does not launch a table build of its own for them
+  // (k_cam_tables in front of the pass cost more than it saves: 25.6 against 23.9 us per
+  // step), unless DAB_FUSED_TAB=1 asks for it
+  const bool fused_tab = h->fused && (h->knobs.fused_tab > 0 || (h->knobs.fused_tab < 0 && camtab_ready));
   const bool need_tab = (h->NC > 0 && (h->chunks.ngen > 0 || h->ncross > 0)) || eval_points_needs_camtab(h->eval_wps) ||
                         fused_tab;
   if (!camtab_ready && need_tab) launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
@@ -2676,7 +2759,7 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
   if (h->fused && !h->fused_split) {  // both halves of the pass in one launch (launch_eval_fused)
     launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
                       h->cost_fx(h->fx_last ^ 1), h->ncu, 0, h->d_cmx, h->knobs.fused_variant,
-                      fused_tab ? h->d_camtab : nullptr);
+                      fused_tab ? h->d_camtab : nullptr, h->knobs.fused_gv);
     if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
     if (h->NC > 0) CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
     return 0;
@@ -2756,9 +2839,11 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
 
 // Residual + Jacobian at the current x and the J^T J / J^T r blocks (camera side
 // all-reduced). Leaves cost / gradient scalars in d_scal (point parts all-reduced).
-static int eval_jacobian_and_blocks(dab_handle* h, bool with_norms) {
+// tables_current: d_camtab already holds the tables of d_ext (after an accepted step, the
+// candidate's tables swapped in with its parameters), so none are built here
+static int eval_jacobian_and_blocks(dab_handle* h, bool with_norms, bool tables_current = false) {
   hipStream_t s = h->stream;
-  launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
+  if (!tables_current) launch_cam_tables(s, h->E, h->d_ext, h->d_camtab);
   CHECK_RC(eval_pass(h, true));
   if (with_norms) {
     launch_grad_points(s, h->NP, h->d_points, h->d_g, h->d_gpart, h->red_grid);
@@ -2823,7 +2908,7 @@ static void print_iter(const dab_iteration& it, double total) {
 // Wall-clock since solve start, maxed over ranks so every rank takes the
 // "Maximum solver time reached" exit on the same iteration. Returns < 0 on error.
 static double elapsed_collective(dab_handle* h, double local) {
-  if (h->world <= 1) return local;
+  if (!h->coll()) return local;
   hipStream_t s = h->stream;
   h->h_scal[S_TIME] = local;
   if (hipMemcpyAsync(h->d_scal + S_TIME, &h->h_scal[S_TIME], sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess)
@@ -3097,10 +3182,11 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
       const double xc_norm = std::sqrt(h->h_scal[S_XCNORM_P] + h->h_scal[S_CAM0 + 1]);
       std::swap(h->d_points, h->d_points_c);
       std::swap(h->d_ext, h->d_ext_c);
+      std::swap(h->d_camtab, h->d_camtab_c);  // the candidate pass built the tables of x + delta
       ++h->pts_version;
       x_norm = xc_norm;
       const double tj = now_s();
-      CHECK_RC(eval_jacobian_and_blocks(h, true));
+      CHECK_RC(eval_jacobian_and_blocks(h, true, true));
       CHECK_RC(read_scalars(h));
       sum->jacobian_evaluation_time_in_seconds += now_s() - tj;
       if (h->h_scal[S_COST_BAD] != 0.0) {

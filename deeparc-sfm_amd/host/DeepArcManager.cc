@@ -3,9 +3,14 @@
 // (SURVEY App. C). The residuals behind filterPoint3d come from the GPU (dab_filter).
 #include "DeepArcManager.hh"
 
+#include <algorithm>
 #include <cctype>
+#include <cstdlib>
 #include <charconv>
 #include <cstdio>
+#include <cstring>
+#include <thread>
+#include <type_traits>
 #include <fstream>
 #include <iostream>
 #include <unordered_map>
@@ -27,16 +32,84 @@ class Tokens {
   explicit Tokens(std::string text) : buf_(std::move(text)), p_(buf_.data()), end_(buf_.data() + buf_.size()) {}
   template <class T>
   T take() {
-    while (p_ < end_ && std::isspace((unsigned char)*p_)) ++p_;
-    const char* q = p_;
-    if (q < end_ && *q == '+') ++q;
-    if (q >= end_ || !(std::isdigit((unsigned char)*q) || *q == '-' || *q == '.')) throw "Malformed .deeparc file";
     T v{};
-    const auto r = std::from_chars(q, end_, v);
-    if (r.ec != std::errc()) throw "Malformed .deeparc file";
-    p_ = r.ptr;
+    if (!take_at(p_, end_, v)) throw "Malformed .deeparc file";
     return v;
   }
+  // one token from [p, end) into v, p moved past it; false on a malformed token
+  template <class T>
+  static bool take_at(const char*& p, const char* end, T& v) {
+    while (p < end && std::isspace((unsigned char)*p)) ++p;
+    const char* q = p;
+    if (q < end && *q == '+') ++q;
+    if (q >= end || !(std::isdigit((unsigned char)*q) || *q == '-' || *q == '.')) return false;
+    if constexpr (std::is_same<T, double>::value) {
+      if (fast_double(q, end, v)) {
+        p = q;
+        return true;
+      }
+    }
+    const auto r = std::from_chars(q, end, v);
+    if (r.ec != std::errc()) return false;
+    p = r.ptr;
+    return true;
+  }
+  // Decimal -> double without libstdc++'s from_chars (GCC 11: strtod under a per-call locale,
+  // ~25 ns a token and serialised across threads). Up to 19 significant digits and a decimal
+  // exponent within +-27: the digits and the power of ten are exact in x87 long double (64-bit
+  // mantissa), one multiply or divide rounds correctly to it, and the rounding to double is
+  // then correct unless the long double sits within one of its ulps of a double half-way
+  // point; those, and every other form, go to from_chars. Same value as strtod either way.
+  static bool fast_double(const char*& p, const char* end, double& out) {
+    static const long double kPow10[28] = {1e0L,  1e1L,  1e2L,  1e3L,  1e4L,  1e5L,  1e6L,  1e7L,  1e8L,  1e9L,
+                                           1e10L, 1e11L, 1e12L, 1e13L, 1e14L, 1e15L, 1e16L, 1e17L, 1e18L, 1e19L,
+                                           1e20L, 1e21L, 1e22L, 1e23L, 1e24L, 1e25L, 1e26L, 1e27L};
+    const char* q = p;
+    bool neg = false;
+    if (q < end && *q == '-') {
+      neg = true;
+      ++q;
+    }
+    unsigned long long m = 0;
+    int sig = 0, exp10 = 0;
+    bool any = false;
+    for (; q < end && *q >= '0' && *q <= '9'; ++q) {
+      any = true;
+      if (m == 0 && *q == '0') continue;
+      if (++sig > 19) return false;
+      m = m * 10 + (unsigned)(*q - '0');
+    }
+    if (q < end && *q == '.') {
+      ++q;
+      for (; q < end && *q >= '0' && *q <= '9'; ++q) {
+        any = true;
+        --exp10;
+        if (m == 0 && *q == '0') continue;
+        if (++sig > 19) return false;
+        m = m * 10 + (unsigned)(*q - '0');
+      }
+    }
+    if (!any) return false;
+    if (q < end && (*q == 'e' || *q == 'E')) return false;  // exponent forms: from_chars
+    if (m == 0) {
+      out = neg ? -0.0 : 0.0;
+      p = q;
+      return true;
+    }
+    if (exp10 < -27 || exp10 > 27) return false;
+    long double v = (long double)m;
+    v = exp10 >= 0 ? v * kPow10[exp10] : v / kPow10[-exp10];
+    unsigned long long mant;
+    std::memcpy(&mant, &v, 8);  // x87 extended: the 64-bit significand (explicit leading bit)
+    const unsigned low = (unsigned)(mant & 0x7FF);
+    if (low >= 0x3FF && low <= 0x401) return false;  // near a double half-way point
+    out = neg ? -(double)v : (double)v;
+    p = q;
+    return true;
+  }
+  const char* pos() const { return p_; }
+  const char* end() const { return end_; }
+  void seek(const char* p) { p_ = p; }
 
  private:
   std::string buf_;
@@ -46,6 +119,93 @@ class Tokens {
 
 void fmt6(FILE* f, double v) { std::fprintf(f, "%.6f", v); }  // std::fixed, setprecision(6)
 void fmtg(FILE* f, double v) { std::fprintf(f, "%g", v); }    // default ostream format
+
+// The observation section (five tokens per block, one block per line as every writer emits
+// it) is most of the file and of its parse time (~25 ns per from_chars double): it is cut at
+// line starts into pieces parsed on several threads into plain arrays, then the blocks are
+// created in file order. A piece whose lines do not hold exactly five well-formed tokens
+// each, or a section that is not line-aligned, is parsed again by the sequential tokenizer,
+// which gives the stream semantics (tokens may span lines) and the same values.
+void read_observations(Tokens& f, int n_blocks, std::vector<ParameterBlock*>& params_) {
+  std::vector<int> ia(n_blocks), ir(n_blocks), ip(n_blocks);
+  std::vector<double> vx(n_blocks), vy(n_blocks);
+  auto sequential = [&](int from, const char* at) -> const char* {
+    f.seek(at);
+    for (int i = from; i < n_blocks; ++i) {
+      ia[i] = f.take<int>();
+      ir[i] = f.take<int>();
+      ip[i] = f.take<int>();
+      vx[i] = f.take<double>();
+      vy[i] = f.take<double>();
+    }
+    return f.pos();
+  };
+  const char* p0 = f.pos();
+  const char* end = f.end();
+  // start of line i of the section: the header line's remainder ends at the first newline
+  // DAB_READ_THREADS: most parser threads (default 8; 1 = sequential)
+  static const int tmax = getenv("DAB_READ_THREADS") ? atoi(getenv("DAB_READ_THREADS")) : 8;
+  const int T = n_blocks >= 32768
+                    ? (int)std::min((unsigned)std::max(1, tmax), std::max(1u, std::thread::hardware_concurrency()))
+                    : 1;
+  bool parallel_ok = T > 1;
+  std::vector<const char*> cut(T + 1, nullptr);
+  if (parallel_ok) {
+    const char* q = static_cast<const char*>(std::memchr(p0, '\n', end - p0));
+    parallel_ok = q != nullptr;
+    if (parallel_ok) {
+      // the header line must end right after its last token
+      for (const char* c = p0; c < q; ++c) parallel_ok = parallel_ok && std::isspace((unsigned char)*c);
+      ++q;
+      long long line = 0;
+      int k = 0;
+      cut[0] = q;
+      for (int t = 1; t <= T && parallel_ok; ++t) {
+        const long long want = (long long)n_blocks * t / T;
+        while (line < want && q && q < end) {
+          q = static_cast<const char*>(std::memchr(q, '\n', end - q));
+          if (q) ++q;
+          ++line;
+        }
+        if (line < want) parallel_ok = false;
+        cut[++k] = q ? q : end;
+      }
+    }
+  }
+  std::vector<char> bad(T, 0);
+  if (parallel_ok) {
+    auto piece = [&](int t) {
+      const char* p = cut[t];
+      const char* e = cut[t + 1];
+      const int i0 = (int)((long long)n_blocks * t / T), i1 = (int)((long long)n_blocks * (t + 1) / T);
+      for (int i = i0; i < i1; ++i) {
+        const char* nl = static_cast<const char*>(std::memchr(p, '\n', e - p));
+        const char* le = nl ? nl : e;
+        if (!(Tokens::take_at(p, le, ia[i]) && Tokens::take_at(p, le, ir[i]) && Tokens::take_at(p, le, ip[i]) &&
+              Tokens::take_at(p, le, vx[i]) && Tokens::take_at(p, le, vy[i]))) {
+          bad[t] = 1;
+          return;
+        }
+        while (p < le && std::isspace((unsigned char)*p)) ++p;
+        if (p != le) {  // a sixth token on the line
+          bad[t] = 1;
+          return;
+        }
+        p = nl ? nl + 1 : e;
+      }
+      if (p != e) bad[t] = 1;
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(piece, t);
+    piece(0);
+    for (auto& x : th) x.join();
+    for (int t = 0; t < T; ++t) parallel_ok = parallel_ok && !bad[t];
+    if (parallel_ok) f.seek(cut[T]);
+  }
+  if (!parallel_ok) sequential(0, p0);
+  params_.reserve(params_.size() + n_blocks);
+  for (int i = 0; i < n_blocks; ++i) params_.push_back(new ParameterBlock(ia[i], ir[i], ip[i], new Point2d(vx[i], vy[i])));
+}
 
 }  // namespace
 
@@ -102,11 +262,7 @@ bool DeepArcManager::read(std::string filename) {
   const int n_ext = share_extrinsic_ ? n_arc + n_ring - 1 : n_arc;
 
   // observation lines: pos_arc pos_ring point_id x y
-  for (int i = 0; i < n_blocks; ++i) {
-    const int a = f.take<int>(), r = f.take<int>(), pid = f.take<int>();
-    const double x = f.take<double>(), y = f.take<double>();
-    params_.push_back(new ParameterBlock(a, r, pid, new Point2d(x, y)));
-  }
+  read_observations(f, n_blocks, params_);
   // intrinsics: cx cy nf f[nf] nk k[nk]; the principal point truncates to int (Q1)
   for (int i = 0; i < n_intr; ++i) {
     Intrinsic* k = new Intrinsic();

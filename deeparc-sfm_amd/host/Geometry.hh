@@ -4,14 +4,70 @@
 // double array that the solver writes back in place (sfm.cc:47-48 semantics).
 #pragma once
 #include <algorithm>
+#include <mutex>
 #include <set>
 #include <vector>
 
 class ParameterBlock;
 
+// Fixed-size object pool behind a class's operator new / delete: the reader allocates one
+// ParameterBlock and one Point2d per observation (320k objects for the 160k-observation
+// config-1 scene) and the filter deletes them one by one; a free list over 64K-object
+// chunks makes each a few instructions instead of a malloc / free pair. Chunks are kept for
+// the life of the process. Guarded by a mutex (managers may live on different threads).
+template <size_t SIZE>
+class ObjectPool {
+ public:
+  static void* take() {
+    std::lock_guard<std::mutex> lk(mu());
+    Node*& f = head();
+    if (!f) refill(f);
+    Node* n = f;
+    f = n->next;
+    return n;
+  }
+  static void give(void* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(mu());
+    Node* n = static_cast<Node*>(p);
+    n->next = head();
+    head() = n;
+  }
+
+ private:
+  union Node {
+    Node* next;
+    alignas(16) unsigned char bytes[SIZE];
+  };
+  static constexpr size_t kChunk = 1 << 16;
+  static std::mutex& mu() {
+    static std::mutex m;
+    return m;
+  }
+  static Node*& head() {
+    static Node* h = nullptr;
+    return h;
+  }
+  static void refill(Node*& f) {
+    Node* c = static_cast<Node*>(::operator new(sizeof(Node) * kChunk));
+    for (size_t i = 0; i + 1 < kChunk; ++i) c[i].next = &c[i + 1];
+    c[kChunk - 1].next = f;
+    f = c;
+  }
+};
+#define DAB_POOLED(T)                                                              \
+  static void* operator new(size_t n) {                                            \
+    return n == sizeof(T) ? ObjectPool<sizeof(T)>::take() : ::operator new(n);    \
+  }                                                                                \
+  static void operator delete(void* p, size_t n) {                                 \
+    if (n == sizeof(T)) ObjectPool<sizeof(T)>::give(p);                            \
+    else ::operator delete(p);                                                     \
+  }
+
 // Point/Point2d.hh
 class Point2d {
  public:
+  DAB_POOLED(Point2d)
   Point2d(double x, double y) : x_(x), y_(y) {}
   double x() { return x_; }
   double y() { return y_; }

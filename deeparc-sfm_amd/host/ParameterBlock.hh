@@ -9,6 +9,7 @@
 
 class ParameterBlock {
  public:
+  DAB_POOLED(ParameterBlock)
   ParameterBlock(int position_arc, int position_ring, int point3d_id, Point2d* point2d)
       : pos_arc_(position_arc), pos_ring_(position_ring), point3d_id_(point3d_id), point2d_(point2d) {}
   ~ParameterBlock() {

@@ -19,7 +19,7 @@ sys.path.insert(0, ROOT)
 import _pkgload  # noqa: E402
 
 KNOBS = ("DAB_EVAL_ROLES", "DAB_ROLES_CBLK", "DAB_ROLES_CPB", "DAB_ROLES_SPLIT", "DAB_ROLES_TAB", "DAB_ROLES_V",
-         "DAB_EVAL_FUSED", "DAB_FUSED_STREAM", "DAB_FUSED_GV", "DAB_FUSED_TAB")
+         "DAB_EVAL_FUSED", "DAB_FUSED_STREAM", "DAB_FUSED_GV", "DAB_FUSED_TAB", "DAB_FUSED_V")
 
 
 def parse(spec):
