@@ -58,9 +58,11 @@ struct CholCtx {
   bool back_flow = true;      // DAB_CHOL_BACK_FLOW=0: the grid-barrier back substitution
   bool prefactor = true;      // DAB_CHOL_PREFACTOR=0: every panel work-group factors the diagonal block
   bool nograph = false;       // DAB_CHOL_NOGRAPH=1: launch directly instead of the captured graph (traces)
+  int graph_min = 16;         // DAB_CHOL_GRAPH_MIN: fewest blocks that use the captured graph
   bool serial = false;        // DAB_CHOL_SERIAL=1: the bulk updates on the chain stream (debugging)
   bool fuse_panel = true;     // DAB_CHOL_FUSE_PANEL=0: the panel step as its own launch after the column update
   unsigned* pready = nullptr; // per block: L_kk published by the fused column update (zeroed per factorisation)
+  int group = 2;            // DAB_CHOL_GROUP: panels per bulk trailing update (2: pairs)
   bool v1 = false;          // DAB_CHOL_V1=1: the per-step schedule (one bulk update per panel, one
                             // back-substitution launch per block)
 };
@@ -80,10 +82,12 @@ CholCtx* chol_create() {
   c->ncu = ncu;
   if (const char* e = getenv("DAB_CHOL_BULK_GRID")) c->bulk_grid = atoi(e);
   if (const char* e = getenv("DAB_CHOL_V1")) c->v1 = atoi(e) != 0;
+  if (const char* e = getenv("DAB_CHOL_GROUP")) c->group = std::max(2, atoi(e));
   if (const char* e = getenv("DAB_CHOL_BACK_FLOW")) c->back_flow = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_PREFACTOR")) c->prefactor = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_FUSE_PANEL")) c->fuse_panel = atoi(e) != 0;
   c->nograph = getenv("DAB_CHOL_NOGRAPH") != nullptr;
+  if (const char* e = getenv("DAB_CHOL_GRAPH_MIN")) c->graph_min = atoi(e);
   c->serial = getenv("DAB_CHOL_SERIAL") != nullptr;
   if (const char* e = getenv("DAB_CHOL_BULK_PAD")) c->bulk_pad = (size_t)atoi(e) * 1024;
   if (const char* e = getenv("DAB_CHOL_BULK_KC")) c->bulk_kc = atoi(e);
@@ -92,24 +96,11 @@ CholCtx* chol_create() {
     const int v = atoi(e);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chol_prio), &v, sizeof(int));
   }
-  // the side stream, the barrier word and the graph machinery set up now (each costs
-  // milliseconds the first time; inside a solve they would land in its first LM iteration)
+  // the side stream and the barrier word now, not inside the first solve. (A warm-up graph
+  // capture here bought nothing: every instantiation costs ~5 ms, the first one no more.)
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess || hipMalloc(&c->bar, sizeof(unsigned)) != hipSuccess) {
     chol_destroy(c);
     return nullptr;
-  }
-  hipGraph_t g = nullptr;
-  hipGraphExec_t x = nullptr;
-  if (hipStreamBeginCapture(c->side, hipStreamCaptureModeThreadLocal) == hipSuccess) {
-    (void)hipMemsetAsync(c->bar, 0, sizeof(unsigned), c->side);
-    if (hipStreamEndCapture(c->side, &g) == hipSuccess && g) {
-      if (hipGraphInstantiate(&x, g, nullptr, nullptr, 0) == hipSuccess && x) {
-        (void)hipGraphLaunch(x, c->side);
-        (void)hipStreamSynchronize(c->side);
-        (void)hipGraphExecDestroy(x);
-      }
-      (void)hipGraphDestroy(g);
-    }
   }
   return c;
 }
@@ -1047,7 +1038,9 @@ static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
     c->ev_panel.push_back(a);
     c->ev_bulk.push_back(b);
   }
-  if (c->nograph) {  // debugging aid: launch directly on the two streams
+  // small systems launch directly: a graph's instantiation (~5 ms measured) costs more than
+  // the host launches it saves over a whole solve (n = 264, 5 blocks: ~20 launches)
+  if (c->nograph || nblk < c->graph_min) {  // nograph: debugging aid
     if (launch) enqueue_factor_solve(c, s, n, A, lda, y, d_flag);
     return 0;
   }
@@ -1113,15 +1106,22 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
                                         kb_of(cb), d_flag, fuse ? c->pready + cb : nullptr);
   };
   panel(0);
-  int pending = -1;  // pair whose bulk update is still running on s2
-  for (int b = 0; b + 1 < nblk; b += 2) {
+  // groups of R = c->group panels (2: the pairs). Within a group the chain updates column c
+  // with the group's panels [b, c) itself; after the group's last panel but one, the bulk
+  // update applies all R panels to the columns >= b + R + 1 while the chain does column b + R.
+  const int R = std::max(2, c->group);
+  int pending = -1;  // group whose bulk update is still running on s2
+  for (int b = 0; b + 1 < nblk; b += R) {
     if (pending >= 0) (void)hipStreamWaitEvent(s, c->ev_bulk[pending], 0);
     pending = -1;
-    col(b + 1, b * NB, kb_of(b));
-    panel(b + 1);
-    if (b + 2 >= nblk) break;  // panel b + 1 was the last (its solve covered the rhs row)
-    const int kk = kb_of(b) + kb_of(b + 1);
-    const int c0 = (b + 3) * NB, m = n + 1 - c0;
+    const int cend = std::min(b + R, nblk);  // first column past the group's panels
+    for (int cc = b + 1; cc < cend; ++cc) {  // every panel before the last is NB wide
+      col(cc, b * NB, (cc - b) * NB);
+      panel(cc);
+    }
+    if (cend >= nblk) break;  // the group ended at the last panel (its solve covered the rhs row)
+    const int kk = (cend - b) * NB;
+    const int c0 = (cend + 1) * NB, m = n + 1 - c0;
     if (m > 1) {
       (void)hipEventRecord(c->ev_panel[b], s);
       (void)hipStreamWaitEvent(s2, c->ev_panel[b], 0);
@@ -1136,8 +1136,8 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
       (void)hipEventRecord(c->ev_bulk[b], s2);
       pending = b;
     }
-    col(b + 2, b * NB, kk);
-    panel(b + 2);
+    col(cend, b * NB, kk);
+    panel(cend);
   }
   if (pending >= 0) (void)hipStreamWaitEvent(s, c->ev_bulk[pending], 0);
   double* z = A + (size_t)n * lda;

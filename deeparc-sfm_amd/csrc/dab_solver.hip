@@ -475,14 +475,27 @@ struct dab_handle {
   }
 
   ~dab_handle() {
-    dev.release();
+    static const bool timing = getenv("DAB_SETUP_TIMING") != nullptr;
+    double td = now_s();
+    auto phase = [&](const char* what) {
+      if (!timing) return;
+      const double t = now_s();
+      std::fprintf(stderr, "destroy %-22s %.2f ms (%zu live, %zu pooled blocks)\n", what, 1e3 * (t - td), dev.live.size(),
+                   dev.pool.size());
+      td = t;
+    };
+    phase("start");
+    dev.clear();
+    phase("device buffers");
     for (Sticky* st : {&st_S, &st_yc, &st_flags})
       if (st->p) (void)hipFree(st->p);
     if (h_scal) (void)hipHostFree(h_scal);
     if (h_flags) (void)hipHostFree(h_flags);
     if (h_pcg_state) (void)hipHostFree(h_pcg_state);
     if (h_stage) (void)hipHostFree(h_stage);
+    phase("pinned");
     if (chol) chol_destroy(chol);
+    phase("Cholesky context");
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (ev2) (void)hipEventDestroy(ev2);
@@ -645,6 +658,14 @@ static int create_common(int device, dab_handle** out) {
                       "runtime's scheduling\n", hipGetErrorString(fe));
     }
   }
+  static const bool timing = getenv("DAB_SETUP_TIMING") != nullptr;
+  double tc = now_s();
+  auto phase = [&](const char* what) {
+    if (!timing) return;
+    const double t = now_s();
+    std::fprintf(stderr, "create %-24s %.2f ms\n", what, 1e3 * (t - tc));
+    tc = t;
+  };
   dab_handle* h = new dab_handle();
   h->device = device;
   h->knobs.read();
@@ -652,7 +673,9 @@ static int create_common(int device, dab_handle** out) {
     delete h;
     return set_error(DAB_E_DEVICE, "hipStreamCreate failed");
   }
+  phase("stream");
   h->chol = chol_create();
+  phase("Cholesky context");
   if (!h->chol) {
     delete h;
     return set_error(DAB_E_DEVICE, "Cholesky context creation failed");
@@ -670,6 +693,7 @@ static int create_common(int device, dab_handle** out) {
     delete h;
     return set_error(DAB_E_NOMEM, "hipHostMalloc failed");
   }
+  phase("events, pinned");
   // every code object of the library loaded on this device now, once per process (the first
   // kernel launch of a translation unit would otherwise pay for it mid-solve)
   static bool warmed[64] = {};
@@ -682,6 +706,7 @@ static int create_common(int device, dab_handle** out) {
     hipFuncAttributes a;
     (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k_scale_points));
     warmed[device] = true;
+    phase("code objects");
   }
   *out = h;
   return 0;
@@ -851,7 +876,10 @@ extern "C" int dab_destroy(dab_handle* h) {
   if (!h) return 0;
   (void)hipSetDevice(h->device);
   (void)hipStreamSynchronize(h->stream);
+  static const bool timing = getenv("DAB_SETUP_TIMING") != nullptr;
+  const double t0 = now_s();
   delete h;
+  if (timing) std::fprintf(stderr, "destroy %.2f ms\n", 1e3 * (now_s() - t0));
   return 0;
 }
 
@@ -2940,12 +2968,18 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
                                  : DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG;
   const bool use_pcg = opt.linear_solver_type == DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG;
   HIP_OK(hipSetDevice(h->device));
+  static const bool timing = getenv("DAB_SETUP_TIMING") != nullptr;
+  const double tp0 = now_s();
   CHECK_RC(use_pcg ? build_pcg_buffers(h) : build_schur_tables(h));
+  const double tp1 = now_s();
   // the dense factorisation's scratch and captured graph belong to the set-up, not to the
   // first LM iteration (kept while the camera count and the buffers stay the same)
   if (!use_pcg && h->NC > 0 &&
       chol_prepare(h->chol, h->stream, 6 * h->NC, h->d_S, h->lds, h->d_yc, h->d_flags + 1) != 0)
     return set_error(DAB_E_DEVICE, "dense Cholesky set-up failed");
+  if (timing)
+    std::fprintf(stderr, "solve prep: %s %.2f ms, Cholesky graph %.2f ms\n", use_pcg ? "pcg buffers" : "schur tables",
+                 1e3 * (tp1 - tp0), 1e3 * (now_s() - tp1));
   // Y records of each step: fp64 (both layouts), or fp32 for the mixed-precision PCG
   // (Jacobians, residuals, V/U/g, the CG vectors and scalars stay fp64)
   // (the matrix-free PCG of small camera sets stores no Y and is all fp64)
@@ -2983,6 +3017,7 @@ extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* 
   double t0 = now_s();
   CHECK_RC(eval_jacobian_and_blocks(h, true));
   CHECK_RC(read_scalars(h));
+  if (timing) std::fprintf(stderr, "solve iteration 0: %.2f ms\n", 1e3 * (now_s() - t0));
   {
     const int g3 = grid_for(3 * NP, 256, 1 << 20);
     k_scale_points<<<g3, 256, 0, s>>>(NP, h->d_V, h->d_scale_p, opt.jacobi_scaling);

@@ -121,53 +121,42 @@ void fmt6(FILE* f, double v) { std::fprintf(f, "%.6f", v); }  // std::fixed, set
 void fmtg(FILE* f, double v) { std::fprintf(f, "%g", v); }    // default ostream format
 
 // The observation section (five tokens per block, one block per line as every writer emits
-// it) is most of the file and of its parse time (~25 ns per from_chars double): it is cut at
-// line starts into pieces parsed on several threads into plain arrays, then the blocks are
-// created in file order. A piece whose lines do not hold exactly five well-formed tokens
-// each, or a section that is not line-aligned, is parsed again by the sequential tokenizer,
-// which gives the stream semantics (tokens may span lines) and the same values.
-void read_observations(Tokens& f, int n_blocks, std::vector<ParameterBlock*>& params_) {
-  std::vector<int> ia(n_blocks), ir(n_blocks), ip(n_blocks);
-  std::vector<double> vx(n_blocks), vy(n_blocks);
-  auto sequential = [&](int from, const char* at) -> const char* {
-    f.seek(at);
-    for (int i = from; i < n_blocks; ++i) {
-      ia[i] = f.take<int>();
-      ir[i] = f.take<int>();
-      ip[i] = f.take<int>();
-      vx[i] = f.take<double>();
-      vy[i] = f.take<double>();
-    }
-    return f.pos();
-  };
+// it) is most of the file and of its parse time (~25 ns per from_chars double), the point
+// section (six tokens per point) the next largest: a section is cut at line starts into
+// pieces parsed on several threads into plain arrays (`line(i, p, le)` parses record i from
+// one line [p, le)), then the objects are created in file order. A piece whose lines do not
+// hold exactly the record's well-formed tokens each, or a section that is not
+// line-aligned, is parsed again by the sequential tokenizer (`seq`), which gives the stream
+// semantics (tokens may span lines) and the same values.
+template <class Line, class Seq>
+void parse_section(Tokens& f, int n, int min_parallel, const Line& line, const Seq& seq) {
   const char* p0 = f.pos();
   const char* end = f.end();
-  // start of line i of the section: the header line's remainder ends at the first newline
   // DAB_READ_THREADS: most parser threads (default 8; 1 = sequential)
   static const int tmax = getenv("DAB_READ_THREADS") ? atoi(getenv("DAB_READ_THREADS")) : 8;
-  const int T = n_blocks >= 32768
+  const int T = n >= min_parallel
                     ? (int)std::min((unsigned)std::max(1, tmax), std::max(1u, std::thread::hardware_concurrency()))
                     : 1;
   bool parallel_ok = T > 1;
   std::vector<const char*> cut(T + 1, nullptr);
   if (parallel_ok) {
+    // the section starts on the line after the previous token: the rest of that line must be blank
     const char* q = static_cast<const char*>(std::memchr(p0, '\n', end - p0));
     parallel_ok = q != nullptr;
     if (parallel_ok) {
-      // the header line must end right after its last token
       for (const char* c = p0; c < q; ++c) parallel_ok = parallel_ok && std::isspace((unsigned char)*c);
       ++q;
-      long long line = 0;
+      long long ln = 0;
       int k = 0;
       cut[0] = q;
       for (int t = 1; t <= T && parallel_ok; ++t) {
-        const long long want = (long long)n_blocks * t / T;
-        while (line < want && q && q < end) {
+        const long long want = (long long)n * t / T;
+        while (ln < want && q && q < end) {
           q = static_cast<const char*>(std::memchr(q, '\n', end - q));
           if (q) ++q;
-          ++line;
+          ++ln;
         }
-        if (line < want) parallel_ok = false;
+        if (ln < want) parallel_ok = false;
         cut[++k] = q ? q : end;
       }
     }
@@ -177,17 +166,16 @@ void read_observations(Tokens& f, int n_blocks, std::vector<ParameterBlock*>& pa
     auto piece = [&](int t) {
       const char* p = cut[t];
       const char* e = cut[t + 1];
-      const int i0 = (int)((long long)n_blocks * t / T), i1 = (int)((long long)n_blocks * (t + 1) / T);
+      const int i0 = (int)((long long)n * t / T), i1 = (int)((long long)n * (t + 1) / T);
       for (int i = i0; i < i1; ++i) {
         const char* nl = static_cast<const char*>(std::memchr(p, '\n', e - p));
         const char* le = nl ? nl : e;
-        if (!(Tokens::take_at(p, le, ia[i]) && Tokens::take_at(p, le, ir[i]) && Tokens::take_at(p, le, ip[i]) &&
-              Tokens::take_at(p, le, vx[i]) && Tokens::take_at(p, le, vy[i]))) {
+        if (!line(i, p, le)) {
           bad[t] = 1;
           return;
         }
         while (p < le && std::isspace((unsigned char)*p)) ++p;
-        if (p != le) {  // a sixth token on the line
+        if (p != le) {  // a token too many on the line
           bad[t] = 1;
           return;
         }
@@ -202,14 +190,62 @@ void read_observations(Tokens& f, int n_blocks, std::vector<ParameterBlock*>& pa
     for (int t = 0; t < T; ++t) parallel_ok = parallel_ok && !bad[t];
     if (parallel_ok) f.seek(cut[T]);
   }
-  if (!parallel_ok) sequential(0, p0);
+  if (!parallel_ok) {
+    f.seek(p0);
+    seq();
+  }
+}
+
+void read_observations(Tokens& f, int n_blocks, std::vector<ParameterBlock*>& params_) {
+  std::vector<int> ia(n_blocks), ir(n_blocks), ip(n_blocks);
+  std::vector<double> vx(n_blocks), vy(n_blocks);
+  parse_section(
+      f, n_blocks, 32768,
+      [&](int i, const char*& p, const char* le) {
+        return Tokens::take_at(p, le, ia[i]) && Tokens::take_at(p, le, ir[i]) && Tokens::take_at(p, le, ip[i]) &&
+               Tokens::take_at(p, le, vx[i]) && Tokens::take_at(p, le, vy[i]);
+      },
+      [&]() {
+        for (int i = 0; i < n_blocks; ++i) {
+          ia[i] = f.take<int>();
+          ir[i] = f.take<int>();
+          ip[i] = f.take<int>();
+          vx[i] = f.take<double>();
+          vy[i] = f.take<double>();
+        }
+      });
   params_.reserve(params_.size() + n_blocks);
   for (int i = 0; i < n_blocks; ++i) params_.push_back(new ParameterBlock(ia[i], ir[i], ip[i], new Point2d(vx[i], vy[i])));
+}
+
+// points: x y z r g b, colour read as double and truncated (Q2)
+void read_points(Tokens& f, int n_points, std::vector<Point3d*>& point3d_) {
+  std::vector<double> v(6 * (size_t)n_points);
+  parse_section(
+      f, n_points, 8192,
+      [&](int i, const char*& p, const char* le) {
+        double* o = &v[6 * (size_t)i];
+        for (int j = 0; j < 6; ++j)
+          if (!Tokens::take_at(p, le, o[j])) return false;
+        return true;
+      },
+      [&]() {
+        for (size_t j = 0; j < v.size(); ++j) v[j] = f.take<double>();
+      });
+  point3d_.reserve(point3d_.size() + n_points);
+  for (int i = 0; i < n_points; ++i) {
+    const double* o = &v[6 * (size_t)i];
+    point3d_.push_back(new Point3d(o[0], o[1], o[2], (int)o[3], (int)o[4], (int)o[5]));
+  }
 }
 
 }  // namespace
 
 void Extrinsic::rotationMatrix(double R[9]) { dab::AngleAxisToRotationMatrix(rotation_, R); }
+
+Point3d::~Point3d() {
+  for (ParameterBlock* b : blocks_) b->forget_point3d();
+}
 
 DeepArcManager::~DeepArcManager() { clear(); }
 
@@ -219,8 +255,9 @@ DabSession& DeepArcManager::dabSession() {
 }
 
 void DeepArcManager::clear() {
-  for (ParameterBlock* b : params_) delete b;
+  // points first: each one clears its blocks' links, so the blocks need not unlink
   for (Point3d* p : point3d_) delete p;
+  for (ParameterBlock* b : params_) delete b;
   for (Intrinsic* k : intrinsics_) delete k;
   for (Extrinsic* e : extrinsics_) delete e;
   for (Camera* c : camera_) delete c;
@@ -235,6 +272,15 @@ void DeepArcManager::clear() {
 }
 
 bool DeepArcManager::read(std::string filename) {
+  // DAB_READ_TIMING=1: phase times on stderr
+  static const bool timing = getenv("DAB_READ_TIMING") != nullptr;
+  double tr = dab_now_seconds();
+  auto phase = [&](const char* what) {
+    if (!timing) return;
+    const double t = dab_now_seconds();
+    std::fprintf(stderr, "read %-14s %.2f ms\n", what, 1e3 * (t - tr));
+    tr = t;
+  };
   std::ifstream in(filename, std::ios::binary);
   if (in.fail()) {
     std::cout << "Cannot read " << filename << std::endl;
@@ -250,7 +296,9 @@ bool DeepArcManager::read(std::string filename) {
     if (!in) throw "Cannot read input file";
   }
   Tokens f(std::move(text));
+  phase("file");
   clear();
+  phase("clear");
   ++structure_version_;
   (void)f.take<double>();  // version
   const int n_blocks = f.take<int>(), n_intr = f.take<int>(), n_arc = f.take<int>(), n_ring = f.take<int>(),
@@ -263,6 +311,7 @@ bool DeepArcManager::read(std::string filename) {
 
   // observation lines: pos_arc pos_ring point_id x y
   read_observations(f, n_blocks, params_);
+  phase("observations");
   // intrinsics: cx cy nf f[nf] nk k[nk]; the principal point truncates to int (Q1)
   for (int i = 0; i < n_intr; ++i) {
     Intrinsic* k = new Intrinsic();
@@ -296,13 +345,9 @@ bool DeepArcManager::read(std::string filename) {
     else if (nr == 4) dab::QuaternionToAngleAxis(rot, aa);
     e->rotation(nr == 3 ? rot : aa);
   }
-  // points: x y z r g b, colour read as double and truncated (Q2)
-  for (int i = 0; i < n_points; ++i) {
-    const double x = f.take<double>(), y = f.take<double>(), z = f.take<double>();
-    const double r = f.take<double>(), g = f.take<double>(), b = f.take<double>();
-    point3d_.push_back(new Point3d(x, y, z, (int)r, (int)g, (int)b));
-  }
+  read_points(f, n_points, point3d_);
 
+  phase("cameras, points");
   auto need = [](bool ok) {
     if (!ok) throw "Malformed .deeparc file: index out of range";
   };
@@ -326,9 +371,16 @@ bool DeepArcManager::read(std::string filename) {
       camera_.push_back(new Camera(intrinsics_[ei.second], extrinsics_[ei.first]));
     }
   }
+  {  // every point's link list at its final size (no growth reallocations)
+    std::vector<int> nlink(n_points, 0);
+    for (ParameterBlock* b : params_) {
+      need(b->point3d_id() >= 0 && b->point3d_id() < n_points);
+      ++nlink[b->point3d_id()];
+    }
+    for (int i = 0; i < n_points; ++i) point3d_[i]->reserve_links(nlink[i]);
+  }
   for (ParameterBlock* b : params_) {
     need(b->intrinsic_id() >= 0 && b->intrinsic_id() < n_intr);
-    need(b->point3d_id() >= 0 && b->point3d_id() < n_points);
     b->intrinsic(intrinsics_[b->intrinsic_id()]);
     b->point3d(point3d_[b->point3d_id()]);
     if (share_extrinsic_) {
@@ -342,6 +394,7 @@ bool DeepArcManager::read(std::string filename) {
       b->share_extrinsic(false);
     }
   }
+  phase("links");
   return true;
 }
 
@@ -505,8 +558,7 @@ void DeepArcManager::filterPoint3d(double error_boundary, double* hemisphere_cen
     if (keep_pt[i]) {
       point3d_[w++] = point3d_[i];
     } else {
-      for (ParameterBlock* b : point3d_[i]->total_link()) b->point3d(nullptr);  // none remain
-      delete point3d_[i];
+      delete point3d_[i];  // clears the links of any block still on it (none remain)
     }
   }
   const bool changed = w != point3d_.size() || params_.size() != keep_obs.size();

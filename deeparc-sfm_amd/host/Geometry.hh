@@ -12,26 +12,29 @@ class ParameterBlock;
 
 // Fixed-size object pool behind a class's operator new / delete: the reader allocates one
 // ParameterBlock and one Point2d per observation (320k objects for the 160k-observation
-// config-1 scene) and the filter deletes them one by one; a free list over 64K-object
-// chunks makes each a few instructions instead of a malloc / free pair. Chunks are kept for
-// the life of the process. Guarded by a mutex (managers may live on different threads).
+// config-1 scene) and the filter and the manager's destructor delete them one by one. Each
+// thread keeps its own free list and trades nodes with the process-wide list (64K-object
+// chunks, kept for the life of the process) in batches of kBatch under a mutex, so a take or
+// a give is a few instructions and no lock. An object may be freed on another thread than
+// the one that made it.
 template <size_t SIZE>
 class ObjectPool {
  public:
   static void* take() {
-    std::lock_guard<std::mutex> lk(mu());
-    Node*& f = head();
-    if (!f) refill(f);
-    Node* n = f;
-    f = n->next;
+    Local& l = local();
+    if (!l.head) l.refill();
+    Node* n = l.head;
+    l.head = n->next;
+    --l.count;
     return n;
   }
   static void give(void* p) {
     if (!p) return;
-    std::lock_guard<std::mutex> lk(mu());
+    Local& l = local();
     Node* n = static_cast<Node*>(p);
-    n->next = head();
-    head() = n;
+    n->next = l.head;
+    l.head = n;
+    if (++l.count >= 2 * kBatch) l.flush(kBatch);
   }
 
  private:
@@ -39,20 +42,67 @@ class ObjectPool {
     Node* next;
     alignas(16) unsigned char bytes[SIZE];
   };
-  static constexpr size_t kChunk = 1 << 16;
-  static std::mutex& mu() {
-    static std::mutex m;
-    return m;
+  static constexpr size_t kChunk = 1 << 16, kBatch = 4096;
+  struct Global {
+    std::mutex mu;
+    Node* head = nullptr;
+  };
+  static Global& global() {
+    static Global* g = new Global();  // never destroyed: thread-local flushes may run at exit
+    return *g;
   }
-  static Node*& head() {
-    static Node* h = nullptr;
-    return h;
-  }
-  static void refill(Node*& f) {
-    Node* c = static_cast<Node*>(::operator new(sizeof(Node) * kChunk));
-    for (size_t i = 0; i + 1 < kChunk; ++i) c[i].next = &c[i + 1];
-    c[kChunk - 1].next = f;
-    f = c;
+  struct Local {
+    Node* head = nullptr;
+    size_t count = 0;
+    void refill() {
+      Global& g = global();
+      std::lock_guard<std::mutex> lk(g.mu);
+      if (!g.head) {
+        Node* c = static_cast<Node*>(::operator new(sizeof(Node) * kChunk));
+        for (size_t i = 0; i + 1 < kChunk; ++i) c[i].next = &c[i + 1];
+        c[kChunk - 1].next = nullptr;
+        g.head = c;
+      }
+      // up to kBatch nodes from the global list
+      Node* first = g.head;
+      Node* last = first;
+      size_t n = 1;
+      while (n < kBatch && last->next) {
+        last = last->next;
+        ++n;
+      }
+      g.head = last->next;
+      last->next = head;
+      head = first;
+      count += n;
+    }
+    // the nodes past the first `keep` back to the global list
+    void flush(size_t keep) {
+      Node* cut = head;
+      Node** link = &head;
+      for (size_t i = 0; i < keep && cut; ++i) {
+        link = &cut->next;
+        cut = cut->next;
+      }
+      if (!cut) return;
+      Node* last = cut;
+      size_t n = 1;
+      while (last->next) {
+        last = last->next;
+        ++n;
+      }
+      *link = nullptr;
+      count -= n;
+      Global& g = global();
+      std::lock_guard<std::mutex> lk(g.mu);
+      last->next = g.head;
+      g.head = cut;
+    }
+    ~Local() { flush(0); }
+  };
+  static Local& local() {
+    thread_local Local l;
+    return l;
   }
 };
 #define DAB_POOLED(T)                                                              \
@@ -82,6 +132,11 @@ class Point3d {
  public:
   Point3d(double x, double y, double z, int r = 255, int g = 255, int b = 255)
       : require_remove_(false), r_(r), g_(g), b_(b), id_(-1), position_{x, y, z} {}
+  // the blocks still linked to this point forget it (ParameterBlock::point3d() becomes null),
+  // so deleting the points before their blocks needs no per-block unlink (DeepArcManager.cc)
+  ~Point3d();
+  Point3d(const Point3d&) = delete;
+  Point3d& operator=(const Point3d&) = delete;
   int r() { return r_; }
   int g() { return g_; }
   int b() { return b_; }
@@ -105,6 +160,7 @@ class Point3d {
     }
   }
   std::set<ParameterBlock*> total_link() { return std::set<ParameterBlock*>(blocks_.begin(), blocks_.end()); }
+  void reserve_links(size_t n) { blocks_.reserve(n); }
   bool empty() { return blocks_.empty(); }
   // the solver adapter's scratch: this point's index in the manager's list (DabScene::build)
   int slot() { return slot_; }

@@ -45,6 +45,8 @@ class ParameterBlock {
     point3d_ = p;
     if (point3d_) point3d_->link(this);
   }
+  // the linked point is going away (Point3d's destructor): forget it without unlinking
+  void forget_point3d() { point3d_ = nullptr; }
   void share_extrinsic(bool v) { share_extrinsic_ = v; }
   void require_remove(bool v) { require_remove_ = v; }
 

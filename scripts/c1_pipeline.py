@@ -38,13 +38,17 @@ with tempfile.TemporaryDirectory() as td:
 # one handle: set-up and first solve of the config-1 problem, then a warm re-solve
 c1 = pkg.synth(**pkg.CONFIGS["c1_rig_8x36"])
 o1 = pkg.options(max_num_iterations=10)
-s = pkg.Solver(0)
-t0 = time.perf_counter()
-s.set_problem(c1.copy())
-t1 = time.perf_counter()
-g = s.solve(o1)
-t2 = time.perf_counter()
-print(json.dumps({"set_problem_ms": round(1e3 * (t1 - t0), 2), "first_solve_ms": round(1e3 * (t2 - t1), 2),
-                  "lm_ms": round(1e3 * g["total_time"], 2) if "total_time" in g else None,
-                  "iterations": g["num_iterations"]}))
-s.close()
+for rep in range(2):
+    tc = time.perf_counter()
+    s = pkg.Solver(0)
+    t0 = time.perf_counter()
+    s.set_problem(c1.copy())
+    t1 = time.perf_counter()
+    g = s.solve(o1)
+    t2 = time.perf_counter()
+    s.close()
+    t3 = time.perf_counter()
+    print(json.dumps({"create_ms": round(1e3 * (t0 - tc), 2), "set_problem_ms": round(1e3 * (t1 - t0), 2),
+                      "first_solve_ms": round(1e3 * (t2 - t1), 2), "destroy_ms": round(1e3 * (t3 - t2), 2),
+                      "lm_ms": round(1e3 * g["total_time"], 2) if "total_time" in g else None,
+                      "iterations": g["num_iterations"]}), flush=True)
