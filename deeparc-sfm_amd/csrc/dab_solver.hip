@@ -201,23 +201,34 @@ struct Dev {
     void* p;
     size_t bytes;
     int age;
+    bool slab;  // carved from a slab: never freed on its own
   };
-  std::vector<Blk> live, pool;
-  ~Dev() {
-    for (const Blk& b : live) (void)hipFree(b.p);
-    for (const Blk& b : pool) (void)hipFree(b.p);
-  }
+  std::vector<Blk> live, pool, spare;  // spare: slab pieces aged out of the pool
+  // Blocks up to kSmall come from 8 MB slabs (bump-allocated; a handle's few dozen small
+  // buffers cost one hipMalloc instead of one each, and the handle's destruction a few
+  // hipFrees instead of dozens)
+  static constexpr size_t kSlab = (size_t)8 << 20, kSmall = (size_t)1 << 20;
+  std::vector<void*> slabs;
+  size_t slab_off = kSlab;
+  ~Dev() { clear(); }
   void clear() {  // free everything now, pooled blocks included
-    for (const Blk& b : live) (void)hipFree(b.p);
-    for (const Blk& b : pool) (void)hipFree(b.p);
+    for (const Blk& b : live)
+      if (!b.slab) (void)hipFree(b.p);
+    for (const Blk& b : pool)
+      if (!b.slab) (void)hipFree(b.p);
+    for (void* q : slabs) (void)hipFree(q);
     live.clear();
     pool.clear();
+    spare.clear();
+    slabs.clear();
+    slab_off = kSlab;
   }
   void release() {
     std::vector<Blk> keep;
     for (Blk& b : pool) {
-      if (++b.age >= 2) (void)hipFree(b.p);
-      else keep.push_back(b);
+      if (++b.age < 2) keep.push_back(b);
+      else if (b.slab) spare.push_back(b);
+      else (void)hipFree(b.p);
     }
     for (Blk b : live) {
       b.age = 0;
@@ -226,31 +237,58 @@ struct Dev {
     pool.swap(keep);
     live.clear();
   }
+  // best fit in v among blocks of bytes .. cap; v.size() when none
+  static size_t best_fit(const std::vector<Blk>& v, size_t bytes, size_t cap) {
+    size_t best = v.size();
+    for (size_t i = 0; i < v.size(); ++i)
+      if (v[i].bytes >= bytes && v[i].bytes <= cap && (best == v.size() || v[i].bytes < v[best].bytes)) best = i;
+    return best;
+  }
   template <class T>
   int alloc(T** out, size_t n) {
     if (n == 0) n = 1;
     const size_t bytes = (n * sizeof(T) + 255) & ~(size_t)255;
     const size_t cap = std::max(2 * bytes, bytes + ((size_t)1 << 20));
-    size_t best = pool.size();
-    for (size_t i = 0; i < pool.size(); ++i)
-      if (pool[i].bytes >= bytes && pool[i].bytes <= cap && (best == pool.size() || pool[i].bytes < pool[best].bytes))
-        best = i;
-    void* p = nullptr;
-    size_t got = bytes;
-    if (best < pool.size()) {
-      p = pool[best].p;
-      got = pool[best].bytes;
-      pool[best] = pool.back();
-      pool.pop_back();
-    } else if (hipMalloc(&p, bytes) != hipSuccess) {
-      // the pool may hold what the device needs: give it back and try once more
-      for (const Blk& b : pool) (void)hipFree(b.p);
-      pool.clear();
-      if (hipMalloc(&p, bytes) != hipSuccess)
-        return set_error(DAB_E_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
+    Blk got{nullptr, bytes, 0, false};
+    for (std::vector<Blk>* v : {&pool, &spare}) {
+      const size_t i = best_fit(*v, bytes, cap);
+      if (i < v->size()) {
+        got = (*v)[i];
+        got.age = 0;
+        (*v)[i] = v->back();
+        v->pop_back();
+        break;
+      }
     }
-    live.push_back(Blk{p, got, 0});
-    *out = static_cast<T*>(p);
+    if (!got.p && bytes <= kSmall) {
+      if (slab_off + bytes > kSlab) {
+        void* q = nullptr;
+        if (hipMalloc(&q, kSlab) == hipSuccess) {
+          slabs.push_back(q);
+          slab_off = 0;
+        }
+      }
+      if (slab_off + bytes <= kSlab) {
+        got = Blk{static_cast<char*>(slabs.back()) + slab_off, bytes, 0, true};
+        slab_off += bytes;
+      }
+    }
+    if (!got.p) {
+      void* p = nullptr;
+      if (hipMalloc(&p, bytes) != hipSuccess) {
+        // the pool may hold what the device needs: give it back and try once more
+        for (const Blk& b : pool) {
+          if (b.slab) spare.push_back(b);
+          else (void)hipFree(b.p);
+        }
+        pool.clear();
+        if (hipMalloc(&p, bytes) != hipSuccess)
+          return set_error(DAB_E_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
+      }
+      got = Blk{p, bytes, 0, false};
+    }
+    live.push_back(got);
+    *out = static_cast<T*>(got.p);
     return 0;
   }
 };
