@@ -1433,6 +1433,7 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
                                  int* d_flag);
 
 static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag, bool launch);
+static int flow_prepare(CholCtx* c, int n, int lda);
 int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag) {
   return chol_build(c, s, n, A, lda, y, d_flag, true);
 }
@@ -1459,6 +1460,7 @@ static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
     c->nblk_alloc = nblk;
   }
   if (!c->side && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) return -3;
+  if (flow_prepare(c, n, lda) != 0) return -2;
   if (!c->bar && hipMalloc(&c->bar, sizeof(unsigned)) != hipSuccess) return -2;
   while ((int)c->ev_panel.size() < nblk) {
     hipEvent_t a, b;
@@ -1501,9 +1503,15 @@ static void enqueue_back_substitution(CholCtx* c, hipStream_t s, int n, double* 
                                       int* d_flag);
 // The persistent factorisation when it applies (enough blocks, every work-group resident,
 // 32-bit offsets): the flags zeroed, the one launch, then the back substitution.
-static bool flow_enqueue(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag) {
-  const int nblk = (n + NB - 1) / NB, rblk = (n + 1 + NB - 1) / NB;
-  if (!c->flow || nblk < c->flow_min) return false;
+static bool flow_applies(const CholCtx* c, int n, int lda) {
+  const int nblk = (n + NB - 1) / NB;
+  const size_t a_bytes = sizeof(double) * (size_t)(n + 1) * lda, b_bytes = sizeof(double) * (size_t)kBlk * nblk;
+  return c->flow && nblk >= c->flow_min && c->flow_grid > c->flow_ga + 8 && a_bytes < (1ull << 31) &&
+         b_bytes < (1ull << 31);
+}
+// outside any stream capture (occupancy query, allocation): the grid and the flag words
+static int flow_prepare(CholCtx* c, int n, int lda) {
+  if (!c->flow) return 0;
   if (c->flow_grid == 0) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_chol_flow), kFlowThreads,
@@ -1511,17 +1519,25 @@ static bool flow_enqueue(CholCtx* c, hipStream_t s, int n, double* A, int lda, d
       per_cu = 0;
     c->flow_grid = per_cu >= 2 ? 2 * c->ncu : -1;
   }
-  const int G = c->flow_grid;
-  const size_t a_bytes = sizeof(double) * (size_t)(n + 1) * lda, b_bytes = sizeof(double) * (size_t)kBlk * nblk;
-  if (G <= c->flow_ga + 8 || a_bytes >= (1ull << 31) || b_bytes >= (1ull << 31)) return false;
+  if (!flow_applies(c, n, lda)) return 0;
+  const int nblk = (n + NB - 1) / NB, rblk = (n + 1 + NB - 1) / NB;
   const size_t nw = (size_t)nblk + rblk + (size_t)rblk * nblk + 1;
   if (nw > c->words_alloc) {
     if (c->words) (void)hipFree(c->words);
     c->words = nullptr;
     c->words_alloc = 0;
-    if (hipMalloc(&c->words, sizeof(unsigned) * nw) != hipSuccess) return false;
+    if (hipMalloc(&c->words, sizeof(unsigned) * nw) != hipSuccess) return -2;
     c->words_alloc = nw;
   }
+  return 0;
+}
+static bool flow_enqueue(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag) {
+  if (!flow_applies(c, n, lda)) return false;
+  const int nblk = (n + NB - 1) / NB, rblk = (n + 1 + NB - 1) / NB;
+  const size_t nw = (size_t)nblk + rblk + (size_t)rblk * nblk + 1;
+  if (nw > c->words_alloc) return false;
+  const int G = c->flow_grid;
+  const size_t a_bytes = sizeof(double) * (size_t)(n + 1) * lda, b_bytes = sizeof(double) * (size_t)kBlk * nblk;
   (void)hipMemsetAsync(c->words, 0, sizeof(unsigned) * nw, s);
   FlowArgs f{A, (unsigned)a_bytes, lda, n, nblk, rblk, std::max(2, c->group), c->flow_ga, c->blk, (unsigned)b_bytes,
              d_flag, c->words};

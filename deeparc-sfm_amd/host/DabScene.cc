@@ -44,6 +44,7 @@ void DabScene::build(DeepArcManager& m, bool freeze_camera) {
   obs_ext1.resize(N);
   obs_intr.resize(N);
   ext_const.assign(exts.size(), 0);
+  obs_gauge.resize(N);
   for (size_t o = 0; o < N; ++o) {
     ParameterBlock* b = blocks[o];
     xy[2 * o] = b->point2d()->x();
@@ -54,7 +55,8 @@ void DabScene::build(DeepArcManager& m, bool freeze_camera) {
     Extrinsic* e1 = b->second_extrinsic();
     obs_ext1[o] = e1 ? find(exts, e1) : -1;
     // gauge: the extrinsic of a (0,0) block is constant (sfm.cc:50-53)
-    if (b->pos_arc() == 0 && b->pos_ring() == 0) ext_const[obs_ext0[o]] = 1;
+    obs_gauge[o] = b->pos_arc() == 0 && b->pos_ring() == 0;
+    if (obs_gauge[o]) ext_const[obs_ext0[o]] = 1;
   }
   points.resize(3 * pts.size());
   for (size_t i = 0; i < pts.size(); ++i)
@@ -80,11 +82,15 @@ void DabScene::build(DeepArcManager& m, bool freeze_camera) {
     o[4] = intr_nk[i] >= 1 ? k->distrotion()[0] : 0.0;
     o[5] = intr_nk[i] >= 2 ? k->distrotion()[1] : 0.0;
   }
+  bind(freeze_camera);
+}
+
+void DabScene::bind(bool freeze_camera) {
   problem = dab_problem{};
-  problem.num_obs = (int32_t)N;
-  problem.num_points = (int32_t)pts.size();
-  problem.num_ext = (int32_t)exts.size();
-  problem.num_intr = (int32_t)ks.size();
+  problem.num_obs = (int32_t)obs_point.size();
+  problem.num_points = (int32_t)(points.size() / 3);
+  problem.num_ext = (int32_t)(ext.size() / 6);
+  problem.num_intr = (int32_t)intr_nf.size();
   problem.obs_xy = xy.data();
   problem.obs_point = obs_point.data();
   problem.obs_ext0 = obs_ext0.data();
@@ -97,6 +103,42 @@ void DabScene::build(DeepArcManager& m, bool freeze_camera) {
   problem.intr_nk = intr_nk.data();
   problem.ext_const = ext_const.data();
   problem.freeze_camera = freeze_camera ? 1 : 0;
+}
+
+bool DabScene::compact(const uint8_t* keep_obs, const uint8_t* keep_pt) {
+  const size_t N = obs_point.size(), NP = points.size() / 3;
+  std::vector<int32_t> remap(NP, -1);
+  size_t w = 0;
+  for (size_t i = 0; i < NP; ++i)
+    if (keep_pt[i]) {
+      remap[i] = (int32_t)w;
+      for (int k = 0; k < 3; ++k) points[3 * w + k] = points[3 * i + k];
+      ++w;
+    }
+  points.resize(3 * w);
+  std::fill(ext_const.begin(), ext_const.end(), 0);
+  w = 0;
+  for (size_t o = 0; o < N; ++o) {
+    if (!keep_obs[o]) continue;
+    const int32_t p = remap[obs_point[o]];
+    if (p < 0) return false;  // an observation of a removed point: the caller rebuilds
+    xy[2 * w] = xy[2 * o];
+    xy[2 * w + 1] = xy[2 * o + 1];
+    obs_point[w] = p;
+    obs_ext0[w] = obs_ext0[o];
+    obs_ext1[w] = obs_ext1[o];
+    obs_intr[w] = obs_intr[o];
+    obs_gauge[w] = obs_gauge[o];
+    if (obs_gauge[w]) ext_const[obs_ext0[w]] = 1;
+    ++w;
+  }
+  xy.resize(2 * w);
+  obs_point.resize(w);
+  obs_ext0.resize(w);
+  obs_ext1.resize(w);
+  obs_intr.resize(w);
+  obs_gauge.resize(w);
+  return true;
 }
 
 void DabScene::refresh_values(DeepArcManager& m) {
@@ -125,7 +167,17 @@ int DabSession::ensure(DeepArcManager& m, int want_freeze) {
   }
   resident = false;
   freeze = want_freeze > 0;
-  scene.build(m, freeze);  // throws const char* on a block that references a foreign parameter
+  if (scene_valid && scene_version == m.structureVersion() && scene.obs_point.size() == m.parameters()->size() &&
+      scene.points.size() == 3 * m.point3ds()->size() && scene.ext.size() == 6 * m.extrinsics()->size() &&
+      scene.intr_nf.size() == m.intrinsics()->size()) {
+    scene.refresh_values(m);  // the arrays are the compacted ones: only the values may differ
+    scene.bind(freeze);
+  } else {
+    scene_valid = false;
+    scene.build(m, freeze);  // throws const char* on a block that references a foreign parameter
+    scene_valid = true;
+    scene_version = m.structureVersion();
+  }
   const double t1 = dab_now_seconds();
   t.marshal += t1 - t0;
   const int rc = dab_set_problem(handle.h, &scene.problem);
@@ -150,4 +202,19 @@ void DabScene::write_back(DeepArcManager& m) {
       exts[i]->rotation()[k] = ext[6 * i + k];
       exts[i]->translation()[k] = ext[6 * i + 3 + k];
     }
+}
+
+void DabSession::filtered(DeepArcManager& m, unsigned long long old_version, const uint8_t* keep_obs,
+                          const uint8_t* keep_pt) {
+  // DAB_SCENE_COMPACT=0: always rebuild from the blocks (A/B)
+  const char* knob = getenv("DAB_SCENE_COMPACT");
+  const bool on = !knob || atoi(knob) != 0;
+  if (!on || !scene_valid || scene_version != old_version) {
+    scene_valid = false;
+    return;
+  }
+  const double t0 = dab_now_seconds();
+  scene_valid = scene.compact(keep_obs, keep_pt);
+  scene_version = m.structureVersion();
+  t.marshal += dab_now_seconds() - t0;
 }

@@ -563,6 +563,10 @@ void DeepArcManager::filterPoint3d(double error_boundary, double* hemisphere_cen
   }
   const bool changed = w != point3d_.size() || params_.size() != keep_obs.size();
   point3d_.resize(w);
-  if (changed) ++structure_version_;  // the resident problem no longer matches
+  if (changed) {
+    ++structure_version_;  // the resident problem no longer matches
+    // the session's arrays follow the same compaction (the next set-up needs no marshal)
+    if (session_) session_->filtered(*this, structure_version_ - 1, keep_obs.data(), keep_pt.data());
+  }
   dabSession().t.filter_host += dab_now_seconds() - th;
 }

@@ -107,6 +107,27 @@ def test_pipeline_matches_oracle(pkg, host, ref, gpu, tmp_path):
     np.testing.assert_allclose(xyz, np.array([p["X"] for p in s["points"]]).reshape(-1, 3), rtol=0, atol=2e-6)
 
 
+def test_pipeline_scene_compaction_matches_rebuild(pkg, host, gpu, tmp_path, monkeypatch):
+    """After each filter the adapter compacts its marshalled arrays with the filter's keep
+    masks instead of walking the blocks again (DAB_SCENE_COMPACT=0 rebuilds): the pipeline's
+    rounds, solves, LM iterations, cost and output file are identical either way."""
+    import gen_deeparc_fixtures as gen
+    prob = pkg.synth(kind=1, num_arcs=4, num_rings=8, num_points=600, obs_per_point=6, seed=81,
+                     pixel_noise=3.0)
+    path = tmp_path / "rig.deeparc"
+    path.write_text(gen.problem_to_deeparc(prob, True, 4, 8, [3], np.random.default_rng(0)))
+    reps, texts = [], []
+    for knob in ("1", "0"):
+        monkeypatch.setenv("DAB_SCENE_COMPACT", knob)
+        out = tmp_path / ("out%s.deeparc" % knob)
+        reps.append(host.run_pipeline_report(str(path), str(out), max_iteration=50, quiet=True))
+        texts.append(out.read_text())
+    a, b = reps
+    for k in ("rounds", "solves", "lm_iterations", "blocks", "points", "final_cost"):
+        assert a[k] == b[k], k
+    assert texts[0] == texts[1]
+
+
 def test_pipeline_config1_full_size(pkg, host, gpu, tmp_path):
     """BASELINE config 1 shape (rig 8 x 36, 20k points, m = 8) end to end on the GPU:
     properties only (the CPU oracle takes minutes at this size)."""
