@@ -382,7 +382,7 @@ bool DeepArcManager::read(std::string filename) {
   for (ParameterBlock* b : params_) {
     need(b->intrinsic_id() >= 0 && b->intrinsic_id() < n_intr);
     b->intrinsic(intrinsics_[b->intrinsic_id()]);
-    b->point3d(point3d_[b->point3d_id()]);
+    b->attach_new_point3d(point3d_[b->point3d_id()]);  // a new block: linked once
     if (share_extrinsic_) {
       need(b->pos_arc() < n_ext && b->pos_ring() >= 0 && b->pos_ring() < n_ring);
       b->arc(extrinsics_[b->pos_arc()]);

@@ -161,6 +161,8 @@ class Point3d {
   }
   std::set<ParameterBlock*> total_link() { return std::set<ParameterBlock*>(blocks_.begin(), blocks_.end()); }
   void reserve_links(size_t n) { blocks_.reserve(n); }
+  // a block that is linked for the first time (the reader): no duplicate search
+  void link_new(ParameterBlock* b) { blocks_.push_back(b); }
   bool empty() { return blocks_.empty(); }
   // the solver adapter's scratch: this point's index in the manager's list (DabScene::build)
   int slot() { return slot_; }

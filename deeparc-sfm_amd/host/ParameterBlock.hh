@@ -45,6 +45,11 @@ class ParameterBlock {
     point3d_ = p;
     if (point3d_) point3d_->link(this);
   }
+  // the reader's first link of a new block (point3d() == nullptr before)
+  void attach_new_point3d(Point3d* p) {
+    point3d_ = p;
+    p->link_new(this);
+  }
   // the linked point is going away (Point3d's destructor): forget it without unlinking
   void forget_point3d() { point3d_ = nullptr; }
   void share_extrinsic(bool v) { share_extrinsic_ = v; }
