@@ -70,6 +70,9 @@ struct CholCtx {
   int flow_grid = 0;        // work-groups that are resident together (0: the kernel does not fit)
   unsigned* words = nullptr;  // its flags, zeroed per factorisation
   size_t words_alloc = 0;
+  bool stamps_on = false;     // DAB_CHOL_FLOW_STAMPS=1: per-column timeline on stderr after each factorisation
+  unsigned long long* stamps = nullptr;
+  size_t stamps_alloc = 0;
   bool v1 = false;          // DAB_CHOL_V1=1: the per-step schedule (one bulk update per panel, one
                             // back-substitution launch per block)
 };
@@ -93,6 +96,7 @@ CholCtx* chol_create() {
   if (const char* e = getenv("DAB_CHOL_FLOW")) c->flow = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_FLOW_MIN")) c->flow_min = atoi(e);
   if (const char* e = getenv("DAB_CHOL_FLOW_GA")) c->flow_ga = std::max(1, atoi(e));
+  c->stamps_on = getenv("DAB_CHOL_FLOW_STAMPS") != nullptr;
   if (const char* e = getenv("DAB_CHOL_BACK_FLOW")) c->back_flow = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_PREFACTOR")) c->prefactor = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_FUSE_PANEL")) c->fuse_panel = atoi(e) != 0;
@@ -121,6 +125,7 @@ void chol_destroy(CholCtx* c) {
   if (c->blk) (void)hipFree(c->blk);
   if (c->bar) (void)hipFree(c->bar);
   if (c->words) (void)hipFree(c->words);
+  if (c->stamps) (void)hipFree(c->stamps);
   if (c->ready) (void)hipFree(c->ready);
   if (c->pready) (void)hipFree(c->pready);
   for (hipEvent_t e : c->ev_panel) (void)hipEventDestroy(e);
@@ -1073,7 +1078,14 @@ struct FlowArgs {
   unsigned blk_bytes;
   int* flag;
   unsigned* words;  // [pready: nblk][rowdone: rblk][bulkcnt: rblk * nblk][abort: 1], zeroed per launch
+  // DAB_CHOL_FLOW_STAMPS=1 (timeline, s_memrealtime at 100 MHz): [0] start, per column c
+  // [1 + 3c]: the diagonal tile's inputs ready, [2 + 3c]: factor start, [3 + 3c]: L_cc
+  // published; per group g [1 + 3 nblk + g]: its last super-tile done (max); else null
+  unsigned long long* stamps;
 };
+__device__ __forceinline__ void flow_stamp(unsigned long long* st, size_t i) {
+  if (st) __hip_atomic_store(st + i, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // lane 0 of the work-group: wait until *w >= want (relaxed agent-scope polls); false on a
 // timeout (flag |= 2, abort set) or when another work-group has aborted
@@ -1184,6 +1196,7 @@ __device__ __noinline__ void flow_chain_tile(const FlowArgs& f, const Sc1& A, co
       }
     }
     __syncthreads();
+    if (tid == 0) flow_stamp(f.stamps, 2 + 3 * (size_t)c);
     bool bad = false;
     factor64(L, Dsh, bad);
     if (tid == 0 && bad) atomicOr(f.flag, 1);
@@ -1200,7 +1213,10 @@ __device__ __noinline__ void flow_chain_tile(const FlowArgs& f, const Sc1& A, co
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_store(f.words + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {
+      __hip_atomic_store(f.words + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flow_stamp(f.stamps, 3 + 3 * (size_t)c);
+    }
     if (!rows_below) return;
   } else {
     if (w < 4) {
@@ -1357,6 +1373,7 @@ __global__ __launch_bounds__(kFlowThreads, 2) void k_chol_flow(FlowArgs f) {
   unsigned* abortw = bulkcnt + (size_t)f.rblk * f.nblk;
   const int R = f.R, nblk = f.nblk, rblk = f.rblk, n = f.n;
   if (tid == 0) abort_s = 0;
+  if (tid == 0 && blockIdx.x == 0) flow_stamp(f.stamps, 0);
   __syncthreads();
   if ((int)blockIdx.x < f.GA) {
     // ---- chain ----
@@ -1374,6 +1391,7 @@ __global__ __launch_bounds__(kFlowThreads, 2) void k_chol_flow(FlowArgs f) {
         }
         __syncthreads();
         if (abort_s) return;
+        if (t == c && tid == 0) flow_stamp(f.stamps, 1 + 3 * (size_t)c);
         flow_chain_tile(f, A, B, t, c, b, sm, abort_s);
         if (abort_s) return;
         __syncthreads();  // the tile's LDS reads are done before the next tile's staging
@@ -1424,6 +1442,9 @@ __global__ __launch_bounds__(kFlowThreads, 2) void k_chol_flow(FlowArgs f) {
           if (tr < rblk && tr * NB <= n && tc < nblk && tc <= tr)
             __hip_atomic_fetch_add(bulkcnt + (size_t)tr * nblk + tc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        if (f.stamps)
+          __hip_atomic_fetch_max(f.stamps + 1 + 3 * (size_t)nblk + g, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -1434,6 +1455,7 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
 
 static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag, bool launch);
 static int flow_prepare(CholCtx* c, int n, int lda);
+static void flow_print_stamps(CholCtx* c, hipStream_t s, int n);
 int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag) {
   return chol_build(c, s, n, A, lda, y, d_flag, true);
 }
@@ -1472,7 +1494,10 @@ static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
   // small systems launch directly: a graph's instantiation (~5 ms measured) costs more than
   // the host launches it saves over a whole solve (n = 264, 5 blocks: ~20 launches)
   if (c->nograph || nblk < c->graph_min) {  // nograph: debugging aid
-    if (launch) enqueue_factor_solve(c, s, n, A, lda, y, d_flag);
+    if (launch) {
+      enqueue_factor_solve(c, s, n, A, lda, y, d_flag);
+      flow_print_stamps(c, s, n);
+    }
     return 0;
   }
   const bool same = c->exec && c->g_n == n && c->g_lda == lda && c->g_A == A && c->g_y == y && c->g_flag == d_flag;
@@ -1496,7 +1521,9 @@ static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
     c->g_flag = d_flag;
   }
   if (!launch) return 0;
-  return hipGraphLaunch(c->exec, s) == hipSuccess ? 0 : -3;
+  if (hipGraphLaunch(c->exec, s) != hipSuccess) return -3;
+  flow_print_stamps(c, s, n);
+  return 0;
 }
 
 static void enqueue_back_substitution(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y,
@@ -1529,7 +1556,34 @@ static int flow_prepare(CholCtx* c, int n, int lda) {
     if (hipMalloc(&c->words, sizeof(unsigned) * nw) != hipSuccess) return -2;
     c->words_alloc = nw;
   }
+  const size_t ns = 1 + 3 * (size_t)nblk + (size_t)nblk;
+  if (c->stamps_on && ns > c->stamps_alloc) {
+    if (c->stamps) (void)hipFree(c->stamps);
+    c->stamps = nullptr;
+    c->stamps_alloc = 0;
+    if (hipMalloc(&c->stamps, sizeof(unsigned long long) * ns) != hipSuccess) return -2;
+    c->stamps_alloc = ns;
+  }
   return 0;
+}
+// DAB_CHOL_FLOW_STAMPS: the last factorisation's timeline (us from the kernel's start)
+static void flow_print_stamps(CholCtx* c, hipStream_t s, int n) {
+  if (!c->stamps_on || !c->stamps) return;
+  const int nblk = (n + NB - 1) / NB;
+  std::vector<unsigned long long> h(1 + 4 * (size_t)nblk);
+  if (hipStreamSynchronize(s) != hipSuccess ||
+      hipMemcpy(h.data(), c->stamps, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost) != hipSuccess)
+    return;
+  auto us = [&](unsigned long long t) { return t ? 0.01 * (double)(long long)(t - h[0]) : -1.0; };
+  std::fprintf(stderr, "flow n=%d: col ready factor published | factor us | step us (published - previous published)\n", n);
+  double prev = 0.0;
+  for (int cc = 0; cc < nblk; ++cc) {
+    const double r = us(h[1 + 3 * cc]), f0 = us(h[2 + 3 * cc]), p = us(h[3 + 3 * cc]);
+    std::fprintf(stderr, "flow col %3d %9.2f %9.2f %9.2f | %6.2f | %6.2f\n", cc, r, f0, p, p - f0, p - prev);
+    prev = p;
+  }
+  for (int g = 0; g < nblk; ++g)
+    if (h[1 + 3 * nblk + g]) std::fprintf(stderr, "flow group %3d bulk done %9.2f\n", g, us(h[1 + 3 * nblk + g]));
 }
 static bool flow_enqueue(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag) {
   if (!flow_applies(c, n, lda)) return false;
@@ -1539,8 +1593,10 @@ static bool flow_enqueue(CholCtx* c, hipStream_t s, int n, double* A, int lda, d
   const int G = c->flow_grid;
   const size_t a_bytes = sizeof(double) * (size_t)(n + 1) * lda, b_bytes = sizeof(double) * (size_t)kBlk * nblk;
   (void)hipMemsetAsync(c->words, 0, sizeof(unsigned) * nw, s);
+  unsigned long long* st = c->stamps_on ? c->stamps : nullptr;
+  if (st) (void)hipMemsetAsync(st, 0, sizeof(unsigned long long) * c->stamps_alloc, s);
   FlowArgs f{A, (unsigned)a_bytes, lda, n, nblk, rblk, std::max(2, c->group), c->flow_ga, c->blk, (unsigned)b_bytes,
-             d_flag, c->words};
+             d_flag, c->words, st};
   k_chol_flow<<<G, kFlowThreads, 0, s>>>(f);
   enqueue_back_substitution(c, s, n, A, lda, y, d_flag);
   return true;

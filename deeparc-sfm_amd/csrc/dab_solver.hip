@@ -207,7 +207,10 @@ struct Dev {
   // Blocks up to kSmall come from 8 MB slabs (bump-allocated; a handle's few dozen small
   // buffers cost one hipMalloc instead of one each, and the handle's destruction a few
   // hipFrees instead of dozens)
-  static constexpr size_t kSlab = (size_t)8 << 20, kSmall = (size_t)1 << 20;
+  static constexpr size_t kSlab = (size_t)8 << 20;
+  // DAB_DEV_SLAB=1 turns the slabs on (off by default until a C5 PCG trajectory that changed
+  // with them is explained)
+  const size_t kSmall = getenv("DAB_DEV_SLAB") && atoi(getenv("DAB_DEV_SLAB")) != 0 ? (size_t)1 << 20 : 0;
   std::vector<void*> slabs;
   size_t slab_off = kSlab;
   ~Dev() { clear(); }
@@ -244,10 +247,50 @@ struct Dev {
       if (v[i].bytes >= bytes && v[i].bytes <= cap && (best == v.size() || v[i].bytes < v[best].bytes)) best = i;
     return best;
   }
+  // debugging aids (read once): DAB_DEV_GUARD=1 puts a 64-KB canary after every block and
+  // guard_check() reports an overwritten one; DAB_DEV_POISON=1 fills every block handed out
+  // with 0xFF bytes (NaN doubles), so that a read of memory nobody wrote shows
+  static constexpr size_t kGuard = (size_t)64 << 10;
+  struct Guard {
+    char* p;  // the canary's first byte
+    size_t bytes;  // the block's usable size
+    int serial;
+  };
+  std::vector<Guard> guards;
+  int serial = 0;
+  static bool guard_on() {
+    static const bool on = getenv("DAB_DEV_GUARD") && atoi(getenv("DAB_DEV_GUARD")) != 0;
+    return on;
+  }
+  static bool poison_on() {
+    static const bool on = getenv("DAB_DEV_POISON") && atoi(getenv("DAB_DEV_POISON")) != 0;
+    return on;
+  }
+  // 0, or the number of overwritten canaries (each reported on stderr)
+  int guard_check(const char* where) {
+    int bad = 0;
+    std::vector<unsigned char> h(kGuard);
+    for (const Guard& g : guards) {
+      if (hipMemcpy(h.data(), g.p, kGuard, hipMemcpyDeviceToHost) != hipSuccess) continue;
+      size_t first = kGuard;
+      for (size_t i = 0; i < kGuard; ++i)
+        if (h[i] != 0xA5) {
+          first = i;
+          break;
+        }
+      if (first < kGuard) {
+        ++bad;
+        std::fprintf(stderr, "dab guard (%s): block #%d of %zu bytes overrun at +%zu\n", where, g.serial, g.bytes,
+                     first);
+      }
+    }
+    return bad;
+  }
   template <class T>
   int alloc(T** out, size_t n) {
     if (n == 0) n = 1;
-    const size_t bytes = (n * sizeof(T) + 255) & ~(size_t)255;
+    const size_t want = (n * sizeof(T) + 255) & ~(size_t)255;
+    const size_t bytes = want + (guard_on() ? kGuard : 0);
     const size_t cap = std::max(2 * bytes, bytes + ((size_t)1 << 20));
     Blk got{nullptr, bytes, 0, false};
     for (std::vector<Blk>* v : {&pool, &spare}) {
@@ -289,6 +332,15 @@ struct Dev {
     }
     live.push_back(got);
     *out = static_cast<T*>(got.p);
+    if (poison_on()) (void)hipMemset(got.p, 0xFF, want);
+    if (guard_on()) {
+      char* g = static_cast<char*>(got.p) + want;
+      (void)hipMemset(g, 0xA5, kGuard);
+      guards.erase(std::remove_if(guards.begin(), guards.end(), [&](const Guard& x) { return x.p == g; }),
+                   guards.end());
+      guards.push_back(Guard{g, want, serial});
+    }
+    ++serial;
     return 0;
   }
 };
@@ -2989,7 +3041,17 @@ static double elapsed_collective(dab_handle* h, double local) {
 // ------------------------------------------------------------------------------------
 // dab_solve: the trust-region LM loop
 // ------------------------------------------------------------------------------------
+static int solve_impl(dab_handle* h, const dab_options* opt_in, dab_summary* sum);
 extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* sum) {
+  const int rc = solve_impl(h, opt_in, sum);
+  if (Dev::guard_on() && h) {
+    (void)hipDeviceSynchronize();
+    if (h->dev.guard_check("solve") + h->setup_tmp.guard_check("solve, set-up scratch") > 0)
+      std::fprintf(stderr, "dab guard: overrun detected after dab_solve\n");
+  }
+  return rc;
+}
+static int solve_impl(dab_handle* h, const dab_options* opt_in, dab_summary* sum) {
   clear_error();
   if (!h || !h->have_problem) return set_error(DAB_E_STATE, "no problem set");
   if (!sum) return set_error(DAB_E_INVALID, "null summary");
