@@ -42,6 +42,7 @@ struct CholCtx {
                           // blocks), then L_kk [64][64]; stride kBlk
 
   hipStream_t side = nullptr;                     // bulk trailing updates (captured into the graph)
+  int device = 0;
   std::vector<hipEvent_t> ev_panel, ev_bulk;      // per block column
   size_t nblk_alloc = 0;
   // the ~5 x n/64 dependent launches are captured once per (n, buffers) and replayed
@@ -113,7 +114,10 @@ CholCtx* chol_create() {
   c->flow_grid = 0;  // set by chol_flow_fits on first use
   // the side stream and the barrier word now, not inside the first solve. (A warm-up graph
   // capture here bought nothing: every instantiation costs ~5 ms, the first one no more.)
-  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess || hipMalloc(&c->bar, sizeof(unsigned)) != hipSuccess) {
+  int dev_now = 0;
+  (void)hipGetDevice(&dev_now);
+  c->device = dev_now;
+  if (!(c->side = stream_take(dev_now)) || hipMalloc(&c->bar, sizeof(unsigned)) != hipSuccess) {
     chol_destroy(c);
     return nullptr;
   }
@@ -130,7 +134,7 @@ void chol_destroy(CholCtx* c) {
   if (c->pready) (void)hipFree(c->pready);
   for (hipEvent_t e : c->ev_panel) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_bulk) (void)hipEventDestroy(e);
-  if (c->side) (void)hipStreamDestroy(c->side);
+  stream_give(c->device, c->side);
   delete c;
 }
 
@@ -175,7 +179,12 @@ struct RowB {
 };
 #define ROWB(v, j) RowB<0>::get((v), (j))
 
-// wave 0: factor L[o:o+16, o:o+16] in place, its inverse into D[16][DS]
+// wave 0: factor L[o:o+16, o:o+16] in place, its inverse into D[16][DS]. ROWINV: the inverse
+// by rows (each broadcast depends on the step before: 137 VGPRs; the persistent factorisation,
+// whose work-groups must fit two per CU); else by columns (every lane its own column: more
+// independent work per step, but the compiler keeps the 120 broadcasts live: 256 VGPRs plus
+// AGPRs, fine for the one-work-group-per-CU launch schedule, and ~0.7 us faster per block)
+template <bool ROWINV = false>
 __device__ __noinline__ void factor16(double (*L)[LS], double (*D)[DS], int o, bool& bad) {
   const int lane = threadIdx.x & 63, r = lane & 15;
   double a[16], rd[16];
@@ -192,6 +201,26 @@ __device__ __noinline__ void factor16(double (*L)[LS], double (*D)[DS], int o, b
     // lanes r < l update entries above the diagonal that are never read: no mask
 #pragma unroll
     for (int l = j + 1; l < 16; ++l) a[l] = fma(-lmj, ROWB(lmj, l), a[l]);
+  }
+  if constexpr (!ROWINV) {
+    // lane c: column c of the inverse, x[i] = (delta_ic - sum_{c<=m<i} L[i][m] x[m]) / L[i][i]
+    const int cc = r;
+    double x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      double s = (i == cc) ? 1.0 : 0.0;
+#pragma unroll
+      for (int m = 0; m < i; ++m) s -= ROWB(a[m], i) * x[m];
+      x[i] = (i >= cc) ? s * rd[i] : 0.0;
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (j <= r) L[o + r][o + j] = a[j];
+        D[j][cc] = x[j];
+      }
+    }
+    return;
   }
   // the inverse X = L^-1 by rows, lane r holding row r: once the rows above are final,
   // lane m scales its row by 1/L[m][m] and broadcasts it, and every lane below subtracts
@@ -249,13 +278,14 @@ __device__ __forceinline__ void tile_store(double* M, int i0, int j0, const dbl4
 }
 
 // the 64x64 diagonal block (in LDS) -> L in place, D[p] = inverse of its p-th 16x16 block
+template <bool ROWINV = false>
 __device__ __forceinline__ void factor64(double (*L)[LS], double (*D)[16][DS], bool& bad) {
   const int tid = threadIdx.x, w = tid >> 6;
   double* Lf = &L[0][0];
 #pragma unroll 1
   for (int p = 0; p < 4; ++p) {
     const int o = 16 * p;
-    if (w == 0) factor16(L, D[p], o, bad);
+    if (w == 0) factor16<ROWINV>(L, D[p], o, bad);
     __syncthreads();
     PROF_MARK(2 + 2 * p);
     if (p == 3) break;
@@ -1198,7 +1228,7 @@ __device__ __noinline__ void flow_chain_tile(const FlowArgs& f, const Sc1& A, co
     __syncthreads();
     if (tid == 0) flow_stamp(f.stamps, 2 + 3 * (size_t)c);
     bool bad = false;
-    factor64(L, Dsh, bad);
+    factor64<true>(L, Dsh, bad);
     if (tid == 0 && bad) atomicOr(f.flag, 1);
     const Sc1& Bk = B;
 #pragma unroll
@@ -1377,24 +1407,35 @@ __global__ __launch_bounds__(kFlowThreads, 2) void k_chol_flow(FlowArgs f) {
   __syncthreads();
   if ((int)blockIdx.x < f.GA) {
     // ---- chain ----
+    // Per block column c, the owner of row c + 1 first solves its tile (c + 1, c) and at once
+    // factors the next diagonal tile (c + 1, c + 1), the chain's next step; then every owner
+    // solves its other tiles of column c. (Without that lookahead the next diagonal waited
+    // behind its owner's other tiles of the column: ~36 us per column at n = 5994.)
     if (g_chol_prio) __builtin_amdgcn_s_setprio(3);
     const int a = blockIdx.x, GA = f.GA;
-    for (int c = 0; c < nblk; ++c) {
+    auto tile = [&](int t, int c) -> bool {  // false: abort
       const int b = R * ((c - 1) / R);                      // the current group's panels [b, c)
       const unsigned ncov = c >= R + 1 ? (unsigned)((c - R - 1) / R + 1) : 0u;  // bulk groups before
-      int t = c + ((a - c) % GA + GA) % GA;
-      for (; t < rblk; t += GA) {
-        if (tid == 0) {
-          bool ok = flow_poll(bulkcnt + (size_t)t * nblk + c, ncov, abortw, f.flag);
-          if (ok && t != c) ok = flow_poll(rowdone + c, (unsigned)c, abortw, f.flag);
-          abort_s = !ok;
-        }
-        __syncthreads();
-        if (abort_s) return;
-        if (t == c && tid == 0) flow_stamp(f.stamps, 1 + 3 * (size_t)c);
-        flow_chain_tile(f, A, B, t, c, b, sm, abort_s);
-        if (abort_s) return;
-        __syncthreads();  // the tile's LDS reads are done before the next tile's staging
+      if (tid == 0) {
+        bool ok = flow_poll(bulkcnt + (size_t)t * nblk + c, ncov, abortw, f.flag);
+        if (ok && t != c) ok = flow_poll(rowdone + c, (unsigned)c, abortw, f.flag);
+        abort_s = !ok;
+      }
+      __syncthreads();
+      if (abort_s) return false;
+      if (t == c && tid == 0) flow_stamp(f.stamps, 1 + 3 * (size_t)c);
+      flow_chain_tile(f, A, B, t, c, b, sm, abort_s);
+      if (abort_s) return false;
+      __syncthreads();  // the tile's LDS reads are done before the next tile's staging
+      return true;
+    };
+    if (a == 0 && !tile(0, 0)) return;
+    for (int c = 0; c < nblk; ++c) {
+      const bool own_next = c + 1 < nblk && (c + 1) % GA == a;
+      if (own_next && !(tile(c + 1, c) && tile(c + 1, c + 1))) return;
+      for (int t = c + ((a - c) % GA + GA) % GA; t < rblk; t += GA) {
+        if (t == c || (own_next && t == c + 1)) continue;  // done above (this or the previous column)
+        if (!tile(t, c)) return;
       }
     }
     (void)pready;
@@ -1481,7 +1522,7 @@ static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
     if (hipMalloc(&c->pready, sizeof(unsigned) * (size_t)nblk) != hipSuccess) return -2;
     c->nblk_alloc = nblk;
   }
-  if (!c->side && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) return -3;
+  if (!c->side && !(c->side = stream_take(c->device))) return -3;
   if (flow_prepare(c, n, lda) != 0) return -2;
   if (!c->bar && hipMalloc(&c->bar, sizeof(unsigned)) != hipSuccess) return -2;
   while ((int)c->ev_panel.size() < nblk) {

@@ -337,6 +337,14 @@ void launch_pcg_fused_final(hipStream_t s, int grid, int NC6, const double* part
 // the first n rows end as L and row n as z = L^-1 b; then solve L^T y = z into y.
 // d_flag[0] is set when a pivot is not positive. Returns 0, or <0 on a library error.
 struct CholCtx;
+// Process-wide caches of the handle's runtime objects (each hipStreamCreate / Destroy took
+// ~2 ms, a handle makes three): an idle non-blocking stream of the current device, created
+// when the cache has none; stream_give synchronises it and keeps it for the next handle.
+// pinned_take / pinned_give do the same for small pinned host blocks (by size).
+hipStream_t stream_take(int device);
+void stream_give(int device, hipStream_t s);
+void* pinned_take(size_t bytes);
+void pinned_give(void* p, size_t bytes);
 CholCtx* chol_create();
 void chol_destroy(CholCtx*);
 int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag);

@@ -18,6 +18,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <iterator>
 #include <array>
 #include <chrono>
@@ -56,6 +58,65 @@ using namespace dab;
     int rc_ = (expr);        \
     if (rc_ != 0) return rc_; \
   } while (0)
+
+namespace dab {
+namespace {
+std::mutex& cache_mu() {
+  static std::mutex* m = new std::mutex();  // never destroyed: handles may outlive static teardown
+  return *m;
+}
+std::map<int, std::vector<hipStream_t>>& stream_cache() {
+  static auto* c = new std::map<int, std::vector<hipStream_t>>();
+  return *c;
+}
+std::map<size_t, std::vector<void*>>& pinned_cache() {
+  static auto* c = new std::map<size_t, std::vector<void*>>();
+  return *c;
+}
+}  // namespace
+hipStream_t stream_take(int device) {
+  {
+    std::lock_guard<std::mutex> lk(cache_mu());
+    auto& v = stream_cache()[device];
+    if (!v.empty()) {
+      hipStream_t s = v.back();
+      v.pop_back();
+      return s;
+    }
+  }
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  return s;
+}
+void stream_give(int device, hipStream_t s) {
+  if (!s) return;
+  if (hipStreamSynchronize(s) != hipSuccess) {  // a stream in an error state is not reused
+    (void)hipStreamDestroy(s);
+    return;
+  }
+  std::lock_guard<std::mutex> lk(cache_mu());
+  stream_cache()[device].push_back(s);
+}
+void* pinned_take(size_t bytes) {
+  {
+    std::lock_guard<std::mutex> lk(cache_mu());
+    auto& v = pinned_cache()[bytes];
+    if (!v.empty()) {
+      void* p = v.back();
+      v.pop_back();
+      return p;
+    }
+  }
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes) != hipSuccess) return nullptr;
+  return p;
+}
+void pinned_give(void* p, size_t bytes) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(cache_mu());
+  pinned_cache()[bytes].push_back(p);
+}
+}  // namespace dab
 
 namespace {
 
@@ -579,9 +640,9 @@ struct dab_handle {
     phase("device buffers");
     for (Sticky* st : {&st_S, &st_yc, &st_flags})
       if (st->p) (void)hipFree(st->p);
-    if (h_scal) (void)hipHostFree(h_scal);
-    if (h_flags) (void)hipHostFree(h_flags);
-    if (h_pcg_state) (void)hipHostFree(h_pcg_state);
+    pinned_give(h_scal, sizeof(double) * S_NSLOTS);
+    pinned_give(h_flags, sizeof(int) * 4);
+    pinned_give(h_pcg_state, sizeof(PcgState));
     if (h_stage) (void)hipHostFree(h_stage);
     phase("pinned");
     if (chol) chol_destroy(chol);
@@ -594,11 +655,11 @@ struct dab_handle {
       for (hipEvent_t x : e) (void)hipEventDestroy(x);
     if (ev_cam) (void)hipEventDestroy(ev_cam);
     if (ev_comm) (void)hipEventDestroy(ev_comm);
-    if (comm_stream) (void)hipStreamDestroy(comm_stream);
+    stream_give(device, comm_stream);
     p2p_destroy(p2p_main);
     p2p_destroy(p2p_comm);
     if (comm) ncclCommDestroy(comm);
-    if (stream) (void)hipStreamDestroy(stream);
+    stream_give(device, stream);
   }
 
   double* ug() { return d_camred; }  // [NC][27]: U upper-packed (21) | g_c (6)
@@ -759,7 +820,7 @@ static int create_common(int device, dab_handle** out) {
   dab_handle* h = new dab_handle();
   h->device = device;
   h->knobs.read();
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (!(h->stream = stream_take(device))) {
     delete h;
     return set_error(DAB_E_DEVICE, "hipStreamCreate failed");
   }
@@ -774,12 +835,12 @@ static int create_common(int device, dab_handle** out) {
       hipEventCreate(&h->ev2) != hipSuccess || hipEventCreate(&h->ev3) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_cam, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_comm, hipEventDisableTiming) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking) != hipSuccess) {
+      !(h->comm_stream = stream_take(device))) {
     delete h;
     return set_error(DAB_E_DEVICE, "hipEventCreate failed");
   }
-  if (hipHostMalloc(reinterpret_cast<void**>(&h->h_scal), sizeof(double) * S_NSLOTS) != hipSuccess ||
-      hipHostMalloc(reinterpret_cast<void**>(&h->h_flags), sizeof(int) * 4) != hipSuccess) {
+  if (!(h->h_scal = static_cast<double*>(pinned_take(sizeof(double) * S_NSLOTS))) ||
+      !(h->h_flags = static_cast<int*>(pinned_take(sizeof(int) * 4)))) {
     delete h;
     return set_error(DAB_E_NOMEM, "hipHostMalloc failed");
   }
@@ -2698,8 +2759,7 @@ static int build_pcg_buffers(dab_handle* h) {
     h->fused_grid = pcg_fused_grid(h->NP, h->ncu);
     CHECK_RC(d.alloc(&h->d_fused_partial, (size_t)h->fused_grid * 6 * h->NC));
   }
-  if (!h->h_pcg_state &&
-      hipHostMalloc(reinterpret_cast<void**>(&h->h_pcg_state), sizeof(PcgState)) != hipSuccess)
+  if (!h->h_pcg_state && !(h->h_pcg_state = static_cast<PcgState*>(pinned_take(sizeof(PcgState)))))
     return set_error(DAB_E_NOMEM, "pinned PCG state allocation failed");
   h->pcg_built = true;
   return 0;
