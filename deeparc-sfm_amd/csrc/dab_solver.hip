@@ -327,6 +327,12 @@ struct Dev {
     static const bool on = getenv("DAB_DEV_POISON") && atoi(getenv("DAB_DEV_POISON")) != 0;
     return on;
   }
+  // 1: 0xFF (NaN doubles, also caught when multiplied by zero); 2: 0x41 (finite, ~2.3e6
+  // as a double: caught only where the value is used)
+  static int poison_byte() {
+    static const int b = getenv("DAB_DEV_POISON") && atoi(getenv("DAB_DEV_POISON")) == 2 ? 0x41 : 0xFF;
+    return b;
+  }
   // 0, or the number of overwritten canaries (each reported on stderr)
   int guard_check(const char* where) {
     int bad = 0;
@@ -393,7 +399,7 @@ struct Dev {
     }
     live.push_back(got);
     *out = static_cast<T*>(got.p);
-    if (poison_on()) (void)hipMemset(got.p, 0xFF, want);
+    if (poison_on()) (void)hipMemset(got.p, poison_byte(), want);
     if (guard_on()) {
       char* g = static_cast<char*>(got.p) + want;
       (void)hipMemset(g, 0xA5, kGuard);
