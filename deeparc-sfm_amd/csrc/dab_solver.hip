@@ -399,10 +399,17 @@ struct Dev {
     }
     live.push_back(got);
     *out = static_cast<T*>(got.p);
+    // (the fills run on the null stream, which does not order against the handle's
+    // non-blocking stream: the device is synchronised after them, or the handle's own
+    // uploads could land first and be overwritten)
     if (poison_on()) (void)hipMemset(got.p, poison_byte(), want);
     if (guard_on()) {
       char* g = static_cast<char*>(got.p) + want;
       (void)hipMemset(g, 0xA5, kGuard);
+    }
+    if (poison_on() || guard_on()) (void)hipDeviceSynchronize();
+    if (guard_on()) {
+      char* g = static_cast<char*>(got.p) + want;
       guards.erase(std::remove_if(guards.begin(), guards.end(), [&](const Guard& x) { return x.p == g; }),
                    guards.end());
       guards.push_back(Guard{g, want, serial});
