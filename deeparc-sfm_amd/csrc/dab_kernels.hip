@@ -481,14 +481,23 @@ __device__ __forceinline__ SmallTabs stage_small_tabs(double* lds, int E, int NI
   __syncthreads();
   return SmallTabs{t_s, k_s};
 }
-template <bool K_IN_LDS, bool KMASK = false>
+// R,t rows of the fused pass's LDS table, bank-spread: four cameras' 6 16-B pieces then one
+// 16-B pad, so the first piece of camera e sits at 16-B slot 25 (e / 4) + 6 (e % 4). Lanes
+// read the pieces of random cameras: with the plain 6-slot stride a piece's slot mod 8
+// took only 4 of 8 values (6 e mod 8), halving the banks a wave's b128 reads spread over.
+#ifndef DAB_FUSED_RTPAD
+#define DAB_FUSED_RTPAD 1
+#endif
+__host__ __device__ constexpr int rt_pad_off(int e) { return 2 * (25 * (e >> 2) + 6 * (e & 3)); }  // doubles
+__host__ __device__ constexpr int rt_pad_size(int E) { return 2 * 25 * ((E + 3) >> 2); }           // doubles
+template <bool K_IN_LDS, bool KMASK = false, bool RTPAD = false>
 struct LdsTabs {
-  const double* rt_s;  // LDS [E][12]: R t
+  const double* rt_s;  // LDS [E][12]: R t (RTPAD: rt_pad_off layout)
   const double* k_s;   // LDS [NI][6] when K_IN_LDS
   const double* __restrict__ camtab;
   const double* __restrict__ intr;
   __device__ __forceinline__ void rt(int e, double (&T)[12]) const {
-    const double2* p = reinterpret_cast<const double2*>(rt_s + 12 * e);
+    const double2* p = reinterpret_cast<const double2*>(rt_s + (RTPAD ? rt_pad_off(e) : 12 * e));
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       const double2 v = p[i];
@@ -2008,7 +2017,8 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
                                                      const double* __restrict__ cmx,
                                                      const double* __restrict__ camtab, int wpc, int wps,
                                                      int wxor, int side = 0) {
-  __shared__ double rt_s[kLdsCams * 12];
+  constexpr bool RTP = DAB_FUSED_RTPAD != 0;
+  __shared__ double rt_s[RTP ? rt_pad_size(kLdsCams) : kLdsCams * 12];
   __shared__ double k_s[kLdsCams * 6];
   __shared__ double csum[kFusedCW][27];     // camera waves' sums: [camera slot * wpc + part][component]
   __shared__ double cjl[kFusedCW][9];       // camera waves' J_l (eval_cams_uni_frame)
@@ -2158,15 +2168,21 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
 #pragma unroll
   for (int which = 0; which < (TAB ? 2 : 1); ++which) {
     const int per = which ? 6 : 3, npiece = per * (which ? v.E : v.NI);
+    // LDS slots: pieces in order, or (R,t with RTP) 25 slots per four cameras (slot 24 a pad)
+    const int nslot = (which && RTP) ? rt_pad_size(v.E) / 2 : npiece;
     const double* src0 = which ? camtab : v.intr;
     const int stride = which ? kCamTab : kIntr;
     double* dst = which ? rt_s : k_s;
-    const int nch = (npiece + 63) >> 6;
+    const int nch = (nslot + 63) >> 6;
     const int rot = (int)((xrot * (unsigned)nch) >> 5);
     for (int j = pw; j < nch; j += kFusedPW) {
       int jr = j + rot;
       if (jr >= nch) jr -= nch;
-      const int i = min(jr * 64 + lane, npiece - 1);
+      int i = min(jr * 64 + lane, nslot - 1);
+      if (which && RTP) {  // slot -> piece (a pad slot repeats the group's last piece)
+        const int gq = i / 25, w = min(i - 25 * gq, 23);
+        i = min(24 * gq + w, npiece - 1);
+      }
       __builtin_amdgcn_global_load_lds(src0 + (size_t)stride * (i / per) + 2 * (i % per), dst + 2 * (size_t)(jr * 64),
                                        16, 0, 0);
     }
@@ -2187,7 +2203,8 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
       cam_table(x6, T);
     }
 #pragma unroll
-    for (int i = 0; i < 6; ++i) reinterpret_cast<double2*>(rt_s + 12 * e0)[i] = make_double2(T[2 * i], T[2 * i + 1]);
+    for (int i = 0; i < 6; ++i)
+      reinterpret_cast<double2*>(rt_s + (RTP ? rt_pad_off(e0) : 12 * e0))[i] = make_double2(T[2 * i], T[2 * i + 1]);
   }
   // barrier of the point waves only (LDS counter): own LDS writes and LDS-DMAs retired
   // before the arrival, acquire before the first table read
@@ -2196,7 +2213,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
   while (__hip_atomic_load(&pbar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)kFusedPW)
     __builtin_amdgcn_s_sleep(1);
   DAB_STAMP(1);
-  const LdsTabs<true> tabs{rt_s, k_s, nullptr, v.intr};
+  const LdsTabs<true, false, RTP> tabs{rt_s, k_s, nullptr, v.intr};
   double acc[2] = {0.0, 0.0};
   for (int r = 0; r < rounds; ++r) {
     if (r > 0) {
@@ -2234,7 +2251,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
         }
         const bool live = id.x >= 0;
         double ru, rv, jx0[3], jx1[3];
-        obs_rows<true, -1, LdsTabs<true>, false>(id, xy, X, tabs, ru, rv, jx0, jx1, nullptr, nullptr);
+        obs_rows<true, -1, LdsTabs<true, false, RTP>, false>(id, xy, X, tabs, ru, rv, jx0, jx1, nullptr, nullptr);
         if (!live) ru = rv = jx0[0] = jx0[1] = jx0[2] = jx1[0] = jx1[1] = jx1[2] = 0.0;
         c[0] = fma(jx1[0], jx1[0], fma(jx0[0], jx0[0], c[0]));
         c[1] = fma(jx1[0], jx1[1], fma(jx0[0], jx0[1], c[1]));
@@ -2254,7 +2271,7 @@ __global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __res
     if (wps > 1) {
       // (one round by construction) parts -> LDS after the tables (fused_wps keeps
       // 12 E + kFusedPW * 9 * 64 doubles inside rt_s); the last part sums them in order
-      double* cbuf = rt_s + ((12 * v.E + 1) & ~1);
+      double* cbuf = rt_s + (RTP ? rt_pad_size(v.E) : ((12 * v.E + 1) & ~1));
 #pragma unroll
       for (int k = 0; k < 9; ++k) cbuf[(pw * 9 + k) * 64 + lane] = c[k];
       unsigned old = 0;
@@ -2317,8 +2334,9 @@ static int fused_wpc(int NC, int grid) {
 // per-part sums fit in rt_s beside the tables
 static int fused_wps(int nslice, int E, int grid) {
   int w = kFusedPW;
-  while (w > 1 && ((long long)nslice * w > (long long)kFusedPW * grid ||
-                   ((12 * E + 1) & ~1) + kFusedPW * 9 * 64 > kLdsCams * 12))
+  constexpr bool RTP = DAB_FUSED_RTPAD != 0;
+  const int used = RTP ? rt_pad_size(E) : ((12 * E + 1) & ~1), cap = RTP ? rt_pad_size(kLdsCams) : kLdsCams * 12;
+  while (w > 1 && ((long long)nslice * w > (long long)kFusedPW * grid || used + kFusedPW * 9 * 64 > cap))
     w >>= 1;
   return w;
 }

@@ -2,7 +2,7 @@
 created, so each variant gets its own handle with its environment set first).
 
 usage: python scripts/eval_ab.py CONFIG REPS NAME=ENV1=V1,ENV2=V2 [NAME=...]
-  (a bare NAME with no '=' runs the defaults)
+  (a bare NAME with no '=' runs the defaults; LIB=path runs that build of libdab instead)
 
 Per variant and rep: step wall time over 200 back-to-back passes, the kernel's HIP-event
 mean, and a 3-iteration PCG LM solve whose per-iteration costs are compared with the first
@@ -18,8 +18,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import _pkgload  # noqa: E402
 
-KNOBS = ("DAB_EVAL_ROLES", "DAB_ROLES_CBLK", "DAB_ROLES_CPB", "DAB_ROLES_SPLIT", "DAB_ROLES_TAB", "DAB_ROLES_V",
-         "DAB_EVAL_FUSED", "DAB_FUSED_STREAM", "DAB_FUSED_GV", "DAB_FUSED_TAB", "DAB_FUSED_V")
+KNOBS = ("DAB_EVAL_FUSED", "DAB_FUSED_STREAM", "DAB_FUSED_GV", "DAB_FUSED_TAB", "DAB_FUSED_V")
+
+
+DEFAULT_LIB = []
 
 
 def parse(spec):
@@ -32,6 +34,10 @@ def parse(spec):
 
 
 def run(pkg, prob, env, passes=200):
+    abi = sys.modules[pkg.__name__ + "._abi"]
+    env = dict(env)
+    lib = env.pop("LIB", None)
+    abi._LIB = abi.load_library(os.path.join(ROOT, lib)) if lib else DEFAULT_LIB[0]
     for k in KNOBS:
         os.environ.pop(k, None)
     os.environ.update(env)
@@ -57,6 +63,7 @@ def main():
     cfg, reps = sys.argv[1], int(sys.argv[2])
     variants = [parse(a) for a in sys.argv[3:]]
     pkg = _pkgload.load()
+    DEFAULT_LIB.append(pkg.load_library())
     prob = pkg.synth(**pkg.CONFIGS[cfg])
     res = {n: [] for n, _ in variants}
     ref = None
