@@ -481,12 +481,14 @@ __device__ __forceinline__ SmallTabs stage_small_tabs(double* lds, int E, int NI
   __syncthreads();
   return SmallTabs{t_s, k_s};
 }
-// R,t rows of the fused pass's LDS table, bank-spread: four cameras' 6 16-B pieces then one
-// 16-B pad, so the first piece of camera e sits at 16-B slot 25 (e / 4) + 6 (e % 4). Lanes
-// read the pieces of random cameras: with the plain 6-slot stride a piece's slot mod 8
-// took only 4 of 8 values (6 e mod 8), halving the banks a wave's b128 reads spread over.
+// R,t rows of the fused pass's LDS table, bank-spread (DAB_FUSED_RTPAD=1 builds): four
+// cameras' 6 16-B pieces then one 16-B pad, so the first piece of camera e sits at 16-B
+// slot 25 (e / 4) + 6 (e % 4) (with the plain 6-slot stride a piece's slot mod 8 takes only
+// 4 of 8 values). Measured A/B at C3 (`scripts/eval_ab.py`, one box): 23.42 against 22.81 us
+// with the in-kernel tables, 21.42 against 21.87 us with the candidate's tables; C2 equal.
+// Not the default.
 #ifndef DAB_FUSED_RTPAD
-#define DAB_FUSED_RTPAD 1
+#define DAB_FUSED_RTPAD 0
 #endif
 __host__ __device__ constexpr int rt_pad_off(int e) { return 2 * (25 * (e >> 2) + 6 * (e & 3)); }  // doubles
 __host__ __device__ constexpr int rt_pad_size(int E) { return 2 * 25 * ((E + 3) >> 2); }           // doubles
