@@ -846,7 +846,12 @@ void launch_cg_update(hipStream_t s, int NC, int mode, const double* Ad, const d
   k_cg_xr<<<gx, kCgBlock, 0, s>>>(NC, mode, bvec, p, q, x, r, Minv, z, st, partial, cnt, fold_p);
   if (mode != 1 && !fold_p) k_cg_p<<<(6 * NC + 255) / 256, 256, 0, s>>>(6 * NC, z, p, st);
 }
-int cg_partial_size(int NC) { return 2 * ((NC + 3) / 4) + 2 * ((NC + kCgBlock - 1) / kCgBlock); }
+// the CG update's grid partials: k_cg_q writes K = 1 per work-group over NC / (kCgBlock / L)
+// work-groups (L = 64 with cross blocks: one camera per work-group, NC partials), then
+// k_cg_xr K = 2 per work-group over ceil(NC / kCgBlock). (Sized for the earlier L = 16,
+// 2 ceil(NC / 4), this ran past its end by NC / 2 doubles on the rig, which the allocator's
+// padding hid until buffers were packed.)
+int cg_partial_size(int NC) { return NC + 2 * ((NC + kCgBlock - 1) / kCgBlock); }
 
 void launch_pcg_update(hipStream_t s, int NC, int mode, const double* Ad, const double* w, const int* xptr,
                        const int* xlist, const int2* xcam, const double* X, const double* scale_c,

@@ -308,8 +308,8 @@ struct Dev {
       if (v[i].bytes >= bytes && v[i].bytes <= cap && (best == v.size() || v[i].bytes < v[best].bytes)) best = i;
     return best;
   }
-  // debugging aids (read once): DAB_DEV_GUARD=1 puts a 64-KB canary after every block and
-  // guard_check() reports an overwritten one; DAB_DEV_POISON=1 fills every block handed out
+  // debugging aids (read once): DAB_DEV_GUARD=1 puts a 64-KB zero canary after every block
+  // and guard_check() reports one with a nonzero byte (found the CG partials' overrun); DAB_DEV_POISON=1 fills every block handed out
   // with 0xFF bytes (NaN doubles), so that a read of memory nobody wrote shows
   static constexpr size_t kGuard = (size_t)64 << 10;
   struct Guard {
@@ -341,7 +341,7 @@ struct Dev {
       if (hipMemcpy(h.data(), g.p, kGuard, hipMemcpyDeviceToHost) != hipSuccess) continue;
       size_t first = kGuard;
       for (size_t i = 0; i < kGuard; ++i)
-        if (h[i] != 0xA5) {
+        if (h[i] != 0) {
           first = i;
           break;
         }
@@ -405,7 +405,7 @@ struct Dev {
     if (poison_on()) (void)hipMemset(got.p, poison_byte(), want);
     if (guard_on()) {
       char* g = static_cast<char*>(got.p) + want;
-      (void)hipMemset(g, 0xA5, kGuard);
+      (void)hipMemset(g, 0, kGuard);  // zeros: a stray read of the canary is a harmless 0 / index 0
     }
     if (poison_on() || guard_on()) (void)hipDeviceSynchronize();
     if (guard_on()) {
