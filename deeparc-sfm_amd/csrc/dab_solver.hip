@@ -410,7 +410,10 @@ struct Dev {
     if (poison_on() || guard_on()) (void)hipDeviceSynchronize();
     if (guard_on()) {
       char* g = static_cast<char*>(got.p) + want;
-      guards.erase(std::remove_if(guards.begin(), guards.end(), [&](const Guard& x) { return x.p == g; }),
+      // a reused block drops the canaries of its earlier uses (now inside its usable bytes)
+      char* lo = static_cast<char*>(got.p);
+      char* hi = lo + got.bytes;
+      guards.erase(std::remove_if(guards.begin(), guards.end(), [&](const Guard& x) { return x.p >= lo && x.p < hi; }),
                    guards.end());
       guards.push_back(Guard{g, want, serial});
     }
