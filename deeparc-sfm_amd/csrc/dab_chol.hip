@@ -64,6 +64,7 @@ struct CholCtx {
   bool fuse_panel = true;     // DAB_CHOL_FUSE_PANEL=0: the panel step as its own launch after the column update
   unsigned* pready = nullptr; // per block: L_kk published by the fused column update (zeroed per factorisation)
   int group = 2;            // DAB_CHOL_GROUP: panels per bulk trailing update (2: pairs)
+  int col_grid = 0;         // DAB_CHOL_COL_GRID: most work-groups of a column update (0: one per tile)
   // the persistent dataflow factorisation (k_chol_flow): DAB_CHOL_FLOW=0 keeps the launches
   bool flow = false;  // DAB_CHOL_FLOW=1 (default once measured on the GPU)
   int flow_min = 32;        // DAB_CHOL_FLOW_MIN: fewest blocks that use it
@@ -94,6 +95,7 @@ CholCtx* chol_create() {
   if (const char* e = getenv("DAB_CHOL_BULK_GRID")) c->bulk_grid = atoi(e);
   if (const char* e = getenv("DAB_CHOL_V1")) c->v1 = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_GROUP")) c->group = std::max(2, atoi(e));
+  if (const char* e = getenv("DAB_CHOL_COL_GRID")) c->col_grid = std::max(0, atoi(e));
   if (const char* e = getenv("DAB_CHOL_FLOW")) c->flow = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_FLOW_MIN")) c->flow_min = atoi(e);
   if (const char* e = getenv("DAB_CHOL_FLOW_GA")) c->flow_ga = std::max(1, atoi(e));
@@ -1678,8 +1680,12 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
     const int r0 = cb * NB, m = n + 1 - r0;
     if (m <= 1) return;
     const int nt = (m + NB - 1) / NB;
-    k_syrk_mfma<<<nt, kThreads, 0, s>>>(A, lda, r0, m, k, kk, 1, nt, pre ? c->blk + (size_t)cb * kBlk : nullptr,
-                                        kb_of(cb), d_flag, fuse ? c->pready + cb : nullptr);
+    // col_grid: at most that many work-groups, each walking tiles t, t + grid, ... (the
+    // diagonal tile is work-group 0's first), so that the column fits the CUs the bulk
+    // update leaves in one round instead of a second round queued behind the first
+    const int g = c->col_grid > 0 ? std::min(nt, c->col_grid) : nt;
+    k_syrk_mfma<<<g, kThreads, 0, s>>>(A, lda, r0, m, k, kk, 1, nt, pre ? c->blk + (size_t)cb * kBlk : nullptr,
+                                       kb_of(cb), d_flag, fuse ? c->pready + cb : nullptr);
   };
   panel(0);
   // groups of R = c->group panels (2: the pairs). Within a group the chain updates column c
