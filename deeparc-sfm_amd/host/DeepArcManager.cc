@@ -4,6 +4,7 @@
 #include "DeepArcManager.hh"
 
 #include <algorithm>
+#include <sched.h>
 #include <cctype>
 #include <cstdlib>
 #include <charconv>
@@ -132,11 +133,16 @@ template <class Line, class Seq>
 void parse_section(Tokens& f, int n, int min_parallel, const Line& line, const Seq& seq) {
   const char* p0 = f.pos();
   const char* end = f.end();
-  // DAB_READ_THREADS: most parser threads (default 8; 1 = sequential)
-  static const int tmax = getenv("DAB_READ_THREADS") ? atoi(getenv("DAB_READ_THREADS")) : 8;
-  const int T = n >= min_parallel
-                    ? (int)std::min((unsigned)std::max(1, tmax), std::max(1u, std::thread::hardware_concurrency()))
-                    : 1;
+  // DAB_READ_THREADS: most parser threads (default: the CPUs this process may run on, at
+  // most 16; 1 = sequential)
+  static const int tmax = [] {
+    if (const char* e = getenv("DAB_READ_THREADS")) return std::max(1, atoi(e));
+    int n = (int)std::thread::hardware_concurrency();
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
+    return std::max(1, std::min(n, 16));
+  }();
+  const int T = n >= min_parallel ? tmax : 1;
   bool parallel_ok = T > 1;
   std::vector<const char*> cut(T + 1, nullptr);
   if (parallel_ok) {
@@ -546,23 +552,24 @@ void DeepArcManager::filterPoint3d(double error_boundary, double* hemisphere_cen
     std::fill(keep_pt.begin(), keep_pt.end(), 0);  // no observations: every point is empty
   }
   const double th = dab_now_seconds();
-  // host: drop blocks, then points, preserving the survivors' order (std::remove_if)
+  // host: drop points, then blocks, preserving the survivors' order (std::remove_if). A
+  // dropped point clears the links of its blocks (Point3d's destructor), so the blocks
+  // dropped with it need no unlink; the filter drops every block of a dropped point.
   size_t w = 0;
+  for (size_t i = 0; i < point3d_.size(); ++i) {
+    if (keep_pt[i]) point3d_[w++] = point3d_[i];
+    else delete point3d_[i];
+  }
+  const size_t np_old = point3d_.size();
+  point3d_.resize(w);
+  const size_t np_new = w;
+  w = 0;
   for (size_t i = 0; i < params_.size(); ++i) {
     if (keep_obs[i]) params_[w++] = params_[i];
-    else delete params_[i];  // unlinks from its point
+    else delete params_[i];  // unlinks from its point if that one stays
   }
+  const bool changed = np_new != np_old || w != keep_obs.size();
   params_.resize(w);
-  w = 0;
-  for (size_t i = 0; i < point3d_.size(); ++i) {
-    if (keep_pt[i]) {
-      point3d_[w++] = point3d_[i];
-    } else {
-      delete point3d_[i];  // clears the links of any block still on it (none remain)
-    }
-  }
-  const bool changed = w != point3d_.size() || params_.size() != keep_obs.size();
-  point3d_.resize(w);
   if (changed) {
     ++structure_version_;  // the resident problem no longer matches
     // the session's arrays follow the same compaction (the next set-up needs no marshal)
