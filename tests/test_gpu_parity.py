@@ -454,6 +454,40 @@ def test_lm_freeze_camera_matches_oracle(pkg, orc, gpu):
     assert g["num_free_ext"] == 0
 
 
+SMALL_SHAPES = {
+    "one_point_two_cameras": dict(kind=0, num_cameras=2, num_points=1, obs_per_point=2, seed=71),
+    "slice_63": dict(kind=0, num_cameras=3, num_points=63, obs_per_point=3, seed=72),
+    "slice_64": dict(kind=0, num_cameras=3, num_points=64, obs_per_point=3, seed=73),
+    "slice_65": dict(kind=0, num_cameras=3, num_points=65, obs_per_point=2, seed=74),
+    "gauge_camera_only": dict(kind=0, num_cameras=1, num_points=7, obs_per_point=1, seed=75),
+    "rig_one_arc_two_rings": dict(kind=1, num_arcs=1, num_rings=2, num_points=10, obs_per_point=2, seed=76),
+    "rig_two_arcs_one_ring": dict(kind=1, num_arcs=2, num_rings=1, num_points=129, obs_per_point=2, seed=77),
+}
+
+
+@pytest.mark.parametrize("solver", ["explicit", "pcg"])
+@pytest.mark.parametrize("shape", sorted(SMALL_SHAPES))
+def test_small_shapes_match_oracle(pkg, orc, gpu, shape, solver):
+    """Degenerate sizes against the oracle's trajectory: one point, SELL slices of 63/64/65
+    points (a full slice, one short, one point over), no free camera (the only camera is the
+    gauge: NC = 0), the smallest rigs. Costs that reach round-off (1e-15 .. 1e-20 on the
+    noise-free shapes) are compared with an absolute floor of 1e-12 x the initial cost."""
+    prob = pkg.synth(**SMALL_SHAPES[shape])
+    lst = (pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR if solver == "explicit"
+           else pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)
+    g, o, ref = run_both(pkg, orc, prob, max_num_iterations=20, linear_solver_type=lst)
+    floor = 1e-12 * o["initial_cost"]
+    assert g["termination"] == o["termination"], (g["message"], o["message"])
+    assert g["num_iterations"] == o["num_iterations"]
+    assert g["initial_cost"] == pytest.approx(o["initial_cost"], rel=1e-12)
+    for a, b in zip(g["iterations"], o["iterations"]):
+        assert a["success"] == b["success"]
+        assert abs(a["cost"] - b["cost"]) <= 1e-9 * abs(b["cost"]) + floor, (a, b)
+    assert abs(g["final_cost"] - o["final_cost"]) <= 1e-9 * abs(o["final_cost"]) + floor
+    assert np.abs(prob.points - ref.points).max() < 1e-7
+    assert np.abs(prob.ext - ref.ext).max() < 1e-7
+
+
 def test_gauge_and_unreferenced_blocks_untouched(pkg, orc, gpu):
     prob = pkg.synth(kind=0, num_cameras=20, num_points=600, obs_per_point=5, seed=24)
     # drop every observation of point 7 and of camera 3: those blocks leave the problem
