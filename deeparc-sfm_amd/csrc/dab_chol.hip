@@ -158,6 +158,13 @@ __device__ long long g_prof[16];
 #define PROF_MARK(i)
 #endif
 
+// factor16's off-chain multipliers and the inverse's L entries from LDS (1) or by DPP
+// broadcasts (0: the round-3 form, kept for A/B builds of scripts/potrf_micro.hip)
+#ifndef DAB_F16_LDS
+#define DAB_F16_LDS 0
+#endif
+constexpr bool kF16Lds = DAB_F16_LDS != 0;
+
 // 1/sqrt(d): v_rsq_f64 and two Newton steps
 __device__ __forceinline__ double rsqrt_nr(double d) {
   double y = __builtin_amdgcn_rsq(d);
@@ -192,6 +199,44 @@ __device__ __noinline__ void factor16(double (*L)[LS], double (*D)[DS], int o, b
   double a[16], rd[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) a[j] = (j <= r) ? L[o + r][o + j] : 0.0;
+  if constexpr (!ROWINV && kF16Lds) {
+    // only the next pivot's column takes its multiplier L[j+1][j] by DPP (the dependent
+    // chain); the later columns read L[l][j] back from LDS as one-address broadcasts, off the
+    // VALU (a DPP f64 broadcast is two VALU moves). Column j goes to LDS as soon as it is
+    // final: this wave's own LDS accesses complete in order. T: the tile as an LDS
+    // address-space pointer (one base register, every entry an immediate offset; the
+    // generic pointer costs a null check per access)
+    typedef __attribute__((address_space(3))) double lds_f64;
+    lds_f64* T = (lds_f64*)&L[o][o];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const double d = ROWB(a[j], j);
+      bad |= !(d > 0.0) || !isfinite(d);
+      const double y = rsqrt_nr(d);
+      rd[j] = y;
+      const double lmj = (r == j) ? d * y : a[j] * y;
+      a[j] = lmj;
+      if (lane < 16 && r >= j) T[r * LS + j] = lmj;
+      if (j + 1 < 16) a[j + 1] = fma(-lmj, ROWB(lmj, j + 1), a[j + 1]);
+#pragma unroll
+      for (int l = j + 2; l < 16; ++l) a[l] = fma(-lmj, T[l * LS + j], a[l]);
+    }
+    // the inverse by columns (below), its L[i][m] also broadcast from LDS
+    const int cc = r;
+    double x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      double s = (i == cc) ? 1.0 : 0.0;
+#pragma unroll
+      for (int m = 0; m < i; ++m) s -= T[i * LS + m] * x[m];
+      x[i] = (i >= cc) ? s * rd[i] : 0.0;
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) D[j][cc] = x[j];
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const double d = ROWB(a[j], j);

@@ -2,6 +2,7 @@
 // SPD 64x64 block (L_kk against a CPU Cholesky) and on a 6000-row panel, with the phase
 // profile of one launch (wall clock, 100 MHz).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/potrf_micro.hip -o scripts/potrf_micro
+// (-DDAB_F16_LDS=0: the round-3 factor16, all multipliers by DPP broadcasts)
 #define DAB_CHOL_PROFILE
 #include "../deeparc-sfm_amd/csrc/dab_chol.hip"
 
@@ -11,6 +12,16 @@
 #include <vector>
 
 using namespace dab;
+
+// the solver's process-wide stream cache, which dab_chol.hip links against
+namespace dab {
+hipStream_t stream_take(int) {
+  hipStream_t s = nullptr;
+  (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  return s;
+}
+void stream_give(int, hipStream_t s) { (void)hipStreamDestroy(s); }
+}  // namespace dab
 
 __global__ void k_empty() {}
 
