@@ -61,11 +61,33 @@ def parse():
     return ap.parse_args()
 
 
+def launch_ranks(args):
+    """`bench.py --gpus N` run without a launcher: start the N ranks (one process per GPU)
+    through torch.distributed.run as CHILD processes and return their exit code. Runs before
+    anything in this process touches HIP (no exec from a GPU-initialised process)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, DAB_BENCH_LAUNCHED="1")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        # the line's n_gpus must be the ranks that actually run: refuse a mismatch
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s); no line printed")
     import _pkgload
     pkg = _pkgload.load()
 
@@ -73,6 +95,9 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)  # control plane only
+        joined = dist.get_world_size()
+        if joined != args.gpus:
+            sys.exit(f"bench.py: {joined} rank(s) joined, --gpus {args.gpus}; no line printed")
     import numpy as np
 
     cfg = dict(pkg.CONFIGS[args.config])

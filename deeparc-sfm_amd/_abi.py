@@ -103,6 +103,7 @@ SIGNATURES = {
     "dab_create_dist_host": (C.c_int, [C.c_int, C.c_int, C.c_int, HostAllreduceFn, C.c_void_p,
                                        C.POINTER(C.c_void_p)]),
     "dab_destroy": (C.c_int, [C.c_void_p]),
+    "dab_release_caches": (C.c_int, []),
     "dab_set_problem": (C.c_int, [C.c_void_p, C.POINTER(DabProblem)]),
     "dab_update_parameters": (C.c_int, [C.c_void_p, _dp, _dp]),
     "dab_solve": (C.c_int, [C.c_void_p, C.POINTER(DabOptions), C.POINTER(DabSummary)]),

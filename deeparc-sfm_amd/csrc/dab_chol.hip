@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <vector>
 
+#include "dab_devmem.h"
 #include "dab_kernels.h"
 #include "dab_wave.h"
 
@@ -38,6 +39,7 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 __constant__ int g_chol_prio = 1;  // DAB_CHOL_PRIO=0: no wave priority for the panel chain (A/B)
 
 struct CholCtx {
+  Dev mem{"Cholesky scratch"};  // every device buffer below (guarded like the problem's)
   double* blk = nullptr;  // per block column: D [4][16][16] (inverses of the 16x16 diagonal
                           // blocks), then L_kk [64][64]; stride kBlk
 
@@ -65,16 +67,6 @@ struct CholCtx {
   unsigned* pready = nullptr; // per block: L_kk published by the fused column update (zeroed per factorisation)
   int group = 2;            // DAB_CHOL_GROUP: panels per bulk trailing update (2: pairs)
   int col_grid = 0;         // DAB_CHOL_COL_GRID: most work-groups of a column update (0: one per tile)
-  // the persistent dataflow factorisation (k_chol_flow): DAB_CHOL_FLOW=0 keeps the launches
-  bool flow = false;  // DAB_CHOL_FLOW=1 (default once measured on the GPU)
-  int flow_min = 32;        // DAB_CHOL_FLOW_MIN: fewest blocks that use it
-  int flow_ga = 64;         // DAB_CHOL_FLOW_GA: chain work-groups
-  int flow_grid = 0;        // work-groups that are resident together (0: the kernel does not fit)
-  unsigned* words = nullptr;  // its flags, zeroed per factorisation
-  size_t words_alloc = 0;
-  bool stamps_on = false;     // DAB_CHOL_FLOW_STAMPS=1: per-column timeline on stderr after each factorisation
-  unsigned long long* stamps = nullptr;
-  size_t stamps_alloc = 0;
   bool v1 = false;          // DAB_CHOL_V1=1: the per-step schedule (one bulk update per panel, one
                             // back-substitution launch per block)
 };
@@ -96,10 +88,6 @@ CholCtx* chol_create() {
   if (const char* e = getenv("DAB_CHOL_V1")) c->v1 = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_GROUP")) c->group = std::max(2, atoi(e));
   if (const char* e = getenv("DAB_CHOL_COL_GRID")) c->col_grid = std::max(0, atoi(e));
-  if (const char* e = getenv("DAB_CHOL_FLOW")) c->flow = atoi(e) != 0;
-  if (const char* e = getenv("DAB_CHOL_FLOW_MIN")) c->flow_min = atoi(e);
-  if (const char* e = getenv("DAB_CHOL_FLOW_GA")) c->flow_ga = std::max(1, atoi(e));
-  c->stamps_on = getenv("DAB_CHOL_FLOW_STAMPS") != nullptr;
   if (const char* e = getenv("DAB_CHOL_BACK_FLOW")) c->back_flow = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_PREFACTOR")) c->prefactor = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_FUSE_PANEL")) c->fuse_panel = atoi(e) != 0;
@@ -113,13 +101,12 @@ CholCtx* chol_create() {
     const int v = atoi(e);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chol_prio), &v, sizeof(int));
   }
-  c->flow_grid = 0;  // set by chol_flow_fits on first use
   // the side stream and the barrier word now, not inside the first solve. (A warm-up graph
   // capture here bought nothing: every instantiation costs ~5 ms, the first one no more.)
   int dev_now = 0;
   (void)hipGetDevice(&dev_now);
   c->device = dev_now;
-  if (!(c->side = stream_take(dev_now)) || hipMalloc(&c->bar, sizeof(unsigned)) != hipSuccess) {
+  if (!(c->side = stream_take(dev_now)) || c->mem.alloc(&c->bar, 1) != 0) {
     chol_destroy(c);
     return nullptr;
   }
@@ -128,12 +115,7 @@ CholCtx* chol_create() {
 void chol_destroy(CholCtx* c) {
   if (!c) return;
   if (c->exec) (void)hipGraphExecDestroy(c->exec);
-  if (c->blk) (void)hipFree(c->blk);
-  if (c->bar) (void)hipFree(c->bar);
-  if (c->words) (void)hipFree(c->words);
-  if (c->stamps) (void)hipFree(c->stamps);
-  if (c->ready) (void)hipFree(c->ready);
-  if (c->pready) (void)hipFree(c->pready);
+  c->mem.clear();
   for (hipEvent_t e : c->ev_panel) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_bulk) (void)hipEventDestroy(e);
   stream_give(c->device, c->side);
@@ -158,13 +140,6 @@ __device__ long long g_prof[16];
 #define PROF_MARK(i)
 #endif
 
-// factor16's off-chain multipliers and the inverse's L entries from LDS (1) or by DPP
-// broadcasts (0: the round-3 form, kept for A/B builds of scripts/potrf_micro.hip)
-#ifndef DAB_F16_LDS
-#define DAB_F16_LDS 0
-#endif
-constexpr bool kF16Lds = DAB_F16_LDS != 0;
-
 // 1/sqrt(d): v_rsq_f64 and two Newton steps
 __device__ __forceinline__ double rsqrt_nr(double d) {
   double y = __builtin_amdgcn_rsq(d);
@@ -188,55 +163,14 @@ struct RowB {
 };
 #define ROWB(v, j) RowB<0>::get((v), (j))
 
-// wave 0: factor L[o:o+16, o:o+16] in place, its inverse into D[16][DS]. ROWINV: the inverse
-// by rows (each broadcast depends on the step before: 137 VGPRs; the persistent factorisation,
-// whose work-groups must fit two per CU); else by columns (every lane its own column: more
-// independent work per step, but the compiler keeps the 120 broadcasts live: 256 VGPRs plus
-// AGPRs, fine for the one-work-group-per-CU launch schedule, and ~0.7 us faster per block)
-template <bool ROWINV = false>
+// wave 0: factor L[o:o+16, o:o+16] in place, its inverse into D[16][DS] by columns (every
+// lane its own column; the compiler keeps the 120 broadcasts live: 256 VGPRs plus AGPRs,
+// fine for the one-work-group-per-CU launch schedule)
 __device__ __noinline__ void factor16(double (*L)[LS], double (*D)[DS], int o, bool& bad) {
   const int lane = threadIdx.x & 63, r = lane & 15;
   double a[16], rd[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) a[j] = (j <= r) ? L[o + r][o + j] : 0.0;
-  if constexpr (!ROWINV && kF16Lds) {
-    // only the next pivot's column takes its multiplier L[j+1][j] by DPP (the dependent
-    // chain); the later columns read L[l][j] back from LDS as one-address broadcasts, off the
-    // VALU (a DPP f64 broadcast is two VALU moves). Column j goes to LDS as soon as it is
-    // final: this wave's own LDS accesses complete in order. T: the tile as an LDS
-    // address-space pointer (one base register, every entry an immediate offset; the
-    // generic pointer costs a null check per access)
-    typedef __attribute__((address_space(3))) double lds_f64;
-    lds_f64* T = (lds_f64*)&L[o][o];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const double d = ROWB(a[j], j);
-      bad |= !(d > 0.0) || !isfinite(d);
-      const double y = rsqrt_nr(d);
-      rd[j] = y;
-      const double lmj = (r == j) ? d * y : a[j] * y;
-      a[j] = lmj;
-      if (lane < 16 && r >= j) T[r * LS + j] = lmj;
-      if (j + 1 < 16) a[j + 1] = fma(-lmj, ROWB(lmj, j + 1), a[j + 1]);
-#pragma unroll
-      for (int l = j + 2; l < 16; ++l) a[l] = fma(-lmj, T[l * LS + j], a[l]);
-    }
-    // the inverse by columns (below), its L[i][m] also broadcast from LDS
-    const int cc = r;
-    double x[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      double s = (i == cc) ? 1.0 : 0.0;
-#pragma unroll
-      for (int m = 0; m < i; ++m) s -= T[i * LS + m] * x[m];
-      x[i] = (i >= cc) ? s * rd[i] : 0.0;
-    }
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) D[j][cc] = x[j];
-    }
-    return;
-  }
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const double d = ROWB(a[j], j);
@@ -249,48 +183,21 @@ __device__ __noinline__ void factor16(double (*L)[LS], double (*D)[DS], int o, b
 #pragma unroll
     for (int l = j + 1; l < 16; ++l) a[l] = fma(-lmj, ROWB(lmj, l), a[l]);
   }
-  if constexpr (!ROWINV) {
-    // lane c: column c of the inverse, x[i] = (delta_ic - sum_{c<=m<i} L[i][m] x[m]) / L[i][i]
-    const int cc = r;
-    double x[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      double s = (i == cc) ? 1.0 : 0.0;
-#pragma unroll
-      for (int m = 0; m < i; ++m) s -= ROWB(a[m], i) * x[m];
-      x[i] = (i >= cc) ? s * rd[i] : 0.0;
-    }
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        if (j <= r) L[o + r][o + j] = a[j];
-        D[j][cc] = x[j];
-      }
-    }
-    return;
-  }
-  // the inverse X = L^-1 by rows, lane r holding row r: once the rows above are final,
-  // lane m scales its row by 1/L[m][m] and broadcasts it, and every lane below subtracts
-  // L[r][m] X[m][.]. Each broadcast depends on the step before, so none is hoisted (the
-  // column form broadcast the factor's entries, which the compiler took from the pivot loop
-  // and kept live: 240 VGPRs)
+  // lane c: column c of the inverse, x[i] = (delta_ic - sum_{c<=m<i} L[i][m] x[m]) / L[i][i]
+  const int cc = r;
   double x[16];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) x[c] = (c == r) ? 1.0 : 0.0;
+  for (int i = 0; i < 16; ++i) {
+    double s = (i == cc) ? 1.0 : 0.0;
 #pragma unroll
-  for (int m = 0; m < 16; ++m) {
-#pragma unroll
-    for (int c = 0; c <= m; ++c) {
-      if (r == m) x[c] *= rd[m];
-      const double b = ROWB(x[c], m);
-      if (r > m) x[c] = fma(-a[m], b, x[c]);
-    }
+    for (int m = 0; m < i; ++m) s -= ROWB(a[m], i) * x[m];
+    x[i] = (i >= cc) ? s * rd[i] : 0.0;
   }
   if (lane < 16) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       if (j <= r) L[o + r][o + j] = a[j];
-      D[r][j] = x[j];
+      D[j][cc] = x[j];
     }
   }
 }
@@ -325,14 +232,13 @@ __device__ __forceinline__ void tile_store(double* M, int i0, int j0, const dbl4
 }
 
 // the 64x64 diagonal block (in LDS) -> L in place, D[p] = inverse of its p-th 16x16 block
-template <bool ROWINV = false>
 __device__ __forceinline__ void factor64(double (*L)[LS], double (*D)[16][DS], bool& bad) {
   const int tid = threadIdx.x, w = tid >> 6;
   double* Lf = &L[0][0];
 #pragma unroll 1
   for (int p = 0; p < 4; ++p) {
     const int o = 16 * p;
-    if (w == 0) factor16<ROWINV>(L, D[p], o, bad);
+    if (w == 0) factor16(L, D[p], o, bad);
     __syncthreads();
     PROF_MARK(2 + 2 * p);
     if (p == 3) break;
@@ -346,8 +252,6 @@ __device__ __forceinline__ void factor64(double (*L)[LS], double (*D)[16][DS], b
     }
     __syncthreads();
     // rank-16 update of the trailing lower tiles (ti >= tj), round robin over waves 0-3
-    // (the persistent factorisation's work-groups have 8 waves; the upper four only join the
-    // barriers)
     for (int t = w; w < 4 && t < nrc * (nrc + 1) / 2; t += 4) {
       int ti = 0;
       while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
@@ -1103,447 +1007,10 @@ __global__ __launch_bounds__(kThreads) void k_trsv_back_flow(const double* __res
   }
 }
 
-// ---- the persistent dataflow factorisation: the whole right-looking schedule in ONE launch ----
-// The multi-launch schedule above pays a graph dependency gap (~10 us) per block column, 93
-// of them at n = 5994, and its bulk launches wait for the chain and vice versa at stream
-// granularity. Here every work-group is resident for the whole factorisation and the same
-// dependencies are per-tile flags:
-//   chain work-groups [0, GA): row block t belongs to work-group t % GA. For each block column
-//     c in order, each owner updates its tiles (t, c), t >= c, with the panels [b, c) of the
-//     current group (b = R floor((c - 1) / R)) once the bulk updates of the earlier groups
-//     have reached the tile (bulkcnt) and row c's panels are final (rowdone[c] >= c); the
-//     owner of the diagonal tile factors it (factor64) and publishes L_cc and the 16x16
-//     inverses (pready[c]); the other owners wait for them, solve their rows and publish the
-//     panel tile (rowdone[t] = c + 1).
-//   bulk work-groups [GA, G): for each group g of R panels [b, b + R) (not the last), the
-//     rank-64R update of the trailing lower triangle from block b + R + 1 on, on 128 x 128
-//     super-tiles in column-major order (the columns the chain needs next come first), each
-//     once its rows' panels are final and the previous group's update of its tiles is done
-//     (bulkcnt, so every tile sees its updates in group order: the sums are the same on every
-//     run), then bulkcnt += 1 on its 64-tiles.
-// Every work-group walks its tasks in an order consistent with one global order (column,
-// then group), and every task waits only on earlier ones, so with all work-groups resident
-// the factorisation cannot deadlock; every wait is bounded anyway (flag |= 2, and an abort
-// word that releases every other waiter). The tiles cross work-groups and XCDs inside the
-// launch: every load and store of A and of the block scratch is write-through (sc1), the
-// publishing work-group drains its stores (vmcnt(0)) and meets at a barrier before one lane
-// stores the flag, and a consumer polls the flag from one lane, then the work-group meets at
-// a barrier before loading (MI355X_MICROARCH.md, the sc1 hand-off).
-constexpr int kFlowThreads = 256;  // 4 waves: two work-groups per CU at the 256 VGPRs factor64 needs
-typedef unsigned int fu2 __attribute__((ext_vector_type(2)));
-typedef unsigned int fu4 __attribute__((ext_vector_type(4)));
-
-struct Sc1 {  // write-through loads and stores of one buffer (32-bit byte offsets)
-  __amdgpu_buffer_rsrc_t r;
-  // i: element index (the buffer is < 2 GB: 32-bit arithmetic)
-  __device__ __forceinline__ double2 ld2(unsigned i) const {
-    return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(8u * i), 0, 16));
-  }
-  __device__ __forceinline__ double ld1(unsigned i) const {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)(8u * i), 0, 16));
-  }
-  __device__ __forceinline__ void st1(unsigned i, double v) const {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(fu2, v), r, (int)(8u * i), 0, 16);
-  }
-};
-
-struct FlowArgs {
-  double* A;
-  unsigned a_bytes;
-  int lda, n, nblk, rblk, R, GA;
-  double* blk;
-  unsigned blk_bytes;
-  int* flag;
-  unsigned* words;  // [pready: nblk][rowdone: rblk][bulkcnt: rblk * nblk][abort: 1], zeroed per launch
-  // DAB_CHOL_FLOW_STAMPS=1 (timeline, s_memrealtime at 100 MHz): [0] start, per column c
-  // [1 + 3c]: the diagonal tile's inputs ready, [2 + 3c]: factor start, [3 + 3c]: L_cc
-  // published; per group g [1 + 3 nblk + g]: its last super-tile done (max); else null
-  unsigned long long* stamps;
-};
-__device__ __forceinline__ void flow_stamp(unsigned long long* st, size_t i) {
-  if (st) __hip_atomic_store(st + i, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// lane 0 of the work-group: wait until *w >= want (relaxed agent-scope polls); false on a
-// timeout (flag |= 2, abort set) or when another work-group has aborted
-__device__ __forceinline__ bool flow_poll(const unsigned* w, unsigned want, unsigned* abortw, int* flag) {
-  for (int spins = 0;; ++spins) {
-    if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) return true;
-    if ((spins & 63) == 63 && __hip_atomic_load(abortw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
-    if (spins > (1 << 22)) {
-      atomicOr(flag, 2);
-      __hip_atomic_store(abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-// chain role: tile (t, c) updated with panels [b, c), then factored (t == c) or solved
-__device__ __noinline__ void flow_chain_tile(const FlowArgs& f, const Sc1& A, const Sc1& B, int t, int c, int b, double* sm,
-                                int& abort_s) {
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int li = lane & 15, lk = lane >> 4, wr = (w & 3) >> 1, wc = w & 1;
-  const int n = f.n, lda = f.lda;
-  const bool diag = t == c;
-  const bool skip = w >= 4 || (diag && wr < wc);  // MFMA on waves 0-3; strictly upper quadrant of a diagonal tile
-  double* Pa = sm;
-  double* Pb = sm + NB * LDP;
-  double (*Dsh)[16][DS] = reinterpret_cast<double (*)[16][DS]>(sm + 2 * NB * LDP);
-  const int r0 = t * NB, q0 = c * NB;  // first row, first column of the tile
-  dbl4 acc[2][2];
-#pragma unroll
-  for (int a2 = 0; a2 < 2; ++a2)
-#pragma unroll
-    for (int b2 = 0; b2 < 2; ++b2)
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int row = r0 + wr * 32 + a2 * 16 + lk + 4 * reg, col = q0 + wc * 32 + b2 * 16 + li;
-        acc[a2][b2][reg] = (!skip && row <= n && col < n) ? A.ld1((unsigned)row * lda + col) : 0.0;
-      }
-  for (int p = b; p < c; ++p) {
-    // panels A(t rows, p cols) and A(c rows, p cols): 64 x 32 double2 each, 4 per thread
-#pragma unroll
-    for (int q = 0; q < NB * NB / 2 / kFlowThreads; ++q) {
-      const int idx = tid + q * kFlowThreads, rr = idx >> 5, c2 = idx & 31;
-      const int ra = r0 + rr, rb = q0 + rr;
-      const double2 va = ra <= n ? A.ld2((unsigned)ra * lda + p * NB + 2 * c2) : make_double2(0.0, 0.0);
-      *reinterpret_cast<double2*>(&Pa[rr * LDP + 2 * c2]) = va;
-      if (!diag) {
-        const double2 vb = rb <= n ? A.ld2((unsigned)rb * lda + p * NB + 2 * c2) : make_double2(0.0, 0.0);
-        *reinterpret_cast<double2*>(&Pb[rr * LDP + 2 * c2]) = vb;
-      }
-    }
-    __syncthreads();
-    const double* PB = diag ? Pa : Pb;
-    if (!skip) {
-#pragma unroll 4
-      for (int ks = 0; ks < NB / 4; ++ks) {
-        double fa[2], fb[2];
-#pragma unroll
-        for (int a2 = 0; a2 < 2; ++a2) fa[a2] = -Pa[(wr * 32 + a2 * 16 + li) * LDP + ks * 4 + lk];
-#pragma unroll
-        for (int b2 = 0; b2 < 2; ++b2) fb[b2] = PB[(wc * 32 + b2 * 16 + li) * LDP + ks * 4 + lk];
-#pragma unroll
-        for (int a2 = 0; a2 < 2; ++a2)
-#pragma unroll
-          for (int b2 = 0; b2 < 2; ++b2)
-            acc[a2][b2] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a2], fb[b2], acc[a2][b2], 0, 0, 0);
-      }
-    }
-    __syncthreads();
-  }
-  const int kb = min(NB, n - q0);  // the block column's width
-  double (*P)[LS] = reinterpret_cast<double (*)[LS]>(Pa);
-  double (*L)[LS] = reinterpret_cast<double (*)[LS]>(Pb);
-    bool rows_below = !diag;  // panel rows to solve: the whole tile, or the rhs row under a short last block
-  if (diag) {
-#pragma unroll
-    for (int q = 0; q < NB * NB / kFlowThreads; ++q) {
-      const int idx = tid + q * kFlowThreads, i = idx >> 6, j = idx & 63;
-      L[i][j] = (i == j) ? 1.0 : 0.0;
-      P[i][j] = 0.0;
-    }
-    __syncthreads();
-    if (!skip) {
-#pragma unroll
-      for (int a2 = 0; a2 < 2; ++a2)
-#pragma unroll
-        for (int b2 = 0; b2 < 2; ++b2)
-#pragma unroll
-          for (int reg = 0; reg < 4; ++reg) {
-            const int i = wr * 32 + a2 * 16 + lk + 4 * reg, j = wc * 32 + b2 * 16 + li;
-            if (i < kb && j <= i) L[i][j] = acc[a2][b2][reg];
-          }
-    }
-    // a short last block: its rows from kb on (the rhs row) are panel rows of this column;
-    // they sit in the (lower-left) quadrants that the MFMA waves own whole
-    if (kb < NB && r0 + kb <= n) {
-      rows_below = true;
-      if (w < 4) {
-#pragma unroll
-        for (int a2 = 0; a2 < 2; ++a2)
-#pragma unroll
-          for (int b2 = 0; b2 < 2; ++b2)
-#pragma unroll
-            for (int reg = 0; reg < 4; ++reg) {
-              const int i = wr * 32 + a2 * 16 + lk + 4 * reg, j = wc * 32 + b2 * 16 + li;
-              if (i >= kb && j < kb && !(wr < wc)) P[i][j] = acc[a2][b2][reg];
-            }
-      }
-    }
-    __syncthreads();
-    if (tid == 0) flow_stamp(f.stamps, 2 + 3 * (size_t)c);
-    bool bad = false;
-    factor64<true>(L, Dsh, bad);
-    if (tid == 0 && bad) atomicOr(f.flag, 1);
-    const Sc1& Bk = B;
-#pragma unroll
-    for (int q = 0; q < NB * NB / kFlowThreads; ++q) {
-      const int idx = tid + q * kFlowThreads, i = idx >> 6, j = idx & 63;
-      Bk.st1((unsigned)c * kBlk + 1024 + idx, (j <= i) ? L[i][j] : 0.0);
-    }
-#pragma unroll
-    for (int q = 0; q < 1024 / kFlowThreads; ++q) {
-      const int idx = tid + q * kFlowThreads;  // [4][16][16]
-      Bk.st1((unsigned)c * kBlk + idx, Dsh[idx >> 8][(idx >> 4) & 15][idx & 15]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      __hip_atomic_store(f.words + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      flow_stamp(f.stamps, 3 + 3 * (size_t)c);
-    }
-    if (!rows_below) return;
-  } else {
-    if (w < 4) {
-#pragma unroll
-      for (int a2 = 0; a2 < 2; ++a2)
-#pragma unroll
-        for (int b2 = 0; b2 < 2; ++b2)
-#pragma unroll
-          for (int reg = 0; reg < 4; ++reg) {
-            const int i = wr * 32 + a2 * 16 + lk + 4 * reg, j = wc * 32 + b2 * 16 + li;
-            P[i][j] = j < kb ? acc[a2][b2][reg] : 0.0;
-          }
-    }
-    if (tid == 0) abort_s = !flow_poll(f.words + c, 1u, f.words + f.nblk + f.rblk + (size_t)f.rblk * f.nblk, f.flag);
-    __syncthreads();
-    if (abort_s) return;
-#pragma unroll
-    for (int q = 0; q < NB * NB / kFlowThreads; ++q) {
-      const int idx = tid + q * kFlowThreads, i = idx >> 6, j = idx & 63;
-      L[i][j] = B.ld1((unsigned)c * kBlk + 1024 + idx);
-    }
-#pragma unroll
-    for (int q = 0; q < 1024 / kFlowThreads; ++q) {
-      const int idx = tid + q * kFlowThreads;
-      Dsh[idx >> 8][(idx >> 4) & 15][idx & 15] = B.ld1((unsigned)c * kBlk + idx);
-    }
-    __syncthreads();
-  }
-  // P <- P L^-T, wave w < 4: rows [16 w, 16 w + 16) (as k_panel)
-  if (w < 4) {
-    double* Pf = &P[0][0];
-    const double* Lf = &L[0][0];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      dbl4 tt = tile_load<LS>(Pf, 16 * w, 16 * q);
-      if (q > 0) mma_nt<LS, LS>(16 * q, tt, Pf, 16 * w, 0, Lf, 16 * q, 0, -1.0);
-      __builtin_amdgcn_wave_barrier();
-      tile_store<LS>(Pf, 16 * w, 16 * q, tt);
-      __builtin_amdgcn_wave_barrier();
-      dbl4 x = {0.0, 0.0, 0.0, 0.0};
-      mma_nt<LS, DS>(16, x, Pf, 16 * w, 16 * q, &Dsh[q][0][0], 0, 0, 1.0);
-      __builtin_amdgcn_wave_barrier();
-      tile_store<LS>(Pf, 16 * w, 16 * q, x);
-    }
-  }
-  __syncthreads();
-  const int i0 = diag ? kb : 0;
-#pragma unroll
-  for (int q = 0; q < NB * NB / kFlowThreads; ++q) {
-    const int idx = tid + q * kFlowThreads, i = idx >> 6, j = idx & 63;
-    if (i >= i0 && r0 + i <= n && j < kb) A.st1((unsigned)(r0 + i) * lda + q0 + j, P[i][j]);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) __hip_atomic_store(f.words + f.nblk + t, (unsigned)(c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// bulk role: super-tile (bi, bj) (128 x 128, relative to element c0) -= A(rows, k0 .. k0 + kk)
-// A(cols, k0 .. k0 + kk)^T, kk a multiple of 16, on write-through accesses. Wave w owns the
-// 64 x 64 quadrant (w >> 1, w & 1): 4 x 4 tiles of v_mfma_f64_16x16x4f64; K in chunks of 16
-// through two LDS stages (the next chunk's loads in flight during the current MFMAs)
-__device__ __noinline__ void flow_bulk_tile(const FlowArgs& f, const Sc1& A, int c0, int m, int k0, int kk, int bi, int bj,
-                               double* sm) {
-  constexpr int KC = 16, LKC = KC + 2;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
-  const int wr = w >> 1, wc = w & 1;
-  const int lr = tid >> 1, lh = (tid & 1) * 8;  // loader: row lr, k columns lh .. lh + 7
-  const int nch = kk / KC;
-  const int lda = f.lda;
-  const bool diag = bi == bj;
-  const bool skip = diag && wr < wc;
-  const int ri0 = bi * TB, rj0 = bj * TB;
-  double2 ra[4], rb[4];
-  auto gload = [&](int ch) {
-    const int ia = ri0 + lr, ib = rj0 + lr;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int kc = ch * KC + lh + 2 * q;
-      ra[q] = ia < m ? A.ld2((unsigned)(c0 + ia) * lda + k0 + kc) : make_double2(0.0, 0.0);
-      rb[q] = (!diag && ib < m) ? A.ld2((unsigned)(c0 + ib) * lda + k0 + kc) : make_double2(0.0, 0.0);
-    }
-  };
-  auto sstore = [&](int st) {
-    double* a = sm + 2 * st * TB * LKC + lr * LKC + lh;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) *reinterpret_cast<double2*>(a + 2 * q) = ra[q];
-    if (!diag) {
-      double* bb = a + TB * LKC;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) *reinterpret_cast<double2*>(bb + 2 * q) = rb[q];
-    }
-  };
-  dbl4 acc[4][4];
-#pragma unroll
-  for (int tr = 0; tr < 4; ++tr)
-#pragma unroll
-    for (int tc = 0; tc < 4; ++tc)
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int row = ri0 + 64 * wr + 16 * tr + lk + 4 * reg, col = rj0 + 64 * wc + 16 * tc + li;
-        acc[tr][tc][reg] = (!skip && row < m && col < m) ? A.ld1((unsigned)(c0 + row) * lda + c0 + col) : 0.0;
-      }
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  for (int ch = 0; ch < nch; ++ch) {
-    const int st = ch & 1;
-    if (ch + 1 < nch) gload(ch + 1);
-    if (!skip) {
-      const double* As = sm + 2 * st * TB * LKC;
-      const double* Bs = diag ? As : As + TB * LKC;
-#pragma unroll
-      for (int ks = 0; ks < KC / 4; ++ks) {
-        double fa[4], fb[4];
-#pragma unroll
-        for (int tr = 0; tr < 4; ++tr) fa[tr] = -As[(64 * wr + 16 * tr + li) * LKC + 4 * ks + lk];
-#pragma unroll
-        for (int tc = 0; tc < 4; ++tc) fb[tc] = Bs[(64 * wc + 16 * tc + li) * LKC + 4 * ks + lk];
-#pragma unroll
-        for (int tr = 0; tr < 4; ++tr)
-#pragma unroll
-          for (int tc = 0; tc < 4; ++tc)
-            acc[tr][tc] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[tr], fb[tc], acc[tr][tc], 0, 0, 0);
-      }
-    }
-    if (ch + 1 < nch) sstore(st ^ 1);
-    __syncthreads();
-  }
-  if (!skip) {
-#pragma unroll
-    for (int tr = 0; tr < 4; ++tr)
-#pragma unroll
-      for (int tc = 0; tc < 4; ++tc)
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-          const int row = ri0 + 64 * wr + 16 * tr + lk + 4 * reg, col = rj0 + 64 * wc + 16 * tc + li;
-          if (row < m && col < m) A.st1((unsigned)(c0 + row) * lda + c0 + col, acc[tr][tc][reg]);
-        }
-  }
-}
-
-constexpr int kFlowLds = 2 * NB * LDP + 4 * 16 * DS;  // doubles: the chain role (Pa, Pb, D)
-static_assert(kFlowLds >= 2 * 2 * TB * 18, "the bulk role's double buffer fits the chain's LDS");
-
-__global__ __launch_bounds__(kFlowThreads, 2) void k_chol_flow(FlowArgs f) {
-  __shared__ double sm[kFlowLds];
-  __shared__ int abort_s;
-  const int tid = threadIdx.x;
-  const Sc1 A{__builtin_amdgcn_make_buffer_rsrc(f.A, (short)0, (int)f.a_bytes, 0x00020000)};
-  const Sc1 B{__builtin_amdgcn_make_buffer_rsrc(f.blk, (short)0, (int)f.blk_bytes, 0x00020000)};
-  unsigned* pready = f.words;
-  unsigned* rowdone = f.words + f.nblk;
-  unsigned* bulkcnt = rowdone + f.rblk;
-  unsigned* abortw = bulkcnt + (size_t)f.rblk * f.nblk;
-  const int R = f.R, nblk = f.nblk, rblk = f.rblk, n = f.n;
-  if (tid == 0) abort_s = 0;
-  if (tid == 0 && blockIdx.x == 0) flow_stamp(f.stamps, 0);
-  __syncthreads();
-  if ((int)blockIdx.x < f.GA) {
-    // ---- chain ----
-    // Per block column c, the owner of row c + 1 first solves its tile (c + 1, c) and at once
-    // factors the next diagonal tile (c + 1, c + 1), the chain's next step; then every owner
-    // solves its other tiles of column c. (Without that lookahead the next diagonal waited
-    // behind its owner's other tiles of the column: ~36 us per column at n = 5994.)
-    if (g_chol_prio) __builtin_amdgcn_s_setprio(3);
-    const int a = blockIdx.x, GA = f.GA;
-    auto tile = [&](int t, int c) -> bool {  // false: abort
-      const int b = R * ((c - 1) / R);                      // the current group's panels [b, c)
-      const unsigned ncov = c >= R + 1 ? (unsigned)((c - R - 1) / R + 1) : 0u;  // bulk groups before
-      if (tid == 0) {
-        bool ok = flow_poll(bulkcnt + (size_t)t * nblk + c, ncov, abortw, f.flag);
-        if (ok && t != c) ok = flow_poll(rowdone + c, (unsigned)c, abortw, f.flag);
-        abort_s = !ok;
-      }
-      __syncthreads();
-      if (abort_s) return false;
-      if (t == c && tid == 0) flow_stamp(f.stamps, 1 + 3 * (size_t)c);
-      flow_chain_tile(f, A, B, t, c, b, sm, abort_s);
-      if (abort_s) return false;
-      __syncthreads();  // the tile's LDS reads are done before the next tile's staging
-      return true;
-    };
-    if (a == 0 && !tile(0, 0)) return;
-    for (int c = 0; c < nblk; ++c) {
-      const bool own_next = c + 1 < nblk && (c + 1) % GA == a;
-      if (own_next && !(tile(c + 1, c) && tile(c + 1, c + 1))) return;
-      for (int t = c + ((a - c) % GA + GA) % GA; t < rblk; t += GA) {
-        if (t == c || (own_next && t == c + 1)) continue;  // done above (this or the previous column)
-        if (!tile(t, c)) return;
-      }
-    }
-    (void)pready;
-    return;
-  }
-  // ---- bulk ----
-  const int GB = gridDim.x - f.GA, beta = blockIdx.x - f.GA;
-  for (int g = 0;; ++g) {
-    const int b = g * R, cend = b + R;
-    if (cend >= nblk) break;
-    const int c0 = cend + 1, m = n + 1 - c0 * NB;
-    if (m <= 1) break;
-    const int T2 = (m + TB - 1) / TB, ntb = T2 * (T2 + 1) / 2;
-    const int start = (int)(((long long)beta + (long long)g * 37) % GB);
-    for (int s = start; s < ntb; s += GB) {
-      // column-major over the lower triangle: column J holds T2 - J super-tiles
-      int J = 0, s0 = 0;
-      while (s0 + (T2 - J) <= s) {
-        s0 += T2 - J;
-        ++J;
-      }
-      const int I = J + (s - s0);
-      if (tid == 0) {
-        bool ok = true;
-        // the rows of both operands: their panels [b, cend) final
-        for (int u = 0; u < 4 && ok; ++u) {
-          const int rbk = c0 + 2 * (u < 2 ? I : J) + (u & 1);
-          if (rbk < rblk && rbk * NB <= n) ok = flow_poll(rowdone + rbk, (unsigned)cend, abortw, f.flag);
-        }
-        // the previous groups' updates of its 64-tiles
-        for (int u = 0; u < 4 && ok; ++u) {
-          const int tr = c0 + 2 * I + (u >> 1), tc = c0 + 2 * J + (u & 1);
-          if (tr < rblk && tr * NB <= n && tc < nblk && tc <= tr) ok = flow_poll(bulkcnt + (size_t)tr * nblk + tc, (unsigned)g, abortw, f.flag);
-        }
-        abort_s = !ok;
-      }
-      __syncthreads();
-      if (abort_s) return;
-      flow_bulk_tile(f, A, c0 * NB, m, b * NB, R * NB, I, J, sm);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        for (int u = 0; u < 4; ++u) {
-          const int tr = c0 + 2 * I + (u >> 1), tc = c0 + 2 * J + (u & 1);
-          if (tr < rblk && tr * NB <= n && tc < nblk && tc <= tr)
-            __hip_atomic_fetch_add(bulkcnt + (size_t)tr * nblk + tc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (f.stamps)
-          __hip_atomic_fetch_max(f.stamps + 1 + 3 * (size_t)nblk + g, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-}
-
 static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y,
                                  int* d_flag);
 
 static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag, bool launch);
-static int flow_prepare(CholCtx* c, int n, int lda);
-static void flow_print_stamps(CholCtx* c, hipStream_t s, int n);
 int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag) {
   return chol_build(c, s, n, A, lda, y, d_flag, true);
 }
@@ -1558,20 +1025,16 @@ static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
   if ((size_t)nblk > c->nblk_alloc) {
     if (c->exec) (void)hipGraphExecDestroy(c->exec);
     c->exec = nullptr;
-    if (c->blk) (void)hipFree(c->blk);
+    for (void* p : {(void*)c->blk, (void*)c->ready, (void*)c->pready}) c->mem.drop(p);
     c->blk = nullptr;
-    if (c->ready) (void)hipFree(c->ready);
-    c->ready = nullptr;
-    if (c->pready) (void)hipFree(c->pready);
-    c->pready = nullptr;
-    if (hipMalloc(&c->blk, sizeof(double) * kBlk * (size_t)nblk) != hipSuccess) return -2;
-    if (hipMalloc(&c->ready, sizeof(unsigned) * (size_t)nblk) != hipSuccess) return -2;
-    if (hipMalloc(&c->pready, sizeof(unsigned) * (size_t)nblk) != hipSuccess) return -2;
+    c->ready = c->pready = nullptr;
+    if (c->mem.alloc(&c->blk, (size_t)kBlk * nblk) != 0) return -2;
+    if (c->mem.alloc(&c->ready, (size_t)nblk) != 0) return -2;
+    if (c->mem.alloc(&c->pready, (size_t)nblk) != 0) return -2;
     c->nblk_alloc = nblk;
   }
   if (!c->side && !(c->side = stream_take(c->device))) return -3;
-  if (flow_prepare(c, n, lda) != 0) return -2;
-  if (!c->bar && hipMalloc(&c->bar, sizeof(unsigned)) != hipSuccess) return -2;
+  if (!c->bar && c->mem.alloc(&c->bar, 1) != 0) return -2;
   while ((int)c->ev_panel.size() < nblk) {
     hipEvent_t a, b;
     if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess) return -3;
@@ -1584,7 +1047,6 @@ static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
   if (c->nograph || nblk < c->graph_min) {  // nograph: debugging aid
     if (launch) {
       enqueue_factor_solve(c, s, n, A, lda, y, d_flag);
-      flow_print_stamps(c, s, n);
     }
     return 0;
   }
@@ -1610,86 +1072,11 @@ static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
   }
   if (!launch) return 0;
   if (hipGraphLaunch(c->exec, s) != hipSuccess) return -3;
-  flow_print_stamps(c, s, n);
   return 0;
 }
 
 static void enqueue_back_substitution(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y,
                                       int* d_flag);
-// The persistent factorisation when it applies (enough blocks, every work-group resident,
-// 32-bit offsets): the flags zeroed, the one launch, then the back substitution.
-static bool flow_applies(const CholCtx* c, int n, int lda) {
-  const int nblk = (n + NB - 1) / NB;
-  const size_t a_bytes = sizeof(double) * (size_t)(n + 1) * lda, b_bytes = sizeof(double) * (size_t)kBlk * nblk;
-  return c->flow && nblk >= c->flow_min && c->flow_grid > c->flow_ga + 8 && a_bytes < (1ull << 31) &&
-         b_bytes < (1ull << 31);
-}
-// outside any stream capture (occupancy query, allocation): the grid and the flag words
-static int flow_prepare(CholCtx* c, int n, int lda) {
-  if (!c->flow) return 0;
-  if (c->flow_grid == 0) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_chol_flow), kFlowThreads,
-                                                     0) != hipSuccess)
-      per_cu = 0;
-    c->flow_grid = per_cu >= 2 ? 2 * c->ncu : -1;
-  }
-  if (!flow_applies(c, n, lda)) return 0;
-  const int nblk = (n + NB - 1) / NB, rblk = (n + 1 + NB - 1) / NB;
-  const size_t nw = (size_t)nblk + rblk + (size_t)rblk * nblk + 1;
-  if (nw > c->words_alloc) {
-    if (c->words) (void)hipFree(c->words);
-    c->words = nullptr;
-    c->words_alloc = 0;
-    if (hipMalloc(&c->words, sizeof(unsigned) * nw) != hipSuccess) return -2;
-    c->words_alloc = nw;
-  }
-  const size_t ns = 1 + 3 * (size_t)nblk + (size_t)nblk;
-  if (c->stamps_on && ns > c->stamps_alloc) {
-    if (c->stamps) (void)hipFree(c->stamps);
-    c->stamps = nullptr;
-    c->stamps_alloc = 0;
-    if (hipMalloc(&c->stamps, sizeof(unsigned long long) * ns) != hipSuccess) return -2;
-    c->stamps_alloc = ns;
-  }
-  return 0;
-}
-// DAB_CHOL_FLOW_STAMPS: the last factorisation's timeline (us from the kernel's start)
-static void flow_print_stamps(CholCtx* c, hipStream_t s, int n) {
-  if (!c->stamps_on || !c->stamps) return;
-  const int nblk = (n + NB - 1) / NB;
-  std::vector<unsigned long long> h(1 + 4 * (size_t)nblk);
-  if (hipStreamSynchronize(s) != hipSuccess ||
-      hipMemcpy(h.data(), c->stamps, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost) != hipSuccess)
-    return;
-  auto us = [&](unsigned long long t) { return t ? 0.01 * (double)(long long)(t - h[0]) : -1.0; };
-  std::fprintf(stderr, "flow n=%d: col ready factor published | factor us | step us (published - previous published)\n", n);
-  double prev = 0.0;
-  for (int cc = 0; cc < nblk; ++cc) {
-    const double r = us(h[1 + 3 * cc]), f0 = us(h[2 + 3 * cc]), p = us(h[3 + 3 * cc]);
-    std::fprintf(stderr, "flow col %3d %9.2f %9.2f %9.2f | %6.2f | %6.2f\n", cc, r, f0, p, p - f0, p - prev);
-    prev = p;
-  }
-  for (int g = 0; g < nblk; ++g)
-    if (h[1 + 3 * nblk + g]) std::fprintf(stderr, "flow group %3d bulk done %9.2f\n", g, us(h[1 + 3 * nblk + g]));
-}
-static bool flow_enqueue(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag) {
-  if (!flow_applies(c, n, lda)) return false;
-  const int nblk = (n + NB - 1) / NB, rblk = (n + 1 + NB - 1) / NB;
-  const size_t nw = (size_t)nblk + rblk + (size_t)rblk * nblk + 1;
-  if (nw > c->words_alloc) return false;
-  const int G = c->flow_grid;
-  const size_t a_bytes = sizeof(double) * (size_t)(n + 1) * lda, b_bytes = sizeof(double) * (size_t)kBlk * nblk;
-  (void)hipMemsetAsync(c->words, 0, sizeof(unsigned) * nw, s);
-  unsigned long long* st = c->stamps_on ? c->stamps : nullptr;
-  if (st) (void)hipMemsetAsync(st, 0, sizeof(unsigned long long) * c->stamps_alloc, s);
-  FlowArgs f{A, (unsigned)a_bytes, lda, n, nblk, rblk, std::max(2, c->group), c->flow_ga, c->blk, (unsigned)b_bytes,
-             d_flag, c->words, st};
-  k_chol_flow<<<G, kFlowThreads, 0, s>>>(f);
-  enqueue_back_substitution(c, s, n, A, lda, y, d_flag);
-  return true;
-}
-
 static void enqueue_factor_solve_v1(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y,
                                     int* d_flag);
 // Panel PAIRS with lookahead. Chain stream s, per pair (b, b+1): [wait the previous pair's
@@ -1704,7 +1091,6 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
     return;
   }
   const int nblk = (n + NB - 1) / NB;
-  if (flow_enqueue(c, s, n, A, lda, y, d_flag)) return;
   hipStream_t s2 = c->serial ? s : c->side;  // serial: debugging aid
   auto kb_of = [&](int b) { return std::min(NB, n - b * NB); };
   // every panel after the first follows the column update of its block, which factors the
@@ -1836,6 +1222,12 @@ static void enqueue_factor_solve_v1(CholCtx* c, hipStream_t s, int n, double* A,
     k_trsv_back<<<grid, kThreads, 0, s>>>(A, lda, k, kb, c->blk + (size_t)b * kBlk, z, y);
   }
 }
+
+// DAB_DEV_GUARD: the canaries after the scratch blocks (the caller has synchronised)
+int chol_guard_check(CholCtx* c, const char* where, std::string* first) {
+  return c ? c->mem.guard_check(where, first) : 0;
+}
+Dev* chol_mem(CholCtx* c) { return c ? &c->mem : nullptr; }
 
 // Loads this translation unit's code object on the current device now: otherwise the first
 // launch of any of its kernels pays for it (10-40 ms, inside a process's first LM iteration).

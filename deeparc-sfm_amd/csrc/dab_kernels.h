@@ -1,5 +1,6 @@
 // dab_kernels.h — launchers of the gfx950 kernels (dab_kernels.hip, dab_chol.hip).
 #pragma once
+#include <string>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -349,6 +350,9 @@ CholCtx* chol_create();
 void chol_destroy(CholCtx*);
 int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag);
 int chol_prepare(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag);
+int chol_guard_check(CholCtx* c, const char* where, std::string* first);
+struct Dev;
+Dev* chol_mem(CholCtx* c);  // the Cholesky scratch's allocator (dab_devmem.h)
 
 int grid_for(int n, int block, int cap);
 

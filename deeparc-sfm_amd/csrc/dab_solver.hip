@@ -34,6 +34,7 @@
 #include <thread>
 #include <vector>
 
+#include "dab_devmem.h"
 #include "dab_internal.h"
 #include "dab_kernels.h"
 #include "dab_p2p.h"
@@ -78,10 +79,13 @@ hipStream_t stream_take(int device) {
   {
     std::lock_guard<std::mutex> lk(cache_mu());
     auto& v = stream_cache()[device];
-    if (!v.empty()) {
+    while (!v.empty()) {
       hipStream_t s = v.back();
       v.pop_back();
-      return s;
+      const hipError_t q = hipStreamQuery(s);  // a stream left in an error state is not reused
+      if (q == hipSuccess || q == hipErrorNotReady) return s;
+      (void)hipGetLastError();
+      (void)hipStreamDestroy(s);
     }
   }
   hipStream_t s = nullptr;
@@ -117,6 +121,17 @@ void pinned_give(void* p, size_t bytes) {
   pinned_cache()[bytes].push_back(p);
 }
 }  // namespace dab
+
+extern "C" int dab_release_caches(void) {
+  std::lock_guard<std::mutex> lk(dab::cache_mu());
+  for (auto& kv : dab::stream_cache())
+    for (hipStream_t s : kv.second) (void)hipStreamDestroy(s);
+  dab::stream_cache().clear();
+  for (auto& kv : dab::pinned_cache())
+    for (void* p : kv.second) (void)hipHostFree(p);
+  dab::pinned_cache().clear();
+  return 0;
+}
 
 namespace {
 
@@ -249,178 +264,14 @@ enum Slot {
   S_NSLOTS = S_CFX + 2 * kFxWords
 };
 
-// Device buffers of one problem. dab_set_problem releases them all and the new problem
-// allocates its own; a release keeps the memory in a pool instead of freeing it, and an
-// allocation takes the smallest pooled block that holds it without wasting more than half
-// (or 1 MiB), so the sfm.cc loop's re-set-up after every filter round (the same problem,
-// a little smaller) finds its ~50 buffers there instead of paying a hipMalloc / hipFree pair
-// each (a few ms per set-up at 160k observations). A pooled block unused through one whole
-// set-up and solve cycle is freed at the next release. The stream is synchronised before a
-// release (dab_set_problem), so no queued kernel still reads a block that gets reused.
-struct Dev {
-  struct Blk {
-    void* p;
-    size_t bytes;
-    int age;
-    bool slab;  // carved from a slab: never freed on its own
-  };
-  std::vector<Blk> live, pool, spare;  // spare: slab pieces aged out of the pool
-  // Blocks up to kSmall come from 8 MB slabs (bump-allocated; a handle's few dozen small
-  // buffers cost one hipMalloc instead of one each, and the handle's destruction a few
-  // hipFrees instead of dozens)
-  static constexpr size_t kSlab = (size_t)8 << 20;
-  // DAB_DEV_SLAB=1 turns the slabs on (off by default until a C5 PCG trajectory that changed
-  // with them is explained)
-  const size_t kSmall = getenv("DAB_DEV_SLAB") && atoi(getenv("DAB_DEV_SLAB")) != 0 ? (size_t)1 << 20 : 0;
-  std::vector<void*> slabs;
-  size_t slab_off = kSlab;
-  ~Dev() { clear(); }
-  void clear() {  // free everything now, pooled blocks included
-    for (const Blk& b : live)
-      if (!b.slab) (void)hipFree(b.p);
-    for (const Blk& b : pool)
-      if (!b.slab) (void)hipFree(b.p);
-    for (void* q : slabs) (void)hipFree(q);
-    live.clear();
-    pool.clear();
-    spare.clear();
-    slabs.clear();
-    slab_off = kSlab;
-  }
-  void release() {
-    std::vector<Blk> keep;
-    for (Blk& b : pool) {
-      if (++b.age < 2) keep.push_back(b);
-      else if (b.slab) spare.push_back(b);
-      else (void)hipFree(b.p);
-    }
-    for (Blk b : live) {
-      b.age = 0;
-      keep.push_back(b);
-    }
-    pool.swap(keep);
-    live.clear();
-  }
-  // best fit in v among blocks of bytes .. cap; v.size() when none
-  static size_t best_fit(const std::vector<Blk>& v, size_t bytes, size_t cap) {
-    size_t best = v.size();
-    for (size_t i = 0; i < v.size(); ++i)
-      if (v[i].bytes >= bytes && v[i].bytes <= cap && (best == v.size() || v[i].bytes < v[best].bytes)) best = i;
-    return best;
-  }
-  // debugging aids (read once): DAB_DEV_GUARD=1 puts a 64-KB zero canary after every block
-  // and guard_check() reports one with a nonzero byte (found the CG partials' overrun); DAB_DEV_POISON=1 fills every block handed out
-  // with 0xFF bytes (NaN doubles), so that a read of memory nobody wrote shows
-  static constexpr size_t kGuard = (size_t)64 << 10;
-  struct Guard {
-    char* p;  // the canary's first byte
-    size_t bytes;  // the block's usable size
-    int serial;
-  };
-  std::vector<Guard> guards;
-  int serial = 0;
-  static bool guard_on() {
-    static const bool on = getenv("DAB_DEV_GUARD") && atoi(getenv("DAB_DEV_GUARD")) != 0;
-    return on;
-  }
-  static bool poison_on() {
-    static const bool on = getenv("DAB_DEV_POISON") && atoi(getenv("DAB_DEV_POISON")) != 0;
-    return on;
-  }
-  // 1: 0xFF (NaN doubles, also caught when multiplied by zero); 2: 0x41 (finite, ~2.3e6
-  // as a double: caught only where the value is used)
-  static int poison_byte() {
-    static const int b = getenv("DAB_DEV_POISON") && atoi(getenv("DAB_DEV_POISON")) == 2 ? 0x41 : 0xFF;
-    return b;
-  }
-  // 0, or the number of overwritten canaries (each reported on stderr)
-  int guard_check(const char* where) {
-    int bad = 0;
-    std::vector<unsigned char> h(kGuard);
-    for (const Guard& g : guards) {
-      if (hipMemcpy(h.data(), g.p, kGuard, hipMemcpyDeviceToHost) != hipSuccess) continue;
-      size_t first = kGuard;
-      for (size_t i = 0; i < kGuard; ++i)
-        if (h[i] != 0) {
-          first = i;
-          break;
-        }
-      if (first < kGuard) {
-        ++bad;
-        std::fprintf(stderr, "dab guard (%s): block #%d of %zu bytes overrun at +%zu\n", where, g.serial, g.bytes,
-                     first);
-      }
-    }
-    return bad;
-  }
-  template <class T>
-  int alloc(T** out, size_t n) {
-    if (n == 0) n = 1;
-    const size_t want = (n * sizeof(T) + 255) & ~(size_t)255;
-    const size_t bytes = want + (guard_on() ? kGuard : 0);
-    const size_t cap = std::max(2 * bytes, bytes + ((size_t)1 << 20));
-    Blk got{nullptr, bytes, 0, false};
-    for (std::vector<Blk>* v : {&pool, &spare}) {
-      const size_t i = best_fit(*v, bytes, cap);
-      if (i < v->size()) {
-        got = (*v)[i];
-        got.age = 0;
-        (*v)[i] = v->back();
-        v->pop_back();
-        break;
-      }
-    }
-    if (!got.p && bytes <= kSmall) {
-      if (slab_off + bytes > kSlab) {
-        void* q = nullptr;
-        if (hipMalloc(&q, kSlab) == hipSuccess) {
-          slabs.push_back(q);
-          slab_off = 0;
-        }
-      }
-      if (slab_off + bytes <= kSlab) {
-        got = Blk{static_cast<char*>(slabs.back()) + slab_off, bytes, 0, true};
-        slab_off += bytes;
-      }
-    }
-    if (!got.p) {
-      void* p = nullptr;
-      if (hipMalloc(&p, bytes) != hipSuccess) {
-        // the pool may hold what the device needs: give it back and try once more
-        for (const Blk& b : pool) {
-          if (b.slab) spare.push_back(b);
-          else (void)hipFree(b.p);
-        }
-        pool.clear();
-        if (hipMalloc(&p, bytes) != hipSuccess)
-          return set_error(DAB_E_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
-      }
-      got = Blk{p, bytes, 0, false};
-    }
-    live.push_back(got);
-    *out = static_cast<T*>(got.p);
-    // (the fills run on the null stream, which does not order against the handle's
-    // non-blocking stream: the device is synchronised after them, or the handle's own
-    // uploads could land first and be overwritten)
-    if (poison_on()) (void)hipMemset(got.p, poison_byte(), want);
-    if (guard_on()) {
-      char* g = static_cast<char*>(got.p) + want;
-      (void)hipMemset(g, 0, kGuard);  // zeros: a stray read of the canary is a harmless 0 / index 0
-    }
-    if (poison_on() || guard_on()) (void)hipDeviceSynchronize();
-    if (guard_on()) {
-      char* g = static_cast<char*>(got.p) + want;
-      // a reused block drops the canaries of its earlier uses (now inside its usable bytes)
-      char* lo = static_cast<char*>(got.p);
-      char* hi = lo + got.bytes;
-      guards.erase(std::remove_if(guards.begin(), guards.end(), [&](const Guard& x) { return x.p >= lo && x.p < hi; }),
-                   guards.end());
-      guards.push_back(Guard{g, want, serial});
-    }
-    ++serial;
-    return 0;
-  }
-};
+// Device buffers of one problem come from a Dev (dab_devmem.h): dab_set_problem releases
+// them all into a pool instead of freeing them, and an allocation takes the smallest pooled
+// block that holds it without wasting more than half (or 1 MiB), so the sfm.cc loop's
+// re-set-up after every filter round (the same problem, a little smaller) finds its ~50
+// buffers there instead of paying a hipMalloc / hipFree pair each. A pooled block unused
+// through one whole set-up and solve cycle is freed at the next release. The stream is
+// synchronised before a release (dab_set_problem), so no queued kernel still reads a block
+// that gets reused.
 
 template <class T, class A>
 int upload(T** dptr, Dev& dev, const std::vector<T, A>& h, hipStream_t s) {
@@ -527,8 +378,9 @@ struct dab_handle {
   big_vec<int> h_ent_cam, h_ent_pos, h_ent_os;
 
   // ---- device buffers ----
-  Dev dev;
-  Dev setup_tmp;  // the device set-up's scratch (released by the next set-up)
+  Dev dev{"problem buffers"};
+  Dev setup_tmp{"set-up scratch"};  // the device set-up's scratch (released by the next set-up)
+  Dev keep_dev{"kept buffers"};     // the Sticky buffers below (never released, re-sized by drop + alloc)
   DevView view{};
   int4* d_obs_idx = nullptr;
   double2* d_obs_xy = nullptr;
@@ -630,11 +482,12 @@ struct dab_handle {
   int sticky(Sticky& st, T** out, size_t n) {
     const size_t bytes = std::max<size_t>(1, n) * sizeof(T);
     if (bytes > st.cap) {
-      if (st.p) (void)hipFree(st.p);
+      keep_dev.drop(st.p);
       st.p = nullptr;
       st.cap = 0;
-      if (hipMalloc(&st.p, bytes) != hipSuccess)
-        return set_error(DAB_E_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
+      char* q = nullptr;
+      CHECK_RC(keep_dev.alloc(&q, bytes));
+      st.p = q;
       st.cap = bytes;
     }
     *out = static_cast<T*>(st.p);
@@ -654,8 +507,7 @@ struct dab_handle {
     phase("start");
     dev.clear();
     phase("device buffers");
-    for (Sticky* st : {&st_S, &st_yc, &st_flags})
-      if (st->p) (void)hipFree(st->p);
+    keep_dev.clear();
     pinned_give(h_scal, sizeof(double) * S_NSLOTS);
     pinned_give(h_flags, sizeof(int) * 4);
     pinned_give(h_pcg_state, sizeof(PcgState));
@@ -847,6 +699,10 @@ static int create_common(int device, dab_handle** out) {
     delete h;
     return set_error(DAB_E_DEVICE, "Cholesky context creation failed");
   }
+  // an allocation that fails in one allocator first empties the others' idle pools
+  h->keep_dev.donors = {&h->dev, &h->setup_tmp};
+  chol_mem(h->chol)->donors = {&h->dev, &h->setup_tmp};
+  h->dev.donors = {&h->setup_tmp};
   if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
       hipEventCreate(&h->ev2) != hipSuccess || hipEventCreate(&h->ev3) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_cam, hipEventDisableTiming) != hipSuccess ||
@@ -877,6 +733,26 @@ static int create_common(int device, dab_handle** out) {
   }
   *out = h;
   return 0;
+}
+
+// DAB_DEV_GUARD=1: after an entry point's device work, every canary of the handle's
+// allocators (problem buffers, set-up scratch, kept buffers, Cholesky scratch, and `extra`,
+// an entry point's own temporaries) is read back; an overwritten one fails the call closed
+// (DAB_E_DEVICE, the first block named in dab_last_error) instead of returning its result
+static int guard_fail(dab_handle* h, const char* where, Dev* extra = nullptr) {
+  if (!Dev::guard_on() || !h) return 0;
+  (void)hipDeviceSynchronize();
+  if (Dev::guard_mode() == 2 && std::strcmp(where, "dab_set_problem") == 0 && !h->dev.guards.empty()) {
+    const unsigned char one = 1;  // the net's self-test: one byte past the first block
+    (void)hipMemcpy(h->dev.guards.front().p, &one, 1, hipMemcpyHostToDevice);
+  }
+  std::string first;
+  int bad = h->dev.guard_check(where, &first) + h->setup_tmp.guard_check(where, &first) +
+            h->keep_dev.guard_check(where, &first) + chol_guard_check(h->chol, where, &first);
+  if (extra) bad += extra->guard_check(where, &first);
+  if (bad == 0) return 0;
+  return set_error(DAB_E_DEVICE, "device guard: " + first +
+                                     (bad > 1 ? " (and " + std::to_string(bad - 1) + " more)" : std::string()));
 }
 
 extern "C" int dab_create(int device, dab_handle** out) {
@@ -2104,7 +1980,13 @@ static int setup_device(dab_handle* h, const dab_problem* p, const std::function
   return 0;
 }
 
+static int set_problem_impl(dab_handle* h, const dab_problem* p);
 extern "C" int dab_set_problem(dab_handle* h, const dab_problem* p) {
+  const int rc = set_problem_impl(h, p);
+  CHECK_RC(guard_fail(h, "dab_set_problem"));
+  return rc;
+}
+static int set_problem_impl(dab_handle* h, const dab_problem* p) {
   clear_error();
   if (!h) return set_error(DAB_E_INVALID, "null handle");
   CHECK_RC(validate(p));
@@ -2789,9 +2671,10 @@ static int pcg_matvec(dab_handle* h, YBufs yb, const double* vec, bool exact = f
   // hands its work-group partials to the CG update (never left over from an earlier problem)
   h->cg_wpart = nullptr;
   if (h->mf) {
-    // one rank with cross blocks (the rig): the product's partials are summed inside the CG
-    // update (no all-reduce in between), one launch fewer per iteration
-    const bool fuse = h->world == 1 && h->nxlist > 0 && h->knobs.cg_onewg == 0;
+    // one rank without a communicator, with cross blocks (the rig): the product's partials
+    // are summed inside the CG update (no all-reduce in between), one launch fewer per
+    // iteration; a communicator (a one-rank RCCL handle included) all-reduces them
+    const bool fuse = !h->coll() && h->nxlist > 0 && h->knobs.cg_onewg == 0;
     h->cg_wpart = fuse ? h->d_mf_partial : nullptr;
     double* w = fuse ? nullptr : h->d_pcg_w;
     if (h->mf32 && !exact)
@@ -3120,11 +3003,7 @@ static double elapsed_collective(dab_handle* h, double local) {
 static int solve_impl(dab_handle* h, const dab_options* opt_in, dab_summary* sum);
 extern "C" int dab_solve(dab_handle* h, const dab_options* opt_in, dab_summary* sum) {
   const int rc = solve_impl(h, opt_in, sum);
-  if (Dev::guard_on() && h) {
-    (void)hipDeviceSynchronize();
-    if (h->dev.guard_check("solve") + h->setup_tmp.guard_check("solve, set-up scratch") > 0)
-      std::fprintf(stderr, "dab guard: overrun detected after dab_solve\n");
-  }
+  CHECK_RC(guard_fail(h, "dab_solve"));
   return rc;
 }
 static int solve_impl(dab_handle* h, const dab_options* opt_in, dab_summary* sum) {
@@ -3503,7 +3382,7 @@ extern "C" int dab_filter(dab_handle* h, double error_boundary, const double cen
   if (!center) return set_error(DAB_E_INVALID, "null hemisphere center");
   HIP_OK(hipSetDevice(h->device));
   hipStream_t s = h->stream;
-  Dev tmp;
+  Dev tmp{"entry-point temporaries"};
   unsigned char *d_slot = nullptr, *d_pt = nullptr;
   CHECK_RC(tmp.alloc(&d_slot, (size_t)std::max(1, h->NS)));
   CHECK_RC(tmp.alloc(&d_pt, (size_t)std::max(1, h->NP)));
@@ -3513,6 +3392,7 @@ extern "C" int dab_filter(dab_handle* h, double error_boundary, const double cen
   if (h->NS > 0) HIP_OK(hipMemcpyAsync(slot.data(), d_slot, slot.size(), hipMemcpyDeviceToHost, s));
   if (h->NP > 0) HIP_OK(hipMemcpyAsync(pt.data(), d_pt, pt.size(), hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
+  CHECK_RC(guard_fail(h, "dab_filter", &tmp));
   int32_t no = 0, np = 0;
   if (obs_keep) std::memset(obs_keep, 0, (size_t)h->N);
   for (int s2 = 0; s2 < h->NS; ++s2) {
@@ -3541,7 +3421,7 @@ extern "C" int dab_dense_spd_solve(dab_handle* h, int n, const double* A, const 
   hipStream_t s = h->stream;
   int lds = ((n + 1 + 7) / 8) * 8;
   if (lds % 512 == 0) lds += 8;
-  Dev tmp;
+  Dev tmp{"entry-point temporaries"};
   double *dA = nullptr, *dy = nullptr;
   int* dflag = nullptr;
   CHECK_RC(tmp.alloc(&dA, (size_t)(n + 1) * lds));
@@ -3560,6 +3440,7 @@ extern "C" int dab_dense_spd_solve(dab_handle* h, int n, const double* A, const 
   HIP_OK(hipMemcpyAsync(x, dy, n * sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_OK(hipMemcpyAsync(&flag, dflag, sizeof(int), hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
+  CHECK_RC(guard_fail(h, "dab_dense_spd_solve", &tmp));
   float ms = 0.f;
   HIP_OK(hipEventElapsedTime(&ms, h->ev0, h->ev1));
   if (factor_ms) *factor_ms = ms;

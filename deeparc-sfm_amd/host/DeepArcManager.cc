@@ -13,6 +13,7 @@
 #include <thread>
 #include <type_traits>
 #include <fstream>
+#include <iterator>
 #include <iostream>
 #include <unordered_map>
 
@@ -294,12 +295,17 @@ bool DeepArcManager::read(std::string filename) {
   }
   std::string text;
   in.seekg(0, std::ios::end);
-  const std::streamoff size = in.tellg();
+  const std::streamoff size = in.fail() ? -1 : (std::streamoff)in.tellg();
   if (size > 0) {
     text.resize((size_t)size);
     in.seekg(0, std::ios::beg);
     in.read(&text[0], size);
     if (!in) throw "Cannot read input file";
+  } else if (size < 0) {
+    // not seekable (a pipe, /dev/stdin, a FIFO): read through to EOF
+    in.clear();
+    text.assign(std::istreambuf_iterator<char>(in), std::istreambuf_iterator<char>());
+    if (in.bad()) throw "Cannot read input file";
   }
   Tokens f(std::move(text));
   phase("file");
@@ -575,5 +581,7 @@ void DeepArcManager::filterPoint3d(double error_boundary, double* hemisphere_cen
     // the session's arrays follow the same compaction (the next set-up needs no marshal)
     if (session_) session_->filtered(*this, structure_version_ - 1, keep_obs.data(), keep_pt.data());
   }
-  dabSession().t.filter_host += dab_now_seconds() - th;
+  // only a session that exists takes the timer: filtering a manager without observations
+  // must not create one (that would initialise the GPU on a host-only path)
+  if (session_) session_->t.filter_host += dab_now_seconds() - th;
 }

@@ -192,9 +192,11 @@ int dab_create(int device, dab_handle** out);
 /* Multi-GPU (one process per GPU, RCCL over xGMI). `unique_id` is the 128-byte
  * ncclUniqueId produced on rank 0 by dab_comm_unique_id and broadcast by the caller.
  * world_size 1 with a non-null unique_id builds a one-rank RCCL communicator and runs
- * every collective of the multi-rank path through it (the split evaluation schedule with
- * its camera all-reduce on the communication stream included): the same results as
- * dab_create, with the multi-GPU transport executed on one GPU. */
+ * the solve's collectives through it — the evaluation pass's (the split schedule with its
+ * camera all-reduce on the communication stream included), the LM step's and every PCG
+ * iteration's: the same results as dab_create, with the multi-GPU transport executed on one
+ * GPU. The set-up's free-camera and pair-set unions and the LINEAR_SOLVER_AUTO choice follow
+ * world_size (a single rank needs no union), so they take the one-rank paths. */
 int dab_comm_unique_id(uint8_t out_id[128]);
 int dab_create_dist(int device, int rank, int world_size, const uint8_t unique_id[128],
                     dab_handle** out);
@@ -208,8 +210,12 @@ int dab_create_dist_host(int device, int rank, int world_size, dab_host_allreduc
                          dab_handle** out);
 /* Frees the handle's device buffers. Its streams and small pinned host blocks go to a
  * process-wide cache that the next dab_create on the same device takes from (creating and
- * destroying a stream cost ~2 ms each); they are released only when the process exits. */
+ * destroying a stream cost ~2 ms each); a cached stream that reports an error is destroyed
+ * instead of reused. */
 int dab_destroy(dab_handle* h);
+/* Destroys the cached streams and frees the cached pinned blocks (an embedding process that
+ * resets the device, or wants the memory back). Call with no handle alive. */
+int dab_release_caches(void);
 
 /* ---- problem upload / solve ------------------------------------------------------------
  * dab_set_problem copies the problem to the device and builds the point-major and
