@@ -2,7 +2,7 @@
 // SPD 64x64 block (L_kk against a CPU Cholesky) and on a 6000-row panel, with the phase
 // profile of one launch (wall clock, 100 MHz).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/potrf_micro.hip -o scripts/potrf_micro
-// (-DDAB_F16_LDS=0: the round-3 factor16, all multipliers by DPP broadcasts)
+// (factor16 as shipped: every multiplier by DPP broadcasts)
 #define DAB_CHOL_PROFILE
 #include "../deeparc-sfm_amd/csrc/dab_chol.hip"
 

@@ -12,24 +12,6 @@ def test_dense_spd_solve_matches_numpy(pkg, gpu, n):
     check_solve(pkg, n)
 
 
-@pytest.mark.parametrize("n", [2048, 2050, 3001])
-def test_dense_flow_factorisation(pkg, gpu, n, monkeypatch):
-    """The persistent dataflow factorisation (k_chol_flow) at its default minimum size and
-    above: the rhs row in a block of its own (2048) or under a short last block."""
-    monkeypatch.setenv("DAB_CHOL_FLOW", "1")
-    check_solve(pkg, n)
-
-
-@pytest.mark.parametrize("n", [6, 64, 65, 128, 130, 193, 257, 449, 1000])
-def test_dense_flow_factorisation_small_sizes(pkg, gpu, n, monkeypatch):
-    """The persistent dataflow factorisation forced on small systems (DAB_CHOL_FLOW_MIN=1):
-    one block, a short last block holding the rhs row, the rhs row in a block of its own,
-    groups that end at the last panel."""
-    monkeypatch.setenv("DAB_CHOL_FLOW", "1")
-    monkeypatch.setenv("DAB_CHOL_FLOW_MIN", "1")
-    check_solve(pkg, n)
-
-
 def check_solve(pkg, n):
     rng = np.random.default_rng(n)
     M = rng.standard_normal((n, n))
