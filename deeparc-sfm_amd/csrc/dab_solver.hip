@@ -2671,10 +2671,12 @@ static int pcg_matvec(dab_handle* h, YBufs yb, const double* vec, bool exact = f
   // hands its work-group partials to the CG update (never left over from an earlier problem)
   h->cg_wpart = nullptr;
   if (h->mf) {
-    // one rank without a communicator, with cross blocks (the rig): the product's partials
-    // are summed inside the CG update (no all-reduce in between), one launch fewer per
-    // iteration; a communicator (a one-rank RCCL handle included) all-reduces them
-    const bool fuse = !h->coll() && h->nxlist > 0 && h->knobs.cg_onewg == 0;
+    // one rank with cross blocks (the rig): the product's partials are summed inside the CG
+    // update (no all-reduce in between), one launch fewer per iteration. A one-rank RCCL
+    // handle takes this path too (its all-reduce of a single rank is the identity, and the
+    // separate partial-sum launch would regroup the sums: the trajectory would leave
+    // dab_create's in the last bits)
+    const bool fuse = h->world == 1 && h->nxlist > 0 && h->knobs.cg_onewg == 0;
     h->cg_wpart = fuse ? h->d_mf_partial : nullptr;
     double* w = fuse ? nullptr : h->d_pcg_w;
     if (h->mf32 && !exact)

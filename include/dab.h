@@ -195,8 +195,9 @@ int dab_create(int device, dab_handle** out);
  * the solve's collectives through it — the evaluation pass's (the split schedule with its
  * camera all-reduce on the communication stream included), the LM step's and every PCG
  * iteration's: the same results as dab_create, with the multi-GPU transport executed on one
- * GPU. The set-up's free-camera and pair-set unions and the LINEAR_SOLVER_AUTO choice follow
- * world_size (a single rank needs no union), so they take the one-rank paths. */
+ * GPU. The set-up's free-camera and pair-set unions, the LINEAR_SOLVER_AUTO choice and the
+ * rig's matrix-free PCG product (whose work-group partials a single rank sums inside the CG
+ * update, no all-reduce) follow world_size, so they take the one-rank paths. */
 int dab_comm_unique_id(uint8_t out_id[128]);
 int dab_create_dist(int device, int rank, int world_size, const uint8_t unique_id[128],
                     dab_handle** out);
