@@ -1506,6 +1506,16 @@ struct UniFrame {
       for (int q = 0; q < 9; ++q) jl[q] = J[q];
     }
   }
+  // the same from a frame shared in LDS (k_eval_bal: R t K J_l small, kBalFrame doubles),
+  // every lane reading the same address (broadcast), then held in SGPRs
+  struct FromShared {};
+  __device__ __forceinline__ UniFrame(FromShared, const double* fr) {
+#pragma unroll
+    for (int q = 0; q < 12; ++q) T[q] = UniTabs::uniform(fr[q]);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) K[q] = UniTabs::uniform(fr[12 + q]);
+    small = UniTabs::uniform(fr[27]) != 0.0;
+  }
   // the same from the precomputed table camtab[e] (k_cam_tables: R t Rd Jd), scalar loads
   struct FromTable {};
   __device__ __forceinline__ UniFrame(FromTable, const double* __restrict__ camtab,
@@ -1738,6 +1748,45 @@ __device__ __forceinline__ void eval_cams_gather(const int* __restrict__ cm_pt, 
       } else if (i0 + 64 * st < e) {
         frame_rows_acc(xy[u], X[u], f, acc);
       }
+    }
+  }
+}
+
+// eval_cams_gather with the camera's frame from the caller (get_frame(), called once the
+// first indices and gathers are in flight: k_eval_bal's frames shared in LDS)
+template <class GetFrame>
+__device__ __forceinline__ void eval_cams_gather_f(const int* __restrict__ cm_pt, const double2* __restrict__ cmxy,
+                                                   const double* __restrict__ points, int i0, int e,
+                                                   double (&acc)[27], GetFrame get_frame) {
+  constexpr int DG = 2, DI = 4, R = 3;
+  const int lo = i0 - (int)(threadIdx.x & 63);
+  const int n = (e - lo + 63) >> 6;  // steps of 64 entries
+  int pid[R];
+  double2 xy[R];
+  double X[R][3];
+  auto load_idx = [&](int slot, int step) { pid[slot] = cm_pt[min(i0 + 64 * step, e - 1)]; };
+  auto gather = [&](int islot, int slot, int step) {
+    const int p = pid[islot];
+    xy[slot] = cmxy[min(i0 + 64 * step, e - 1)];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) X[slot][q] = points[3 * (size_t)p + q];
+  };
+  if (n > 0) {
+#pragma unroll
+    for (int st = 0; st < DG; ++st) load_idx(st % R, st);
+#pragma unroll
+    for (int st = 0; st < DG; ++st) gather(st % R, st % R, st);
+#pragma unroll
+    for (int st = DG; st < DI; ++st) load_idx(st % R, st);
+  }
+  const UniFrame f = get_frame();
+  for (int st0 = 0; st0 < n; st0 += R) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int st = st0 + u;
+      gather((st + DG) % R, (st + DG) % R, st + DG);
+      load_idx((st + DI) % R, st + DI);
+      if (i0 + 64 * st < e) frame_rows_acc(xy[u], X[u], f, acc);
     }
   }
 }
@@ -2425,6 +2474,383 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
 #endif
     k_eval_fused<2><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
 #undef DAB_FUSED_ARGS
+}
+
+// ------------------------------------------------------------------------------------
+// k_eval_bal: the fused evaluation pass with the camera tables built ONCE per XCD
+// ------------------------------------------------------------------------------------
+// k_eval_fused's two redundant trigonometry phases were a third of its VALU stream (PMC,
+// profiles/r05_eval_fused_mix.txt: 6.61 M VALU per C3 launch, of which ~0.95 M the point
+// waves' R,t of all 1000 extrinsics in each of the 256 work-groups and ~1 M the camera waves'
+// own frames, one per wave), and the point waves could not start their rows before 5.5-7 us.
+// Here:
+//  * R,t of every extrinsic is built once per XCD inside the launch: a work-group's first
+//    point wave claims 64-extrinsic chunks from its XCD's counter (HW_REG_XCC_ID), builds
+//    them (one lane each) into that XCD's copy of the table with plain stores (the lines stay
+//    in the XCD's L2), drains them (vmcnt(0)) and counts the chunk done; a work-group's point
+//    waves wait until all chunks of their XCD are done, then load the copy with sc1 loads
+//    (L2-served, past the CU's L1) into LDS. Producer and consumer share the XCD's L2, the
+//    single point of coherence of its CUs; a record carries the launch's stamp, checked on
+//    every load (a mismatch raises the error word: the pass fails closed). Every claim is
+//    made by a resident work-group, which finishes its chunk without waiting on anything,
+//    so no placement or residency is assumed.
+//  * the camera frames of a work-group's cameras (R, t, K, J_l) are built once, one lane per
+//    camera, by its first camera wave and shared through LDS; every camera wave issues its
+//    first index loads and gathers before it waits for them.
+// Everything else — the SELL point rows, the camera waves' gathered three-slot pipeline, the
+// fixed-order reductions, the fixed-point cost — is k_eval_fused's streamed form (ST, CG).
+constexpr int kXcd = 8;
+constexpr int kXtabRec = 16;    // doubles per extrinsic record: R(9) t(3) stamp(1) pad(3) = 128 B
+constexpr int kXtabChunk = 64;  // extrinsics per claimed chunk (one wave, one lane each)
+constexpr int kXsyncWords = 32; // words per (parity, XCD) counter pair: claim, done (own 128-B line)
+__device__ __forceinline__ int xcc_id() {
+  return __builtin_amdgcn_s_getreg(20 | (3 << 11)) & (kXcd - 1);  // HW_REG_XCC_ID, bits [3:0]
+}
+struct XtabArgs {
+  const double* camtab;  // non-null: the tables of the current x exist (k_cam_tables / the LM
+                         // loop's candidate, [E][kCamTab]): read them, build nothing
+  double* tab;         // [kXcd][E][kXtabRec]
+  unsigned* sync;      // [2][kXcd][kXsyncWords]
+  unsigned* err;       // error word (0 = ok)
+  unsigned stamp;      // this launch's stamp (nonzero)
+  int par;             // counter set of this launch (the other set is zeroed for the next)
+};
+// claim chunks of this XCD's table until none is left; each claimed chunk is built and
+// counted done
+__device__ __forceinline__ void xtab_produce(const XtabArgs& xa, int x, const double* __restrict__ ext, int E) {
+  const int lane = threadIdx.x & 63;
+  unsigned* ctr = xa.sync + (size_t)(xa.par * kXcd + x) * kXsyncWords;
+  const unsigned nch = (unsigned)((E + kXtabChunk - 1) / kXtabChunk);
+  for (;;) {
+    unsigned o = 0;
+    if (lane == 0) o = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    o = __builtin_amdgcn_readfirstlane(o);
+    if (o >= nch) return;
+    const int e = (int)o * kXtabChunk + lane;
+    if (e < E) {
+      double x6[6];
+#pragma unroll
+      for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)e + q];
+      double T[30];
+      cam_table(x6, T);
+      double2* rec = reinterpret_cast<double2*>(xa.tab + ((size_t)x * E + e) * kXtabRec);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) rec[q] = make_double2(T[2 * q], T[2 * q + 1]);
+      rec[6] = make_double2(__longlong_as_double((long long)(((unsigned long long)xa.stamp << 32) | (unsigned)e)), 0.0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of the chunk acknowledged by the L2
+    if (lane == 0) __hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// one lane: until this XCD's table is complete (bounded; a timeout raises the error word)
+__device__ __forceinline__ void xtab_wait(const XtabArgs& xa, int x, int E) {
+  const unsigned* ctr = xa.sync + (size_t)(xa.par * kXcd + x) * kXsyncWords;
+  const unsigned nch = (unsigned)((E + kXtabChunk - 1) / kXtabChunk);
+  unsigned spins = 0;
+  while (__hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nch) {
+    __builtin_amdgcn_s_sleep(2);
+    if (++spins > (1u << 22)) {
+      __hip_atomic_fetch_or(xa.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  }
+}
+
+constexpr int kBalPW = 8;              // point waves per work-group
+constexpr int kBalCW = 16 - kBalPW;    // camera waves
+constexpr int kBalFrame = 28;          // doubles per shared camera frame: R t K J_l small
+__global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restrict__ chunk_beg,
+                                                   const double* __restrict__ points, const double* __restrict__ ext,
+                                                   double* __restrict__ V, double* __restrict__ g,
+                                                   double* __restrict__ ug, unsigned long long* __restrict__ costfx,
+                                                   unsigned long long* __restrict__ fx_next, XtabArgs xa, int wpc,
+                                                   int wps, int side) {
+  __shared__ double rt_s[kLdsCams * 12];
+  __shared__ double k_s[kLdsCams * 6];
+  __shared__ double csum[kBalCW][27];            // camera waves' sums: [slot * wpc + part]
+  __shared__ double cfr[kBalCW / 2][kBalFrame];  // the work-group's camera frames, by slot
+  __shared__ double shp[kBalPW][2];
+  __shared__ unsigned ccount[kBalCW + kBalPW], pbar, pdone, cfr_ready, tab_ready;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (threadIdx.x < kBalCW + kBalPW) ccount[threadIdx.x] = 0u;
+  if (threadIdx.x == 0) pbar = pdone = cfr_ready = tab_ready = 0u;
+  if (blockIdx.x == 0) {
+    if (fx_next)
+      for (int i = threadIdx.x; i < kFxWords; i += blockDim.x) fx_next[i] = 0ull;
+    // the other counter set, for the next launch (nothing of this launch touches it)
+    for (int i = threadIdx.x; i < kXcd * kXsyncWords; i += blockDim.x)
+      xa.sync[(size_t)(xa.par ^ 1) * kXcd * kXsyncWords + i] = 0u;
+  }
+  __syncthreads();
+
+  if (wave >= kBalPW) {
+    // ---------------- camera side ----------------
+    const int nsl = kBalCW / wpc, cw = wave - kBalPW, part = cw / nsl, slot = cw - part * nsl;
+    if (side == 1) return;
+    if (cw == 0) {
+      // the frames of the work-group's cameras, one lane per camera slot
+      const int c = lane * gridDim.x + blockIdx.x;
+      if (lane < nsl && c < v.NC) {
+        const int2 u = v.chunk_uni[c];
+        double F[30];
+        if (xa.camtab) {
+#pragma unroll
+          for (int q = 0; q < 30; ++q) F[q] = xa.camtab[(size_t)kCamTab * u.x + q];
+        } else {
+          double x6[6];
+#pragma unroll
+          for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)u.x + q];
+          cam_table(x6, F);
+        }
+        double* o = cfr[lane];
+#pragma unroll
+        for (int q = 0; q < 12; ++q) o[q] = F[q];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) o[12 + q] = v.intr[(size_t)kIntr * u.y + q];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int cc = 0; cc < 3; ++cc)
+            o[18 + 3 * r + cc] = F[12 + 3 * r] * F[21 + cc] + F[12 + 3 * r + 1] * F[24 + cc] + F[12 + 3 * r + 2] * F[27 + cc];
+        // cam_table's branch (its small-angle Rd is exactly I, R never is otherwise)
+        o[27] = (F[12] == 1.0 && F[13] == 0.0 && F[14] == 0.0 && F[15] == 0.0 && F[16] == 1.0 && F[17] == 0.0 &&
+                 F[18] == 0.0 && F[19] == 0.0 && F[20] == 1.0 && F[21] == 1.0 && F[25] == 1.0 && F[29] == 1.0)
+                    ? 1.0
+                    : 0.0;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(&cfr_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    const int c = slot * gridDim.x + blockIdx.x;  // one round (fused_eval_fits / fused_wpc)
+    if (c >= v.NC) return;
+    const int b = chunk_beg[c], e = chunk_beg[c + 1];
+    auto cut = [&](int q) -> int {
+      if (wpc == 2 && q == 1) return b + (int)(((long long)(e - b) * kCamSplit) >> 10);
+      return b + (int)(((long long)(e - b) * q) / wpc);
+    };
+    const int lo = cut(part), hi = cut(part + 1);
+    double acc[27];
+#pragma unroll
+    for (int i = 0; i < 27; ++i) acc[i] = 0.0;
+    const double* fr = cfr[slot];
+    eval_cams_gather_f(v.cm_pt, v.cm_xy, points, lo + lane, hi, acc, [&]() {
+      while (__hip_atomic_load(&cfr_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+        __builtin_amdgcn_s_sleep(1);
+      return UniFrame(UniFrame::FromShared{}, fr);
+    });
+    wave_sums_transposed<27>(acc, csum[slot * wpc + part]);
+    unsigned old = 0;
+    if (lane == 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      old = __hip_atomic_fetch_add(&ccount[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != (unsigned)wpc - 1) return;  // another part is still running: the last one writes the row
+    double* cs = csum[slot * wpc];
+    if (lane < 27) {
+      double t = cs[lane];
+      for (int q = 1; q < wpc; ++q) t += csum[slot * wpc + q][lane];
+      cs[lane] = t;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane < 27) ug[27 * (size_t)c + lane] = cam_frame_entry(cs, fr + 18, lane);
+    return;
+  }
+
+  // ---------------- point side ----------------
+  if (side == 2) return;
+  const size_t NPs = (size_t)v.NP;
+  const int pw = wave, pslots = kBalPW / wps, slot = pw / wps, part = pw - slot * wps;
+  const int rounds = (v.nslice + pslots * gridDim.x - 1) / (pslots * gridDim.x);
+  constexpr int D = 3;
+  int qe[D];      // packed records (ext | intr << 16, -1 = padding)
+  double2 qxy[D];
+  double X[3] = {0.0, 0.0, 0.0};
+  int sl = slot * gridDim.x + blockIdx.x, off = 0, len = 0;
+  // every load of a round's set-up is unconditional (clamped to valid addresses; a lane
+  // past the points or a wave past the slices computes nothing from what it read), so the
+  // row queue's waits count exactly
+  auto setup_round = [&]() {
+    const bool has = sl < v.nslice;
+    const int slc = min(sl, v.nslice - 1);
+    const int o0 = v.slice_off[slc], o1 = v.slice_off[slc + 1];
+    off = has ? o0 : 0;
+    len = has ? (o1 - o0) >> 6 : 0;
+    const int p = min(64 * slc + lane, v.NP - 1);
+    X[0] = points[3 * (size_t)p];
+    X[1] = points[3 * (size_t)p + 1];
+    X[2] = points[3 * (size_t)p + 2];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int kk = max(0, min(part + d * wps, len - 1));
+      qe[d] = v.obs_e[off + 64 * kk + lane];
+      qxy[d] = v.obs_xy[off + 64 * kk + lane];
+    }
+  };
+  setup_round();
+  // K of every intrinsic by LDS-DMA (static: no other work-group writes it); 16-B pieces,
+  // each CU of an XCD starting at its own 1/32 of the array
+  const unsigned xrot = blockIdx.x >> 3;
+  {
+    const int npiece = 3 * v.NI, nch = (npiece + 63) >> 6;
+    const int rot = (int)((xrot * (unsigned)nch) >> 5);
+    for (int j = pw; j < nch; j += kBalPW) {
+      int jr = j + rot;
+      if (jr >= nch) jr -= nch;
+      const int i = min(jr * 64 + lane, npiece - 1);
+      __builtin_amdgcn_global_load_lds(v.intr + (size_t)kIntr * (i / 3) + 2 * (i % 3), k_s + 2 * (size_t)(jr * 64), 16,
+                                       0, 0);
+    }
+  }
+  if (xa.camtab) {
+    // R, t from the tables of the current x by LDS-DMA: pieces 0-5 of each record
+    const int npiece = 6 * v.E, nch = (npiece + 63) >> 6;
+    const int rot = (int)((xrot * (unsigned)nch) >> 5);
+    for (int j = pw; j < nch; j += kBalPW) {
+      int jr = j + rot;
+      if (jr >= nch) jr -= nch;
+      const int i = min(jr * 64 + lane, npiece - 1);
+      __builtin_amdgcn_global_load_lds(xa.camtab + (size_t)kCamTab * (i / 6) + 2 * (i % 6), rt_s + 2 * (size_t)(jr * 64),
+                                       16, 0, 0);
+    }
+  }
+  // R, t: this XCD's copy of the table, built inside the launch (xtab_produce)
+  const int x = xcc_id();
+  if (xa.camtab) {
+  } else if (pw == 0) {
+    xtab_produce(xa, x, ext, v.E);
+    if (lane == 0) {
+      xtab_wait(xa, x, v.E);
+      __hip_atomic_store(&tab_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  if (!xa.camtab) {
+    while (__hip_atomic_load(&tab_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+      __builtin_amdgcn_s_sleep(1);
+    // one record per lane: 7 sc1 loads of 16 B (R t, then the stamp), L2-served
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(xa.tab + (size_t)x * v.E * kXtabRec, (short)0, v.E * kXtabRec * 8, 0x00020000);
+    bool bad = false;
+#pragma unroll 2
+    for (int e = pw * 64 + lane; e < v.E; e += kBalPW * 64) {
+      double2 val[7];
+#pragma unroll
+      for (int q = 0; q < 7; ++q)
+        val[q] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, (e * kXtabRec + 2 * q) * 8, 0, 16));
+#pragma unroll
+      for (int q = 0; q < 6; ++q) reinterpret_cast<double2*>(rt_s + 12 * e)[q] = val[q];
+      bad |= (unsigned long long)__double_as_longlong(val[6].x) != (((unsigned long long)xa.stamp << 32) | (unsigned)e);
+    }
+    if (bad) __hip_atomic_fetch_or(xa.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // barrier of the point waves only (LDS counter): own LDS writes and LDS-DMAs retired
+  // before the arrival, acquire before the first table read
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_add(&pbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (__hip_atomic_load(&pbar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)kBalPW)
+    __builtin_amdgcn_s_sleep(1);
+  const LdsTabs<true, false, false> tabs{rt_s, k_s, nullptr, v.intr};
+  double acc[2] = {0.0, 0.0};
+  for (int r = 0; r < rounds; ++r) {
+    if (r > 0) {
+      sl = (r * pslots + slot) * gridDim.x + blockIdx.x;
+      setup_round();
+    }
+    double c[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) c[k] = 0.0;
+#pragma unroll 1
+    for (int k0 = part; k0 < len; k0 += D * wps) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int k = k0 + d * wps;
+        const int pk = qe[d], pe = pk >= 0 ? pk : 0;
+        const int4 id = make_int4(pk >= 0 ? 0 : -1, pe & 0xffff, -1, pe >> 16);
+        const double2 xy = qxy[d];
+        const int kn = min(k + D * wps, len - 1);
+        qe[d] = v.obs_e[off + 64 * kn + lane];
+        qxy[d] = v.obs_xy[off + 64 * kn + lane];
+        if (k >= len) continue;  // wave-uniform; no load below
+        const bool live = id.x >= 0;
+        double ru, rv, jx0[3], jx1[3];
+        obs_rows<true, -1, LdsTabs<true, false, false>, false>(id, xy, X, tabs, ru, rv, jx0, jx1, nullptr, nullptr);
+        if (!live) ru = rv = jx0[0] = jx0[1] = jx0[2] = jx1[0] = jx1[1] = jx1[2] = 0.0;
+        c[0] = fma(jx1[0], jx1[0], fma(jx0[0], jx0[0], c[0]));
+        c[1] = fma(jx1[0], jx1[1], fma(jx0[0], jx0[1], c[1]));
+        c[2] = fma(jx1[0], jx1[2], fma(jx0[0], jx0[2], c[2]));
+        c[3] = fma(jx1[1], jx1[1], fma(jx0[1], jx0[1], c[3]));
+        c[4] = fma(jx1[1], jx1[2], fma(jx0[1], jx0[2], c[4]));
+        c[5] = fma(jx1[2], jx1[2], fma(jx0[2], jx0[2], c[5]));
+        c[6] = fma(jx1[0], rv, fma(jx0[0], ru, c[6]));
+        c[7] = fma(jx1[1], rv, fma(jx0[1], ru, c[7]));
+        c[8] = fma(jx1[2], rv, fma(jx0[2], ru, c[8]));
+        // a non-finite residual makes the lane's r^2 sum non-finite, which the
+        // fixed-point add below flags: no per-row finiteness test
+        acc[0] = fma(rv, rv, fma(ru, ru, acc[0]));
+      }
+    }
+    const int p = 64 * sl + lane;
+    if (wps > 1) {
+      // (one round by construction) parts -> LDS after the tables (fused_wps keeps
+      // 12 E + kBalPW * 9 * 64 doubles inside rt_s); the last part sums them in order
+      double* cbuf = rt_s + ((12 * v.E + 1) & ~1);
+      // every part's table reads are done before any part overwrites the space after E
+#pragma unroll
+      for (int k = 0; k < 9; ++k) cbuf[(pw * 9 + k) * 64 + lane] = c[k];
+      unsigned old = 0;
+      if (lane == 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        old = __hip_atomic_fetch_add(&ccount[kBalCW + slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      old = __builtin_amdgcn_readfirstlane(old);
+      if (old != (unsigned)wps - 1) continue;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        double t = cbuf[((slot * wps) * 9 + k) * 64 + lane];
+        for (int q2 = 1; q2 < wps; ++q2) t += cbuf[((slot * wps + q2) * 9 + k) * 64 + lane];
+        c[k] = t;
+      }
+    }
+    if (sl < v.nslice && p < v.NP) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) V[k * NPs + p] = c[k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) g[k * NPs + p] = c[6 + k];
+    }
+  }
+  // cost: wave sums, summed in wave order by the last point wave, added in fixed point
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double t = wave_sum_lane63(acc[i]);
+    if (lane == 63) shp[pw][i] = t;
+  }
+  unsigned old = 0;
+  if (lane == 63) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    old = __hip_atomic_fetch_add(&pdone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  old = __builtin_amdgcn_readlane(old, 63);
+  if (old != (unsigned)kBalPW - 1 || lane != 0) return;
+  double pc = shp[0][0], bc = shp[0][1];
+#pragma unroll
+  for (int w = 1; w < kBalPW; ++w) {
+    pc += shp[w][0];
+    bc += shp[w][1];
+  }
+  cost_fx_commit(pc, bc, costfx + kFxStride * (blockIdx.x % kFxCopies));
+}
+
+size_t xtab_doubles(int E) { return (size_t)kXcd * (size_t)std::max(E, 1) * kXtabRec; }
+size_t xtab_sync_words() { return 2 * (size_t)kXcd * kXsyncWords; }
+void launch_eval_bal(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
+                     double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
+                     int grid, int side, double* xtab, unsigned* xsync, unsigned* xerr, unsigned stamp, int par,
+                     const double* camtab) {
+  const int wpc = fused_wpc(v.NC, grid), wps = fused_wps(v.nslice, v.E, grid);
+  const XtabArgs xa{camtab, xtab, xsync, xerr, stamp, par};
+  k_eval_bal<<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, xa, wpc, wps, side);
 }
 
 // camera-major point copy for the streamed fused pass: cmx[q][i] = points[cm_pt[i]][q].

@@ -261,7 +261,8 @@ enum Slot {
   // fixed-point cost shards of the prefetch point kernel (uint64 bit patterns: sum r^2
   // integer part, fraction * 2^52, non-finite count per shard; cost_fx_add)
   S_CFX = 16,  // two sets of kFxWords, alternating between passes
-  S_NSLOTS = S_CFX + 2 * kFxWords
+  S_XERR = S_CFX + 2 * kFxWords,  // k_eval_bal's error word (uint32 bits; 0 = ok)
+  S_NSLOTS
 };
 
 // Device buffers of one problem come from a Dev (dab_devmem.h): dab_set_problem releases
@@ -304,6 +305,7 @@ struct Knobs {
   int fused_variant = 0;    // DAB_FUSED_V: pipeline depths of the streamed fused pass (DAB_ABLATIONS builds)
   int setup_host = 0;       // DAB_SETUP_HOST=1: dab_set_problem's host passes instead of the device ones
   int fused_gv = 0;         // DAB_FUSED_GV (DAB_ABLATIONS builds): fused-pass camera-side timing ablations
+  int eval_bal = 1;         // DAB_EVAL_BAL=0: k_eval_fused (tables in every work-group) instead of k_eval_bal
   int fused_tab = -1;       // DAB_FUSED_TAB: the fused pass reads the camera tables of the current x
                             // instead of building them in every work-group — -1 (default) when they
                             // exist already (the LM loop: the accepted candidate's tables), 1 always
@@ -331,6 +333,7 @@ struct Knobs {
     get("DAB_FUSED_TAB", fused_tab);
     get("DAB_SETUP_HOST", setup_host);
     get("DAB_FUSED_GV", fused_gv);
+    get("DAB_EVAL_BAL", eval_bal);
   }
 };
 
@@ -530,6 +533,13 @@ struct dab_handle {
     stream_give(device, stream);
   }
 
+  // k_eval_bal: per-XCD camera tables built inside the launch, their counters (two sets,
+  // alternating launches), the launch stamp
+  double* d_xtab = nullptr;
+  unsigned* d_xsync = nullptr;
+  unsigned xstamp = 0;
+  int xpar = 0;
+  unsigned* xerr() { return reinterpret_cast<unsigned*>(d_scal + S_XERR); }
   double* ug() { return d_camred; }  // [NC][27]: U upper-packed (21) | g_c (6)
   double* Ux() { return d_camred + (size_t)27 * NC; }
   size_t camred_count() const { return (size_t)27 * NC + (size_t)36 * ncross; }
@@ -1544,6 +1554,15 @@ static int setup_buffers(dab_handle* h, const std::function<void(const char*)>& 
     CHECK_RC(d.alloc(&h->d_obs_e, (size_t)std::max(1, NS)));
     su_obs_e(s, NS, h->d_obs_idx, h->d_obs_e);
     if (h->knobs.fused_stream == 1) CHECK_RC(d.alloc(&h->d_cmx, (size_t)3 * std::max(1, NE)));
+    if (h->knobs.fused_stream == 2 && h->knobs.eval_bal) {
+      CHECK_RC(d.alloc(&h->d_xtab, xtab_doubles(h->E)));
+      CHECK_RC(d.alloc(&h->d_xsync, xtab_sync_words()));
+      HIP_OK(hipMemsetAsync(h->d_xsync, 0, sizeof(unsigned) * xtab_sync_words(), s));  // the first launch's set
+      h->xpar = 0;
+    } else {
+      h->d_xtab = nullptr;
+      h->d_xsync = nullptr;
+    }
     HIP_OK(hipStreamSynchronize(s));
     v.obs_e = h->d_obs_e;
   }
@@ -2835,10 +2854,24 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
     launch_cmx_gather(s, v, h->d_points, h->d_cmx);
     h->cmx_version = h->pts_version;
   }
-  if (h->fused && !h->fused_split) {  // both halves of the pass in one launch (launch_eval_fused)
-    launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
-                      h->cost_fx(h->fx_last ^ 1), h->ncu, 0, h->d_cmx, h->knobs.fused_variant,
-                      fused_tab ? h->d_camtab : nullptr, h->knobs.fused_gv);
+  // k_eval_bal (the default where it applies): the fused pass with the camera tables built
+  // once per XCD inside the launch; each launch takes the next stamp and counter set
+  const bool bal = h->fused && h->d_xtab;
+  auto eval_fused = [&](int grid, int side) {
+    if (bal) {
+      if (++h->xstamp == 0) h->xstamp = 1;
+      launch_eval_bal(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
+                      h->cost_fx(h->fx_last ^ 1), grid, side, h->d_xtab, h->d_xsync, h->xerr(), h->xstamp, h->xpar,
+                      fused_tab ? h->d_camtab : nullptr);
+      h->xpar ^= 1;
+    } else {
+      launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
+                        h->cost_fx(h->fx_last ^ 1), grid, side, h->d_cmx, side == 0 ? h->knobs.fused_variant : 0,
+                        fused_tab ? h->d_camtab : nullptr, side == 0 ? h->knobs.fused_gv : 0);
+    }
+  };
+  if (h->fused && !h->fused_split) {  // both halves of the pass in one launch
+    eval_fused(h->ncu, 0);
     if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
     if (h->NC > 0) CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
     return 0;
@@ -2848,8 +2881,7 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
     // RCCL all-reduce runs on the communication stream during the point side (which
     // leaves one CU per XCD free for it: eval_grid)
     if (ev_mid) HIP_OK(hipEventRecord(ev_mid, s));
-    launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
-                      h->cost_fx(h->fx_last ^ 1), h->ncu, 2, h->d_cmx, 0, fused_tab ? h->d_camtab : nullptr);
+    eval_fused(h->ncu, 2);
     bool ovl = false;
     if (h->can_overlap()) {
       HIP_OK(hipEventRecord(h->ev_cam, s));
@@ -2860,8 +2892,7 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
     } else {
       CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
     }
-    launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
-                      h->cost_fx(h->fx_last ^ 1), h->eval_grid, 1, h->d_cmx, 0, fused_tab ? h->d_camtab : nullptr);
+    eval_fused(h->eval_grid, 1);
     if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
     if (ovl) HIP_OK(hipStreamWaitEvent(s, h->ev_comm, 0));
     return 0;
@@ -2939,6 +2970,15 @@ static int eval_jacobian_and_blocks(dab_handle* h, bool with_norms, bool tables_
   return 0;
 }
 
+// k_eval_bal's in-launch table hand-off failed (1: a wait timed out, 2: a record's stamp was
+// not this launch's): the pass's results are not to be used
+static int xerr_check(dab_handle* h) {
+  unsigned e = 0;
+  std::memcpy(&e, h->h_scal + S_XERR, sizeof(e));
+  if (e == 0) return 0;
+  return set_error(DAB_E_DEVICE, "evaluation pass: in-launch camera table hand-off failed (code " + std::to_string(e) +
+                                     ")");
+}
 static int read_scalars(dab_handle* h) {
   HIP_OK(hipMemcpyAsync(h->h_scal, h->d_scal, sizeof(double) * S_NSLOTS, hipMemcpyDeviceToHost, h->stream));
   HIP_OK(hipMemcpyAsync(h->h_flags, h->d_flags, sizeof(int) * 4, hipMemcpyDeviceToHost, h->stream));
@@ -2947,6 +2987,7 @@ static int read_scalars(dab_handle* h) {
   // before any decision is taken on it (every rank's next call fails the same way)
   CHECK_RC(p2p_check(h->p2p_main));
   CHECK_RC(p2p_check(h->p2p_comm));
+  CHECK_RC(xerr_check(h));
   if (h->cost_fx_pending) {
     // the last evaluation pass left its cost in fixed point (cost_fx_commit): exact
     // integer limb sums, converted once here
@@ -3538,6 +3579,10 @@ extern "C" int dab_sync(dab_handle* h) {
   if (!h) return set_error(DAB_E_INVALID, "null handle");
   HIP_OK(hipSetDevice(h->device));
   HIP_OK(hipStreamSynchronize(h->stream));
+  if (h->d_scal) {
+    HIP_OK(hipMemcpy(h->h_scal + S_XERR, h->d_scal + S_XERR, sizeof(double), hipMemcpyDeviceToHost));
+    CHECK_RC(xerr_check(h));
+  }
   return 0;
 }
 
