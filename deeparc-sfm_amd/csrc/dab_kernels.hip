@@ -2546,10 +2546,11 @@ __device__ __forceinline__ void xtab_produce(const XtabArgs& xa, int x, const do
 __device__ __forceinline__ void xtab_wait(const XtabArgs& xa, int x, int E) {
   const unsigned* ctr = xa.sync + (size_t)(xa.par * kXcd + x) * kXsyncWords;
   const unsigned nch = (unsigned)((E + kXtabChunk - 1) / kXtabChunk);
-  unsigned spins = 0;
+  // bounded by the clock (s_memrealtime, 100 MHz): 20 ms, ~1000x the table's build time
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (__hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nch) {
     __builtin_amdgcn_s_sleep(2);
-    if (++spins > (1u << 22)) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {
       __hip_atomic_fetch_or(xa.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
@@ -2572,6 +2573,11 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   __shared__ double shp[kBalPW][2];
   __shared__ unsigned ccount[kBalCW + kBalPW], pbar, pdone, cfr_ready, tab_ready;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  DAB_STAMP(0);
+  // camera slot -> camera: slot s of work-group b takes camera s G + (G - 1 - b), so that the
+  // work-groups short of a camera are the ones with an extra point slice (slices are dealt
+  // from work-group 0 up), and a small camera set leaves the point side's work-groups alone
+  auto cam_of = [&](int slot) { return slot * (int)gridDim.x + ((int)gridDim.x - 1 - (int)blockIdx.x); };
   if (threadIdx.x < kBalCW + kBalPW) ccount[threadIdx.x] = 0u;
   if (threadIdx.x == 0) pbar = pdone = cfr_ready = tab_ready = 0u;
   if (blockIdx.x == 0) {
@@ -2589,7 +2595,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     if (side == 1) return;
     if (cw == 0) {
       // the frames of the work-group's cameras, one lane per camera slot
-      const int c = lane * gridDim.x + blockIdx.x;
+      const int c = cam_of(lane);
       if (lane < nsl && c < v.NC) {
         const int2 u = v.chunk_uni[c];
         double F[30];
@@ -2621,8 +2627,11 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(&cfr_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    const int c = slot * gridDim.x + blockIdx.x;  // one round (fused_eval_fits / fused_wpc)
-    if (c >= v.NC) return;
+    const int c = cam_of(slot);  // one round (fused_eval_fits / fused_wpc)
+    if (c >= v.NC) {
+      DAB_STAMP(3);
+      return;
+    }
     const int b = chunk_beg[c], e = chunk_beg[c + 1];
     auto cut = [&](int q) -> int {
       if (wpc == 2 && q == 1) return b + (int)(((long long)(e - b) * kCamSplit) >> 10);
@@ -2636,8 +2645,11 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     eval_cams_gather_f(v.cm_pt, v.cm_xy, points, lo + lane, hi, acc, [&]() {
       while (__hip_atomic_load(&cfr_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
         __builtin_amdgcn_s_sleep(1);
-      return UniFrame(UniFrame::FromShared{}, fr);
+      const UniFrame f(UniFrame::FromShared{}, fr);
+      DAB_STAMP(1);
+      return f;
     });
+    DAB_STAMP(2);
     wave_sums_transposed<27>(acc, csum[slot * wpc + part]);
     unsigned old = 0;
     if (lane == 0) {
@@ -2645,7 +2657,10 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
       old = __hip_atomic_fetch_add(&ccount[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     old = __builtin_amdgcn_readfirstlane(old);
-    if (old != (unsigned)wpc - 1) return;  // another part is still running: the last one writes the row
+    if (old != (unsigned)wpc - 1) {  // another part is still running: the last one writes the row
+      DAB_STAMP(3);
+      return;
+    }
     double* cs = csum[slot * wpc];
     if (lane < 27) {
       double t = cs[lane];
@@ -2656,6 +2671,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (lane < 27) ug[27 * (size_t)c + lane] = cam_frame_entry(cs, fr + 18, lane);
+    DAB_STAMP(3);
     return;
   }
 
@@ -2751,6 +2767,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   if (lane == 0) __hip_atomic_fetch_add(&pbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   while (__hip_atomic_load(&pbar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)kBalPW)
     __builtin_amdgcn_s_sleep(1);
+  DAB_STAMP(1);
   const LdsTabs<true, false, false> tabs{rt_s, k_s, nullptr, v.intr};
   double acc[2] = {0.0, 0.0};
   for (int r = 0; r < rounds; ++r) {
@@ -2820,6 +2837,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
       for (int k = 0; k < 3; ++k) g[k * NPs + p] = c[6 + k];
     }
   }
+  DAB_STAMP(2);
   // cost: wave sums, summed in wave order by the last point wave, added in fixed point
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -2832,6 +2850,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     old = __hip_atomic_fetch_add(&pdone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   old = __builtin_amdgcn_readlane(old, 63);
+  DAB_STAMP(3);
   if (old != (unsigned)kBalPW - 1 || lane != 0) return;
   double pc = shp[0][0], bc = shp[0][1];
 #pragma unroll

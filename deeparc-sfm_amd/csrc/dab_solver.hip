@@ -3581,6 +3581,16 @@ extern "C" int dab_sync(dab_handle* h) {
   HIP_OK(hipStreamSynchronize(h->stream));
   if (h->d_scal) {
     HIP_OK(hipMemcpy(h->h_scal + S_XERR, h->d_scal + S_XERR, sizeof(double), hipMemcpyDeviceToHost));
+    static const bool dbg = getenv("DAB_XTAB_DEBUG") != nullptr;  // k_eval_bal's counters on stderr
+    if (dbg && h->d_xsync) {
+      std::vector<unsigned> w(xtab_sync_words());
+      HIP_OK(hipMemcpy(w.data(), h->d_xsync, sizeof(unsigned) * w.size(), hipMemcpyDeviceToHost));
+      unsigned e = 0;
+      std::memcpy(&e, h->h_scal + S_XERR, sizeof(e));
+      std::fprintf(stderr, "xtab: err %u par %d stamp %u |", e, h->xpar, h->xstamp);
+      for (size_t i = 0; i < w.size(); i += 32) std::fprintf(stderr, " %u/%u", w[i], w[i + 1]);
+      std::fprintf(stderr, "\n");
+    }
     CHECK_RC(xerr_check(h));
   }
   return 0;
