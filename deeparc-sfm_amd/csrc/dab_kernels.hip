@@ -2557,6 +2557,18 @@ __device__ __forceinline__ void xtab_wait(const XtabArgs& xa, int x, int E) {
   }
 }
 
+// spin on a work-group word until it reaches `want` (bounded by the clock: 50 ms, then the
+// error word gets `code` and the wave goes on; its results are then void)
+__device__ __forceinline__ void lds_wait_ge(const unsigned* w, unsigned want, unsigned* err, unsigned code) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
+    __builtin_amdgcn_s_sleep(1);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
+      __hip_atomic_fetch_or(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  }
+}
 constexpr int kBalPW = 8;              // point waves per work-group
 constexpr int kBalCW = 16 - kBalPW;    // camera waves
 constexpr int kBalFrame = 28;          // doubles per shared camera frame: R t K J_l small
@@ -2643,8 +2655,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     for (int i = 0; i < 27; ++i) acc[i] = 0.0;
     const double* fr = cfr[slot];
     eval_cams_gather_f(v.cm_pt, v.cm_xy, points, lo + lane, hi, acc, [&]() {
-      while (__hip_atomic_load(&cfr_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
-        __builtin_amdgcn_s_sleep(1);
+      lds_wait_ge(&cfr_ready, 1u, xa.err, 4u);
       const UniFrame f(UniFrame::FromShared{}, fr);
       DAB_STAMP(1);
       return f;
@@ -2743,8 +2754,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     }
   }
   if (!xa.camtab) {
-    while (__hip_atomic_load(&tab_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
-      __builtin_amdgcn_s_sleep(1);
+    lds_wait_ge(&tab_ready, 1u, xa.err, 8u);
     // one record per lane: 7 sc1 loads of 16 B (R t, then the stamp), L2-served
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(xa.tab + (size_t)x * v.E * kXtabRec, (short)0, v.E * kXtabRec * 8, 0x00020000);
@@ -2765,8 +2775,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   // before the arrival, acquire before the first table read
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_fetch_add(&pbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  while (__hip_atomic_load(&pbar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)kBalPW)
-    __builtin_amdgcn_s_sleep(1);
+  lds_wait_ge(&pbar, (unsigned)kBalPW, xa.err, 16u);
   DAB_STAMP(1);
   const LdsTabs<true, false, false> tabs{rt_s, k_s, nullptr, v.intr};
   double acc[2] = {0.0, 0.0};
