@@ -17,7 +17,7 @@ pkg = _pkgload.load()
 prob = pkg.synth(**pkg.CONFIGS[cfg])
 print("problem", cfg, prob.num_obs, flush=True)
 res = {}
-for bal in ("1", "0"):
+for bal in sys.argv[2].split(",") if len(sys.argv) > 2 else ("1", "0"):
     os.environ["DAB_EVAL_BAL"] = bal
     s = pkg.Solver(0)
     s.set_problem(prob.copy())
@@ -33,4 +33,6 @@ for bal in ("1", "0"):
     res[bal] = [it["cost"] for it in summ["iterations"]]
     print("  costs", res[bal], flush=True)
     s.close()
-print("max rel cost dev", max(abs(a - b) / abs(b) for a, b in zip(res["1"], res["0"])))
+keys = list(res)
+for k in keys[1:]:
+    print("max rel cost dev", keys[0], k, max(abs(a - b) / abs(b) for a, b in zip(res[keys[0]], res[k])))
