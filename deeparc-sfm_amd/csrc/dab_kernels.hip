@@ -2522,31 +2522,36 @@ __device__ __forceinline__ void xtab_produce(const XtabArgs& xa, int x, const do
   const int lane = threadIdx.x & 63;
   unsigned* ctr = xa.sync + (size_t)(xa.par * kXcd + x) * kXsyncWords;
   const unsigned nch = (unsigned)((E + kXtabChunk - 1) / kXtabChunk);
-  for (;;) {
-    unsigned o = 0;
-    if (lane == 0) o = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    o = __builtin_amdgcn_readfirstlane(o);
+  // No divergent control flow in here: all 64 lanes take part in every claim and every
+  // done count with the same value 1 (the compiler makes a full wave's 64 adds one atomic of
+  // 64: the counters run in units of 64, chunk = claim / 64) and every lane builds a table
+  // (lanes past E build the last one; their stores are predicated off). Written with a
+  // lane-0-only claim inside a loop whose body branched, the structurised loop lost lane 0
+  // from exec on gfx950 and never ended (the r05d bisection).
+  for (int it = 0; it < 64; ++it) {
+    unsigned o = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    o = __builtin_amdgcn_readfirstlane(o) >> 6;
     if (o >= nch) return;
-    const int e = (int)o * kXtabChunk + lane;
-    if (e < E) {
-      double x6[6];
+    const int e = (int)o * kXtabChunk + lane, ee = min(e, E - 1);
+    double x6[6];
 #pragma unroll
-      for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)e + q];
-      double T[30];
-      cam_table(x6, T);
+    for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)ee + q];
+    double T[30];
+    cam_table(x6, T);
+    if (e < E) {
       double2* rec = reinterpret_cast<double2*>(xa.tab + ((size_t)x * E + e) * kXtabRec);
 #pragma unroll
       for (int q = 0; q < 6; ++q) rec[q] = make_double2(T[2 * q], T[2 * q + 1]);
       rec[6] = make_double2(__longlong_as_double((long long)(((unsigned long long)xa.stamp << 32) | (unsigned)e)), 0.0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of the chunk acknowledged by the L2
-    if (lane == 0) __hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 // one lane: until this XCD's table is complete (bounded; a timeout raises the error word)
 __device__ __forceinline__ void xtab_wait(const XtabArgs& xa, int x, int E) {
   const unsigned* ctr = xa.sync + (size_t)(xa.par * kXcd + x) * kXsyncWords;
-  const unsigned nch = (unsigned)((E + kXtabChunk - 1) / kXtabChunk);
+  const unsigned nch = 64u * (unsigned)((E + kXtabChunk - 1) / kXtabChunk);  // done counts in units of 64
   // bounded by the clock (s_memrealtime, 100 MHz): 20 ms, ~1000x the table's build time
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (__hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nch) {
