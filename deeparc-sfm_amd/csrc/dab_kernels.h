@@ -141,7 +141,7 @@ size_t xtab_sync_words();
 void launch_eval_bal(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
                      double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
                      int grid, int side, double* xtab, unsigned* xsync, unsigned* xerr, unsigned stamp, int par,
-                     const double* camtab = nullptr, int dbg = 0);
+                     const double* camtab = nullptr);
 //  arc∘ring cross blocks Jc0^T Jc1 over composed observations (pair-major copy) -> partial[chunk][36]
 void launch_eval_cross(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
                        const double2* x_xy, const double* points, const double* camtab, double* partial);

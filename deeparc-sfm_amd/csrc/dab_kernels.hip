@@ -2514,7 +2514,6 @@ struct XtabArgs {
   unsigned* err;       // error word (0 = ok)
   unsigned stamp;      // this launch's stamp (nonzero)
   int par;             // counter set of this launch (the other set is zeroed for the next)
-  int dbg;             // bisection aid: 1 point waves build R,t in the work-group, 2 camera waves their own frames
 };
 // claim chunks of this XCD's table until none is left; each claimed chunk is built and
 // counted done
@@ -2552,24 +2551,24 @@ __device__ __forceinline__ void xtab_produce(const XtabArgs& xa, int x, const do
 __device__ __forceinline__ void xtab_wait(const XtabArgs& xa, int x, int E) {
   const unsigned* ctr = xa.sync + (size_t)(xa.par * kXcd + x) * kXsyncWords;
   const unsigned nch = 64u * (unsigned)((E + kXtabChunk - 1) / kXtabChunk);  // done counts in units of 64
-  // bounded by the clock (s_memrealtime, 100 MHz): 20 ms, ~1000x the table's build time
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while (__hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nch) {
+  // bounded by an iteration count (2^18 polls of ~1 us: a fraction of a second)
+  for (unsigned n = 0; __hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nch; ++n) {
     __builtin_amdgcn_s_sleep(2);
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {
+    if (n > (1u << 18)) {
       __hip_atomic_fetch_or(xa.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
   }
 }
 
-// spin on a work-group word until it reaches `want` (bounded by the clock: 50 ms, then the
-// error word gets `code` and the wave goes on; its results are then void)
+// spin on a work-group word until it reaches `want`, bounded by an iteration count (~2^20
+// sleeps, a fraction of a second; then the error word gets `code` and the wave goes on, its
+// results void). No clock read in the loop: s_memrealtime is a memory-path read, and
+// thousands of spinning waves polling it slowed the whole chip (r05f: C3 31.8 us)
 __device__ __forceinline__ void lds_wait_ge(const unsigned* w, unsigned want, unsigned* err, unsigned code) {
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while (__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
+  for (unsigned n = 0; __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want; ++n) {
     __builtin_amdgcn_s_sleep(1);
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
+    if (n > (1u << 20)) {
       __hip_atomic_fetch_or(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
@@ -2611,7 +2610,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     // ---------------- camera side ----------------
     const int nsl = kBalCW / wpc, cw = wave - kBalPW, part = cw / nsl, slot = cw - part * nsl;
     if (side == 1) return;
-    if (cw == 0 && !(xa.dbg & 2)) {
+    if (cw == 0) {
       // the frames of the work-group's cameras, one lane per camera slot
       const int c = cam_of(lane);
       if (lane < nsl && c < v.NC) {
@@ -2660,24 +2659,12 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
 #pragma unroll
     for (int i = 0; i < 27; ++i) acc[i] = 0.0;
     const double* fr = cfr[slot];
-    if (xa.dbg & 2) {
-      const int2 u = v.chunk_uni[c];
-      if (lane < 9) {
-        double F[30];
-        double x6[6];
-        for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)u.x + q];
-        cam_table(x6, F);
-        if (part == 0) cfr[slot][18 + lane] = F[12 + 3 * (lane / 3)] * F[21 + lane % 3] + F[12 + 3 * (lane / 3) + 1] * F[24 + lane % 3] + F[12 + 3 * (lane / 3) + 2] * F[27 + lane % 3];
-      }
-      eval_cams_gather<0, false>(v.cm_pt, v.cm_xy, points, lo + lane, hi, u.x, u.y, ext, v.intr, acc, csum[kBalCW - 1]);
-    } else {
     eval_cams_gather_f(v.cm_pt, v.cm_xy, points, lo + lane, hi, acc, [&]() {
       lds_wait_ge(&cfr_ready, 1u, xa.err, 4u);
       const UniFrame f(UniFrame::FromShared{}, fr);
       DAB_STAMP(1);
       return f;
     });
-    }
     DAB_STAMP(2);
     wave_sums_transposed<27>(acc, csum[slot * wpc + part]);
     unsigned old = 0;
@@ -2763,22 +2750,14 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   }
   // R, t: this XCD's copy of the table, built inside the launch (xtab_produce)
   const int x = xcc_id();
-  if (xa.dbg & 1) {
-    for (int e1 = pw * 64 + lane; e1 < v.E; e1 += kBalPW * 64) {
-      double x6[6], T[30];
-      for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)e1 + q];
-      cam_table(x6, T);
-      for (int i = 0; i < 6; ++i) reinterpret_cast<double2*>(rt_s + 12 * e1)[i] = make_double2(T[2 * i], T[2 * i + 1]);
-    }
-  } else if (xa.camtab) {
-  } else if (pw == 0) {
+  if (!xa.camtab && pw == 0) {
     xtab_produce(xa, x, ext, v.E);
     if (lane == 0) {
       xtab_wait(xa, x, v.E);
       __hip_atomic_store(&tab_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
-  if (!xa.camtab && !(xa.dbg & 1)) {
+  if (!xa.camtab) {
     lds_wait_ge(&tab_ready, 1u, xa.err, 8u);
     // one record per lane: 7 sc1 loads of 16 B (R t, then the stamp), L2-served
     const __amdgpu_buffer_rsrc_t rs =
@@ -2900,9 +2879,9 @@ size_t xtab_sync_words() { return 2 * (size_t)kXcd * kXsyncWords; }
 void launch_eval_bal(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
                      double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
                      int grid, int side, double* xtab, unsigned* xsync, unsigned* xerr, unsigned stamp, int par,
-                     const double* camtab, int dbg) {
+                     const double* camtab) {
   const int wpc = fused_wpc(v.NC, grid), wps = fused_wps(v.nslice, v.E, grid);
-  const XtabArgs xa{camtab, xtab, xsync, xerr, stamp, par, dbg};
+  const XtabArgs xa{camtab, xtab, xsync, xerr, stamp, par};
   k_eval_bal<<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, xa, wpc, wps, side);
 }
 

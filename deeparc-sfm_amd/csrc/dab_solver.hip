@@ -2862,7 +2862,7 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
       if (++h->xstamp == 0) h->xstamp = 1;
       launch_eval_bal(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
                       h->cost_fx(h->fx_last ^ 1), grid, side, h->d_xtab, h->d_xsync, h->xerr(), h->xstamp, h->xpar,
-                      fused_tab ? h->d_camtab : nullptr, std::max(0, h->knobs.eval_bal - 1));
+                      fused_tab ? h->d_camtab : nullptr);
       h->xpar ^= 1;
     } else {
       launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
