@@ -2750,8 +2750,20 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   }
   // R, t: this XCD's copy of the table, built inside the launch (xtab_produce)
   const int x = xcc_id();
+#ifdef DAB_TRACE_XTAB  // point-wave stamps of the table hand-off instead of the loop phases
+#define DAB_STAMPX(k)                                                                       \
+  do {                                                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                          \
+    if (lane == 0 && blockIdx.x < 256) g_trace[(blockIdx.x * 16 + wave) * 4 + (k)] = t_;     \
+  } while (0)
+#undef DAB_STAMP
+#define DAB_STAMP(k) do {} while (0)
+#else
+#define DAB_STAMPX(k) do {} while (0)
+#endif
   if (!xa.camtab && pw == 0) {
     xtab_produce(xa, x, ext, v.E);
+    DAB_STAMPX(1);
     if (lane == 0) {
       xtab_wait(xa, x, v.E);
       __hip_atomic_store(&tab_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2759,6 +2771,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   }
   if (!xa.camtab) {
     lds_wait_ge(&tab_ready, 1u, xa.err, 8u);
+    if (pw != 0) DAB_STAMPX(1);
     // one record per lane: 7 sc1 loads of 16 B (R t, then the stamp), L2-served
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(xa.tab + (size_t)x * v.E * kXtabRec, (short)0, v.E * kXtabRec * 8, 0x00020000);
@@ -2774,12 +2787,14 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
       bad |= (unsigned long long)__double_as_longlong(val[6].x) != (((unsigned long long)xa.stamp << 32) | (unsigned)e);
     }
     if (bad) __hip_atomic_fetch_or(xa.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    DAB_STAMPX(2);
   }
   // barrier of the point waves only (LDS counter): own LDS writes and LDS-DMAs retired
   // before the arrival, acquire before the first table read
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_fetch_add(&pbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   lds_wait_ge(&pbar, (unsigned)kBalPW, xa.err, 16u);
+  DAB_STAMPX(3);
   DAB_STAMP(1);
   const LdsTabs<true, false, false> tabs{rt_s, k_s, nullptr, v.intr};
   double acc[2] = {0.0, 0.0};
@@ -2873,6 +2888,15 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   }
   cost_fx_commit(pc, bc, costfx + kFxStride * (blockIdx.x % kFxCopies));
 }
+#ifdef DAB_TRACE_XTAB
+#undef DAB_STAMP
+#define DAB_STAMP(k)                                                                        \
+  do {                                                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                          \
+    if (lane == 0 && blockIdx.x < 256) g_trace[(blockIdx.x * 16 + wave) * 4 + (k)] = t_;     \
+  } while (0)
+#endif
+#undef DAB_STAMPX
 
 size_t xtab_doubles(int E) { return (size_t)kXcd * (size_t)std::max(E, 1) * kXtabRec; }
 size_t xtab_sync_words() { return 2 * (size_t)kXcd * kXsyncWords; }
