@@ -131,17 +131,12 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
                        int grid, int side, const double* cmx = nullptr, int variant = 0,
                        const double* camtab = nullptr, int gv = 0);
 void launch_cmx_gather(hipStream_t s, const DevView& v, const double* points, double* cmx);
-// k_eval_bal: the fused pass (needs v.obs_e) with R,t of every extrinsic built once per XCD
-// inside the launch into xtab [xtab_doubles(E)]; xsync [xtab_sync_words()] holds two counter
-// sets (set `par` is used, the other zeroed for the next launch: alternate par, zero both
-// before the first launch); stamp: nonzero, new per launch; xerr: error word (0 = ok);
-// camtab (nullable): the tables of the current x, read instead of building any
-size_t xtab_doubles(int E);
-size_t xtab_sync_words();
+// k_eval_bal: the fused pass (needs v.obs_e; fused_eval_fits) with the tables built by every
+// wave of the work-group (camtab non-null: R,t copied from the tables of the current x); err:
+// error word (a bounded wait timed out; 0 = ok)
 void launch_eval_bal(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
-                     double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
-                     int grid, int side, double* xtab, unsigned* xsync, unsigned* xerr, unsigned stamp, int par,
-                     const double* camtab = nullptr);
+                     const double* camtab, double* V, double* g, double* ug, unsigned long long* costfx,
+                     unsigned long long* fx_next, unsigned* err, int grid, int side);
 //  arc∘ring cross blocks Jc0^T Jc1 over composed observations (pair-major copy) -> partial[chunk][36]
 void launch_eval_cross(hipStream_t s, const DevView& v, int nchunk, const int* chunk_beg, const int4* x_idx,
                        const double2* x_xy, const double* points, const double* camtab, double* partial);

@@ -2477,94 +2477,32 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
 }
 
 // ------------------------------------------------------------------------------------
-// k_eval_bal: the fused evaluation pass with the camera tables built ONCE per XCD
+// k_eval_bal: the fused evaluation pass with every wave of the work-group on the tables
 // ------------------------------------------------------------------------------------
-// k_eval_fused's two redundant trigonometry phases were a third of its VALU stream (PMC,
+// k_eval_fused's two trigonometry phases were a third of its VALU stream (PMC,
 // profiles/r05_eval_fused_mix.txt: 6.61 M VALU per C3 launch, of which ~0.95 M the point
-// waves' R,t of all 1000 extrinsics in each of the 256 work-groups and ~1 M the camera waves'
-// own frames, one per wave), and the point waves could not start their rows before 5.5-7 us.
+// waves' R,t of all 1000 extrinsics, two per point thread, and ~1 M the camera waves' own
+// frames, one per wave, wave-uniform) and the point waves could not start their rows before
+// 5.5-7 us, while the camera waves' younger halves were starved behind their older halves.
 // Here:
-//  * R,t of every extrinsic is built once per XCD inside the launch: a work-group's first
-//    point wave claims 64-extrinsic chunks from its XCD's counter (HW_REG_XCC_ID), builds
-//    them (one lane each) into that XCD's copy of the table with plain stores (the lines stay
-//    in the XCD's L2), drains them (vmcnt(0)) and counts the chunk done; a work-group's point
-//    waves wait until all chunks of their XCD are done, then load the copy with sc1 loads
-//    (L2-served, past the CU's L1) into LDS. Producer and consumer share the XCD's L2, the
-//    single point of coherence of its CUs; a record carries the launch's stamp, checked on
-//    every load (a mismatch raises the error word: the pass fails closed). Every claim is
-//    made by a resident work-group, which finishes its chunk without waiting on anything,
-//    so no placement or residency is assumed.
-//  * the camera frames of a work-group's cameras (R, t, K, J_l) are built once, one lane per
-//    camera, by its first camera wave and shared through LDS; every camera wave issues its
-//    first index loads and gathers before it waits for them.
-// Everything else — the SELL point rows, the camera waves' gathered three-slot pipeline, the
-// fixed-order reductions, the fixed-point cost — is k_eval_fused's streamed form (ST, CG).
-constexpr int kXcd = 8;
-constexpr int kXtabRec = 16;    // doubles per extrinsic record: R(9) t(3) stamp(1) pad(3) = 128 B
-constexpr int kXtabChunk = 64;  // extrinsics per claimed chunk (one wave, one lane each)
-constexpr int kXsyncWords = 32; // words per (parity, XCD) counter pair: claim, done (own 128-B line)
-__device__ __forceinline__ int xcc_id() {
-  return __builtin_amdgcn_s_getreg(20 | (3 << 11)) & (kXcd - 1);  // HW_REG_XCC_ID, bits [3:0]
-}
-struct XtabArgs {
-  const double* camtab;  // non-null: the tables of the current x exist (k_cam_tables / the LM
-                         // loop's candidate, [E][kCamTab]): read them, build nothing
-  double* tab;         // [kXcd][E][kXtabRec]
-  unsigned* sync;      // [2][kXcd][kXsyncWords]
-  unsigned* err;       // error word (0 = ok)
-  unsigned stamp;      // this launch's stamp (nonzero)
-  int par;             // counter set of this launch (the other set is zeroed for the next)
-};
-// claim chunks of this XCD's table until none is left; each claimed chunk is built and
-// counted done
-__device__ __forceinline__ void xtab_produce(const XtabArgs& xa, int x, const double* __restrict__ ext, int E) {
-  const int lane = threadIdx.x & 63;
-  unsigned* ctr = xa.sync + (size_t)(xa.par * kXcd + x) * kXsyncWords;
-  const unsigned nch = (unsigned)((E + kXtabChunk - 1) / kXtabChunk);
-  // No divergent control flow in here: all 64 lanes take part in every claim and every
-  // done count with the same value 1 (the compiler makes a full wave's 64 adds one atomic of
-  // 64: the counters run in units of 64, chunk = claim / 64) and every lane builds a table
-  // (lanes past E build the last one; their stores are predicated off). Written with a
-  // lane-0-only claim inside a loop whose body branched, the structurised loop lost lane 0
-  // from exec on gfx950 and never ended (the r05d bisection).
-  for (int it = 0; it < 64; ++it) {
-    unsigned o = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    o = __builtin_amdgcn_readfirstlane(o) >> 6;
-    if (o >= nch) return;
-    const int e = (int)o * kXtabChunk + lane, ee = min(e, E - 1);
-    double x6[6];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)ee + q];
-    double T[30];
-    cam_table(x6, T);
-    if (e < E) {
-      double2* rec = reinterpret_cast<double2*>(xa.tab + ((size_t)x * E + e) * kXtabRec);
-#pragma unroll
-      for (int q = 0; q < 6; ++q) rec[q] = make_double2(T[2 * q], T[2 * q + 1]);
-      rec[6] = make_double2(__longlong_as_double((long long)(((unsigned long long)xa.stamp << 32) | (unsigned)e)), 0.0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of the chunk acknowledged by the L2
-    __hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-// one lane: until this XCD's table is complete (bounded; a timeout raises the error word)
-__device__ __forceinline__ void xtab_wait(const XtabArgs& xa, int x, int E) {
-  const unsigned* ctr = xa.sync + (size_t)(xa.par * kXcd + x) * kXsyncWords;
-  const unsigned nch = 64u * (unsigned)((E + kXtabChunk - 1) / kXtabChunk);  // done counts in units of 64
-  // bounded by an iteration count (2^18 polls of ~1 us: a fraction of a second)
-  for (unsigned n = 0; __hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nch; ++n) {
-    __builtin_amdgcn_s_sleep(2);
-    if (n > (1u << 18)) {
-      __hip_atomic_fetch_or(xa.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-  }
-}
-
+//  * all 16 waves build R,t of the extrinsics (one per thread at E <= 1024: one round of
+//    trigonometry instead of two), after issuing their first loads; the work-group's camera
+//    frames (R, t, K, J_l of its own cameras) come from one lane per camera and are shared
+//    through LDS (no per-wave frame trigonometry);
+//  * the waves meet at an LDS-counter barrier (the camera waves' index and point gathers,
+//    issued before it, are in flight meanwhile), then run the point rows and the camera
+//    entries as k_eval_fused's streamed form (ST, CG).
+// Tried first (r05c-r05h, `scripts/experiments/eval_bal_xcd_tables.patch`): R,t built ONCE per
+// XCD inside the launch — 64-extrinsic chunks claimed from a per-XCD counter, published with
+// plain stores into the XCD's L2 copy, consumed after a done count with sc1 loads. Correct
+// (identical costs), but the hand-off's chain of device-scope round trips put the point waves'
+// tables at 10 us and the sc1 table loads took 4-9 us more: 32 against 23.5 us per C3 launch.
+constexpr int kBalPW = 8;              // point waves per work-group
+constexpr int kBalCW = 16 - kBalPW;    // camera waves
+constexpr int kBalFrame = 28;          // doubles per shared camera frame: R t K J_l small
 // spin on a work-group word until it reaches `want`, bounded by an iteration count (~2^20
 // sleeps, a fraction of a second; then the error word gets `code` and the wave goes on, its
-// results void). No clock read in the loop: s_memrealtime is a memory-path read, and
-// thousands of spinning waves polling it slowed the whole chip (r05f: C3 31.8 us)
+// results void: the pass fails closed)
 __device__ __forceinline__ void lds_wait_ge(const unsigned* w, unsigned want, unsigned* err, unsigned code) {
   for (unsigned n = 0; __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want; ++n) {
     __builtin_amdgcn_s_sleep(1);
@@ -2574,51 +2512,59 @@ __device__ __forceinline__ void lds_wait_ge(const unsigned* w, unsigned want, un
     }
   }
 }
-constexpr int kBalPW = 8;              // point waves per work-group
-constexpr int kBalCW = 16 - kBalPW;    // camera waves
-constexpr int kBalFrame = 28;          // doubles per shared camera frame: R t K J_l small
 __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restrict__ chunk_beg,
                                                    const double* __restrict__ points, const double* __restrict__ ext,
-                                                   double* __restrict__ V, double* __restrict__ g,
-                                                   double* __restrict__ ug, unsigned long long* __restrict__ costfx,
-                                                   unsigned long long* __restrict__ fx_next, XtabArgs xa, int wpc,
-                                                   int wps, int side) {
+                                                   const double* __restrict__ camtab, double* __restrict__ V,
+                                                   double* __restrict__ g, double* __restrict__ ug,
+                                                   unsigned long long* __restrict__ costfx,
+                                                   unsigned long long* __restrict__ fx_next, unsigned* __restrict__ err,
+                                                   int wpc, int wps, int side) {
   __shared__ double rt_s[kLdsCams * 12];
   __shared__ double k_s[kLdsCams * 6];
   __shared__ double csum[kBalCW][27];            // camera waves' sums: [slot * wpc + part]
   __shared__ double cfr[kBalCW / 2][kBalFrame];  // the work-group's camera frames, by slot
   __shared__ double shp[kBalPW][2];
-  __shared__ unsigned ccount[kBalCW + kBalPW], pbar, pdone, cfr_ready, tab_ready;
+  __shared__ unsigned ccount[kBalCW + kBalPW], tbar, kbar, pdone;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   DAB_STAMP(0);
   // camera slot -> camera: slot s of work-group b takes camera s G + (G - 1 - b), so that the
   // work-groups short of a camera are the ones with an extra point slice (slices are dealt
   // from work-group 0 up), and a small camera set leaves the point side's work-groups alone
   auto cam_of = [&](int slot) { return slot * (int)gridDim.x + ((int)gridDim.x - 1 - (int)blockIdx.x); };
+  const int nsl = kBalCW / wpc;
   if (threadIdx.x < kBalCW + kBalPW) ccount[threadIdx.x] = 0u;
-  if (threadIdx.x == 0) pbar = pdone = cfr_ready = tab_ready = 0u;
-  if (blockIdx.x == 0) {
-    if (fx_next)
-      for (int i = threadIdx.x; i < kFxWords; i += blockDim.x) fx_next[i] = 0ull;
-    // the other counter set, for the next launch (nothing of this launch touches it)
-    for (int i = threadIdx.x; i < kXcd * kXsyncWords; i += blockDim.x)
-      xa.sync[(size_t)(xa.par ^ 1) * kXcd * kXsyncWords + i] = 0u;
-  }
+  if (threadIdx.x == 0) tbar = kbar = pdone = 0u;
+  if (blockIdx.x == 0 && fx_next)
+    for (int i = threadIdx.x; i < kFxWords; i += blockDim.x) fx_next[i] = 0ull;
   __syncthreads();
-
-  if (wave >= kBalPW) {
-    // ---------------- camera side ----------------
-    const int nsl = kBalCW / wpc, cw = wave - kBalPW, part = cw / nsl, slot = cw - part * nsl;
-    if (side == 1) return;
-    if (cw == 0) {
+  // every wave's share of the tables, then the work-group barrier (LDS counter). A side that
+  // does not run (the multi-rank split's one-sided launches) still builds and arrives.
+  auto build_tables = [&]() {
+    if (camtab) {
+      for (int e = threadIdx.x; e < v.E; e += blockDim.x) {
+        const double2* src = reinterpret_cast<const double2*>(camtab + (size_t)kCamTab * e);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) reinterpret_cast<double2*>(rt_s + 12 * e)[i] = src[i];
+      }
+    } else {
+      for (int e = threadIdx.x; e < v.E; e += blockDim.x) {
+        double x6[6], T[30];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)e + q];
+        cam_table(x6, T);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) reinterpret_cast<double2*>(rt_s + 12 * e)[i] = make_double2(T[2 * i], T[2 * i + 1]);
+      }
+    }
+    if (wave == kBalPW) {
       // the frames of the work-group's cameras, one lane per camera slot
       const int c = cam_of(lane);
       if (lane < nsl && c < v.NC) {
         const int2 u = v.chunk_uni[c];
         double F[30];
-        if (xa.camtab) {
+        if (camtab) {
 #pragma unroll
-          for (int q = 0; q < 30; ++q) F[q] = xa.camtab[(size_t)kCamTab * u.x + q];
+          for (int q = 0; q < 30; ++q) F[q] = camtab[(size_t)kCamTab * u.x + q];
         } else {
           double x6[6];
 #pragma unroll
@@ -2641,11 +2587,17 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
                     ? 1.0
                     : 0.0;
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_store(&cfr_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(&tbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+
+  if (wave >= kBalPW) {
+    // ---------------- camera side ----------------
+    const int cw = wave - kBalPW, part = cw / nsl, slot = cw - part * nsl;
     const int c = cam_of(slot);  // one round (fused_eval_fits / fused_wpc)
-    if (c >= v.NC) {
+    if (side == 1 || c >= v.NC) {
+      build_tables();
       DAB_STAMP(3);
       return;
     }
@@ -2660,7 +2612,8 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     for (int i = 0; i < 27; ++i) acc[i] = 0.0;
     const double* fr = cfr[slot];
     eval_cams_gather_f(v.cm_pt, v.cm_xy, points, lo + lane, hi, acc, [&]() {
-      lds_wait_ge(&cfr_ready, 1u, xa.err, 4u);
+      build_tables();  // while the first index loads and gathers are in flight
+      lds_wait_ge(&tbar, 16u, err, 1u);
       const UniFrame f(UniFrame::FromShared{}, fr);
       DAB_STAMP(1);
       return f;
@@ -2692,10 +2645,9 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   }
 
   // ---------------- point side ----------------
-  if (side == 2) return;
   const size_t NPs = (size_t)v.NP;
   const int pw = wave, pslots = kBalPW / wps, slot = pw / wps, part = pw - slot * wps;
-  const int rounds = (v.nslice + pslots * gridDim.x - 1) / (pslots * gridDim.x);
+  const int rounds = side == 2 ? 0 : (v.nslice + pslots * gridDim.x - 1) / (pslots * gridDim.x);
   constexpr int D = 3;
   int qe[D];      // packed records (ext | intr << 16, -1 = padding)
   double2 qxy[D];
@@ -2721,11 +2673,10 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
       qxy[d] = v.obs_xy[off + 64 * kk + lane];
     }
   };
-  setup_round();
-  // K of every intrinsic by LDS-DMA (static: no other work-group writes it); 16-B pieces,
-  // each CU of an XCD starting at its own 1/32 of the array
-  const unsigned xrot = blockIdx.x >> 3;
+  // K of every intrinsic by LDS-DMA (no registers), each CU of an XCD starting at its own
+  // 1/32 of the array, before the first rows' loads
   {
+    const unsigned xrot = blockIdx.x >> 3;
     const int npiece = 3 * v.NI, nch = (npiece + 63) >> 6;
     const int rot = (int)((xrot * (unsigned)nch) >> 5);
     for (int j = pw; j < nch; j += kBalPW) {
@@ -2736,66 +2687,14 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
                                        0, 0);
     }
   }
-  if (xa.camtab) {
-    // R, t from the tables of the current x by LDS-DMA: pieces 0-5 of each record
-    const int npiece = 6 * v.E, nch = (npiece + 63) >> 6;
-    const int rot = (int)((xrot * (unsigned)nch) >> 5);
-    for (int j = pw; j < nch; j += kBalPW) {
-      int jr = j + rot;
-      if (jr >= nch) jr -= nch;
-      const int i = min(jr * 64 + lane, npiece - 1);
-      __builtin_amdgcn_global_load_lds(xa.camtab + (size_t)kCamTab * (i / 6) + 2 * (i % 6), rt_s + 2 * (size_t)(jr * 64),
-                                       16, 0, 0);
-    }
-  }
-  // R, t: this XCD's copy of the table, built inside the launch (xtab_produce)
-  const int x = xcc_id();
-#ifdef DAB_TRACE_XTAB  // point-wave stamps of the table hand-off instead of the loop phases
-#define DAB_STAMPX(k)                                                                       \
-  do {                                                                                      \
-    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                          \
-    if (lane == 0 && blockIdx.x < 256) g_trace[(blockIdx.x * 16 + wave) * 4 + (k)] = t_;     \
-  } while (0)
-#undef DAB_STAMP
-#define DAB_STAMP(k) do {} while (0)
-#else
-#define DAB_STAMPX(k) do {} while (0)
-#endif
-  if (!xa.camtab && pw == 0) {
-    xtab_produce(xa, x, ext, v.E);
-    DAB_STAMPX(1);
-    if (lane == 0) {
-      xtab_wait(xa, x, v.E);
-      __hip_atomic_store(&tab_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  }
-  if (!xa.camtab) {
-    lds_wait_ge(&tab_ready, 1u, xa.err, 8u);
-    if (pw != 0) DAB_STAMPX(1);
-    // one record per lane: 7 sc1 loads of 16 B (R t, then the stamp), L2-served
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(xa.tab + (size_t)x * v.E * kXtabRec, (short)0, v.E * kXtabRec * 8, 0x00020000);
-    bool bad = false;
-#pragma unroll 2
-    for (int e = pw * 64 + lane; e < v.E; e += kBalPW * 64) {
-      double2 val[7];
-#pragma unroll
-      for (int q = 0; q < 7; ++q)
-        val[q] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, (e * kXtabRec + 2 * q) * 8, 0, 16));
-#pragma unroll
-      for (int q = 0; q < 6; ++q) reinterpret_cast<double2*>(rt_s + 12 * e)[q] = val[q];
-      bad |= (unsigned long long)__double_as_longlong(val[6].x) != (((unsigned long long)xa.stamp << 32) | (unsigned)e);
-    }
-    if (bad) __hip_atomic_fetch_or(xa.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    DAB_STAMPX(2);
-  }
-  // barrier of the point waves only (LDS counter): own LDS writes and LDS-DMAs retired
-  // before the arrival, acquire before the first table read
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  if (lane == 0) __hip_atomic_fetch_add(&pbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  lds_wait_ge(&pbar, (unsigned)kBalPW, xa.err, 16u);
-  DAB_STAMPX(3);
+  if (rounds > 0) setup_round();
+  build_tables();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the K pieces (and the first rows) have landed
+  if (lane == 0) __hip_atomic_fetch_add(&kbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  lds_wait_ge(&tbar, 16u, err, 1u);
+  lds_wait_ge(&kbar, (unsigned)kBalPW, err, 1u);
   DAB_STAMP(1);
+  if (side == 2) return;
   const LdsTabs<true, false, false> tabs{rt_s, k_s, nullptr, v.intr};
   double acc[2] = {0.0, 0.0};
   for (int r = 0; r < rounds; ++r) {
@@ -2841,7 +2740,6 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
       // (one round by construction) parts -> LDS after the tables (fused_wps keeps
       // 12 E + kBalPW * 9 * 64 doubles inside rt_s); the last part sums them in order
       double* cbuf = rt_s + ((12 * v.E + 1) & ~1);
-      // every part's table reads are done before any part overwrites the space after E
 #pragma unroll
       for (int k = 0; k < 9; ++k) cbuf[(pw * 9 + k) * 64 + lane] = c[k];
       unsigned old = 0;
@@ -2888,25 +2786,12 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   }
   cost_fx_commit(pc, bc, costfx + kFxStride * (blockIdx.x % kFxCopies));
 }
-#ifdef DAB_TRACE_XTAB
-#undef DAB_STAMP
-#define DAB_STAMP(k)                                                                        \
-  do {                                                                                      \
-    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                          \
-    if (lane == 0 && blockIdx.x < 256) g_trace[(blockIdx.x * 16 + wave) * 4 + (k)] = t_;     \
-  } while (0)
-#endif
-#undef DAB_STAMPX
 
-size_t xtab_doubles(int E) { return (size_t)kXcd * (size_t)std::max(E, 1) * kXtabRec; }
-size_t xtab_sync_words() { return 2 * (size_t)kXcd * kXsyncWords; }
 void launch_eval_bal(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
-                     double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
-                     int grid, int side, double* xtab, unsigned* xsync, unsigned* xerr, unsigned stamp, int par,
-                     const double* camtab) {
+                     const double* camtab, double* V, double* g, double* ug, unsigned long long* costfx,
+                     unsigned long long* fx_next, unsigned* err, int grid, int side) {
   const int wpc = fused_wpc(v.NC, grid), wps = fused_wps(v.nslice, v.E, grid);
-  const XtabArgs xa{camtab, xtab, xsync, xerr, stamp, par};
-  k_eval_bal<<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, xa, wpc, wps, side);
+  k_eval_bal<<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, camtab, V, g, ug, costfx, fx_next, err, wpc, wps, side);
 }
 
 // camera-major point copy for the streamed fused pass: cmx[q][i] = points[cm_pt[i]][q].

@@ -533,13 +533,7 @@ struct dab_handle {
     stream_give(device, stream);
   }
 
-  // k_eval_bal: per-XCD camera tables built inside the launch, their counters (two sets,
-  // alternating launches), the launch stamp
-  double* d_xtab = nullptr;
-  unsigned* d_xsync = nullptr;
-  unsigned xstamp = 0;
-  int xpar = 0;
-  unsigned* xerr() { return reinterpret_cast<unsigned*>(d_scal + S_XERR); }
+  unsigned* xerr() { return reinterpret_cast<unsigned*>(d_scal + S_XERR); }  // k_eval_bal's error word
   double* ug() { return d_camred; }  // [NC][27]: U upper-packed (21) | g_c (6)
   double* Ux() { return d_camred + (size_t)27 * NC; }
   size_t camred_count() const { return (size_t)27 * NC + (size_t)36 * ncross; }
@@ -1554,15 +1548,6 @@ static int setup_buffers(dab_handle* h, const std::function<void(const char*)>& 
     CHECK_RC(d.alloc(&h->d_obs_e, (size_t)std::max(1, NS)));
     su_obs_e(s, NS, h->d_obs_idx, h->d_obs_e);
     if (h->knobs.fused_stream == 1) CHECK_RC(d.alloc(&h->d_cmx, (size_t)3 * std::max(1, NE)));
-    if (h->knobs.fused_stream == 2 && h->knobs.eval_bal) {
-      CHECK_RC(d.alloc(&h->d_xtab, xtab_doubles(h->E)));
-      CHECK_RC(d.alloc(&h->d_xsync, xtab_sync_words()));
-      HIP_OK(hipMemsetAsync(h->d_xsync, 0, sizeof(unsigned) * xtab_sync_words(), s));  // the first launch's set
-      h->xpar = 0;
-    } else {
-      h->d_xtab = nullptr;
-      h->d_xsync = nullptr;
-    }
     HIP_OK(hipStreamSynchronize(s));
     v.obs_e = h->d_obs_e;
   }
@@ -2854,16 +2839,13 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
     launch_cmx_gather(s, v, h->d_points, h->d_cmx);
     h->cmx_version = h->pts_version;
   }
-  // k_eval_bal (the default where it applies): the fused pass with the camera tables built
-  // once per XCD inside the launch; each launch takes the next stamp and counter set
-  const bool bal = h->fused && h->d_xtab;
+  // k_eval_bal (the default where it applies: the packed point records of fused_stream 2):
+  // the fused pass with the tables built by every wave of the work-group
+  const bool bal = h->fused && h->d_obs_e && !h->d_cmx && h->knobs.eval_bal;
   auto eval_fused = [&](int grid, int side) {
     if (bal) {
-      if (++h->xstamp == 0) h->xstamp = 1;
-      launch_eval_bal(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
-                      h->cost_fx(h->fx_last ^ 1), grid, side, h->d_xtab, h->d_xsync, h->xerr(), h->xstamp, h->xpar,
-                      fused_tab ? h->d_camtab : nullptr);
-      h->xpar ^= 1;
+      launch_eval_bal(s, v, h->d_chunk_beg, h->d_points, h->d_ext, fused_tab ? h->d_camtab : nullptr, h->d_V, h->d_g,
+                      h->ug(), h->cost_fx(h->fx_last), h->cost_fx(h->fx_last ^ 1), h->xerr(), grid, side);
     } else {
       launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
                         h->cost_fx(h->fx_last ^ 1), grid, side, h->d_cmx, side == 0 ? h->knobs.fused_variant : 0,
@@ -2970,14 +2952,12 @@ static int eval_jacobian_and_blocks(dab_handle* h, bool with_norms, bool tables_
   return 0;
 }
 
-// k_eval_bal's in-launch table hand-off failed (1: a wait timed out, 2: a record's stamp was
-// not this launch's): the pass's results are not to be used
+// k_eval_bal's error word: a bounded work-group wait timed out, the pass's results are void
 static int xerr_check(dab_handle* h) {
   unsigned e = 0;
   std::memcpy(&e, h->h_scal + S_XERR, sizeof(e));
   if (e == 0) return 0;
-  return set_error(DAB_E_DEVICE, "evaluation pass: in-launch camera table hand-off failed (code " + std::to_string(e) +
-                                     ")");
+  return set_error(DAB_E_DEVICE, "evaluation pass: a work-group wait timed out (code " + std::to_string(e) + ")");
 }
 static int read_scalars(dab_handle* h) {
   HIP_OK(hipMemcpyAsync(h->h_scal, h->d_scal, sizeof(double) * S_NSLOTS, hipMemcpyDeviceToHost, h->stream));
@@ -3581,16 +3561,6 @@ extern "C" int dab_sync(dab_handle* h) {
   HIP_OK(hipStreamSynchronize(h->stream));
   if (h->d_scal) {
     HIP_OK(hipMemcpy(h->h_scal + S_XERR, h->d_scal + S_XERR, sizeof(double), hipMemcpyDeviceToHost));
-    static const bool dbg = getenv("DAB_XTAB_DEBUG") != nullptr;  // k_eval_bal's counters on stderr
-    if (dbg && h->d_xsync) {
-      std::vector<unsigned> w(xtab_sync_words());
-      HIP_OK(hipMemcpy(w.data(), h->d_xsync, sizeof(unsigned) * w.size(), hipMemcpyDeviceToHost));
-      unsigned e = 0;
-      std::memcpy(&e, h->h_scal + S_XERR, sizeof(e));
-      std::fprintf(stderr, "xtab: err %u par %d stamp %u |", e, h->xpar, h->xstamp);
-      for (size_t i = 0; i < w.size(); i += 32) std::fprintf(stderr, " %u/%u", w[i], w[i + 1]);
-      std::fprintf(stderr, "\n");
-    }
     CHECK_RC(xerr_check(h));
   }
   return 0;
