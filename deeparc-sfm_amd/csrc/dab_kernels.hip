@@ -2596,7 +2596,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     // ---------------- camera side ----------------
     const int cw = wave - kBalPW, part = cw / nsl, slot = cw - part * nsl;
     const int c = cam_of(slot);  // one round (fused_eval_fits / fused_wpc)
-    if (side == 1 || c >= v.NC) {
+    if (side == 1 || side == 3 || c >= v.NC) {  // 3 (timing ablation): the tables only
       build_tables();
       DAB_STAMP(3);
       return;
@@ -2647,7 +2647,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   // ---------------- point side ----------------
   const size_t NPs = (size_t)v.NP;
   const int pw = wave, pslots = kBalPW / wps, slot = pw / wps, part = pw - slot * wps;
-  const int rounds = side == 2 ? 0 : (v.nslice + pslots * gridDim.x - 1) / (pslots * gridDim.x);
+  const int rounds = side >= 2 ? 0 : (v.nslice + pslots * gridDim.x - 1) / (pslots * gridDim.x);
   constexpr int D = 3;
   int qe[D];      // packed records (ext | intr << 16, -1 = padding)
   double2 qxy[D];
@@ -2694,7 +2694,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   lds_wait_ge(&tbar, 16u, err, 1u);
   lds_wait_ge(&kbar, (unsigned)kBalPW, err, 1u);
   DAB_STAMP(1);
-  if (side == 2) return;
+  if (side >= 2) return;
   const LdsTabs<true, false, false> tabs{rt_s, k_s, nullptr, v.intr};
   double acc[2] = {0.0, 0.0};
   for (int r = 0; r < rounds; ++r) {

@@ -306,6 +306,8 @@ struct Knobs {
   int setup_host = 0;       // DAB_SETUP_HOST=1: dab_set_problem's host passes instead of the device ones
   int fused_gv = 0;         // DAB_FUSED_GV (DAB_ABLATIONS builds): fused-pass camera-side timing ablations
   int eval_bal = 1;         // DAB_EVAL_BAL=0: k_eval_fused (tables in every work-group) instead of k_eval_bal
+  int eval_side = 0;        // DAB_EVAL_SIDE (timing ablation, wrong results): k_eval_bal's single launch runs
+                            // 1 the point side only, 2 the camera side only, 3 the tables only
   int fused_tab = -1;       // DAB_FUSED_TAB: the fused pass reads the camera tables of the current x
                             // instead of building them in every work-group — -1 (default) when they
                             // exist already (the LM loop: the accepted candidate's tables), 1 always
@@ -334,6 +336,7 @@ struct Knobs {
     get("DAB_SETUP_HOST", setup_host);
     get("DAB_FUSED_GV", fused_gv);
     get("DAB_EVAL_BAL", eval_bal);
+    get("DAB_EVAL_SIDE", eval_side);
   }
 };
 
@@ -2853,7 +2856,7 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
     }
   };
   if (h->fused && !h->fused_split) {  // both halves of the pass in one launch
-    eval_fused(h->ncu, 0);
+    eval_fused(h->ncu, bal ? h->knobs.eval_side : 0);
     if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
     if (h->NC > 0) CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
     return 0;
