@@ -2540,7 +2540,8 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   // every wave's share of the tables, then the work-group barrier (LDS counter). A side that
   // does not run (the multi-rank split's one-sided launches) still builds and arrives.
   auto build_tables = [&]() {
-    if (camtab) {
+    if (side == 4) {  // timing ablation: no tables at all
+    } else if (camtab) {
       for (int e = threadIdx.x; e < v.E; e += blockDim.x) {
         const double2* src = reinterpret_cast<const double2*>(camtab + (size_t)kCamTab * e);
 #pragma unroll

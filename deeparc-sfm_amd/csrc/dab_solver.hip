@@ -307,7 +307,7 @@ struct Knobs {
   int fused_gv = 0;         // DAB_FUSED_GV (DAB_ABLATIONS builds): fused-pass camera-side timing ablations
   int eval_bal = 1;         // DAB_EVAL_BAL=0: k_eval_fused (tables in every work-group) instead of k_eval_bal
   int eval_side = 0;        // DAB_EVAL_SIDE (timing ablation, wrong results): k_eval_bal's single launch runs
-                            // 1 the point side only, 2 the camera side only, 3 the tables only
+                            // 1 the point side only, 2 the camera side only, 3 the tables only, 4 nothing
   int fused_tab = -1;       // DAB_FUSED_TAB: the fused pass reads the camera tables of the current x
                             // instead of building them in every work-group — -1 (default) when they
                             // exist already (the LM loop: the accepted candidate's tables), 1 always
