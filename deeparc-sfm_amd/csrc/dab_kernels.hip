@@ -2574,68 +2574,48 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   if (blockIdx.x == 0 && fx_next)
     for (int i = threadIdx.x; i < kFxWords; i += blockDim.x) fx_next[i] = 0ull;
   __syncthreads();
-  // every wave's share of the tables, then the work-group barrier (LDS counter). A side that
-  // does not run (the multi-rank split's one-sided launches) still builds and arrives.
-  auto build_tables = [&]() {
-    if (side == 4) {  // timing ablation: no tables at all
-    } else if (camtab) {
-      for (int e = threadIdx.x; e < v.E; e += blockDim.x) {
-        const double2* src = reinterpret_cast<const double2*>(camtab + (size_t)kCamTab * e);
+  // the frames of the work-group's cameras, one lane per camera slot (wave kBalPW), shared
+  // through LDS; the camera waves wait only for these
+  auto build_frames = [&]() {
+    const int c = cam_of(lane);
+    if (lane < nsl && c < v.NC) {
+      const int2 u = v.chunk_uni[c];
+      double F[30];
+      if (camtab) {
 #pragma unroll
-        for (int i = 0; i < 6; ++i) reinterpret_cast<double2*>(rt_s + 12 * e)[i] = src[i];
+        for (int q = 0; q < 30; ++q) F[q] = camtab[(size_t)kCamTab * u.x + q];
+      } else {
+        double x6[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)u.x + q];
+        cam_table(x6, F);
       }
-    } else {
-      for (int e = threadIdx.x; e < v.E; e += blockDim.x) {
-        double x6[6], T[30];
+      double* o = cfr[lane];
 #pragma unroll
-        for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)e + q];
-        cam_table(x6, T);
+      for (int q = 0; q < 12; ++q) o[q] = F[q];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) reinterpret_cast<double2*>(rt_s + 12 * e)[i] = make_double2(T[2 * i], T[2 * i + 1]);
-      }
-    }
-    if (wave == kBalPW) {
-      // the frames of the work-group's cameras, one lane per camera slot
-      const int c = cam_of(lane);
-      if (lane < nsl && c < v.NC) {
-        const int2 u = v.chunk_uni[c];
-        double F[30];
-        if (camtab) {
+      for (int q = 0; q < 6; ++q) o[12 + q] = v.intr[(size_t)kIntr * u.y + q];
 #pragma unroll
-          for (int q = 0; q < 30; ++q) F[q] = camtab[(size_t)kCamTab * u.x + q];
-        } else {
-          double x6[6];
+      for (int r = 0; r < 3; ++r)
 #pragma unroll
-          for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)u.x + q];
-          cam_table(x6, F);
-        }
-        double* o = cfr[lane];
-#pragma unroll
-        for (int q = 0; q < 12; ++q) o[q] = F[q];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) o[12 + q] = v.intr[(size_t)kIntr * u.y + q];
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-          for (int cc = 0; cc < 3; ++cc)
-            o[18 + 3 * r + cc] = F[12 + 3 * r] * F[21 + cc] + F[12 + 3 * r + 1] * F[24 + cc] + F[12 + 3 * r + 2] * F[27 + cc];
-        // cam_table's branch (its small-angle Rd is exactly I, R never is otherwise)
-        o[27] = (F[12] == 1.0 && F[13] == 0.0 && F[14] == 0.0 && F[15] == 0.0 && F[16] == 1.0 && F[17] == 0.0 &&
-                 F[18] == 0.0 && F[19] == 0.0 && F[20] == 1.0 && F[21] == 1.0 && F[25] == 1.0 && F[29] == 1.0)
-                    ? 1.0
-                    : 0.0;
-      }
+        for (int cc = 0; cc < 3; ++cc)
+          o[18 + 3 * r + cc] = F[12 + 3 * r] * F[21 + cc] + F[12 + 3 * r + 1] * F[24 + cc] + F[12 + 3 * r + 2] * F[27 + cc];
+      // cam_table's branch (its small-angle Rd is exactly I, R never is otherwise)
+      o[27] = (F[12] == 1.0 && F[13] == 0.0 && F[14] == 0.0 && F[15] == 0.0 && F[16] == 1.0 && F[17] == 0.0 &&
+               F[18] == 0.0 && F[19] == 0.0 && F[20] == 1.0 && F[21] == 1.0 && F[25] == 1.0 && F[29] == 1.0)
+                  ? 1.0
+                  : 0.0;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_fetch_add(&tbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0) __hip_atomic_store(&tbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
 
   if (wave >= kBalPW) {
     // ---------------- camera side ----------------
     const int cw = wave - kBalPW, part = cw / nsl, slot = cw - part * nsl;
     const int c = cam_of(slot);  // one round (fused_eval_fits / fused_wpc)
+    if (cw == 0 && side != 4) build_frames();
     if (side == 1 || side == 3 || c >= v.NC) {  // 3 (timing ablation): the tables only
-      build_tables();
       DAB_STAMP(3);
       return;
     }
@@ -2650,8 +2630,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     for (int i = 0; i < 27; ++i) acc[i] = 0.0;
     const double* fr = cfr[slot];
     eval_cams_gather_f(v.cm_pt, v.cm_xy, points, lo + lane, hi, acc, [&]() {
-      build_tables();  // while the first index loads and gathers are in flight
-      lds_wait_ge(&tbar, 16u, err, 1u);
+      if (side != 4) lds_wait_ge(&tbar, 1u, err, 1u);  // the frames, built while the first gathers fly
       const UniFrame f(UniFrame::FromShared{}, fr);
       DAB_STAMP(1);
       return f;
@@ -2726,10 +2705,27 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     }
   }
   if (rounds > 0) setup_round();
-  build_tables();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the K pieces (and the first rows) have landed
+  // R, t of every extrinsic: the point threads (R,t only: the rest of cam_table folds away)
+  if (side == 4) {  // timing ablation: no tables at all
+  } else if (camtab) {
+    for (int e = pw * 64 + lane; e < v.E; e += kBalPW * 64) {
+      const double2* src = reinterpret_cast<const double2*>(camtab + (size_t)kCamTab * e);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) reinterpret_cast<double2*>(rt_s + 12 * e)[i] = src[i];
+    }
+  } else {
+    for (int e = pw * 64 + lane; e < v.E; e += kBalPW * 64) {
+      double x6[6], T[30];
+#pragma unroll
+      for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)e + q];
+      cam_table(x6, T);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) reinterpret_cast<double2*>(rt_s + 12 * e)[i] = make_double2(T[2 * i], T[2 * i + 1]);
+    }
+  }
+  // barrier of the point waves only (LDS counter): own LDS writes and the K LDS-DMA retired
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_fetch_add(&kbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  lds_wait_ge(&tbar, 16u, err, 1u);
   lds_wait_ge(&kbar, (unsigned)kBalPW, err, 1u);
   DAB_STAMP(1);
   if (side >= 2) return;
