@@ -2614,8 +2614,9 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     // ---------------- camera side ----------------
     const int cw = wave - kBalPW, part = cw / nsl, slot = cw - part * nsl;
     const int c = cam_of(slot);  // one round (fused_eval_fits / fused_wpc)
-    if (cw == 0 && side != 4) build_frames();
-    if (side == 1 || side == 3 || c >= v.NC) {  // 3 (timing ablation): the tables only
+    if (cw == 0 && side != 4 && side != 6) build_frames();
+    if (side == 1 || side == 3 || c >= v.NC) {  // timing ablations: 3 the tables only, 5 no point tables,
+                                                 // 6 no camera frames (both sides run, wrong results)
       DAB_STAMP(3);
       return;
     }
@@ -2630,7 +2631,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     for (int i = 0; i < 27; ++i) acc[i] = 0.0;
     const double* fr = cfr[slot];
     eval_cams_gather_f(v.cm_pt, v.cm_xy, points, lo + lane, hi, acc, [&]() {
-      if (side != 4) lds_wait_ge(&tbar, 1u, err, 1u);  // the frames, built while the first gathers fly
+      if (side != 4 && side != 6) lds_wait_ge(&tbar, 1u, err, 1u);  // the frames, built while the first gathers fly
       const UniFrame f(UniFrame::FromShared{}, fr);
       DAB_STAMP(1);
       return f;
@@ -2664,7 +2665,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   // ---------------- point side ----------------
   const size_t NPs = (size_t)v.NP;
   const int pw = wave, pslots = kBalPW / wps, slot = pw / wps, part = pw - slot * wps;
-  const int rounds = side >= 2 ? 0 : (v.nslice + pslots * gridDim.x - 1) / (pslots * gridDim.x);
+  const int rounds = (side == 2 || side == 3) ? 0 : (v.nslice + pslots * gridDim.x - 1) / (pslots * gridDim.x);
   constexpr int D = 3;
   int qe[D];      // packed records (ext | intr << 16, -1 = padding)
   double2 qxy[D];
@@ -2706,7 +2707,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   }
   if (rounds > 0) setup_round();
   // R, t of every extrinsic: the point threads (R,t only: the rest of cam_table folds away)
-  if (side == 4) {  // timing ablation: no tables at all
+  if (side == 4 || side == 5) {  // timing ablations: no point tables
   } else if (camtab) {
     for (int e = pw * 64 + lane; e < v.E; e += kBalPW * 64) {
       const double2* src = reinterpret_cast<const double2*>(camtab + (size_t)kCamTab * e);
@@ -2728,7 +2729,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   if (lane == 0) __hip_atomic_fetch_add(&kbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   lds_wait_ge(&kbar, (unsigned)kBalPW, err, 1u);
   DAB_STAMP(1);
-  if (side >= 2) return;
+  if (side == 2 || side == 3) return;
   const LdsTabs<true, false, false> tabs{rt_s, k_s, nullptr, v.intr};
   double acc[2] = {0.0, 0.0};
   for (int r = 0; r < rounds; ++r) {

@@ -2,9 +2,6 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
-timeout -k 10 300 python -u scripts/eval_ab.py c3_1kcam 3 bal=DAB_EVAL_SIDE=0 old=DAB_EVAL_BAL=0 empty=DAB_EVAL_SIDE=4 tables=DAB_EVAL_SIDE=3 point=DAB_EVAL_SIDE=1 camera=DAB_EVAL_SIDE=2 > gpurun_out/r05l_abl_c3.log 2>&1
+timeout -k 10 300 python -u scripts/eval_ab.py c3_1kcam 3 bal=DAB_EVAL_SIDE=0 empty=DAB_EVAL_SIDE=4 nopt=DAB_EVAL_SIDE=5 nofr=DAB_EVAL_SIDE=6 > gpurun_out/r05l_abl_c3.log 2>&1
 rc=$?; echo "abl rc=$rc"; tail -7 gpurun_out/r05l_abl_c3.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python -u scripts/eval_ab.py c2_100cam 3 bal=DAB_EVAL_BAL=1 old=DAB_EVAL_BAL=0 > gpurun_out/r05l_ab_c2.log 2>&1
 rc=$?; echo "ab c2 rc=$rc"; tail -3 gpurun_out/r05l_ab_c2.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/r05l_pytest.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/r05l_pytest.log; exit $rc
