@@ -72,7 +72,7 @@ def main():
             step, kern, costs, fused = run(pkg, prob, env)
             if ref is None:
                 ref = costs
-            dev = max(abs(a - b) / abs(b) for a, b in zip(costs, ref))
+            dev = max((abs(a - b) / abs(b) for a, b in zip(costs, ref)), default=float("nan"))
             res[n].append((step, kern))
             print(f"rep {r} {n:14s} step {step:7.2f} us  kernel {kern:7.2f} us  sched {fused}  cost dev {dev:.1e}",
                   flush=True)
