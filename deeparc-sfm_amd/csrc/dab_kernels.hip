@@ -2521,14 +2521,18 @@ void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, co
 // waves' R,t of all 1000 extrinsics, two per point thread, and ~1 M the camera waves' own
 // frames, one per wave, wave-uniform) and the point waves could not start their rows before
 // 5.5-7 us, while the camera waves' younger halves were starved behind their older halves.
-// Here:
-//  * all 16 waves build R,t of the extrinsics (one per thread at E <= 1024: one round of
-//    trigonometry instead of two), after issuing their first loads; the work-group's camera
-//    frames (R, t, K, J_l of its own cameras) come from one lane per camera and are shared
-//    through LDS (no per-wave frame trigonometry);
-//  * the waves meet at an LDS-counter barrier (the camera waves' index and point gathers,
-//    issued before it, are in flight meanwhile), then run the point rows and the camera
-//    entries as k_eval_fused's streamed form (ST, CG).
+// Here (v3):
+//  * the camera waves' frames (R, t, K, J_l of the work-group's own cameras, at most 8) are
+//    built by one lane per camera of the first camera wave and shared through LDS; each
+//    camera wave waits for them only after its first index and point gathers are in flight
+//    (eval_cams_gather_f), so there is no per-wave frame trigonometry;
+//  * the point waves alone build R,t of every extrinsic into LDS (all loads first, then at
+//    most two tables per thread) and meet at an LDS-counter barrier of their own before
+//    their rows; the camera waves never wait for the point tables;
+//  * then the point rows and the camera entries run as k_eval_fused's streamed form.
+// Ablations (`DAB_EVAL_SIDE`, timing only, wrong results; r05l): without the point tables a
+// C3 launch takes 20.7 us against 25.1, without the camera frames 24.9: the point tables
+// are the critical path's set-up cost.
 // Tried first (r05c-r05h, `scripts/experiments/eval_bal_xcd_tables.patch`): R,t built ONCE per
 // XCD inside the launch — 64-extrinsic chunks claimed from a per-XCD counter, published with
 // plain stores into the XCD's L2 copy, consumed after a done count with sc1 loads. Correct
@@ -2691,6 +2695,25 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
       qxy[d] = v.obs_xy[off + 64 * kk + lane];
     }
   };
+  // this thread's extrinsics (E <= kLdsCams = 2 x 512: at most two) leave first, so that one
+  // load latency covers both tables (a loop of load -> table, twice, paid it twice: 4.4 us of
+  // a C3 launch went to the point tables, r05l)
+  constexpr int kTabPer = (kLdsCams + kBalPW * 64 - 1) / (kBalPW * 64);
+  double xr[kTabPer][12];  // camtab: R,t as they are; else the 6 parameters
+  const bool tabs_now = side != 4 && side != 5;
+  if (tabs_now) {
+#pragma unroll
+    for (int j = 0; j < kTabPer; ++j) {
+      const int e = min(pw * 64 + lane + j * kBalPW * 64, v.E - 1);
+      if (camtab) {
+#pragma unroll
+        for (int q = 0; q < 12; ++q) xr[j][q] = camtab[(size_t)kCamTab * e + q];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) xr[j][q] = ext[6 * (size_t)e + q];
+      }
+    }
+  }
   // K of every intrinsic by LDS-DMA (no registers), each CU of an XCD starting at its own
   // 1/32 of the array, before the first rows' loads
   {
@@ -2706,20 +2729,19 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     }
   }
   if (rounds > 0) setup_round();
-  // R, t of every extrinsic: the point threads (R,t only: the rest of cam_table folds away)
-  if (side == 4 || side == 5) {  // timing ablations: no point tables
-  } else if (camtab) {
-    for (int e = pw * 64 + lane; e < v.E; e += kBalPW * 64) {
-      const double2* src = reinterpret_cast<const double2*>(camtab + (size_t)kCamTab * e);
+  // R, t of every extrinsic (R,t only: the rest of cam_table folds away)
+  if (tabs_now) {
 #pragma unroll
-      for (int i = 0; i < 6; ++i) reinterpret_cast<double2*>(rt_s + 12 * e)[i] = src[i];
-    }
-  } else {
-    for (int e = pw * 64 + lane; e < v.E; e += kBalPW * 64) {
-      double x6[6], T[30];
+    for (int j = 0; j < kTabPer; ++j) {
+      const int e = pw * 64 + lane + j * kBalPW * 64;
+      if (e >= v.E) break;
+      double T[30];
+      if (camtab) {
 #pragma unroll
-      for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)e + q];
-      cam_table(x6, T);
+        for (int q = 0; q < 12; ++q) T[q] = xr[j][q];
+      } else {
+        cam_table(xr[j], T);
+      }
 #pragma unroll
       for (int i = 0; i < 6; ++i) reinterpret_cast<double2*>(rt_s + 12 * e)[i] = make_double2(T[2 * i], T[2 * i + 1]);
     }
