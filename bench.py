@@ -6,7 +6,7 @@ metric (BASELINE.json): "M observations/sec residual+Jacobian; wall-clock/LM-ite
           pass derives from the points is rebuilt inside the timed step):
           residual + analytic Jacobian of every observation, reduced on chip into the
           J^T J / J^T r blocks (matrix-free; BAL-shaped problems on one GPU: one fused
-          launch k_eval_fused with camera-side and point-side waves side by side; else point
+          launch k_eval_bal with camera-side and point-side waves side by side; else point
           side k_eval_points -> V, g; camera
           side k_eval_cams -> U, g_c, all-reduced over RCCL when N > 1).
   value = observations processed by all ranks / max-over-ranks wall time, in M obs/s.
@@ -21,7 +21,7 @@ metric (BASELINE.json): "M observations/sec residual+Jacobian; wall-clock/LM-ite
           the N ranks (strong scaling): the evaluation pass (step time, M obs/s, the point
           kernel's time and HBM roofline fraction on rank 0's shard) and the mixed-precision
           PCG LM iteration (wall-clock, median).
-  roofline: the evaluation kernel (k_eval_fused, or k_eval_points for the two-kernel
+  roofline: the evaluation kernel (k_eval_bal, or k_eval_points for the two-kernel
           pass), algorithmic bytes / HIP-event time. Bytes follow SURVEY §8(d)'s minimal
           convention: per observation the 16-B pixel + its index words once per traversal
           order (point-major; camera-major for the fused pass's camera side), per point 24 B
@@ -166,7 +166,7 @@ def main():
     jac_bytes = solver.jacobian_bytes()
     achieved = jac_bytes / (jac_ms * 1e-3) / 1e9
     fused = solver.eval_fused()
-    eval_kernel = "k_eval_fused" if fused else "k_eval_points"
+    eval_kernel = "k_eval_bal" if fused else "k_eval_points"
 
     # ---- LM iterations (wall-clock per iteration, same problem) ----
     # "lm_*": exact reduced-camera solve (dense Schur + device Cholesky, the reference's

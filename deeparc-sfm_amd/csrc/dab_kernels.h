@@ -122,18 +122,12 @@ void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, con
 // point side -> V, g, cost in fixed point as launch_eval_points): one launch, camera and
 // point waves side by side. fused_eval_fits: whether the problem qualifies for `grid`.
 bool fused_eval_fits(const DevView& v, int nchunk, int ngen, int ncross, int grid);
-// side: 0 both halves; 1 the point side only (V, g, cost); 2 the camera side only (ug)
-// cmx (nullable): the camera-major point copy [3][NE] (launch_cmx_gather of the current
-// points) together with v.obs_e selects the streamed form; variant = its pipeline depths
-// (DAB_ABLATIONS builds; 0 = default)
-void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
-                       double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
-                       int grid, int side, const double* cmx = nullptr, int variant = 0,
-                       const double* camtab = nullptr, int gv = 0);
-void launch_cmx_gather(hipStream_t s, const DevView& v, const double* points, double* cmx);
-// k_eval_bal: the fused pass (needs v.obs_e; fused_eval_fits) with the tables built by every
-// wave of the work-group (camtab non-null: R,t copied from the tables of the current x); err:
-// error word (a bounded wait timed out; 0 = ok)
+// k_eval_bal (needs v.obs_e, the packed point-side records): side 0 both halves; 1 the point
+// side only (V, g, cost); 2 the camera side only (ug) — the multi-rank split schedule runs the
+// same machine code with a run-time side, so both schedules give bitwise the same sums;
+// 3..6 timing ablations (wrong results). camtab non-null: R,t and the camera frames copied
+// from the tables of the current x instead of built. err: error word (a bounded wait timed
+// out; 0 = ok)
 void launch_eval_bal(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
                      const double* camtab, double* V, double* g, double* ug, unsigned long long* costfx,
                      unsigned long long* fx_next, unsigned* err, int grid, int side);

@@ -518,25 +518,14 @@ __device__ __forceinline__ SmallTabs stage_small_tabs(double* lds, int E, int NI
   __syncthreads();
   return SmallTabs{t_s, k_s};
 }
-// R,t rows of the fused pass's LDS table, bank-spread (DAB_FUSED_RTPAD=1 builds): four
-// cameras' 6 16-B pieces then one 16-B pad, so the first piece of camera e sits at 16-B
-// slot 25 (e / 4) + 6 (e % 4) (with the plain 6-slot stride a piece's slot mod 8 takes only
-// 4 of 8 values). Measured A/B at C3 (`scripts/eval_ab.py`, one box): 23.42 against 22.81 us
-// with the in-kernel tables, 21.42 against 21.87 us with the candidate's tables; C2 equal.
-// Not the default.
-#ifndef DAB_FUSED_RTPAD
-#define DAB_FUSED_RTPAD 0
-#endif
-__host__ __device__ constexpr int rt_pad_off(int e) { return 2 * (25 * (e >> 2) + 6 * (e & 3)); }  // doubles
-__host__ __device__ constexpr int rt_pad_size(int E) { return 2 * 25 * ((E + 3) >> 2); }           // doubles
-template <bool K_IN_LDS, bool KMASK = false, bool RTPAD = false>
+template <bool K_IN_LDS, bool KMASK = false>
 struct LdsTabs {
-  const double* rt_s;  // LDS [E][12]: R t (RTPAD: rt_pad_off layout)
+  const double* rt_s;  // LDS [E][12]: R t
   const double* k_s;   // LDS [NI][6] when K_IN_LDS
   const double* __restrict__ camtab;
   const double* __restrict__ intr;
   __device__ __forceinline__ void rt(int e, double (&T)[12]) const {
-    const double2* p = reinterpret_cast<const double2*>(rt_s + (RTPAD ? rt_pad_off(e) : 12 * e));
+    const double2* p = reinterpret_cast<const double2*>(rt_s + 12 * e);
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       const double2 v = p[i];
@@ -1504,47 +1493,8 @@ struct UniFrame {
   double T[12];  // R | t
   double K[6];
   bool small;
-  // jl: J_l (row-major; I for the small-angle tables) goes to LDS for cam_frame_entry, so
-  // that it holds no registers through the entry loop
-  __device__ __forceinline__ UniFrame(const double* __restrict__ ext, const double* __restrict__ intr, int e,
-                                      int i, double* jl) {
-    double F[30];
-    cam_table(ext + 6 * (size_t)e, F);
-    init(F, intr + (size_t)kIntr * i, jl);
-  }
-  // the same from the extrinsic's 6 parameters and the intrinsic's 6 values already in
-  // registers (loaded at the top of the caller, so that the trigonometry can run while its
-  // first gathers are in flight instead of waiting behind them)
-  struct FromValues {};
-  __device__ __forceinline__ UniFrame(FromValues, const double (&x6)[6], const double (&k6)[6], double* jl) {
-    double F[30];
-    cam_table(x6, F);
-    init(F, k6, jl);
-  }
-  __device__ __forceinline__ void init(const double (&F)[30], const double* k, double* jl) {
-    // cam_table's branch (its small-angle Rd is exactly I, R never is otherwise)
-    small = F[12] == 1.0 && F[13] == 0.0 && F[14] == 0.0 && F[15] == 0.0 && F[16] == 1.0 && F[17] == 0.0 &&
-            F[18] == 0.0 && F[19] == 0.0 && F[20] == 1.0 && F[21] == 1.0 && F[25] == 1.0 && F[29] == 1.0;
-#pragma unroll
-    for (int q = 0; q < 12; ++q) T[q] = UniTabs::uniform(F[q]);
-#pragma unroll
-    for (int q = 0; q < 6; ++q) K[q] = UniTabs::uniform(k[q]);
-    // J_l = Rd Jd (Rd = R, or I with Jd = I for the small-angle tables), wave-uniform,
-    // stored by lane 0
-    double J[9];
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-        J[3 * r + c] = UniTabs::uniform(F[12 + 3 * r] * F[21 + c] + F[12 + 3 * r + 1] * F[24 + c] +
-                                        F[12 + 3 * r + 2] * F[27 + c]);
-    if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-      for (int q = 0; q < 9; ++q) jl[q] = J[q];
-    }
-  }
-  // the same from a frame shared in LDS (k_eval_bal: R t K J_l small, kBalFrame doubles),
-  // every lane reading the same address (broadcast), then held in SGPRs
+  // from a frame shared in LDS (k_eval_bal: R t K J_l small, kBalFrame doubles), every
+  // lane reading the same address (broadcast), then held in SGPRs
   struct FromShared {};
   __device__ __forceinline__ UniFrame(FromShared, const double* fr) {
 #pragma unroll
@@ -1552,33 +1502,6 @@ struct UniFrame {
 #pragma unroll
     for (int q = 0; q < 6; ++q) K[q] = UniTabs::uniform(fr[12 + q]);
     small = UniTabs::uniform(fr[27]) != 0.0;
-  }
-  // the same from the precomputed table camtab[e] (k_cam_tables: R t Rd Jd), scalar loads
-  struct FromTable {};
-  __device__ __forceinline__ UniFrame(FromTable, const double* __restrict__ camtab,
-                                      const double* __restrict__ intr, int e, int i, double* jl) {
-    const double* F = camtab + (size_t)kCamTab * e;
-    double Fr[30];
-#pragma unroll
-    for (int q = 0; q < 30; ++q) Fr[q] = UniTabs::uniform(F[q]);
-    small = Fr[12] == 1.0 && Fr[13] == 0.0 && Fr[14] == 0.0 && Fr[15] == 0.0 && Fr[16] == 1.0 && Fr[17] == 0.0 &&
-            Fr[18] == 0.0 && Fr[19] == 0.0 && Fr[20] == 1.0 && Fr[21] == 1.0 && Fr[25] == 1.0 && Fr[29] == 1.0;
-#pragma unroll
-    for (int q = 0; q < 12; ++q) T[q] = Fr[q];
-    const double* k = intr + (size_t)kIntr * i;
-#pragma unroll
-    for (int q = 0; q < 6; ++q) K[q] = UniTabs::uniform(k[q]);
-    double J[9];
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-        J[3 * r + c] = UniTabs::uniform(Fr[12 + 3 * r] * Fr[21 + c] + Fr[12 + 3 * r + 1] * Fr[24 + c] +
-                                        Fr[12 + 3 * r + 2] * Fr[27 + c]);
-    if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-      for (int q = 0; q < 9; ++q) jl[q] = J[q];
-    }
   }
 };
 
@@ -1622,175 +1545,15 @@ __device__ __forceinline__ void frame_rows_acc(const double2 xy, const double (&
   }
 }
 
-// eval_cams_uni_pipe's three-slot pipeline over the frame accumulation; jl (LDS, 9
-// doubles) receives the camera's J_l for cam_frame_entry
-template <int NS>
-__device__ __forceinline__ void frame_pipe(const DevView& v, int i0, int e, int stride,
-                                           const double* __restrict__ points, const UniFrame& f,
-                                           int (&pt)[NS], double2 (&xy)[NS], double (&X)[NS][3],
-                                           double (&acc)[27]) {
-  const int* __restrict__ cm_pt = v.cm_pt;
-  for (int i = i0; i < e; i += NS * stride) {
-#pragma unroll
-    for (int u = 0; u < NS; ++u) {
-      const int ii = i + u * stride;
-      if (ii >= e) break;
-      const int sg = (u + NS - 2) % NS, sl = (u + NS - 1) % NS;
-      if (pt[sg] >= 0 && ii + (NS - 2) * stride < e) {
-#pragma unroll
-        for (int q = 0; q < 3; ++q) X[sg][q] = points[3 * (size_t)pt[sg] + q];
-      }
-      if (ii + (NS - 1) * stride < e) {
-        pt[sl] = cm_pt[ii + (NS - 1) * stride];
-        xy[sl] = v.cm_xy[ii + (NS - 1) * stride];
-      }
-      frame_rows_acc(xy[u], X[u], f, acc);
-    }
-  }
-}
-template <int NS = 3>
-__device__ __forceinline__ void eval_cams_uni_frame(const DevView& v, int i0, int e, int stride,
-                                                    const double* __restrict__ points, int ext_i, int intr_i,
-                                                    const double* __restrict__ ext, double (&acc)[27],
-                                                    double* jl) {
-  static_assert(NS >= 3, "at least three slots");
-  const int* __restrict__ cm_pt = v.cm_pt;
-  int pt[NS];
-  double2 xy[NS];
-  double X[NS][3];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    pt[s] = -1;
-    xy[s] = make_double2(0.0, 0.0);
-    X[s][0] = X[s][1] = X[s][2] = 0.0;
-  }
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (i0 + s * stride < e) {
-      pt[s] = cm_pt[i0 + s * stride];
-      xy[s] = v.cm_xy[i0 + s * stride];
-    }
-#pragma unroll
-  for (int s = 0; s < NS - 2; ++s)
-    if (pt[s] >= 0) {
-#pragma unroll
-      for (int q = 0; q < 3; ++q) X[s][q] = points[3 * (size_t)pt[s] + q];
-    }
-  const UniFrame f(ext, v.intr, ext_i, intr_i, jl);  // built while the first loads fly
-  DAB_STAMP_ANY(1);
-  frame_pipe<NS>(v, i0, e, stride, points, f, pt, xy, X, acc);
-}
-
-// The fused pass's camera loop over a STREAMED camera-major copy of the point coordinates
-// (cmx, planar [3][NE], refreshed whenever the points change: launch_cmx_gather): every
-// load is a coalesced stream, none depends on another, so the pipeline is NS - 1 steps of
-// 64 entries deep (10 VGPRs per slot) instead of the index -> point gather chain of
-// eval_cams_uni_frame, whose every step waited one dependent L2 round trip.
-template <int NS, bool TAB = false>
-__device__ __forceinline__ void eval_cams_stream(const double* __restrict__ cmx, size_t NE,
-                                                 const double2* __restrict__ cmxy, int i0, int e, int ext_i,
-                                                 int intr_i, const double* __restrict__ ext,
-                                                 const double* __restrict__ intr, double (&acc)[27], double* jl,
-                                                 const double* __restrict__ camtab = nullptr) {
-  static_assert(NS >= 2, "at least two slots");
-  // Every load is unconditional (entries past the range re-read the last one, which is
-  // then not used), so the number of loads in flight is the same on every path and the
-  // compiler's wait before slot u covers exactly that slot (vmcnt((NS-1) x 4)), not every
-  // outstanding load; the step count is wave-uniform.
-  const int lo = i0 - (int)(threadIdx.x & 63);
-  const int n = (e - lo + 63) >> 6;  // steps of 64 entries
-  double2 xy[NS];
-  double X[NS][3];
-  auto load = [&](int slot, int step) {
-    const int i = min(i0 + 64 * step, e - 1);
-    xy[slot] = cmxy[i];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) X[slot][q] = cmx[q * NE + i];
-  };
-  if (n > 0) {
-#pragma unroll
-    for (int st = 0; st < NS - 1; ++st) load(st, st);
-  }
-  // built while the first loads fly
-  const UniFrame f = TAB ? UniFrame(UniFrame::FromTable{}, camtab, intr, ext_i, intr_i, jl)
-                         : UniFrame(ext, intr, ext_i, intr_i, jl);
-  DAB_STAMP_ANY(1);
-  for (int st0 = 0; st0 < n; st0 += NS) {
-#pragma unroll
-    for (int u = 0; u < NS; ++u) {
-      load((u + NS - 1) % NS, st0 + u + NS - 1);
-      if (i0 + 64 * (st0 + u) < e) frame_rows_acc(xy[u], X[u], f, acc);
-    }
-  }
-}
-
-// The fused pass's camera loop gathering the points itself (no camera-major copy to
-// refresh when the points move). Three register slots per ring; per 64-entry step the
-// point index is loaded four steps ahead and the point (with the pixel) gathered two
-// steps ahead, so the index -> gather -> compute chain has two steps of arithmetic to hide
-// each hop. Every load is unconditional (clamped to the last entry; the step count is
-// wave-uniform), so the waits the compiler places count exactly: the gather of step
-// st + 2 waits only for its index (vmcnt(5)), the compute of step st only for its point.
-// AB (timing ablations, wrong results): 2 gathers confined to the first 1024 points (L1/L2
-// hits), 4 no per-entry arithmetic (one add per entry keeps the loads live).
-// camtab (TAB): the camera's frame from the precomputed table (scalar loads, no trigonometry)
-template <int AB = 0, bool TAB = false>
-__device__ __forceinline__ void eval_cams_gather(const int* __restrict__ cm_pt, const double2* __restrict__ cmxy,
-                                                 const double* __restrict__ points, int i0, int e, int ext_i,
-                                                 int intr_i, const double* __restrict__ ext,
-                                                 const double* __restrict__ intr, double (&acc)[27], double* jl,
-                                                 const double* __restrict__ camtab = nullptr) {
-  constexpr int DG = 2, DI = 4, R = 3;
-  const int lo = i0 - (int)(threadIdx.x & 63);
-  const int n = (e - lo + 63) >> 6;  // steps of 64 entries
-  int pid[R];
-  double2 xy[R];
-  double X[R][3];
-  auto load_idx = [&](int slot, int step) { pid[slot] = cm_pt[min(i0 + 64 * step, e - 1)]; };
-  auto gather = [&](int islot, int slot, int step) {
-    const int p = (AB & 2) ? (pid[islot] & 1023) : pid[islot];
-    xy[slot] = cmxy[min(i0 + 64 * step, e - 1)];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) X[slot][q] = points[3 * (size_t)p + q];
-  };
-  // the camera's parameters leave with the first indices (one round trip for both); its
-  // table is then built while the first points are gathered
-  double x6[6], k6[6];
-  if constexpr (!TAB) {
-#pragma unroll
-    for (int q = 0; q < 6; ++q) x6[q] = ext[6 * (size_t)ext_i + q];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) k6[q] = intr[(size_t)kIntr * intr_i + q];
-  }
-  if (n > 0) {
-    // prologue: indices of steps 0 .. DI-1 ... in the order the loop body issues them
-#pragma unroll
-    for (int st = 0; st < DG; ++st) load_idx(st % R, st);
-#pragma unroll
-    for (int st = 0; st < DG; ++st) gather(st % R, st % R, st);
-#pragma unroll
-    for (int st = DG; st < DI; ++st) load_idx(st % R, st);
-  }
-  const UniFrame f = TAB ? UniFrame(UniFrame::FromTable{}, camtab, intr, ext_i, intr_i, jl)
-                         : UniFrame(UniFrame::FromValues{}, x6, k6, jl);  // built while the first gathers fly
-  DAB_STAMP_ANY(1);
-  for (int st0 = 0; st0 < n; st0 += R) {
-#pragma unroll
-    for (int u = 0; u < R; ++u) {
-      const int st = st0 + u;
-      gather((st + DG) % R, (st + DG) % R, st + DG);  // index of step st + DG -> its point
-      load_idx((st + DI) % R, st + DI);                // slot of step st + DI - R = st + 1: consumed
-      if constexpr ((AB & 4) != 0) {
-        if (i0 + 64 * st < e) acc[0] += xy[u].x + X[u][0] + X[u][1] + X[u][2];
-      } else if (i0 + 64 * st < e) {
-        frame_rows_acc(xy[u], X[u], f, acc);
-      }
-    }
-  }
-}
-
-// eval_cams_gather with the camera's frame from the caller (get_frame(), called once the
-// first indices and gathers are in flight: k_eval_bal's frames shared in LDS)
+// The fused pass's camera loop, gathering the points itself (no camera-major copy to refresh
+// when the points move). Three register slots per ring; per 64-entry step the point index is
+// loaded four steps ahead and the point (with the pixel) gathered two steps ahead, so the
+// index -> gather -> compute chain has two steps of arithmetic to hide each hop. Every load is
+// unconditional (clamped to the last entry; the step count is wave-uniform), so the waits the
+// compiler places count exactly: the gather of step st + 2 waits only for its index, the
+// compute of step st only for its point. The camera's frame comes from the caller
+// (get_frame(), called once the first indices and gathers are in flight: k_eval_bal's frames
+// shared in LDS).
 template <class GetFrame>
 __device__ __forceinline__ void eval_cams_gather_f(const int* __restrict__ cm_pt, const double2* __restrict__ cmxy,
                                                    const double* __restrict__ points, int i0, int e,
@@ -2059,488 +1822,66 @@ void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, con
 }
 
 // ------------------------------------------------------------------------------------
-// Fused evaluation pass (BAL-shaped problems): both halves of the pass in ONE launch,
-// with camera-side and point-side waves side by side on every CU.
+// k_eval_bal: the fused evaluation pass (BAL-shaped problems), both traversal orders in ONE
+// launch, camera-side and point-side waves side by side on every CU
 // ------------------------------------------------------------------------------------
-// Why: the camera side is fp64-VALU heavy (~55 % VALU-busy on its own) and the point
-// side is latency bound (~30 %), but as two kernels they cannot overlap: the point
-// kernel's 1024-thread work-group at 128 VGPRs fills a CU's register file. Here waves
-// 0..kFusedPW-1 of each work-group run the point side (SELL slices, lane = point, a
-// D-deep row queue, R,t and K staged in LDS) and the other waves run the camera side (a
-// pair of waves per free camera, each half of its uniform chunk, table in SGPRs, blocks
-// accumulated in the point frame: eval_cams_uni_frame), so the
-// VALU work of one hides the memory latency of the other. Only the point waves need the
-// LDS tables: they stage them and meet at an LDS-counter barrier of their own, while the
-// camera waves start at once. Every reduction keeps a fixed order: the camera pair's two
-// halves are combined (row sums in LDS) by whichever wave of the pair arrives second,
-// in half-then-row order; the point waves' cost partials are summed by the last point
-// wave in wave order and added as fixed-point integers (cost_fx_add). Bitwise identical
-// results to the two-kernel pass for V, g, U, g_c (same per-lane order for V, g; the
-// camera sums are regrouped, so U, g_c agree to rounding), deterministic run to run.
-// Requirements (checked by fused_eval_fits): every observation single-extrinsic, one
-// uniform chunk per free camera, E, NI <= kLdsCams, NC <= (camera waves / 2) x grid.
-constexpr int kFusedPW = 8;               // point waves per work-group
-constexpr int kFusedCW = 16 - kFusedPW;   // camera waves (kFusedCW / 2 cameras per round)
-#ifndef DAB_CAM_SPLIT
-#define DAB_CAM_SPLIT 688
-#endif
-constexpr int kCamSplit = DAB_CAM_SPLIT;  // first part of a two-part camera chunk, in 1/1024
-// ST: the streamed form — camera waves read the camera-major point copy cmx (eval_cams_stream,
-// NS slots) and point waves the packed 4-B slot records v.obs_e (ext | intr << 16, a D-deep
-// queue at 5 VGPRs per row) instead of the 16-B obs_idx records.
-// CG (with ST): the camera waves gather the points themselves (eval_cams_gather), no cmx.
-template <int D, int ABL = 0, int NS = 3, bool ST = false, bool TAB = false, bool CG = false, int GV = 0>
-                                          // GV (with CG; DAB_ABLATIONS builds): camera-side timing ablations,
-                                          // eval_cams_gather's AB flags
-                                          // ABL: 1 camera waves exit at once (point side
-                                          // only), 2 point waves do (camera side only) — the multi-rank split
-                                          // schedule; timing ablations: 3 no trig in the staging, 21 / 22
-                                          // point / camera waves at raised priority; NS: camera-entry slots
-__global__ __launch_bounds__(1024) void k_eval_fused(DevView v, const int* __restrict__ chunk_beg,
-                                                     const double* __restrict__ points,
-                                                     const double* __restrict__ ext, double* __restrict__ V,
-                                                     double* __restrict__ g, double* __restrict__ ug,
-                                                     unsigned long long* __restrict__ costfx,
-                                                     unsigned long long* __restrict__ fx_next,
-                                                     const double* __restrict__ cmx,
-                                                     const double* __restrict__ camtab, int wpc, int wps,
-                                                     int wxor, int side = 0) {
-  constexpr bool RTP = DAB_FUSED_RTPAD != 0;
-  __shared__ double rt_s[RTP ? rt_pad_size(kLdsCams) : kLdsCams * 12];
-  __shared__ double k_s[kLdsCams * 6];
-  __shared__ double csum[kFusedCW][27];     // camera waves' sums: [camera slot * wpc + part][component]
-  __shared__ double cjl[kFusedCW][9];       // camera waves' J_l (eval_cams_uni_frame)
-  __shared__ double shp[kFusedPW][2];       // point waves' cost partials
-  __shared__ unsigned ccount[kFusedCW + kFusedPW], pbar, pdone;  // camera slots | point slots
-  // wxor = 8: the camera side runs on hardware waves 0-7 (the older waves, which the issue
-  // arbiter serves first) and the point side on 8-15; `wave` is the logical index
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) ^ wxor);
-  DAB_STAMP(0);
-  if (threadIdx.x < kFusedCW + kFusedPW) ccount[threadIdx.x] = 0u;
-  if (threadIdx.x == 0) pbar = pdone = 0u;
-  if (blockIdx.x == 0 && fx_next)
-    for (int i = threadIdx.x; i < kFxWords; i += blockDim.x) fx_next[i] = 0ull;
-  __syncthreads();
-
-  if (wave >= kFusedPW) {
-    // ------- camera side: wpc waves per camera (2 at C3; up to 8 for small camera sets),
-    // each one contiguous part of the camera's uniform chunk -------
-    if constexpr (ABL == 22) __builtin_amdgcn_s_setprio(2);
-    // parts are dealt across the slots (part = cw / slots): part 0 of every camera runs on
-    // the older hardware waves, which the issue arbiter serves first, so with two parts the
-    // first is the larger one (kCamSplit / 1024 of the chunk) and the younger waves, which
-    // start late beside the point waves, get the smaller rest
-    const int nsl = kFusedCW / wpc, cw = wave - kFusedPW, part = cw / nsl, slot = cw - part * nsl;
-    const int c = slot * gridDim.x + blockIdx.x;  // one round (fused_eval_fits / fused_wpc)
-    if (c >= v.NC || ABL == 1 || ABL == 15 || side == 1) return;
-    const int b = chunk_beg[c], e = chunk_beg[c + 1];
-    auto cut = [&](int q) -> int {
-      if (wpc == 2 && q == 1) return b + (int)(((long long)(e - b) * kCamSplit) >> 10);
-      return b + (int)(((long long)(e - b) * q) / wpc);
-    };
-    const int lo = cut(part), hi = cut(part + 1);
-    const int2 u = v.chunk_uni[c];
-    double acc[27];
-#pragma unroll
-    for (int i = 0; i < 27; ++i) acc[i] = 0.0;
-    if constexpr (ABL == 5 || ABL == 25) {  // timing ablation: rows through obs_rows (J_r per row)
-      eval_cams_uni_pipe<NS>(v, lo + lane, hi, 64, points, [&]() { return UniTabs(ext, v.intr, u.x, u.y); },
-                             acc);
-      if (lane < 9) cjl[cw][lane] = (lane % 4 == 0) ? 1.0 : 0.0;
-    } else if constexpr (ST && CG) {
-      eval_cams_gather<GV & 6, TAB>(v.cm_pt, v.cm_xy, points, lo + lane, hi, u.x, u.y, ext, v.intr, acc, cjl[cw],
-                                    camtab);
-    } else if constexpr (ST) {
-      eval_cams_stream<NS, TAB>(cmx, (size_t)v.NE, v.cm_xy, lo + lane, hi, u.x, u.y, ext, v.intr, acc, cjl[cw],
-                                camtab);
-    } else {
-      eval_cams_uni_frame<NS>(v, lo + lane, hi, 64, points, u.x, u.y, ext, acc, cjl[cw]);
-    }
-    DAB_STAMP(2);
-    wave_sums_transposed<27>(acc, csum[slot * wpc + part]);
-    unsigned old = 0;
-    if (lane == 0) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      old = __hip_atomic_fetch_add(&ccount[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    old = __builtin_amdgcn_readfirstlane(old);
-    if (old != (unsigned)wpc - 1) {  // another part is still running: the last one writes the row
-      DAB_STAMP(3);
-      return;
-    }
-    // parts summed in order, then out of the point frame (cam_frame_entry)
-    double* cs = csum[slot * wpc];
-    if (lane < 27) {
-      double t = cs[lane];
-      for (int q = 1; q < wpc; ++q) t += csum[slot * wpc + q][lane];
-      cs[lane] = t;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane < 27) ug[27 * (size_t)c + lane] = cam_frame_entry(cs, cjl[cw], lane);
-    DAB_STAMP(3);
-    return;
-  }
-
-  // ---------------- point side ----------------
-  if constexpr (ABL == 2 || ABL == 25) return;
-  if (side == 2) return;
-  if constexpr (ABL == 21) __builtin_amdgcn_s_setprio(2);
-  const size_t NPs = (size_t)v.NP;
-  // wps point waves per slice (1 at C3; more for small problems, whose slices would
-  // otherwise leave most point waves idle): part `part` of the slot's waves takes rows
-  // part, part + wps, ...; the parts are combined in LDS by the last one to finish
-  const int pw = wave, pslots = kFusedPW / wps, slot = pw / wps, part = pw - slot * wps;
-  const int rounds = (v.nslice + pslots * gridDim.x - 1) / (pslots * gridDim.x);
-  RowQueue<ST ? 1 : D> q;
-  int qe[ST ? D : 1];      // ST: packed records (ext | intr << 16, -1 = padding)
-  double2 qxy[ST ? D : 1];
-  double X[3] = {0.0, 0.0, 0.0};
-  int sl = slot * gridDim.x + blockIdx.x, off = 0, len = 0;
-  auto fill_q = [&]() {
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const int k = part + d * wps;
-      if constexpr (ST) {
-        // unconditional (rows past the slice re-read its last row, never used): the same
-        // number of loads on every path, so each row's wait covers that row only
-        const int kk = max(0, min(k, len - 1));
-        qe[d] = v.obs_e[off + 64 * kk + lane];
-        qxy[d] = v.obs_xy[off + 64 * kk + lane];
-      } else if (k < len) {
-        q.id[d] = v.obs_idx[off + 64 * k + lane];
-        q.xy[d] = v.obs_xy[off + 64 * k + lane];
-      } else {
-        q.id[d] = make_int4(-1, 0, -1, 0);
-        q.xy[d] = make_double2(0.0, 0.0);
-      }
-    }
-  };
-  // ST: every load of a round's set-up is unconditional (clamped to valid addresses; a
-  // lane past the points or a wave past the slices computes nothing from what it read), so
-  // the row queue's waits count exactly
-  auto setup_round = [&]() {
-    if constexpr (ST) {
-      const bool has = sl < v.nslice;
-      const int slc = min(sl, v.nslice - 1);
-      const int o0 = v.slice_off[slc], o1 = v.slice_off[slc + 1];
-      off = has ? o0 : 0;
-      len = has ? (o1 - o0) >> 6 : 0;
-      const int p = min(64 * slc + lane, v.NP - 1);
-      X[0] = points[3 * (size_t)p];
-      X[1] = points[3 * (size_t)p + 1];
-      X[2] = points[3 * (size_t)p + 2];
-    } else if (sl < v.nslice) {
-      off = v.slice_off[sl];
-      len = (v.slice_off[sl + 1] - off) >> 6;
-      const int p = 64 * sl + lane;
-      if (p < v.NP) {
-        X[0] = points[3 * (size_t)p];
-        X[1] = points[3 * (size_t)p + 1];
-        X[2] = points[3 * (size_t)p + 2];
-      }
-    }
-    fill_q();
-  };
-  setup_round();
-  // Table staging. Every CU reads the same tables; in one order the 32 CUs of an XCD would
-  // ask for the same L2 lines at the same moment (one L2 channel at a time), and the
-  // camera waves' first loads would queue behind that in each CU. So each CU of an XCD
-  // starts at its own 1/32 of the table (blockIdx / 8: work-groups are dealt to the XCDs
-  // round robin).
-  const unsigned xrot = blockIdx.x >> 3;
-  // LDS-DMA of 16-B pieces (no registers), 64 lane-linear pieces per instruction; tail lanes
-  // repeat the last piece into the padding after it. Intrinsics: K of intrinsic i / 3,
-  // piece i % 3; tables (TAB): R, t of ext i / 6, piece i % 6 from k_cam_tables' output.
-#pragma unroll
-  for (int which = 0; which < (TAB ? 2 : 1); ++which) {
-    const int per = which ? 6 : 3, npiece = per * (which ? v.E : v.NI);
-    // LDS slots: pieces in order, or (R,t with RTP) 25 slots per four cameras (slot 24 a pad)
-    const int nslot = (which && RTP) ? rt_pad_size(v.E) / 2 : npiece;
-    const double* src0 = which ? camtab : v.intr;
-    const int stride = which ? kCamTab : kIntr;
-    double* dst = which ? rt_s : k_s;
-    const int nch = (nslot + 63) >> 6;
-    const int rot = (int)((xrot * (unsigned)nch) >> 5);
-    for (int j = pw; j < nch; j += kFusedPW) {
-      int jr = j + rot;
-      if (jr >= nch) jr -= nch;
-      int i = min(jr * 64 + lane, nslot - 1);
-      if (which && RTP) {  // slot -> piece (a pad slot repeats the group's last piece)
-        const int gq = i / 25, w = min(i - 25 * gq, 23);
-        i = min(24 * gq + w, npiece - 1);
-      }
-      __builtin_amdgcn_global_load_lds(src0 + (size_t)stride * (i / per) + 2 * (i % per), dst + 2 * (size_t)(jr * 64),
-                                       16, 0, 0);
-    }
-  }
-  // R, t of every extrinsic from the parameters (point threads only)
-  const int erot = (int)((xrot * (unsigned)v.E) >> 5);
-  for (int e1 = pw * 64 + lane; e1 < (TAB ? 0 : v.E); e1 += kFusedPW * 64) {
-    const int e0 = e1 + erot < v.E ? e1 + erot : e1 + erot - v.E;
-    double2 xw[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) xw[i] = reinterpret_cast<const double2*>(ext + 6 * (size_t)e0)[i];
-    const double x6[6] = {xw[0].x, xw[0].y, xw[1].x, xw[1].y, xw[2].x, xw[2].y};
-    double T[30];
-    if constexpr (ABL == 3) {  // timing ablation: no trig (wrong tables)
-#pragma unroll
-      for (int i = 0; i < 12; ++i) T[i] = (i % 4 == 0 ? 1.0 : 0.0) + (i >= 9 ? x6[i - 6] : 0.0);
-    } else {
-      cam_table(x6, T);
-    }
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-      reinterpret_cast<double2*>(rt_s + (RTP ? rt_pad_off(e0) : 12 * e0))[i] = make_double2(T[2 * i], T[2 * i + 1]);
-  }
-  // barrier of the point waves only (LDS counter): own LDS writes and LDS-DMAs retired
-  // before the arrival, acquire before the first table read
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  if (lane == 0) __hip_atomic_fetch_add(&pbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  while (__hip_atomic_load(&pbar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)kFusedPW)
-    __builtin_amdgcn_s_sleep(1);
-  DAB_STAMP(1);
-  const LdsTabs<true, false, RTP> tabs{rt_s, k_s, nullptr, v.intr};
-  double acc[2] = {0.0, 0.0};
-  for (int r = 0; r < rounds; ++r) {
-    if (r > 0) {
-      sl = (r * pslots + slot) * gridDim.x + blockIdx.x;
-      off = len = 0;
-      X[0] = X[1] = X[2] = 0.0;
-      setup_round();
-    }
-    double c[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) c[k] = 0.0;
-#pragma unroll 1
-    for (int k0 = part; k0 < len; k0 += D * wps) {
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const int k = k0 + d * wps;
-        if (!ST && k >= len) break;
-        int4 id;
-        double2 xy;
-        if constexpr (ST) {
-          const int pk = qe[d], pe = pk >= 0 ? pk : 0;
-          id = make_int4(pk >= 0 ? 0 : -1, pe & 0xffff, -1, pe >> 16);
-          xy = qxy[d];
-          const int kn = min(k + D * wps, len - 1);
-          qe[d] = v.obs_e[off + 64 * kn + lane];
-          qxy[d] = v.obs_xy[off + 64 * kn + lane];
-          if (k >= len) continue;  // wave-uniform; no load below
-        } else {
-          id = q.id[d];
-          xy = q.xy[d];
-          if (k + D * wps < len) {
-            q.id[d] = v.obs_idx[off + 64 * (k + D * wps) + lane];
-            q.xy[d] = v.obs_xy[off + 64 * (k + D * wps) + lane];
-          }
-        }
-        const bool live = id.x >= 0;
-        double ru, rv, jx0[3], jx1[3];
-        obs_rows<true, -1, LdsTabs<true, false, RTP>, false>(id, xy, X, tabs, ru, rv, jx0, jx1, nullptr, nullptr);
-        if (!live) ru = rv = jx0[0] = jx0[1] = jx0[2] = jx1[0] = jx1[1] = jx1[2] = 0.0;
-        c[0] = fma(jx1[0], jx1[0], fma(jx0[0], jx0[0], c[0]));
-        c[1] = fma(jx1[0], jx1[1], fma(jx0[0], jx0[1], c[1]));
-        c[2] = fma(jx1[0], jx1[2], fma(jx0[0], jx0[2], c[2]));
-        c[3] = fma(jx1[1], jx1[1], fma(jx0[1], jx0[1], c[3]));
-        c[4] = fma(jx1[1], jx1[2], fma(jx0[1], jx0[2], c[4]));
-        c[5] = fma(jx1[2], jx1[2], fma(jx0[2], jx0[2], c[5]));
-        c[6] = fma(jx1[0], rv, fma(jx0[0], ru, c[6]));
-        c[7] = fma(jx1[1], rv, fma(jx0[1], ru, c[7]));
-        c[8] = fma(jx1[2], rv, fma(jx0[2], ru, c[8]));
-        // a non-finite residual makes the lane's r^2 sum non-finite, which the
-        // fixed-point add below flags: no per-row finiteness test
-        acc[0] = fma(rv, rv, fma(ru, ru, acc[0]));
-      }
-    }
-    const int p = 64 * sl + lane;
-    if (wps > 1) {
-      // (one round by construction) parts -> LDS after the tables (fused_wps keeps
-      // 12 E + kFusedPW * 9 * 64 doubles inside rt_s); the last part sums them in order
-      double* cbuf = rt_s + (RTP ? rt_pad_size(v.E) : ((12 * v.E + 1) & ~1));
-#pragma unroll
-      for (int k = 0; k < 9; ++k) cbuf[(pw * 9 + k) * 64 + lane] = c[k];
-      unsigned old = 0;
-      if (lane == 0) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        old = __hip_atomic_fetch_add(&ccount[kFusedCW + slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      old = __builtin_amdgcn_readfirstlane(old);
-      if (old != (unsigned)wps - 1) continue;
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        double t = cbuf[((slot * wps) * 9 + k) * 64 + lane];
-        for (int q2 = 1; q2 < wps; ++q2) t += cbuf[((slot * wps + q2) * 9 + k) * 64 + lane];
-        c[k] = t;
-      }
-    }
-    if (sl < v.nslice && p < v.NP) {
-#pragma unroll
-      for (int k = 0; k < 6; ++k) V[k * NPs + p] = c[k];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) g[k * NPs + p] = c[6 + k];
-    }
-  }
-  DAB_STAMP(2);
-  // cost: wave sums, summed in wave order by the last point wave, added in fixed point
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const double t = wave_sum_lane63(acc[i]);
-    if (lane == 63) shp[pw][i] = t;
-  }
-  unsigned old = 0;
-  if (lane == 63) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    old = __hip_atomic_fetch_add(&pdone, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-  old = __builtin_amdgcn_readlane(old, 63);
-  DAB_STAMP(3);
-  if (old != (unsigned)kFusedPW - 1 || lane != 0) return;
-  double pc = shp[0][0], bc = shp[0][1];
-#pragma unroll
-  for (int w = 1; w < kFusedPW; ++w) {
-    pc += shp[w][0];
-    bc += shp[w][1];
-  }
-  cost_fx_commit(pc, bc, costfx + kFxStride * (blockIdx.x % kFxCopies));
-}
-
+// Why fused: the camera side is fp64-VALU heavy and the point side latency bound, but as two
+// kernels they cannot overlap: a 1024-thread work-group at 128 VGPRs fills a CU's register
+// file. Here waves 0..kBalPW-1 of each work-group run the point side (SELL slices, lane =
+// point, a 3-deep row queue of packed 4-B records, R,t and K in LDS) and the other waves the
+// camera side (wpc waves per free camera, each a part of its uniform chunk, the frame in
+// SGPRs, blocks accumulated in the point frame), so one side's arithmetic fills the other's
+// memory stalls. Every reduction keeps a fixed order: a camera's parts are combined (row sums
+// in LDS) by whichever of its waves arrives last, in part order; the point waves' cost
+// partials are summed by the last point wave in wave order and added as fixed-point integers
+// (cost_fx_commit). V, g are bitwise those of the two-kernel pass; U, g_c are regrouped sums
+// (equal to rounding); every run is bitwise the same.
+//  * the camera waves' frames (R, t, K, J_l of the work-group's own cameras, at most 8) are
+//    built by one lane per camera of the first camera wave and shared through LDS; each
+//    camera wave waits for them only after its first index and point gathers are in flight
+//    (eval_cams_gather_f), so there is no per-wave frame trigonometry;
+//  * the point waves alone build R,t of every extrinsic into LDS (both of a thread's
+//    extrinsics loaded before either table is built) and meet at an LDS-counter barrier of
+//    their own before their rows; the camera waves never wait for the point tables.
+// Round 5 (`profiles/r05_*`): this kernel replaced k_eval_fused (round 4; every camera wave
+// built its own frame, the point tables in a load -> table loop), whose two trigonometry
+// phases were a third of its VALU stream (6.61 M VALU per C3 launch, `r05_eval_fused_mix.txt`).
+// C3 launch 25.3 -> 22.4 us, C2 9.9 -> 9.2 us on the same boxes (`scripts/eval_ab.py`).
+// Ablations (`DAB_EVAL_SIDE`, timing only, wrong results): the point tables were 4.4 us of the
+// critical path with the loop (r05l), 1.6 us with the loads issued first (r05m).
+// Measured and dropped (same boxes): the camera waves on the older hardware waves 0-7
+// (26.0 against 22.4 us); the larger camera parts on the SIMDs with the lighter point waves
+// (22.4-23.8 against 22.3 us); R,t built ONCE per XCD inside the launch — 64-extrinsic chunks
+// claimed from a per-XCD counter, published into the XCD's L2, consumed with sc1 loads after
+// a done count (`scripts/experiments/eval_bal_xcd_tables.patch`; correct, 32 against 23.5 us:
+// the hand-off's device-scope round trips put the tables at 10 us).
+// Requirements (fused_eval_fits): every observation single-extrinsic, one uniform chunk per
+// free camera, E, NI <= kLdsCams, NC <= (camera waves / 2) x grid.
+constexpr int kBalPW = 8;              // point waves per work-group
+constexpr int kBalCW = 16 - kBalPW;    // camera waves
+constexpr int kBalFrame = 28;          // doubles per shared camera frame: R t K J_l small
+// first part of a two-part camera chunk, in 1/1024: the older waves (part 0) get more, since
+// the SIMDs' oldest-first issue starves the younger ones (round 3's per-wave timeline)
+constexpr int kCamSplit = 688;
 bool fused_eval_fits(const DevView& v, int nchunk, int ngen, int ncross, int grid) {
   return !v.any_comp && ncross == 0 && ngen == 0 && nchunk == v.NC && v.NC > 0 && v.E <= kLdsCams &&
-         v.NI <= kLdsCams && v.NC <= (kFusedCW / 2) * grid;
+         v.NI <= kLdsCams && v.NC <= (kBalCW / 2) * grid;
 }
 // waves per camera: as many as still give every camera a slot in one round (small camera
 // sets split each chunk finer: C2's 99 cameras take 8 waves each, C3's 999 take 2)
 static int fused_wpc(int NC, int grid) {
-  int w = kFusedCW;
-  while (w > 2 && (long long)NC * w > (long long)kFusedCW * grid) w >>= 1;
+  int w = kBalCW;
+  while (w > 2 && (long long)NC * w > (long long)kBalCW * grid) w >>= 1;
   return w;
 }
 // point waves per slice: more when the slices are few (every slice in one round), if the
 // per-part sums fit in rt_s beside the tables
 static int fused_wps(int nslice, int E, int grid) {
-  int w = kFusedPW;
-  constexpr bool RTP = DAB_FUSED_RTPAD != 0;
-  const int used = RTP ? rt_pad_size(E) : ((12 * E + 1) & ~1), cap = RTP ? rt_pad_size(kLdsCams) : kLdsCams * 12;
-  while (w > 1 && ((long long)nslice * w > (long long)kFusedPW * grid || used + kFusedPW * 9 * 64 > cap))
-    w >>= 1;
+  int w = kBalPW;
+  const int used = (12 * E + 1) & ~1, cap = kLdsCams * 12;
+  while (w > 1 && ((long long)nslice * w > (long long)kBalPW * grid || used + kBalPW * 9 * 64 > cap)) w >>= 1;
   return w;
 }
-void launch_eval_fused(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
-                       double* V, double* g, double* ug, unsigned long long* costfx, unsigned long long* fx_next,
-                       int grid, int side, const double* cmx, int variant, const double* camtab, int gv) {
-  const int wpc = fused_wpc(v.NC, grid), wps = fused_wps(v.nslice, v.E, grid);
-  const int wxor = variant >= 1000 ? 8 : 0;  // camera side on the older hardware waves
-  variant %= 1000;
-#define DAB_FUSED_ARGS v, chunk_beg, points, ext, V, g, ug, costfx, fx_next, cmx, camtab, wpc, wps, wxor
-  if (cmx && v.obs_e) {
-    // streamed form: variant = 10 D + NS (point queue depth, camera slots)
-    // D = 3 point rows and NS = 2 camera slots in flight: the measured best at C3 (deeper
-    // queues cost registers the loops need: 20.5 us against 20.8-21.6 us)
-#ifdef DAB_ABLATIONS
-    if (camtab) {  // tables read from k_cam_tables' output
-      if (side == 1) k_eval_fused<3, 1, 2, true, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-      else if (side == 2) k_eval_fused<3, 2, 2, true, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-      else if (variant == 23) k_eval_fused<2, 0, 3, true, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-      else k_eval_fused<3, 0, 2, true, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-      return;
-    }
-    if (side == 0 && variant != 0) {
-      if (variant == 23) k_eval_fused<2, 0, 3, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-      else if (variant == 24) k_eval_fused<2, 0, 4, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-      else if (variant == 43) k_eval_fused<4, 0, 3, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-      else if (variant == 44) k_eval_fused<4, 0, 4, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-      else k_eval_fused<3, 0, 2, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-      return;
-    }
-#endif
-    if (side == 1) k_eval_fused<3, 1, 2, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-    else if (side == 2) k_eval_fused<3, 2, 2, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-    else k_eval_fused<3, 0, 2, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-    return;
-  }
-  if (v.obs_e && camtab) {
-    // the same with the camera tables of the current x read from k_cam_tables' output (built
-    // once per parameter state: the LM loop builds them for the whole iteration anyway)
-    k_eval_fused<3, 0, 3, true, true, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS, side);
-    return;
-  }
-  if (v.obs_e) {
-    // packed point-side records, camera waves gathering the points (nothing to refresh
-    // when the points move). The multi-rank split schedule runs THIS instantiation with a
-    // run-time side, so both schedules execute the same machine code (the same fp
-    // contraction, hence bitwise the same sums).
-#ifdef DAB_ABLATIONS
-    // camera-side timing ablations (wrong results): 2 gathers confined to the first 1024
-    // points, 4 no per-entry arithmetic, 6 both (DAB_FUSED_GV)
-    if (gv == 2) k_eval_fused<3, 0, 3, true, false, true, 2><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS, side);
-    else if (gv == 4) k_eval_fused<3, 0, 3, true, false, true, 4><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS, side);
-    else if (gv == 6) k_eval_fused<3, 0, 3, true, false, true, 6><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS, side);
-    else
-#endif
-    k_eval_fused<3, 0, 3, true, false, true><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS, side);
-    return;
-  }
-  // one side only (the multi-rank split schedule): the same kernel with the other side's
-  // waves leaving at once
-  if (side == 1) {
-    k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-    return;
-  }
-  if (side == 2) {
-    k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-    return;
-  }
-#ifdef DAB_ABLATIONS
-  // timing ablations (wrong results; built only with -DDAB_ABLATIONS, read once)
-  static const int abl = getenv("DAB_FUSED_ABL") ? atoi(getenv("DAB_FUSED_ABL")) : 0;
-  if (abl == 5) k_eval_fused<2, 5><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-  else if (abl == 25) k_eval_fused<2, 25><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-  else if (abl == 1) k_eval_fused<2, 1><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-  else if (abl == 2) k_eval_fused<2, 2><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-  else if (abl == 3) k_eval_fused<2, 3><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-  else if (abl == 21) k_eval_fused<2, 21><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-  else if (abl == 22) k_eval_fused<2, 22><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-  else if (abl == 34) k_eval_fused<2, 0, 4><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-  else if (abl == 35) k_eval_fused<2, 0, 5><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-  else if (abl == 234) k_eval_fused<2, 2, 4><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-  else if (abl == 14) k_eval_fused<4><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-  else
-#endif
-    k_eval_fused<2><<<grid, 1024, 0, s>>>(DAB_FUSED_ARGS);
-#undef DAB_FUSED_ARGS
-}
-
-// ------------------------------------------------------------------------------------
-// k_eval_bal: the fused evaluation pass with every wave of the work-group on the tables
-// ------------------------------------------------------------------------------------
-// k_eval_fused's two trigonometry phases were a third of its VALU stream (PMC,
-// profiles/r05_eval_fused_mix.txt: 6.61 M VALU per C3 launch, of which ~0.95 M the point
-// waves' R,t of all 1000 extrinsics, two per point thread, and ~1 M the camera waves' own
-// frames, one per wave, wave-uniform) and the point waves could not start their rows before
-// 5.5-7 us, while the camera waves' younger halves were starved behind their older halves.
-// Here (v3):
-//  * the camera waves' frames (R, t, K, J_l of the work-group's own cameras, at most 8) are
-//    built by one lane per camera of the first camera wave and shared through LDS; each
-//    camera wave waits for them only after its first index and point gathers are in flight
-//    (eval_cams_gather_f), so there is no per-wave frame trigonometry;
-//  * the point waves alone build R,t of every extrinsic into LDS (all loads first, then at
-//    most two tables per thread) and meet at an LDS-counter barrier of their own before
-//    their rows; the camera waves never wait for the point tables;
-//  * then the point rows and the camera entries run as k_eval_fused's streamed form.
-// Ablations (`DAB_EVAL_SIDE`, timing only, wrong results; r05l): without the point tables a
-// C3 launch takes 20.7 us against 25.1, without the camera frames 24.9: the point tables
-// are the critical path's set-up cost.
-// Tried first (r05c-r05h, `scripts/experiments/eval_bal_xcd_tables.patch`): R,t built ONCE per
-// XCD inside the launch — 64-extrinsic chunks claimed from a per-XCD counter, published with
-// plain stores into the XCD's L2 copy, consumed after a done count with sc1 loads. Correct
-// (identical costs), but the hand-off's chain of device-scope round trips put the point waves'
-// tables at 10 us and the sc1 table loads took 4-9 us more: 32 against 23.5 us per C3 launch.
-constexpr int kBalPW = 8;              // point waves per work-group
-constexpr int kBalCW = 16 - kBalPW;    // camera waves
-constexpr int kBalFrame = 28;          // doubles per shared camera frame: R t K J_l small
 // spin on a work-group word until it reaches `want`, bounded by an iteration count (~2^20
 // sleeps, a fraction of a second; then the error word gets `code` and the wave goes on, its
 // results void: the pass fails closed)
@@ -2752,7 +2093,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   lds_wait_ge(&kbar, (unsigned)kBalPW, err, 1u);
   DAB_STAMP(1);
   if (side == 2 || side == 3) return;
-  const LdsTabs<true, false, false> tabs{rt_s, k_s, nullptr, v.intr};
+  const LdsTabs<true, false> tabs{rt_s, k_s, nullptr, v.intr};
   double acc[2] = {0.0, 0.0};
   for (int r = 0; r < rounds; ++r) {
     if (r > 0) {
@@ -2776,7 +2117,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
         if (k >= len) continue;  // wave-uniform; no load below
         const bool live = id.x >= 0;
         double ru, rv, jx0[3], jx1[3];
-        obs_rows<true, -1, LdsTabs<true, false, false>, false>(id, xy, X, tabs, ru, rv, jx0, jx1, nullptr, nullptr);
+        obs_rows<true, -1, LdsTabs<true, false>, false>(id, xy, X, tabs, ru, rv, jx0, jx1, nullptr, nullptr);
         if (!live) ru = rv = jx0[0] = jx0[1] = jx0[2] = jx1[0] = jx1[1] = jx1[2] = 0.0;
         c[0] = fma(jx1[0], jx1[0], fma(jx0[0], jx0[0], c[0]));
         c[1] = fma(jx1[0], jx1[1], fma(jx0[0], jx0[1], c[1]));
@@ -2851,37 +2192,6 @@ void launch_eval_bal(hipStream_t s, const DevView& v, const int* chunk_beg, cons
   k_eval_bal<<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, camtab, V, g, ug, costfx, fx_next, err, wpc, wps, side);
 }
 
-// camera-major point copy for the streamed fused pass: cmx[q][i] = points[cm_pt[i]][q].
-// Four entries per thread (stride one grid row), every index load issued before the
-// gathers and every gather before the stores, so each thread has 4 x 3 loads in flight.
-__global__ __launch_bounds__(256) void k_cmx_gather(int NE, const int* __restrict__ cm_pt,
-                                                    const double* __restrict__ points, double* __restrict__ cmx) {
-  const size_t NEs = (size_t)NE;
-  const int row = gridDim.x * blockDim.x;
-  for (int i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < NE; i0 += 4 * row) {
-    int p[4];
-    double x[4][3];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) p[k] = cm_pt[min(i0 + k * row, NE - 1)];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int q = 0; q < 3; ++q) x[k][q] = points[3 * (size_t)p[k] + q];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (i0 + k * row < NE) {
-#pragma unroll
-        for (int q = 0; q < 3; ++q) cmx[q * NEs + i0 + k * row] = x[k][q];
-      }
-  }
-}
-void launch_cmx_gather(hipStream_t s, const DevView& v, const double* points, double* cmx) {
-  if (v.NE <= 0) return;
-  k_cmx_gather<<<grid_for((v.NE + 3) / 4, 256, 4096), 256, 0, s>>>(v.NE, v.cm_pt, points, cmx);
-}
-
-// arc∘ring cross blocks Jc0^T Jc1, one block per chunk of composed observations sorted
-// by camera pair, re-evaluated from their pair-major input copy.
 __global__ __launch_bounds__(256) void k_eval_cross(DevView v, const int* __restrict__ chunk_beg,
                                                     const int4* __restrict__ x_idx,
                                                     const double2* __restrict__ x_xy,

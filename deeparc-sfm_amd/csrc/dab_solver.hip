@@ -299,15 +299,10 @@ struct Knobs {
   int tile_balance = 1;     // DAB_TILE_BALANCE=0: one work-group per tile and group of batches
   int p2p = -1;             // DAB_P2P: one-shot xGMI all-reduce of small sums (-1 auto: RCCL handles
                             // only; 1 also on host-staged handles, the one-GPU rehearsal; 0 off)
-  int fused_stream = 2;     // DAB_FUSED_STREAM: fused pass records — 2 packed point-side records, camera
-                            // waves gather the points; 1 the same with the camera-major point copy
-                            // (refreshed after every point change); 0 the 16-B records
-  int fused_variant = 0;    // DAB_FUSED_V: pipeline depths of the streamed fused pass (DAB_ABLATIONS builds)
   int setup_host = 0;       // DAB_SETUP_HOST=1: dab_set_problem's host passes instead of the device ones
-  int fused_gv = 0;         // DAB_FUSED_GV (DAB_ABLATIONS builds): fused-pass camera-side timing ablations
-  int eval_bal = 1;         // DAB_EVAL_BAL=0: k_eval_fused (tables in every work-group) instead of k_eval_bal
   int eval_side = 0;        // DAB_EVAL_SIDE (timing ablation, wrong results): k_eval_bal's single launch runs
-                            // 1 the point side only, 2 the camera side only, 3 the tables only, 4 nothing
+                            // 1 the point side only, 2 the camera side only, 3 the tables only, 4 no
+                            // tables or frames, 5 no point tables, 6 no camera frames
   int fused_tab = -1;       // DAB_FUSED_TAB: the fused pass reads the camera tables of the current x
                             // instead of building them in every work-group — -1 (default) when they
                             // exist already (the LM loop: the accepted candidate's tables), 1 always
@@ -330,12 +325,8 @@ struct Knobs {
     get("DAB_SCHUR_TILES", schur_tiles);
     get("DAB_TILE_BALANCE", tile_balance);
     get("DAB_P2P", p2p);
-    get("DAB_FUSED_STREAM", fused_stream);
-    get("DAB_FUSED_V", fused_variant);
     get("DAB_FUSED_TAB", fused_tab);
     get("DAB_SETUP_HOST", setup_host);
-    get("DAB_FUSED_GV", fused_gv);
-    get("DAB_EVAL_BAL", eval_bal);
     get("DAB_EVAL_SIDE", eval_side);
   }
 };
@@ -390,11 +381,8 @@ struct dab_handle {
   DevView view{};
   int4* d_obs_idx = nullptr;
   double2* d_obs_xy = nullptr;
-  // streamed fused pass: packed slot records (DevView::obs_e) and the camera-major point copy
-  // cmx [3][NE], re-gathered in eval_pass whenever the points changed (pts_version)
+  // fused pass: packed 4-B slot records of the point waves (DevView::obs_e)
   int* d_obs_e = nullptr;
-  double* d_cmx = nullptr;
-  long long pts_version = 0, cmx_version = -1;
   int4* d_cm_idx = nullptr;
   double2* d_cm_xy = nullptr;
   int4* d_x_idx = nullptr;
@@ -473,7 +461,7 @@ struct dab_handle {
   unsigned* d_cg_cnt = nullptr;
   double* d_fused_partial = nullptr;
   int eval_wps = 0;   // 0: LDS tables; else waves per slice (DAB_EVAL_WPS tuning knob)
-  bool fused = false;  // evaluation pass as one launch (launch_eval_fused; DAB_EVAL_FUSED=0 disables)
+  bool fused = false;  // evaluation pass as one launch (k_eval_bal; DAB_EVAL_FUSED=0 disables)
 
   // Buffers kept across dab_set_problem while the new problem's size fits: the dense S, the
   // camera step and the flags. The Cholesky's captured graph is keyed on their addresses, so
@@ -1443,7 +1431,6 @@ static int setup_host(dab_handle* h, const dab_problem* p, const std::function<v
   }
   CHECK_RC(upload(&h->d_intr, d, intr, s));
   CHECK_RC(upload(&h->d_points, d, points, s));
-  ++h->pts_version;
   CHECK_RC(upload(&h->d_ext, d, ext, s));
   h->local_compose = false;
   for (int o = 0; o < N && !h->local_compose; ++o) h->local_compose = p->obs_ext1[o] >= 0;
@@ -1542,15 +1529,11 @@ static int setup_buffers(dab_handle* h, const std::function<void(const char*)>& 
   h->fused = h->fused && fused_eval_fits(v, h->nchunk, h->chunks.ngen, h->ncross, h->ncu);
   v.obs_e = nullptr;
   h->d_obs_e = nullptr;
-  h->d_cmx = nullptr;
-  h->cmx_version = -1;
-  if (h->fused && h->knobs.fused_stream != 0 && h->E < 0x8000 && h->NI < 0x8000) {
-    // packed 4-B slot records for the point waves; fused_stream = 1 also the camera-major
-    // point copy (re-gathered whenever the points move), 2 (default) camera waves that
-    // gather the points themselves
+  if (h->fused) {
+    // packed 4-B slot records for the point waves (ext | intr << 16: fused_eval_fits keeps
+    // E, NI <= kLdsCams)
     CHECK_RC(d.alloc(&h->d_obs_e, (size_t)std::max(1, NS)));
     su_obs_e(s, NS, h->d_obs_idx, h->d_obs_e);
-    if (h->knobs.fused_stream == 1) CHECK_RC(d.alloc(&h->d_cmx, (size_t)3 * std::max(1, NE)));
     HIP_OK(hipStreamSynchronize(s));
     v.obs_e = h->d_obs_e;
   }
@@ -1978,7 +1961,6 @@ static int setup_device(dab_handle* h, const dab_problem* p, const std::function
   CHECK_RC(upload(&h->d_intr, d, intr, s));
   CHECK_RC(d.alloc(&h->d_points, (size_t)3 * NP));
   su_points(s, NP, pt_of_d, r_points, h->d_points);
-  ++h->pts_version;
   CHECK_RC(upload(&h->d_ext, d, ext, s));
   h->host_entries = false;  // build_schur_* fetch the entry lists from the device on first use
   HIP_OK(hipStreamSynchronize(s));
@@ -2779,7 +2761,6 @@ extern "C" int dab_update_parameters(dab_handle* h, const double* points, const 
       for (int k = 0; k < 3; ++k) pts[3 * (size_t)i + k] = points[3 * (size_t)h->pt_of[i] + k];
     HIP_OK(hipMemcpyAsync(h->d_points, pts.data(), pts.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
     HIP_OK(hipStreamSynchronize(h->stream));
-    ++h->pts_version;
   }
   if (ext) {
     HIP_OK(hipMemcpyAsync(h->d_ext, ext, sizeof(double) * 6 * (size_t)h->E, hipMemcpyHostToDevice, h->stream));
@@ -2821,8 +2802,6 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
   hipStream_t s = h->stream;
   const DevView& v = h->view;
   bool overlapped = false;
-  // the streamed fused pass reads R, t (point side) and R, t, Rd, Jd (camera side) from the
-  // tables of the current x instead of building them in every work-group
   // the fused pass reads the tables when the caller has them (the LM loop) — C3: 21.3
   // against 23.2 us per launch — but does not launch a table build of its own for them
   // (k_cam_tables in front of the pass cost more than it saves: 25.6 against 23.9 us per
@@ -2834,29 +2813,14 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
   const bool fx = h->fused || eval_points_fx(h->eval_wps);
   if (fx) h->fx_last ^= 1;  // this pass adds into set fx_last and zeroes the other
   h->cost_fx_pending = fx;
-  // the timed region of the single fused launch includes the refresh of the camera-major
-  // point copy (fused_stream = 1) that an evaluation at a new point needs
   if (h->fused && !h->fused_split && ev_mid) HIP_OK(hipEventRecord(ev_mid, s));
-  if (h->d_cmx && h->cmx_version != h->pts_version) {
-    // the points changed since the camera-major copy was taken (set-up, accepted step)
-    launch_cmx_gather(s, v, h->d_points, h->d_cmx);
-    h->cmx_version = h->pts_version;
-  }
-  // k_eval_bal (the default where it applies: the packed point records of fused_stream 2):
-  // the fused pass with the tables built by every wave of the work-group
-  const bool bal = h->fused && h->d_obs_e && !h->d_cmx && h->knobs.eval_bal;
+  // k_eval_bal: both traversal orders in one launch (side 0), or one side per launch
   auto eval_fused = [&](int grid, int side) {
-    if (bal) {
-      launch_eval_bal(s, v, h->d_chunk_beg, h->d_points, h->d_ext, fused_tab ? h->d_camtab : nullptr, h->d_V, h->d_g,
-                      h->ug(), h->cost_fx(h->fx_last), h->cost_fx(h->fx_last ^ 1), h->xerr(), grid, side);
-    } else {
-      launch_eval_fused(s, v, h->d_chunk_beg, h->d_points, h->d_ext, h->d_V, h->d_g, h->ug(), h->cost_fx(h->fx_last),
-                        h->cost_fx(h->fx_last ^ 1), grid, side, h->d_cmx, side == 0 ? h->knobs.fused_variant : 0,
-                        fused_tab ? h->d_camtab : nullptr, side == 0 ? h->knobs.fused_gv : 0);
-    }
+    launch_eval_bal(s, v, h->d_chunk_beg, h->d_points, h->d_ext, fused_tab ? h->d_camtab : nullptr, h->d_V, h->d_g,
+                    h->ug(), h->cost_fx(h->fx_last), h->cost_fx(h->fx_last ^ 1), h->xerr(), grid, side);
   };
   if (h->fused && !h->fused_split) {  // both halves of the pass in one launch
-    eval_fused(h->ncu, bal ? h->knobs.eval_side : 0);
+    eval_fused(h->ncu, h->knobs.eval_side);
     if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
     if (h->NC > 0) CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
     return 0;
@@ -3299,7 +3263,6 @@ static int solve_impl(dab_handle* h, const dab_options* opt_in, dab_summary* sum
       std::swap(h->d_points, h->d_points_c);
       std::swap(h->d_ext, h->d_ext_c);
       std::swap(h->d_camtab, h->d_camtab_c);  // the candidate pass built the tables of x + delta
-      ++h->pts_version;
       x_norm = xc_norm;
       const double tj = now_s();
       CHECK_RC(eval_jacobian_and_blocks(h, true, true));
@@ -3512,10 +3475,9 @@ extern "C" int dab_bench_eval_pass(dab_handle* h, int with_assembly, int count) 
   const int sample = h->knobs.bench_sample;
   for (int step = 0; step < count; ++step) {
     // every bench pass is an evaluation at a NEW linearization point, as in the LM loop
-    // after an accepted step (sfm.cc:66-73, Ceres re-linearises each iteration): whatever
-    // the pass derives from the points (the camera-major copy of fused_stream = 1) is
-    // rebuilt inside the pass
-    ++h->pts_version;
+    // after an accepted step (sfm.cc:66-73, Ceres re-linearises each iteration): the pass
+    // derives nothing from the points that it could keep between passes (no camera-major
+    // point copy; the tables are built inside the launch)
     if (sample <= 0 || step % sample != 0) {
       CHECK_RC(eval_pass(h, false));
       CHECK_RC(h->allreduce_cost());
@@ -3605,14 +3567,13 @@ extern "C" int dab_jacobian_bytes(dab_handle* h, double* bytes) {
   // LDS variants build R, t from the 48-B extrinsics; the global-table variants read the
   // 96-B R, t part of the camera tables instead. The Jacobian itself never reaches HBM, so
   // its 16 k bytes per observation are not counted (they are not moved).
-  // The fused pass (k_eval_fused) also produces the camera side: it writes U | g_c (216 B
+  // The fused pass (k_eval_bal) also produces the camera side: it writes U | g_c (216 B
   // per free camera) and reads every entry a second time in camera-major order (20 B:
   // point index + pixel; the chunk's camera and intrinsic are per block). A deterministic
   // matrix-free pass needs both traversal orders (point-major for V, g; camera-major for
   // U, g_c: no atomics, no per-observation partials), so both reads are algorithmic.
-  // This is the minimal count whatever the implementation reads: no denormalised copies
-  // (the camera-major point copy of fused_stream = 1 is not counted), no re-gathers of a
-  // point, each traversal's index words once.
+  // This is the minimal count whatever the implementation reads: no denormalised copies, no
+  // re-gathers of a point, each traversal's index words once.
   double b = (24.0 + 72.0) * h->NP + 48.0 * h->E + 48.0 * h->NI;
   if (h->fused) b += 216.0 * h->NC + 20.0 * h->NE;
   for (int o = 0; o < h->N; ++o) b += 16.0 + 4.0 * (h->prob.obs_ext1[o] >= 0 ? 3 : 2);

@@ -15,35 +15,22 @@ import _pkgload  # noqa: E402
 
 pkg = _pkgload.load()
 cfg = sys.argv[1]
-variants = sys.argv[2:]  # DAB_EVAL_WPS values (two-kernel pass), "fused[ABL]", "gather", "stream[V]" or "split"
+variants = sys.argv[2:]  # DAB_EVAL_WPS values (two-kernel pass), "fused[SIDE]", "tab" or "split"
 base = pkg.synth(**pkg.CONFIGS[cfg])
 ref = None
 for wps in variants:
-    os.environ.pop("DAB_EVAL_SPLIT", None)
+    for k in ("DAB_EVAL_SPLIT", "DAB_EVAL_SIDE", "DAB_FUSED_TAB", "DAB_EVAL_WPS"):
+        os.environ.pop(k, None)
     if wps == "split":  # the multi-rank schedule (camera-side, then point-side launch)
         os.environ["DAB_EVAL_FUSED"] = "1"
         os.environ["DAB_EVAL_SPLIT"] = "1"
-        os.environ.pop("DAB_FUSED_ABL", None)
-        os.environ.pop("DAB_EVAL_WPS", None)
-    elif wps.startswith("fused"):  # fused, fused1, fused2 (DAB_FUSED_ABL ablations), gather form
+    elif wps.startswith("fused"):  # k_eval_bal; fused<N>: DAB_EVAL_SIDE=N timing ablation
         os.environ["DAB_EVAL_FUSED"] = "1"
-        os.environ["DAB_FUSED_STREAM"] = "0"
         os.environ["DAB_FUSED_TAB"] = "0"
-        os.environ["DAB_FUSED_ABL"] = wps[5:] or "0"
-        os.environ.pop("DAB_EVAL_WPS", None)
-    elif wps == "gather":  # packed point-side records, camera waves gathering the points (default)
+        os.environ["DAB_EVAL_SIDE"] = wps[5:] or "0"
+    elif wps == "tab":  # k_eval_bal reading the tables of the current x
         os.environ["DAB_EVAL_FUSED"] = "1"
-        os.environ["DAB_FUSED_STREAM"] = "2"
-        os.environ["DAB_FUSED_TAB"] = "0"
-        os.environ.pop("DAB_FUSED_ABL", None)
-        os.environ.pop("DAB_EVAL_WPS", None)
-    elif wps.startswith(("stream", "tab")):  # streamed fused form, stream<DAB_FUSED_V> / tab<V> (tables read)
-        os.environ["DAB_EVAL_FUSED"] = "1"
-        os.environ["DAB_FUSED_STREAM"] = "1"
-        os.environ["DAB_FUSED_TAB"] = "1" if wps.startswith("tab") else "0"
-        os.environ["DAB_FUSED_V"] = wps.lstrip("streamtab") or "0"
-        os.environ.pop("DAB_FUSED_ABL", None)
-        os.environ.pop("DAB_EVAL_WPS", None)
+        os.environ["DAB_FUSED_TAB"] = "1"
     else:
         os.environ["DAB_EVAL_FUSED"] = "0"
         os.environ["DAB_EVAL_WPS"] = str(wps)

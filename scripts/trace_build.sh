@@ -1,5 +1,5 @@
 #!/bin/bash
-# Timing build of libdab with per-wave s_memrealtime stamps in k_eval_fused (-DDAB_TRACE)
+# Timing build of libdab with per-wave s_memrealtime stamps in k_eval_bal (-DDAB_TRACE)
 # into scripts/trace/libdab.so (git-ignored; OUT= and EXTRA= flags for variants). Run here (hipcc cross-compiles); the .so
 # travels with the tree. Used by scripts/trace_fused.py.
 set -e

@@ -1,9 +1,9 @@
-"""Per-wave timeline of k_eval_fused from the timing build (scripts/trace_build.sh:
+"""Per-wave timeline of k_eval_bal from the timing build (scripts/trace_build.sh:
 s_memrealtime stamps, 100 MHz, at kernel entry / after staging / after the entry loop /
 at exit, per work-group and wave). Prints, relative to the earliest entry stamp, the
 distribution of each phase boundary over camera and point waves.
 
-usage: python scripts/trace_fused.py CONFIG [abl]   (DAB_FUSED_ABL: 0 fused, 1 point side, 2 camera side, ...)
+usage: python scripts/trace_fused.py CONFIG [side]   (DAB_EVAL_SIDE: 0 both, 1 point side, 2 camera side, ...)
 """
 import ctypes as C
 import os
@@ -21,7 +21,7 @@ lib = abi.load_library(os.environ.get("DAB_TRACE_LIB", os.path.join(ROOT, "scrip
 abi._LIB = lib
 cfg = sys.argv[1]
 side = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-os.environ["DAB_FUSED_ABL"] = str(side)  # launch_eval_fused's ablation code (1 point side, 2 camera side)
+os.environ["DAB_EVAL_SIDE"] = str(side)  # k_eval_bal's timing ablation (1 point side, 2 camera side)
 prob = pkg.synth(**pkg.CONFIGS[cfg])
 s = pkg.Solver(0)
 s.set_problem(prob)

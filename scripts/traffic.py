@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--valu-dir", default="", help="a third PMC pass with SQ_INSTS_VALU (wave-instructions)")
     ap.add_argument("--lib", default="", help="the libdab.so profiled (its sha256 goes into the record; "
                     "bench.py reports the traffic only for that exact binary)")
-    ap.add_argument("--kernel", default="auto", help="kernel name prefix (auto: k_eval_fused if it ran, "
+    ap.add_argument("--kernel", default="auto", help="kernel name prefix (auto: k_eval_bal if it ran, "
                     "else k_eval_points)")
     a = ap.parse_args()
     fetch, write = load(a.fetch_dir, "FETCH_SIZE"), load(a.write_dir, "WRITE_SIZE")
@@ -57,7 +57,7 @@ def main():
                                bytes_per_launch=(fb or 0.0) + (wb or 0.0),
                                valu_insts=(sum(v) / len(v)) if v else None)
     if a.kernel == "auto":
-        a.kernel = "k_eval_fused" if any(k.startswith("k_eval_fused") for k in table) else "k_eval_points"
+        a.kernel = "k_eval_bal" if any(k.startswith("k_eval_bal") for k in table) else "k_eval_points"
     # the evaluation-kernel variant the bench ran (most launches among the matching names)
     main_k = sorted((k for k in table if k.startswith(a.kernel)), key=lambda k: -table[k]["launches"])
     lib_sha = None

@@ -2,7 +2,7 @@
 
 * C2 (100 cams / 10k pts / 100k obs), C3 (1k / 100k / 1M) and C5 (rig 16 x 64, 1M points,
   10M observations): the HIP path's LM trajectory, through the production kernels
-  (k_eval_fused at C2/C3, k_eval_pair + k_eval_points_lds at C5, the explicit S by pair
+  (k_eval_bal at C2/C3, k_eval_pair + k_eval_points_lds at C5, the explicit S by pair
   tables at C3 and by block tiles at C2/C5, the implicit PCG), against the oracle's
   trajectory on the same generated problem. The oracle runs took 1-300 s per case on the
   CPU, so they are committed as tests/golden/trajectories.json (oracle/gen_trajectories.py);
