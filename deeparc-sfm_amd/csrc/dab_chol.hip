@@ -36,7 +36,6 @@ constexpr int LDP = 66;  // padded LDS row stride (doubles): conflict-free fragm
 constexpr int kBlk = 1024 + NB * NB;
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
-__constant__ int g_chol_prio = 1;  // DAB_CHOL_PRIO=0: no wave priority for the panel chain (A/B)
 
 struct CholCtx {
   Dev mem{"Cholesky scratch"};  // every device buffer below (guarded like the problem's)
@@ -53,9 +52,6 @@ struct CholCtx {
   const void *g_A = nullptr, *g_y = nullptr, *g_flag = nullptr;
   int bulk_grid = 0;  // work-groups of the persistent bulk update (0: one per tile)
   int ncu = 256;
-  size_t bulk_pad = 0;      // DAB_CHOL_BULK_PAD (KB): dynamic LDS padding of the bulk work-groups
-  int bulk_kc = 16;         // DAB_CHOL_BULK_KC: K chunk of the bulk update (16 | 32)
-  int bulk_occ = 4;         // DAB_CHOL_BULK_OCC: waves per SIMD the bulk update is compiled for (2 | 4)
   unsigned* bar = nullptr;  // grid-barrier counter of k_trsv_back_all (zeroed per solve)
   unsigned* ready = nullptr;  // per block: y_b published (k_trsv_back_flow; zeroed per solve)
   bool back_flow = true;      // DAB_CHOL_BACK_FLOW=0: the grid-barrier back substitution
@@ -66,15 +62,12 @@ struct CholCtx {
   bool fuse_panel = true;     // DAB_CHOL_FUSE_PANEL=0: the panel step as its own launch after the column update
   unsigned* pready = nullptr; // per block: L_kk published by the fused column update (zeroed per factorisation)
   int group = 2;            // DAB_CHOL_GROUP: panels per bulk trailing update (2: pairs)
-  int col_grid = 0;         // DAB_CHOL_COL_GRID: most work-groups of a column update (0: one per tile)
   bool v1 = false;          // DAB_CHOL_V1=1: the per-step schedule (one bulk update per panel, one
                             // back-substitution launch per block)
 };
 
 CholCtx* chol_create() {
   CholCtx* c = new CholCtx();
-  // DAB_CHOL_BULK_GRID: work-groups of the bulk trailing update (default: one per CU, so
-  // every CU keeps LDS room for a panel-chain work-group beside it)
   int ncu = 256;
   hipDeviceProp_t prop;
   int dev = 0;
@@ -84,23 +77,14 @@ CholCtx* chol_create() {
   // n = 5994: 6.74 ms against 6.88-6.93 ms for one per CU or all CUs)
   c->bulk_grid = std::max(1, 2 * ncu - 64);
   c->ncu = ncu;
-  if (const char* e = getenv("DAB_CHOL_BULK_GRID")) c->bulk_grid = atoi(e);
   if (const char* e = getenv("DAB_CHOL_V1")) c->v1 = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_GROUP")) c->group = std::max(2, atoi(e));
-  if (const char* e = getenv("DAB_CHOL_COL_GRID")) c->col_grid = std::max(0, atoi(e));
   if (const char* e = getenv("DAB_CHOL_BACK_FLOW")) c->back_flow = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_PREFACTOR")) c->prefactor = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_FUSE_PANEL")) c->fuse_panel = atoi(e) != 0;
   c->nograph = getenv("DAB_CHOL_NOGRAPH") != nullptr;
   if (const char* e = getenv("DAB_CHOL_GRAPH_MIN")) c->graph_min = atoi(e);
   c->serial = getenv("DAB_CHOL_SERIAL") != nullptr;
-  if (const char* e = getenv("DAB_CHOL_BULK_PAD")) c->bulk_pad = (size_t)atoi(e) * 1024;
-  if (const char* e = getenv("DAB_CHOL_BULK_KC")) c->bulk_kc = atoi(e);
-  if (const char* e = getenv("DAB_CHOL_BULK_OCC")) c->bulk_occ = atoi(e);
-  if (const char* e = getenv("DAB_CHOL_PRIO")) {
-    const int v = atoi(e);
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chol_prio), &v, sizeof(int));
-  }
   // the side stream and the barrier word now, not inside the first solve. (A warm-up graph
   // capture here bought nothing: every instantiation costs ~5 ms, the first one no more.)
   int dev_now = 0;
@@ -278,7 +262,7 @@ __global__ __launch_bounds__(kThreads) void k_panel(double* __restrict__ A, int 
   __shared__ double D[4][16][DS];
   // the panel chain is the critical path: its waves win the issue arbitration against the
   // bulk update's waves on shared CUs
-  if (g_chol_prio) __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(3);
   const int tid = threadIdx.x, w = tid >> 6;
   const int row0 = r0 + NB * blockIdx.x;
   if (pre) {
@@ -373,7 +357,7 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
   __shared__ double Pb[NB * LDP];
   __shared__ double Dsh[4][16][DS];
   __shared__ int abort_s;
-  if (col_only && g_chol_prio) __builtin_amdgcn_s_setprio(3);  // on the panel chain
+  if (col_only) __builtin_amdgcn_s_setprio(3);  // on the panel chain
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
   if (t != (int)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
   int bi = t, bj = 0;
@@ -1111,11 +1095,7 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
     const int r0 = cb * NB, m = n + 1 - r0;
     if (m <= 1) return;
     const int nt = (m + NB - 1) / NB;
-    // col_grid: at most that many work-groups, each walking tiles t, t + grid, ... (the
-    // diagonal tile is work-group 0's first), so that the column fits the CUs the bulk
-    // update leaves in one round instead of a second round queued behind the first
-    const int g = c->col_grid > 0 ? std::min(nt, c->col_grid) : nt;
-    k_syrk_mfma<<<g, kThreads, 0, s>>>(A, lda, r0, m, k, kk, 1, nt, pre ? c->blk + (size_t)cb * kBlk : nullptr,
+    k_syrk_mfma<<<nt, kThreads, 0, s>>>(A, lda, r0, m, k, kk, 1, nt, pre ? c->blk + (size_t)cb * kBlk : nullptr,
                                        kb_of(cb), d_flag, fuse ? c->pready + cb : nullptr);
   };
   panel(0);
@@ -1139,13 +1119,10 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
       (void)hipEventRecord(c->ev_panel[b], s);
       (void)hipStreamWaitEvent(s2, c->ev_panel[b], 0);
       const int t2 = (m + TB - 1) / TB, ntb = t2 * (t2 + 1) / 2;
-      // bulk_pad: extra (unused) LDS so that no panel-chain work-group shares a CU with the
-      // bulk (its dependent MFMA chain would queue behind the bulk's MFMAs); the bulk grid
-      // leaves CUs free for the chain instead
+      // the bulk grid leaves CUs free for the panel chain (its dependent MFMA chain would
+      // queue behind the bulk's MFMAs on a shared CU)
       const int g = std::min(ntb, c->bulk_grid > 0 ? c->bulk_grid : ntb);
-      if (c->bulk_kc == 32) k_syrk_big<32, 2><<<g, kBigThreads, c->bulk_pad, s2>>>(A, lda, c0, m, b * NB, kk, ntb);
-      else if (c->bulk_occ == 4) k_syrk_big<16, 4><<<g, kBigThreads, c->bulk_pad, s2>>>(A, lda, c0, m, b * NB, kk, ntb);
-      else k_syrk_big<16, 2><<<g, kBigThreads, c->bulk_pad, s2>>>(A, lda, c0, m, b * NB, kk, ntb);
+      k_syrk_big<16, 4><<<g, kBigThreads, 0, s2>>>(A, lda, c0, m, b * NB, kk, ntb);
       (void)hipEventRecord(c->ev_bulk[b], s2);
       pending = b;
     }

@@ -3283,54 +3283,6 @@ __global__ __launch_bounds__(256) void k_backsub(DevView v, const double* __rest
 constexpr int kMfCams = kMfCamsMax;
 constexpr int kMfBlock = 256;
 bool mf_schur_fits(int NC, int E, int NI) { return NC > 0 && NC <= kMfCams && small_tabs_fit(E, NI); }
-// LDS: tables | s_c o vec [NC][6] | per-wave camera sums [4][NC][6] (products): <= 40 KB for
-// the rig (79 extrinsics, 16 intrinsics), so 4 blocks of 256 fit a CU
-static size_t mf_lds_doubles(int E, int NI, int NC, bool product) {
-  return 30 * (size_t)E + 6 * (size_t)NI + 6 * (size_t)NC + (product ? (kMfBlock / 64) * 6 * (size_t)NC : 0);
-}
-
-// The products never materialise a Jacobian row. With A = d r / d P (2x3) of the
-// projection, Q = P2 (arc∘ring) or X, and the tables' R, Rd, Jd of the arc (a) and ring (r)
-// extrinsics, the directional forms (rows of obs_rows contracted analytically) are
-//   J_c0 d = A (-Rd_a (Q x (Jd_a dw_a)) + dt_a)            J_c1 d = A R_a (-Rd_r (X x (Jd_r dw_r)) + dt_r)
-//   J_c0^T z = [Jd_a^T (Q x (Rd_a^T g)); g], g = A^T z      J_c1^T z = [Jd_r^T (X x (Rd_r^T h)); h], h = R_a^T g
-//   J_p^T u = R_r^T R_a^T A^T u                            J_p u_p = A R_a R_r u_p     (R_r: arc∘ring only)
-// ~80 fp64 operations per observation and sweep after the projection, against ~200 to
-// build the rows (and ~70 fewer live registers).
-struct MfGeo {
-  double A0[3], A1[3];  // d (ru, rv) / d P
-  double Q[3];          // the point the arc / single rotation acts on
-  double R[9];          // R of ext0 (arc / single)
-  bool comp;
-};
-__device__ __forceinline__ void mf_geo(const int4 id, const double2 xy, const double (&X)[3], const SmallTabs& tb,
-                                       MfGeo& g) {
-  g.comp = id.z >= 0;
-  double A[12];
-  tb.rt(id.y, A);
-  double Kr[6];
-  tb.k(id.w, Kr);
-  if (g.comp) {
-    double B[12];
-    tb.rt(id.z, B);
-    matvec_add(B, X, B + 9, g.Q);
-  } else {
-    g.Q[0] = X[0];
-    g.Q[1] = X[1];
-    g.Q[2] = X[2];
-  }
-  double P[3];
-  matvec_add(A, g.Q, A + 9, P);
-  Proj pr;
-  project(P, Kr, xy.x, xy.y, pr, true);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    g.A0[i] = pr.A0[i];
-    g.A1[i] = pr.A1[i];
-  }
-#pragma unroll
-  for (int i = 0; i < 9; ++i) g.R[i] = A[i];
-}
 __device__ __forceinline__ void mv3(const double* __restrict__ M, const double (&x)[3], double (&o)[3]) {
   o[0] = M[0] * x[0] + M[1] * x[1] + M[2] * x[2];
   o[1] = M[3] * x[0] + M[4] * x[1] + M[5] * x[2];
@@ -3346,190 +3298,14 @@ __device__ __forceinline__ void cross3(const double (&a)[3], const double (&b)[3
   o[1] = a[2] * b[0] - a[0] * b[2];
   o[2] = a[0] * b[1] - a[1] * b[0];
 }
-// dP of one camera slot along d = (dw, dt): -Rd (Y x (Jd dw)) + dt, tables D = Rd | Jd
-__device__ __forceinline__ void mf_dp(const double* __restrict__ D, const double (&Y)[3], const double* __restrict__ d,
-                                      double (&o)[3]) {
-  const double dw[3] = {d[0], d[1], d[2]};
-  double y[3], c[3], r[3];
-  mv3(D + 9, dw, y);
-  cross3(Y, y, c);
-  mv3(D, c, r);
-  o[0] = d[3] - r[0];
-  o[1] = d[4] - r[1];
-  o[2] = d[5] - r[2];
-}
-// J_c^T of one slot applied to the 3-vector g (= A^T z, or R_a^T A^T z for the ring):
-// out[0..2] = Jd^T (Y x (Rd^T g)), out[3..5] = g
-__device__ __forceinline__ void mf_jct(const double* __restrict__ D, const double (&Y)[3], const double (&g)[3],
-                                       double (&out)[6]) {
-  double d[3], c[3], w[3];
-  mtv3(D, g, d);
-  cross3(Y, d, c);
-  mtv3(D + 9, c, w);
-  out[0] = w[0];
-  out[1] = w[1];
-  out[2] = w[2];
-  out[3] = g[0];
-  out[4] = g[1];
-  out[5] = g[2];
-}
-
-// MODE 0: product (vec = p) -> partial[block][6 NC]; MODE 1: back substitution (vec = y_c)
-// -> dp[3][NP] = -PU_p (q_p - t_p), the Y-free form of k_backsub; MODE 2: the Schur rhs
-// part -sum_e Y_e q_p (sweep 2 with u_p = PU_p q_p) -> partial[block][6 NC]
-template <int MODE>
-__global__ __launch_bounds__(kMfBlock, 4) void k_mf_points(DevView v, const double* __restrict__ points,
-                                                        const double* __restrict__ camtab,
-                                                        const double* __restrict__ scc,
-                                                        const double* __restrict__ PU,
-                                                        const double* __restrict__ vec,
-                                                        const double* __restrict__ q, double* __restrict__ out,
-                                                        const PcgState* st) {
-  extern __shared__ double mf_lds[];
-  if (MODE == 0 && st->status != kPcgRunning) return;
-  const int NC6 = 6 * v.NC;
-  const SmallTabs tabs = stage_small_tabs(mf_lds, v.E, v.NI, camtab, v.intr);
-  double* sv = mf_lds + 30 * (size_t)v.E + 6 * (size_t)v.NI;  // s_c o vec [NC][6]
-  double* accs = sv + NC6;                                       // [waves][NC][6] (MODE 0, 2)
-  const double* __restrict__ s_c = scc;                          // L1-resident
-  if constexpr (MODE != 2)
-    for (int i = threadIdx.x; i < NC6; i += blockDim.x) sv[i] = scc[i] * vec[i];
-  if constexpr (MODE != 1)
-    for (int i = threadIdx.x; i < (kMfBlock / 64) * NC6; i += blockDim.x) accs[i] = 0.0;
-  __syncthreads();
-  double* acc = accs + (threadIdx.x >> 6) * NC6;
-  const size_t NPs = (size_t)v.NP;
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < v.NP; p += gridDim.x * blockDim.x) {
-    const int sl = p >> 6, lane = p & 63;
-    const int off = v.slice_off[sl], len = (v.slice_off[sl + 1] - off) >> 6;
-    const double X[3] = {points[3 * (size_t)p], points[3 * (size_t)p + 1], points[3 * (size_t)p + 2]};
-    double pu[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) pu[k] = PU[6 * (size_t)p + k];
-    double up[3];
-    if constexpr (MODE == 2) {
-      const double q0 = q[4 * (size_t)p], q1 = q[4 * (size_t)p + 1], q2 = q[4 * (size_t)p + 2];
-      up[0] = pu[0] * q0 + pu[1] * q1 + pu[2] * q2;
-      up[1] = pu[3] * q1 + pu[4] * q2;
-      up[2] = pu[5] * q2;
-    } else {
-      // sweep 1: a = sum_e J_p^T (J_c (s_c o v_c))
-      double a[3] = {0.0, 0.0, 0.0};
-      for (int k = 0; k < len; ++k) {
-        const int s = off + 64 * k + lane;
-        const int4 id = v.obs_idx[s];
-        if (id.x < 0) continue;
-        const int c0 = v.ext_col[id.y], c1 = id.z >= 0 ? v.ext_col[id.z] : -1;
-        if (c0 < 0 && c1 < 0) continue;
-        MfGeo g;
-        mf_geo(id, v.obs_xy[s], X, tabs, g);
-        double dP[3] = {0.0, 0.0, 0.0};
-        if (c0 >= 0) {
-          double D[18];
-          tabs.dj(id.y, D);
-          mf_dp(D, g.Q, sv + 6 * c0, dP);
-        }
-        if (c1 >= 0) {
-          double D[18], d2[3], r2[3];
-          tabs.dj(id.z, D);
-          mf_dp(D, X, sv + 6 * c1, d2);
-          mv3(g.R, d2, r2);
-          dP[0] += r2[0];
-          dP[1] += r2[1];
-          dP[2] += r2[2];
-        }
-        const double u0 = g.A0[0] * dP[0] + g.A0[1] * dP[1] + g.A0[2] * dP[2];
-        const double u1 = g.A1[0] * dP[0] + g.A1[1] * dP[1] + g.A1[2] * dP[2];
-        const double au[3] = {u0 * g.A0[0] + u1 * g.A1[0], u0 * g.A0[1] + u1 * g.A1[1], u0 * g.A0[2] + u1 * g.A1[2]};
-        double h[3];
-        mtv3(g.R, au, h);
-        if (g.comp) {
-          double B[12], h2[3];
-          tabs.rt(id.z, B);
-          mtv3(B, h, h2);
-          h[0] = h2[0];
-          h[1] = h2[1];
-          h[2] = h2[2];
-        }
-        a[0] += h[0];
-        a[1] += h[1];
-        a[2] += h[2];
-      }
-      // t = PU^T a (PU upper triangular: 00 01 02 11 12 22)
-      const double t0 = pu[0] * a[0], t1 = pu[1] * a[0] + pu[3] * a[1];
-      const double t2 = pu[2] * a[0] + pu[4] * a[1] + pu[5] * a[2];
-      if constexpr (MODE == 1) {
-        const double r0 = q[4 * (size_t)p] - t0, r1 = q[4 * (size_t)p + 1] - t1, r2 = q[4 * (size_t)p + 2] - t2;
-        out[p] = -(pu[0] * r0 + pu[1] * r1 + pu[2] * r2);
-        out[NPs + p] = -(pu[3] * r1 + pu[4] * r2);
-        out[2 * NPs + p] = -(pu[5] * r2);
-        continue;
-      }
-      up[0] = pu[0] * t0 + pu[1] * t1 + pu[2] * t2;
-      up[1] = pu[3] * t1 + pu[4] * t2;
-      up[2] = pu[5] * t2;
-    }
-    if constexpr (MODE != 1) {
-      // sweep 2: w_c -= s_c o J_c^T (J_p u_p)
-      for (int k = 0; k < len; ++k) {
-        const int s = off + 64 * k + lane;
-        const int4 id = v.obs_idx[s];
-        if (id.x < 0) continue;
-        const int c0 = v.ext_col[id.y], c1 = id.z >= 0 ? v.ext_col[id.z] : -1;
-        if (c0 < 0 && c1 < 0) continue;
-        MfGeo g;
-        mf_geo(id, v.obs_xy[s], X, tabs, g);
-        double m[3], kk[3];
-        if (g.comp) {
-          double B[12];
-          tabs.rt(id.z, B);
-          mv3(B, up, kk);
-        } else {
-          kk[0] = up[0];
-          kk[1] = up[1];
-          kk[2] = up[2];
-        }
-        mv3(g.R, kk, m);
-        const double z0 = g.A0[0] * m[0] + g.A0[1] * m[1] + g.A0[2] * m[2];
-        const double z1 = g.A1[0] * m[0] + g.A1[1] * m[1] + g.A1[2] * m[2];
-        const double gz[3] = {z0 * g.A0[0] + z1 * g.A1[0], z0 * g.A0[1] + z1 * g.A1[1], z0 * g.A0[2] + z1 * g.A1[2]};
-        if (c0 >= 0) {
-          double D[18], o[6];
-          tabs.dj(id.y, D);
-          mf_jct(D, g.Q, gz, o);
-#pragma unroll
-          for (int a = 0; a < 6; ++a) atomicAdd(acc + 6 * c0 + a, -s_c[6 * c0 + a] * o[a]);
-        }
-        if (c1 >= 0) {
-          double D[18], hz[3], o[6];
-          tabs.dj(id.z, D);
-          mtv3(g.R, gz, hz);
-          mf_jct(D, X, hz, o);
-#pragma unroll
-          for (int a = 0; a < 6; ++a) atomicAdd(acc + 6 * c1 + a, -s_c[6 * c1 + a] * o[a]);
-        }
-      }
-    }
-  }
-  if constexpr (MODE != 1) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < NC6; i += blockDim.x) {
-      double x = accs[i];
-#pragma unroll
-      for (int w = 1; w < kMfBlock / 64; ++w) x += accs[w * NC6 + i];
-      out[(size_t)blockIdx.x * NC6 + i] = x;
-    }
-  }
-}
-
 // The same products in the rotated frame. With J_l = Rd Jd (the left Jacobian; Rd = R, or
 // I for the small-angle tables) and Z = Rd Y (= P - t, or Y itself for the small-angle
 // tables), Rd (Y x (Jd dw)) = Z x (J_l dw) and Jd^T (Y x (Rd^T g)) = J_l^T (Z x g), so
 //   J_c0 d = A (dt_a - Z_a x w~_a)      w~ = J_l dw: one 3-vector per camera and product
 //   J_c0^T z = [J_l^T (Z_a x g); g]     J_l^T applied once per camera to the summed [Z x g]
 // (ring slot: Z_r = Q - t_r or X, and R_a as before). Per observation and sweep the rows
-// need only R, t (and K) from LDS: the 18 Rd | Jd doubles per slot of k_mf_points, the
-// s_c reads and the 3 x 3 products with them drop out. LDS: rt [E][12] | small-angle
+// need only R, t (and K) from LDS: the 18 Rd | Jd doubles per slot of the directional
+// (Rd | Jd) form, the s_c reads and the 3 x 3 products with them drop out. LDS: rt [E][12] | small-angle
 // flags [E] | w~, dt per camera [NC][6] | J_l per camera [NC][9] | per-wave sums [4][NC][6].
 // R | t rows of 14 doubles (12 used): 112 B = 28 banks apart, so the 16-B reads of 16
 // different cameras fall in 16 disjoint bank quads (a 12-double row gives only 8)
@@ -3843,10 +3619,9 @@ static size_t mf32_lds_bytes(int E, int NI, int NC) {
   return sizeof(double) * (9 * (size_t)NC + (kMfBlock / 64) * 6 * (size_t)(NC | 1)) +
          sizeof(float) * (12 * (size_t)E + 4 * (size_t)NI + 6 * (size_t)NC) + 2 * sizeof(int) * (size_t)E;
 }
-// ACC: 0 = fp64 per-wave LDS sums; 2 = no camera sums (ablation, wrong result: DAB_MF32_ACC=2
-// measures what the LDS atomics cost). Measured and dropped: fp32 LDS sums (3x slower) and a
-// copy of the sums per half wave (no gain: the atomics are not bank-conflict bound)
-template <int ACC>
+// The camera sums: fp64 per-wave LDS atomics (round 3: without them the kernel took 81.5
+// against 163.6 us; measured and dropped: fp32 LDS sums, 3x slower, and a copy of the sums
+// per half wave, no gain: the atomics are not bank-conflict bound)
 __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame32(DevView v, const double* __restrict__ points,
                                                          const double* __restrict__ camtab,
                                                          const double* __restrict__ scc,
@@ -3899,8 +3674,7 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame32(DevView v, const dou
   __syncthreads();
   double* acc = accs + (threadIdx.x >> 6) * 6 * NCP;
   auto add = [&](int c, int a, float x) {
-    if constexpr (ACC == 0) atomicAdd(acc + a * NCP + c, (double)x);  // fp64 per-wave sums
-    else if (x == 1234.5f) acc[0] = x;  // keep the arithmetic alive
+    atomicAdd(acc + a * NCP + c, (double)x);  // fp64 per-wave sums
   };
   auto sum_of = [&](int c, int a) {  // fixed order over the waves
     double t = accs[a * NCP + c];
@@ -4146,50 +3920,204 @@ __global__ __launch_bounds__(256) void k_mf_diag_rhs(DevView v, int nchunk, cons
   }
 }
 
-int mf_grid(int NP, int ncu) { return std::max(1, std::min((NP + kMfBlock - 1) / kMfBlock, 4 * ncu)); }
-static bool mf_rd_jd_form() {  // DAB_MF_RDJD=1: the Rd | Jd form (k_mf_points), for A/B timing
-  static const bool f = getenv("DAB_MF_RDJD") && atoi(getenv("DAB_MF_RDJD")) != 0;
-  return f;
+// k_mf_diag_rhs in the rotated frame (as k_mf_frame): a row of J_c is D w with
+// D = blockdiag(J_l^T, I) constant per camera and w = [Z x a | a] (slot 0: the projection
+// row a, Z = P - t_a or Q on small-angle tables; slot 1: a R_a in place of a, Z = Q - t_b or
+// X), so a run's W = D W~ with W~ = sum of w j_p^T, its y = s o (D W~ PU) and
+//   sum y y^T = S D (sum Y~ Y~^T) D^T S,   -sum y q = -S D (sum Y~ q),   Y~ = W~ PU:
+// the loop sums Y~ Y~^T and Y~ q (27) in the frame, and the chunk's J_l and s_c are applied
+// once to the sums (cam_frame_entry). Per entry only R, t (and K) from LDS: no Rd | Jd rows,
+// no per-row J_d products, and no s_c in the loop.
+__global__ __launch_bounds__(256) void k_mf_diag_frame(DevView v, int nchunk, const int* __restrict__ run_beg,
+                                                       const int4* __restrict__ run_rec,
+                                                       const double* __restrict__ points,
+                                                       const double* __restrict__ camtab,
+                                                       const double* __restrict__ scc, const double* __restrict__ PU,
+                                                       const double* __restrict__ q, double* __restrict__ partial) {
+  extern __shared__ double mf_lds[];
+  double* rt_s = mf_lds;                         // [E][kRtStride]: R | t
+  double* k_s = rt_s + kRtStride * (size_t)v.E;  // [NI][6]
+  double* jl_s = k_s + 6 * (size_t)v.NI;        // [NC][9]: J_l per camera column
+  int* sm_s = reinterpret_cast<int*>(jl_s + 9 * (size_t)v.NC);  // [E] small-angle tables
+  __shared__ double wsum[kRedBlock / 64][27];
+  for (int i = threadIdx.x; i < 12 * v.E; i += blockDim.x)
+    rt_s[kRtStride * (i / 12) + i % 12] = camtab[(size_t)kCamTab * (i / 12) + i % 12];
+  for (int i = threadIdx.x; i < 6 * v.NI; i += blockDim.x) k_s[i] = v.intr[(size_t)kIntr * (i / 6) + i % 6];
+  for (int e = threadIdx.x; e < v.E; e += blockDim.x) {
+    const double* T = camtab + (size_t)kCamTab * e;
+    sm_s[e] = (T[12] == 1.0 && T[13] == 0.0 && T[14] == 0.0 && T[15] == 0.0 && T[16] == 1.0 && T[17] == 0.0 &&
+               T[18] == 0.0 && T[19] == 0.0 && T[20] == 1.0)
+                  ? 1
+                  : 0;
+    const int c = v.ext_col[e];
+    if (c < 0) continue;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc)
+        jl_s[9 * c + 3 * r + cc] =
+            T[12 + 3 * r] * T[21 + cc] + T[12 + 3 * r + 1] * T[24 + cc] + T[12 + 3 * r + 2] * T[27 + cc];
+  }
+  __syncthreads();
+  const SmallTabs tabs{nullptr, k_s};
+  auto rt = [&](int e, double (&o)[12]) {
+    const double2* pp = reinterpret_cast<const double2*>(rt_s + kRtStride * e);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const double2 u = pp[k];
+      o[2 * k] = u.x;
+      o[2 * k + 1] = u.y;
+    }
+  };
+  for (int c = blockIdx.x; c < nchunk; c += gridDim.x) {
+    const int b = run_beg[c], e = run_beg[c + 1];
+    const int cam = b < e ? __builtin_amdgcn_readfirstlane(run_rec[b].w) : 0;  // the chunk's camera column
+    double acc[27];
+#pragma unroll
+    for (int i = 0; i < 27; ++i) acc[i] = 0.0;
+    for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
+      const int4 rr = run_rec[k];
+      const int i = rr.x, len = rr.y, p = rr.z;
+      const double X[3] = {points[3 * (size_t)p], points[3 * (size_t)p + 1], points[3 * (size_t)p + 2]};
+      const double* pu = PU + 6 * (size_t)p;
+      const double u00 = pu[0], u01 = pu[1], u02 = pu[2], u11 = pu[3], u12 = pu[4], u22 = pu[5];
+      const double q0 = q[4 * (size_t)p], q1 = q[4 * (size_t)p + 1], q2 = q[4 * (size_t)p + 2];
+      double y[18];  // W~ (6 x 3), then Y~ = W~ PU in place
+#pragma unroll
+      for (int t = 0; t < 18; ++t) y[t] = 0.0;
+      for (int j = 0; j < len; ++j) {
+        int4 id = v.cm_idx[i + j];
+        const bool slot1 = (id.w & kSlotBit) != 0;
+        id.w &= ~kSlotBit;
+        const bool comp = id.z >= 0;
+        double Ta[12], Kr[6], Qp[3], Zb[3], Rb[9];
+        rt(id.y, Ta);
+        tabs.k(id.w, Kr);
+        if (comp) {
+          double Tb[12];
+          rt(id.z, Tb);
+          matvec_add(Tb, X, Tb + 9, Qp);
+          const bool sb = sm_s[id.z] != 0;
+#pragma unroll
+          for (int t = 0; t < 3; ++t) Zb[t] = sb ? X[t] : Qp[t] - Tb[9 + t];
+#pragma unroll
+          for (int t = 0; t < 9; ++t) Rb[t] = Tb[t];
+        } else {
+#pragma unroll
+          for (int t = 0; t < 3; ++t) Qp[t] = Zb[t] = X[t];
+        }
+        double P[3];
+        matvec_add(Ta, Qp, Ta + 9, P);
+        const bool sa = sm_s[id.y] != 0;
+        double Z[3];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) Z[t] = slot1 ? Zb[t] : (sa ? Qp[t] : P[t] - Ta[9 + t]);
+        Proj pr;
+        project(P, Kr, 0.0, 0.0, pr, true);
+#pragma unroll
+        for (int row = 0; row < 2; ++row) {
+          const double* a = row == 0 ? pr.A0 : pr.A1;
+          const double ar[3] = {a[0], a[1], a[2]};
+          double ja[3];  // a R_a
+          mtv3(Ta, ar, ja);
+          double jp[3];  // j_p = a R_a R_b (or a R_a)
+          if (comp) {
+            mtv3(Rb, ja, jp);
+          } else {
+#pragma unroll
+            for (int t = 0; t < 3; ++t) jp[t] = ja[t];
+          }
+          double g[3];
+#pragma unroll
+          for (int t = 0; t < 3; ++t) g[t] = slot1 ? ja[t] : ar[t];
+          double w[6];
+          cross3(Z, g, *reinterpret_cast<double(*)[3]>(w));
+#pragma unroll
+          for (int t = 0; t < 3; ++t) w[3 + t] = g[t];
+#pragma unroll
+          for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int t = 0; t < 3; ++t) y[3 * r + t] = fma(w[r], jp[t], y[3 * r + t]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {  // Y~ = W~ PU, PU upper triangular (00 01 02 11 12 22)
+        const double w0 = y[3 * r], w1 = y[3 * r + 1], w2 = y[3 * r + 2];
+        y[3 * r] = w0 * u00;
+        y[3 * r + 1] = w0 * u01 + w1 * u11;
+        y[3 * r + 2] = w0 * u02 + w1 * u12 + w2 * u22;
+      }
+#pragma unroll
+      for (int a = 0; a < 6; ++a) acc[21 + a] -= y[3 * a] * q0 + y[3 * a + 1] * q1 + y[3 * a + 2] * q2;
+      int t = 0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int bb = a; bb < 6; ++bb)
+          acc[t++] += y[3 * a] * y[3 * bb] + y[3 * a + 1] * y[3 * bb + 1] + y[3 * a + 2] * y[3 * bb + 2];
+    }
+    wave_sums_transposed<27>(acc, wsum[threadIdx.x >> 6]);
+    __syncthreads();
+    if (threadIdx.x < 27) {
+      double t = wsum[0][threadIdx.x];
+#pragma unroll
+      for (int w = 1; w < kRedBlock / 64; ++w) t += wsum[w][threadIdx.x];
+      wsum[0][threadIdx.x] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < 27) {
+      const int k = threadIdx.x;
+      int ia = 0, ib = 0;  // the entry's (row, column), or (row, -) of the 6 q terms
+      if (k >= 21) {
+        ia = k - 21;
+      } else {
+        int r = k;
+        while (r >= 6 - ia) {
+          r -= 6 - ia;
+          ++ia;
+        }
+        ib = ia + r;
+      }
+      const double f = k >= 21 ? scc[6 * cam + ia] : scc[6 * cam + ia] * scc[6 * cam + ib];
+      partial[27 * (size_t)c + k] = f * cam_frame_entry(wsum[0], jl_s + 9 * cam, k);
+    }
+    __syncthreads();  // wsum is reused by the next chunk
+  }
 }
+
+int mf_grid(int NP, int ncu) { return std::max(1, std::min((NP + kMfBlock - 1) / kMfBlock, 4 * ncu)); }
 void launch_mf_product(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                        const double* scale_c, const double* PU, const double* vec, double* partial, double* w,
                        int grid, const PcgState* st) {
-  if (mf_rd_jd_form()) {
-    const size_t lds = sizeof(double) * mf_lds_doubles(v.E, v.NI, v.NC, true);
-    k_mf_points<0><<<grid, kMfBlock, lds, s>>>(v, points, camtab, scale_c, PU, vec, nullptr, partial, st);
-  } else {
-    k_mf_frame<0><<<grid, kMfBlock, mf2_lds_bytes(v.E, v.NI, v.NC, true), s>>>(v, points, camtab, scale_c, PU, vec,
-                                                                              nullptr, partial, st);
-  }
+  k_mf_frame<0><<<grid, kMfBlock, mf2_lds_bytes(v.E, v.NI, v.NC, true), s>>>(v, points, camtab, scale_c, PU, vec,
+                                                                            nullptr, partial, st);
   if (w) launch_pcg_fused_final(s, grid, 6 * v.NC, partial, w, st);
 }
 void launch_mf_product32(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                          const double* scale_c, const double* PU, const double* vec, double* partial, double* w,
                          int grid, const PcgState* st) {
-  static const int acc = getenv("DAB_MF32_ACC") ? atoi(getenv("DAB_MF32_ACC")) : 0;
-  if (acc == 2)
-    k_mf_frame32<2><<<grid, kMfBlock, mf32_lds_bytes(v.E, v.NI, v.NC), s>>>(v, points, camtab, scale_c, PU, vec,
-                                                                           partial, st);
-  else
-    k_mf_frame32<0><<<grid, kMfBlock, mf32_lds_bytes(v.E, v.NI, v.NC), s>>>(v, points, camtab, scale_c, PU, vec,
-                                                                           partial, st);
+  k_mf_frame32<<<grid, kMfBlock, mf32_lds_bytes(v.E, v.NI, v.NC), s>>>(v, points, camtab, scale_c, PU, vec, partial,
+                                                                      st);
   if (w) launch_pcg_fused_final(s, grid, 6 * v.NC, partial, w, st);
 }
 void launch_mf_backsub(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                        const double* scale_c, const double* PU, const double* q, const double* yc, double* dp,
                        int grid) {
-  if (mf_rd_jd_form()) {
-    const size_t lds = sizeof(double) * mf_lds_doubles(v.E, v.NI, v.NC, false);
-    k_mf_points<1><<<grid, kMfBlock, lds, s>>>(v, points, camtab, scale_c, PU, yc, q, dp, nullptr);
-  } else {
-    k_mf_frame<1><<<grid, kMfBlock, mf2_lds_bytes(v.E, v.NI, v.NC, false), s>>>(v, points, camtab, scale_c, PU, yc,
-                                                                               q, dp, nullptr);
-  }
+  k_mf_frame<1><<<grid, kMfBlock, mf2_lds_bytes(v.E, v.NI, v.NC, false), s>>>(v, points, camtab, scale_c, PU, yc, q,
+                                                                             dp, nullptr);
 }
 void launch_mf_diag_rhs(hipStream_t s, const DevView& v, int nchunk, const int* run_beg, const int4* run_rec,
                         const double* points, const double* camtab, const double* scale_c, const double* PU,
                         const double* q, double* partial) {
   if (nchunk <= 0) return;
+  static const int form = getenv("DAB_MF_DIAG") ? atoi(getenv("DAB_MF_DIAG")) : 1;
+  if (form == 1) {
+    const size_t lds =
+        sizeof(double) * (kRtStride * (size_t)v.E + 6 * (size_t)v.NI + 9 * (size_t)v.NC) + sizeof(int) * (size_t)v.E;
+    k_mf_diag_frame<<<std::min(nchunk, kSmallGrid), 256, lds, s>>>(v, nchunk, run_beg, run_rec, points, camtab,
+                                                                   scale_c, PU, q, partial);
+    return;
+  }
   const size_t lds = small_tabs_bytes(v.E, v.NI);
   // persistent blocks: the 20-KB tables are staged once per block, not once per chunk
   k_mf_diag_rhs<<<std::min(nchunk, kSmallGrid), 256, lds, s>>>(v, nchunk, run_beg, run_rec, points, camtab, scale_c,
@@ -4487,14 +4415,10 @@ __global__ __launch_bounds__(256) void k_candidate_frame(DevView v, const double
 void launch_candidate(hipStream_t s, const DevView& v, const double* points, const double* camtab,
                       const double* delta_p, const double* delta_c, const double* camtab_c, double* partial,
                       int grid) {
-  static const bool rows = getenv("DAB_CAND_ROWS") && atoi(getenv("DAB_CAND_ROWS")) != 0;  // A/B: row form
-  if (small_tabs_fit(v.E, v.NI) && !rows) {
+  if (small_tabs_fit(v.E, v.NI)) {
     const size_t lds = sizeof(double) * (2 * kRtStride * (size_t)v.E + 6 * (size_t)v.NI + 6 * (size_t)v.NC) +
                        sizeof(int) * (size_t)v.E;
     k_candidate_frame<<<grid, 256, lds, s>>>(v, points, camtab, delta_p, delta_c, camtab_c, partial);
-  } else if (small_tabs_fit(v.E, v.NI)) {
-    const size_t lds = small_tabs_bytes(v.E, v.NI) + sizeof(double) * 30 * (size_t)v.E;
-    k_candidate<true><<<grid, 256, lds, s>>>(v, points, camtab, delta_p, delta_c, camtab_c, partial);
   } else {
     k_candidate<false><<<grid, 256, 0, s>>>(v, points, camtab, delta_p, delta_c, camtab_c, partial);
   }

@@ -146,7 +146,6 @@ double now_s() {
 int setup_threads() {
   static const int t = [] {
     int n = (int)std::thread::hardware_concurrency();
-    if (const char* e = getenv("DAB_SETUP_THREADS")) n = atoi(e);
     return std::max(1, std::min(n, 16));
   }();
   return t;
@@ -288,7 +287,6 @@ struct Knobs {
   int xchunk = 0;           // DAB_XCHUNK: most entries per pair-major chunk (0: kPairChunk)
   int pair_eval = -1;       // DAB_PAIR_EVAL=0: rig camera side camera-major + cross passes
   int eval_wps = INT_MIN;   // DAB_EVAL_WPS: point-kernel variant of the two-kernel pass
-  int free_cus = 8;         // DAB_EVAL_FREE_CUS: CUs the multi-rank point kernel leaves free
   int eval_fused = 1;       // DAB_EVAL_FUSED=0: two-kernel pass even where the fused one fits
   int eval_split = 0;       // DAB_EVAL_SPLIT=1: the multi-rank split schedule on one rank
   int pcg_fused = 1;        // DAB_PCG_FUSED=0
@@ -300,6 +298,7 @@ struct Knobs {
   int p2p = -1;             // DAB_P2P: one-shot xGMI all-reduce of small sums (-1 auto: RCCL handles
                             // only; 1 also on host-staged handles, the one-GPU rehearsal; 0 off)
   int setup_host = 0;       // DAB_SETUP_HOST=1: dab_set_problem's host passes instead of the device ones
+  int fused_grid = 0;       // DAB_FUSED_GRID (experiment): work-groups of the single fused launch (0: one per CU)
   int eval_side = 0;        // DAB_EVAL_SIDE (timing ablation, wrong results): k_eval_bal's single launch runs
                             // 1 the point side only, 2 the camera side only, 3 the tables only, 4 no
                             // tables or frames, 5 no point tables, 6 no camera frames
@@ -315,7 +314,6 @@ struct Knobs {
     get("DAB_XCHUNK", xchunk);
     get("DAB_PAIR_EVAL", pair_eval);
     get("DAB_EVAL_WPS", eval_wps);
-    get("DAB_EVAL_FREE_CUS", free_cus);
     get("DAB_EVAL_FUSED", eval_fused);
     get("DAB_EVAL_SPLIT", eval_split);
     get("DAB_PCG_FUSED", pcg_fused);
@@ -328,6 +326,7 @@ struct Knobs {
     get("DAB_FUSED_TAB", fused_tab);
     get("DAB_SETUP_HOST", setup_host);
     get("DAB_EVAL_SIDE", eval_side);
+    get("DAB_FUSED_GRID", fused_grid);
   }
 };
 
@@ -1484,12 +1483,11 @@ static int setup_buffers(dab_handle* h, const std::function<void(const char*)>& 
     // On several ranks the camera blocks' RCCL all-reduce runs during the point kernel. The
     // persistent point kernel (one 1024-thread, ~147-KB-LDS work-group per CU) would fill
     // every CU and hold the RCCL kernels off until it ends, so it leaves one CU per XCD
-    // free for them (DAB_EVAL_FREE_CUS overrides; its slices are dealt round robin over
-    // whatever grid it gets).
+    // free for them (its slices are dealt round robin over whatever grid it gets).
     int pcus = ncu;
     // (a one-rank RCCL handle keeps the full grid: the same work-group partition, hence
     // bitwise the same sums, as dab_create)
-    if (h->world > 1 && h->eval_wps <= 0) pcus = std::max(1, ncu - h->knobs.free_cus);
+    if (h->world > 1 && h->eval_wps <= 0) pcus = std::max(1, ncu - 8);
     h->eval_grid = h->eval_wps <= 0 ? std::max(1, std::min(pcus, h->nslice)) : std::max(1, h->nslice);
     h->fused = h->knobs.eval_fused != 0;
     h->fused_split = h->coll() || h->knobs.eval_split != 0;  // the split schedule on one rank too (tests)
@@ -2820,7 +2818,9 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
                     h->ug(), h->cost_fx(h->fx_last), h->cost_fx(h->fx_last ^ 1), h->xerr(), grid, side);
   };
   if (h->fused && !h->fused_split) {  // both halves of the pass in one launch
-    eval_fused(h->ncu, h->knobs.eval_side);
+    int grid = h->ncu;
+    if (h->knobs.fused_grid > 0 && (long long)h->NC <= 4LL * h->knobs.fused_grid) grid = std::min(grid, h->knobs.fused_grid);
+    eval_fused(grid, h->knobs.eval_side);
     if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
     if (h->NC > 0) CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
     return 0;
