@@ -64,3 +64,23 @@ if os.environ.get("DAB_TRACE_PER_WAVE"):
     print("per logical wave: median staged / loop end / exit (us)")
     for w in range(16):
         print(f"  wave {w:2d}: " + " ".join(f"{np.nanmedian(rel[:, w, k]):6.2f}" for k in (1, 2, 3)))
+if os.environ.get("DAB_TRACE_PER_WG"):
+    # the tail: which work-groups end last, and does their lateness come from a late start
+    # (dispatch) or from a slow run? Per work-group: first entry, last exit, by XCD (b % 8)
+    t = runs[-1]
+    have = t[:, :, 0] > 0
+    t0 = t[:, :, 0][have].min()
+    rel = np.where(t > 0, (t - t0) * 0.01, np.nan)
+    ent = np.nanmin(rel[:, :, 0], axis=1)
+    ext_ = np.nanmax(rel[:, :, 3], axis=1)
+    dur = ext_ - ent
+    print("per work-group: entry / exit / duration percentiles 0/10/50/90/100 (us)")
+    for name, a in (("entry", ent), ("exit", ext_), ("duration", dur)):
+        print(f"  {name:8s} " + " ".join(f"{v:6.2f}" for v in np.nanpercentile(a, [0, 10, 50, 90, 100])))
+    print(f"  corr(entry, exit) {np.corrcoef(ent[have.any(axis=1)], ext_[have.any(axis=1)])[0, 1]:.2f}")
+    for x in range(8):
+        sel = np.arange(256) % 8 == x
+        print(f"  XCD {x}: entry median {np.nanmedian(ent[sel]):5.2f}  exit median {np.nanmedian(ext_[sel]):5.2f}  "
+              f"max {np.nanmax(ext_[sel]):5.2f}")
+    last = np.argsort(-np.nan_to_num(ext_, nan=-1))[:12]
+    print("  last 12 work-groups (block: entry exit):", " ".join(f"{b}:{ent[b]:.1f}/{ext_[b]:.1f}" for b in last))

@@ -155,3 +155,30 @@ def test_filter_then_resolve_matches_fresh(pkg, gpu):
         f.close()
     assert [it["cost"] for it in a["iterations"]] == [it["cost"] for it in b["iterations"]]
     np.testing.assert_array_equal(q.points, q_fresh.points)
+
+
+def test_release_caches_between_handles(pkg, gpu):
+    """dab_release_caches (round 5): with one handle alive and after it is destroyed, the
+    cached streams and pinned blocks are dropped; handles created afterwards take fresh ones
+    and give bitwise the same trajectory."""
+    prob = pkg.synth(kind=0, num_cameras=20, num_points=1500, obs_per_point=6, seed=85)
+    lib = pkg.load_library()
+    ex = pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR
+    s = pkg.Solver(0)
+    try:
+        ref = _solve(pkg, s, prob, ex)
+        assert lib.dab_release_caches() == 0  # a live handle keeps its own streams
+        again = _solve(pkg, s, prob, ex)
+    finally:
+        s.close()
+    assert lib.dab_release_caches() == 0
+    assert lib.dab_release_caches() == 0  # idempotent
+    s = pkg.Solver(0)
+    try:
+        got = _solve(pkg, s, prob, ex)
+    finally:
+        s.close()
+    for other in (again, got):
+        assert other[0] == ref[0]
+        np.testing.assert_array_equal(other[2], ref[2])
+        np.testing.assert_array_equal(other[3], ref[3])
