@@ -1914,10 +1914,6 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   // from work-group 0 up), and a small camera set leaves the point side's work-groups alone
   auto cam_of = [&](int slot) { return slot * (int)gridDim.x + ((int)gridDim.x - 1 - (int)blockIdx.x); };
   const int nsl = kBalCW / wpc;
-  // experiment: side & 32 — the camera waves build the upper half of the point tables
-  // (extrinsics 512..1023) during their prologue, the point waves the lower half
-  const bool cam_tabs = (side & 32) != 0;
-  side &= 31;
   if (threadIdx.x < kBalCW + kBalPW) ccount[threadIdx.x] = 0u;
   if (threadIdx.x == 0) tbar = kbar = pdone = 0u;
   if (blockIdx.x == 0 && fx_next)
@@ -1963,41 +1959,9 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     // ---------------- camera side ----------------
     const int cw = wave - kBalPW, part = cw / nsl, slot = cw - part * nsl;
     const int c = cam_of(slot);  // one round (fused_eval_fits / fused_wpc)
-    // cam_tabs: this wave's share of the point tables, loaded first, built once the first
-    // gathers are in flight (or at once when the wave has no camera)
-    const int te = kBalPW * 64 + cw * 64 + lane;
-    double tx[12];
-    const bool my_tabs = cam_tabs && side != 4 && side != 5;
-    if (my_tabs) {
-      const int ee = min(te, v.E - 1);
-      if (camtab) {
-#pragma unroll
-        for (int q = 0; q < 12; ++q) tx[q] = camtab[(size_t)kCamTab * ee + q];
-      } else {
-#pragma unroll
-        for (int q = 0; q < 6; ++q) tx[q] = ext[6 * (size_t)ee + q];
-      }
-    }
-    auto build_my_tabs = [&]() {
-      if (!cam_tabs) return;
-      if (my_tabs && te < v.E) {
-        double T[30];
-        if (camtab) {
-#pragma unroll
-          for (int q = 0; q < 12; ++q) T[q] = tx[q];
-        } else {
-          cam_table(*reinterpret_cast<const double(*)[6]>(tx), T);
-        }
-#pragma unroll
-        for (int i = 0; i < 6; ++i) reinterpret_cast<double2*>(rt_s + 12 * te)[i] = make_double2(T[2 * i], T[2 * i + 1]);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_fetch_add(&kbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
     if (cw == 0 && side != 4 && side != 6) build_frames();
     if (side == 1 || side == 3 || c >= v.NC) {  // timing ablations: 3 the tables only, 5 no point tables,
                                                  // 6 no camera frames (both sides run, wrong results)
-      build_my_tabs();
       DAB_STAMP(3);
       return;
     }
@@ -2012,7 +1976,6 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     for (int i = 0; i < 27; ++i) acc[i] = 0.0;
     const double* fr = cfr[slot];
     eval_cams_gather_f(v.cm_pt, v.cm_xy, points, lo + lane, hi, acc, [&]() {
-      build_my_tabs();
       if (side != 4 && side != 6) lds_wait_ge(&tbar, 1u, err, 1u);  // the frames, built while the first gathers fly
       const UniFrame f(UniFrame::FromShared{}, fr);
       DAB_STAMP(1);
@@ -2079,11 +2042,9 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   constexpr int kTabPer = (kLdsCams + kBalPW * 64 - 1) / (kBalPW * 64);
   double xr[kTabPer][12];  // camtab: R,t as they are; else the 6 parameters
   const bool tabs_now = side != 4 && side != 5;
-  const int ntab = cam_tabs ? 1 : kTabPer;
   if (tabs_now) {
 #pragma unroll
     for (int j = 0; j < kTabPer; ++j) {
-      if (j >= ntab) break;
       const int e = min(pw * 64 + lane + j * kBalPW * 64, v.E - 1);
       if (camtab) {
 #pragma unroll
@@ -2114,7 +2075,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
 #pragma unroll
     for (int j = 0; j < kTabPer; ++j) {
       const int e = pw * 64 + lane + j * kBalPW * 64;
-      if (e >= v.E || j >= ntab) break;
+      if (e >= v.E) break;
       double T[30];
       if (camtab) {
 #pragma unroll
@@ -2129,7 +2090,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   // barrier of the point waves only (LDS counter): own LDS writes and the K LDS-DMA retired
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_fetch_add(&kbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  lds_wait_ge(&kbar, (unsigned)(cam_tabs ? kBalPW + kBalCW : kBalPW), err, 1u);
+  lds_wait_ge(&kbar, (unsigned)kBalPW, err, 1u);
   DAB_STAMP(1);
   if (side == 2 || side == 3) return;
   const LdsTabs<true, false> tabs{rt_s, k_s, nullptr, v.intr};

@@ -298,7 +298,6 @@ struct Knobs {
   int p2p = -1;             // DAB_P2P: one-shot xGMI all-reduce of small sums (-1 auto: RCCL handles
                             // only; 1 also on host-staged handles, the one-GPU rehearsal; 0 off)
   int setup_host = 0;       // DAB_SETUP_HOST=1: dab_set_problem's host passes instead of the device ones
-  int fused_grid = 0;       // DAB_FUSED_GRID (experiment): work-groups of the single fused launch (0: one per CU)
   int eval_side = 0;        // DAB_EVAL_SIDE (timing ablation, wrong results): k_eval_bal's single launch runs
                             // 1 the point side only, 2 the camera side only, 3 the tables only, 4 no
                             // tables or frames, 5 no point tables, 6 no camera frames
@@ -326,7 +325,6 @@ struct Knobs {
     get("DAB_FUSED_TAB", fused_tab);
     get("DAB_SETUP_HOST", setup_host);
     get("DAB_EVAL_SIDE", eval_side);
-    get("DAB_FUSED_GRID", fused_grid);
   }
 };
 
@@ -2818,9 +2816,7 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
                     h->ug(), h->cost_fx(h->fx_last), h->cost_fx(h->fx_last ^ 1), h->xerr(), grid, side);
   };
   if (h->fused && !h->fused_split) {  // both halves of the pass in one launch
-    int grid = h->ncu;
-    if (h->knobs.fused_grid > 0 && (long long)h->NC <= 4LL * h->knobs.fused_grid) grid = std::min(grid, h->knobs.fused_grid);
-    eval_fused(grid, h->knobs.eval_side);
+    eval_fused(h->ncu, h->knobs.eval_side);
     if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
     if (h->NC > 0) CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
     return 0;

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import _pkgload  # noqa: E402
 
-KNOBS = ("DAB_EVAL_FUSED", "DAB_FUSED_TAB", "DAB_EVAL_SIDE", "DAB_EVAL_SPLIT", "DAB_FUSED_GRID")
+KNOBS = ("DAB_EVAL_FUSED", "DAB_FUSED_TAB", "DAB_EVAL_SIDE", "DAB_EVAL_SPLIT")
 
 
 DEFAULT_LIB = []
