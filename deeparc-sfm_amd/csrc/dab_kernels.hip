@@ -31,18 +31,27 @@ namespace dab {
 
 #ifdef DAB_TRACE
 // timing build only (scripts/trace_fused.sh): per-wave s_memrealtime stamps (100 MHz)
-__device__ unsigned long long g_trace[256 * 16 * 4];
+__device__ unsigned long long g_trace[256 * 16 * 8];
 #define DAB_STAMP(k)                                                                        \
   do {                                                                                      \
     const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                          \
-    if (lane == 0 && blockIdx.x < 256) g_trace[(blockIdx.x * 16 + wave) * 4 + (k)] = t_;     \
+    if (lane == 0 && blockIdx.x < 256) g_trace[(blockIdx.x * 16 + wave) * 8 + (k)] = t_;     \
   } while (0)
 #define DAB_STAMP_ANY(k)                                                                                     \
   do {                                                                                                       \
     const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                           \
-    if ((threadIdx.x & 63) == 0 && blockIdx.x < 256) g_trace[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 4 + (k)] = t_; \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 256) g_trace[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + (k)] = t_; \
+  } while (0)
+// a stamp once every load in flight has returned (prologue hops; perturbs the schedule a little)
+#define DAB_STAMP_HOP(k)                                   \
+  do {                                                     \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+    DAB_STAMP_ANY(k);                                      \
   } while (0)
 #else
+#define DAB_STAMP_HOP(k) \
+  do {                   \
+  } while (0)
 #define DAB_STAMP_ANY(k) \
   do {                   \
   } while (0)
@@ -1571,14 +1580,17 @@ __device__ __forceinline__ void eval_cams_gather_f(const int* __restrict__ cm_pt
 #pragma unroll
     for (int q = 0; q < 3; ++q) X[slot][q] = points[3 * (size_t)p + q];
   };
+  DAB_STAMP_HOP(4);  // the chunk bounds are here
   if (n > 0) {
 #pragma unroll
     for (int st = 0; st < DG; ++st) load_idx(st % R, st);
+    DAB_STAMP_HOP(5);  // the first indices are here
 #pragma unroll
     for (int st = 0; st < DG; ++st) gather(st % R, st % R, st);
 #pragma unroll
     for (int st = DG; st < DI; ++st) load_idx(st % R, st);
   }
+  DAB_STAMP_HOP(6);  // the first points are here
   const UniFrame f = get_frame();
   for (int st0 = 0; st0 < n; st0 += R) {
 #pragma unroll
@@ -2087,6 +2099,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
       for (int i = 0; i < 6; ++i) reinterpret_cast<double2*>(rt_s + 12 * e)[i] = make_double2(T[2 * i], T[2 * i + 1]);
     }
   }
+  DAB_STAMP_ANY(5);  // this wave's tables are built
   // barrier of the point waves only (LDS counter): own LDS writes and the K LDS-DMA retired
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_fetch_add(&kbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -4470,7 +4483,7 @@ extern "C" int dab_trace_fetch(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(dab::g_trace), sizeof(dab::g_trace)) == hipSuccess ? 0 : -1;
 }
 extern "C" int dab_trace_clear() {
-  static unsigned long long z[256 * 16 * 4];
+  static unsigned long long z[256 * 16 * 8];
   return hipMemcpyToSymbol(HIP_SYMBOL(dab::g_trace), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -32,14 +32,14 @@ s.bench_eval_pass(True, 50)
 s.sync()
 jk, _ = s.bench_kernel_ms()
 print(f"{cfg} abl={side} lib={os.path.basename(os.path.dirname(lib._name))}: kernel {jk * 1e3:.1f} us (50-pass average)")
-buf = np.zeros(256 * 16 * 4, dtype=np.uint64)
+buf = np.zeros(256 * 16 * 8, dtype=np.uint64)
 runs = []
 for rep in range(5):
     lib.dab_trace_clear()
     s.bench_eval_pass(True, 1)
     s.sync()
     lib.dab_trace_fetch(buf.ctypes.data_as(C.POINTER(C.c_ulonglong)))
-    runs.append(buf.reshape(256, 16, 4).astype(np.int64).copy())
+    runs.append(buf.reshape(256, 16, 8).astype(np.int64).copy())
 s.close()
 for r, t in enumerate(runs):
     have = t[:, :, 0] > 0
@@ -84,3 +84,9 @@ if os.environ.get("DAB_TRACE_PER_WG"):
               f"max {np.nanmax(ext_[sel]):5.2f}")
     last = np.argsort(-np.nan_to_num(ext_, nan=-1))[:12]
     print("  last 12 work-groups (block: entry exit):", " ".join(f"{b}:{ent[b]:.1f}/{ext_[b]:.1f}" for b in last))
+    # prologue hops (stamps 4-6 of the camera waves: chunk bounds, first indices, first
+    # points, each once every load in flight has returned; stamp 5 of the point waves:
+    # their tables built, before the barrier)
+    print("prologue (median over waves, us): camera bounds / indices / points / frame:",
+          " ".join(f"{np.nanmedian(rel[:, 8:, k]):6.2f}" for k in (4, 5, 6, 1)),
+          "| point tables built / barrier passed:", " ".join(f"{np.nanmedian(rel[:, :8, k]):6.2f}" for k in (5, 1)))
