@@ -1937,6 +1937,9 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     const int c = cam_of(lane);
     if (lane < nsl && c < v.NC) {
       const int2 u = v.chunk_uni[c];
+      double k6[6];  // the intrinsic leaves with the extrinsic (one round trip for both)
+#pragma unroll
+      for (int q = 0; q < 6; ++q) k6[q] = v.intr[(size_t)kIntr * u.y + q];
       double F[30];
       if (camtab) {
 #pragma unroll
@@ -1951,7 +1954,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
 #pragma unroll
       for (int q = 0; q < 12; ++q) o[q] = F[q];
 #pragma unroll
-      for (int q = 0; q < 6; ++q) o[12 + q] = v.intr[(size_t)kIntr * u.y + q];
+      for (int q = 0; q < 6; ++q) o[12 + q] = k6[q];
 #pragma unroll
       for (int r = 0; r < 3; ++r)
 #pragma unroll
