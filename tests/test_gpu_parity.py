@@ -361,6 +361,33 @@ def test_fused_eval_matches_two_kernel_pass(pkg, gpu, solver, monkeypatch):
     np.testing.assert_array_equal(pts[0], pts[2])
 
 
+@pytest.mark.parametrize("shape", [(1024, 20000, 6), (300, 8000, 6), (33, 3000, 5), (2, 700, 2)])
+def test_fused_eval_edge_shapes(pkg, gpu, shape, monkeypatch):
+    """k_eval_bal at the edges of its schedule: E = NI = 1024 (every LDS table slot, two
+    tables per point thread, 1023 free cameras on 256 work-groups x 4 slots), 300 cameras
+    (4 waves per camera), 33 cameras (8 waves per camera, most work-groups without one) and
+    a single free camera. Against the two-kernel pass: same iteration and CG counts, costs
+    1e-10 relative; the fused pass must actually run (schedule 1)."""
+    ncam, npt, opp = shape
+    prob = pkg.synth(kind=0, num_cameras=ncam, num_points=npt, obs_per_point=opp, seed=60 + ncam)
+    res, sched = [], []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DAB_EVAL_FUSED", fused)
+        p = prob.copy()
+        s = pkg.Solver(0)
+        s.set_problem(p)
+        sched.append(s.eval_fused())
+        res.append(s.solve(pkg.options(max_num_iterations=6,
+                                       linear_solver_type=pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG)))
+        s.close()
+    assert sched == [1, 0]
+    a, b = res
+    assert [it["linear_solver_iterations"] for it in a["iterations"]] == \
+        [it["linear_solver_iterations"] for it in b["iterations"]]
+    for x, y in zip(a["iterations"], b["iterations"]):
+        assert x["cost"] == pytest.approx(y["cost"], rel=1e-10 if x["success"] else 1e-8), (x, y)
+
+
 def test_fused_camera_frame_small_angles(pkg, gpu, monkeypatch):
     """The fused pass accumulates the camera blocks in the point frame and applies J_l per
     camera afterwards; cameras on the small-angle tables (|w|^2 <= DBL_EPSILON, exactly
