@@ -30,25 +30,34 @@
 namespace dab {
 
 #ifdef DAB_TRACE
-// timing build only (scripts/trace_fused.sh): per-wave s_memrealtime stamps (100 MHz)
+// timing build only (scripts/trace_build.sh): per-wave s_memrealtime stamps (100 MHz), kept
+// in LDS while the wave runs (a global store per stamp would sit in the wave's vmcnt and
+// delay the hop stamps below) and copied out by stamp 3, which every exit path takes
 __device__ unsigned long long g_trace[256 * 16 * 8];
-#define DAB_STAMP(k)                                                                        \
-  do {                                                                                      \
-    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                          \
-    if (lane == 0 && blockIdx.x < 256) g_trace[(blockIdx.x * 16 + wave) * 8 + (k)] = t_;     \
+__shared__ unsigned long long g_trace_lds[16 * 8];
+#define DAB_TRACE_INIT()                                                                   \
+  do {                                                                                     \
+    if ((threadIdx.x & 63) < 8) g_trace_lds[(threadIdx.x >> 6) * 8 + (threadIdx.x & 63)] = 0ull; \
   } while (0)
-#define DAB_STAMP_ANY(k)                                                                                     \
-  do {                                                                                                       \
-    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                           \
-    if ((threadIdx.x & 63) == 0 && blockIdx.x < 256) g_trace[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + (k)] = t_; \
+#define DAB_STAMP_ANY(k)                                                                   \
+  do {                                                                                     \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                         \
+    if ((threadIdx.x & 63) == 0) g_trace_lds[(threadIdx.x >> 6) * 8 + (k)] = t_;             \
+    if ((k) == 3 && (threadIdx.x & 63) < 8 && blockIdx.x < 256)                            \
+      g_trace[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + (threadIdx.x & 63)] =            \
+          g_trace_lds[(threadIdx.x >> 6) * 8 + (threadIdx.x & 63)];                        \
   } while (0)
+#define DAB_STAMP(k) DAB_STAMP_ANY(k)
 // a stamp once every load in flight has returned (prologue hops; perturbs the schedule a little)
-#define DAB_STAMP_HOP(k)                                   \
-  do {                                                     \
+#define DAB_STAMP_HOP(k)                                        \
+  do {                                                          \
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
-    DAB_STAMP_ANY(k);                                      \
+    DAB_STAMP_ANY(k);                                           \
   } while (0)
 #else
+#define DAB_TRACE_INIT() \
+  do {                   \
+  } while (0)
 #define DAB_STAMP_HOP(k) \
   do {                   \
   } while (0)
@@ -1920,6 +1929,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   __shared__ double shp[kBalPW][2];
   __shared__ unsigned ccount[kBalCW + kBalPW], tbar, kbar, pdone;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  DAB_TRACE_INIT();
   DAB_STAMP(0);
   // camera slot -> camera: slot s of work-group b takes camera s G + (G - 1 - b), so that the
   // work-groups short of a camera are the ones with an extra point slice (slices are dealt
@@ -1931,6 +1941,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   if (blockIdx.x == 0 && fx_next)
     for (int i = threadIdx.x; i < kFxWords; i += blockDim.x) fx_next[i] = 0ull;
   __syncthreads();
+  DAB_STAMP(7);  // past the work-group's first barrier
   // the frames of the work-group's cameras, one lane per camera slot (wave kBalPW), shared
   // through LDS; the camera waves wait only for these
   auto build_frames = [&]() {

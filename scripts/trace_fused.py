@@ -87,6 +87,8 @@ if os.environ.get("DAB_TRACE_PER_WG"):
     # prologue hops (stamps 4-6 of the camera waves: chunk bounds, first indices, first
     # points, each once every load in flight has returned; stamp 5 of the point waves:
     # their tables built, before the barrier)
-    print("prologue (median over waves, us): camera bounds / indices / points / frame:",
+    print("prologue (median over waves, us): entry / first barrier:",
+          " ".join(f"{np.nanmedian(rel[:, :, k]):6.2f}" for k in (0, 7)),
+          "| camera bounds / indices / points / frame:",
           " ".join(f"{np.nanmedian(rel[:, 8:, k]):6.2f}" for k in (4, 5, 6, 1)),
           "| point tables built / barrier passed:", " ".join(f"{np.nanmedian(rel[:, :8, k]):6.2f}" for k in (5, 1)))
