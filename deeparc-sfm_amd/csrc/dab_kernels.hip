@@ -34,10 +34,13 @@ namespace dab {
 // in LDS while the wave runs (a global store per stamp would sit in the wave's vmcnt and
 // delay the hop stamps below) and copied out by stamp 3, which every exit path takes
 __device__ unsigned long long g_trace[256 * 16 * 8];
+__device__ unsigned g_hwid[256 * 16];  // HW_REG_HW_ID of every wave (its SIMD, CU, SE)
 __shared__ unsigned long long g_trace_lds[16 * 8];
 #define DAB_TRACE_INIT()                                                                   \
   do {                                                                                     \
     if ((threadIdx.x & 63) < 8) g_trace_lds[(threadIdx.x >> 6) * 8 + (threadIdx.x & 63)] = 0ull; \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 256)                                       \
+      g_hwid[blockIdx.x * 16 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_getreg((31 << 11) | 4); \
   } while (0)
 #define DAB_STAMP_ANY(k)                                                                   \
   do {                                                                                     \
@@ -4495,6 +4498,9 @@ void warm_kernels() {
 #ifdef DAB_TRACE
 extern "C" int dab_trace_fetch(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(dab::g_trace), sizeof(dab::g_trace)) == hipSuccess ? 0 : -1;
+}
+extern "C" int dab_trace_hwid(unsigned* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dab::g_hwid), sizeof(dab::g_hwid)) == hipSuccess ? 0 : -1;
 }
 extern "C" int dab_trace_clear() {
   static unsigned long long z[256 * 16 * 8];

@@ -92,3 +92,13 @@ if os.environ.get("DAB_TRACE_PER_WG"):
           "| camera bounds / indices / points / frame:",
           " ".join(f"{np.nanmedian(rel[:, 8:, k]):6.2f}" for k in (4, 5, 6, 1)),
           "| point tables built / barrier passed:", " ".join(f"{np.nanmedian(rel[:, :8, k]):6.2f}" for k in (5, 1)))
+if os.environ.get("DAB_TRACE_PER_WAVE") and hasattr(lib, "dab_trace_hwid"):
+    hw = np.zeros(256 * 16, dtype=np.uint32)
+    lib.dab_trace_hwid(hw.ctypes.data_as(C.POINTER(C.c_uint)))
+    hw = hw.reshape(256, 16)
+    simd = (hw >> 4) & 3
+    print("SIMD of each logical wave relative to wave 0's, (s_w - s_0) mod 4 (most common over the "
+          "work-groups; share):")
+    for w in range(16):
+        vals, cnt = np.unique((simd[:, w] - simd[:, 0]) % 4, return_counts=True)
+        print(f"  wave {w:2d}: {vals[cnt.argmax()]} ({cnt.max() / cnt.sum():.2f})")
