@@ -2005,7 +2005,9 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     for (int i = 0; i < 27; ++i) acc[i] = 0.0;
     const double* fr = cfr[slot];
     eval_cams_gather_f(v.cm_pt, v.cm_xy, points, lo + lane, hi, acc, [&]() {
-      if (side != 4 && side != 6) lds_wait_ge(&tbar, 1u, err, 1u);  // the frames, built while the first gathers fly
+      // the frames, built while the first gathers fly (side 7, a test: a frame flag that never
+      // comes — the wait must run out and fail the pass closed)
+      if (side != 4 && side != 6) lds_wait_ge(&tbar, side == 7 ? 2u : 1u, err, 1u);
       const UniFrame f(UniFrame::FromShared{}, fr);
       DAB_STAMP(1);
       return f;

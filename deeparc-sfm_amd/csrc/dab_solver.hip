@@ -300,7 +300,8 @@ struct Knobs {
   int setup_host = 0;       // DAB_SETUP_HOST=1: dab_set_problem's host passes instead of the device ones
   int eval_side = 0;        // DAB_EVAL_SIDE (timing ablation, wrong results): k_eval_bal's single launch runs
                             // 1 the point side only, 2 the camera side only, 3 the tables only, 4 no
-                            // tables or frames, 5 no point tables, 6 no camera frames
+                            // tables or frames, 5 no point tables, 6 no camera frames; 7 (test) a
+                            // frame wait that times out (the pass must fail with DAB_E_DEVICE)
   int fused_tab = -1;       // DAB_FUSED_TAB: the fused pass reads the camera tables of the current x
                             // instead of building them in every work-group — -1 (default) when they
                             // exist already (the LM loop: the accepted candidate's tables), 1 always

@@ -82,3 +82,20 @@ def test_guard_fails_closed_on_overrun(gpu):
     r = _child(SELFTEST, 2)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "FAILED CLOSED" in r.stdout and "overrun" in r.stdout and "problem buffers" in r.stdout, r.stdout
+
+
+def test_eval_pass_wait_timeout_fails_closed(pkg, gpu, monkeypatch):
+    """k_eval_bal's in-launch waits (the camera frames' flag, the point waves' barrier) are
+    bounded: a wait that runs out sets the pass's error word and the call fails with
+    DAB_E_DEVICE instead of hanging or returning numbers built on missing data.
+    DAB_EVAL_SIDE=7 makes the camera waves wait for a frame flag value that never comes."""
+    monkeypatch.setenv("DAB_EVAL_SIDE", "7")
+    prob = pkg.synth(kind=0, num_cameras=30, num_points=2000, obs_per_point=5, seed=91)
+    s = pkg.Solver(0)
+    try:
+        s.set_problem(prob.copy())
+        assert s.eval_fused() == 1
+        with pytest.raises(RuntimeError, match="timed out"):
+            s.solve(pkg.options(max_num_iterations=2))
+    finally:
+        s.close()
