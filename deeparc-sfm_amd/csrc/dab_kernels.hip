@@ -3871,88 +3871,12 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame32(DevView v, const dou
   }
 }
 
-// Per chunk of camera-major positions, Y re-evaluated: 21 upper of sum Z Z^T over
-// same-point runs (Z = sum of the run's Y_e; the diagonal block of the Schur term) | 6 of
-// -sum Y_e q_p -> partial[chunk][27]. Replaces k_entry_y + k_pcg_diag_rhs_partial.
-__global__ __launch_bounds__(256) void k_mf_diag_rhs(DevView v, int nchunk, const int* __restrict__ run_beg,
-                                                     const int4* __restrict__ run_rec,
-                                                     const double* __restrict__ points,
-                                                     const double* __restrict__ camtab,
-                                                     const double* __restrict__ scc,
-                                                     const double* __restrict__ PU, const double* __restrict__ q,
-                                                     double* __restrict__ partial) {
-  extern __shared__ double mf_lds[];
-  const SmallTabs tabs = stage_small_tabs(mf_lds, v.E, v.NI, camtab, v.intr);  // once per block
-  __shared__ double wsum[kRedBlock / 64][27];
-  for (int c = blockIdx.x; c < nchunk; c += gridDim.x) {
-  const int b = run_beg[c], e = run_beg[c + 1];
-  double acc[27];
-#pragma unroll
-  for (int i = 0; i < 27; ++i) acc[i] = 0.0;
-  // the chunk's camera scales (uniform: a chunk lies in one camera)
-  const int cam = b < e ? __builtin_amdgcn_readfirstlane(run_rec[b].w) : 0;
-  double sc[6];
-#pragma unroll
-  for (int r = 0; r < 6; ++r) sc[r] = scc[6 * cam + r];
-  for (int k = b + threadIdx.x; k < e; k += blockDim.x) {
-    // one run (the entries of one point on this camera; usually one entry): W = sum of
-    // J_c^T J_p over the run, then Z = s_c o (W PU) once. The record carries the point, so
-    // the point's loads go out with the first entry's index.
-    const int4 rr = run_rec[k];
-    const int i = rr.x, len = rr.y, p = rr.z;
-    const double X[3] = {points[3 * (size_t)p], points[3 * (size_t)p + 1], points[3 * (size_t)p + 2]};
-    // PU_p and q_p in flight during the entries
-    const double* pu = PU + 6 * (size_t)p;
-    const double u00 = pu[0], u01 = pu[1], u02 = pu[2], u11 = pu[3], u12 = pu[4], u22 = pu[5];
-    const double q0 = q[4 * (size_t)p], q1 = q[4 * (size_t)p + 1], q2 = q[4 * (size_t)p + 2];
-    double y[18];
-#pragma unroll
-    for (int t = 0; t < 18; ++t) y[t] = 0.0;
-    for (int j = 0; j < len; ++j) {
-      int4 id = v.cm_idx[i + j];
-      const bool slot1 = (id.w & kSlotBit) != 0;
-      id.w &= ~kSlotBit;
-      const double2 xy0 = make_double2(0.0, 0.0);  // the residual is not used
-      double ru, rv, jx0[3], jx1[3], ja[6], jb[6];
-      if (slot1) obs_rows<true, 1>(id, xy0, X, tabs, ru, rv, jx0, jx1, ja, jb);
-      else obs_rows<true, 0>(id, xy0, X, tabs, ru, rv, jx0, jx1, ja, jb);
-#pragma unroll
-      for (int r = 0; r < 6; ++r)
-#pragma unroll
-        for (int t = 0; t < 3; ++t) y[3 * r + t] = fma(jb[r], jx1[t], fma(ja[r], jx0[t], y[3 * r + t]));
-    }
-    {  // in place: y = s_c o (W PU), PU upper triangular (00 01 02 11 12 22)
-#pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        const double w0 = y[3 * r], w1 = y[3 * r + 1], w2 = y[3 * r + 2];
-        y[3 * r] = sc[r] * (w0 * u00);
-        y[3 * r + 1] = sc[r] * (w0 * u01 + w1 * u11);
-        y[3 * r + 2] = sc[r] * (w0 * u02 + w1 * u12 + w2 * u22);
-      }
-    }
-    // the run's Y_e sum is Z (Y is linear in W): -Z q_p and Z Z^T
-#pragma unroll
-    for (int a = 0; a < 6; ++a) acc[21 + a] -= y[3 * a] * q0 + y[3 * a + 1] * q1 + y[3 * a + 2] * q2;
-    int t = 0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a)
-#pragma unroll
-      for (int bb = a; bb < 6; ++bb)
-        acc[t++] += y[3 * a] * y[3 * bb] + y[3 * a + 1] * y[3 * bb + 1] + y[3 * a + 2] * y[3 * bb + 2];
-  }
-  wave_sums_transposed<27>(acc, wsum[threadIdx.x >> 6]);
-  __syncthreads();
-  if (threadIdx.x < 27) {
-    double t = wsum[0][threadIdx.x];
-#pragma unroll
-    for (int w = 1; w < kRedBlock / 64; ++w) t += wsum[w][threadIdx.x];
-    partial[27 * (size_t)c + threadIdx.x] = t;
-  }
-  __syncthreads();  // wsum is reused by the next chunk
-  }
-}
-
-// k_mf_diag_rhs in the rotated frame (as k_mf_frame): a row of J_c is D w with
+// Per chunk of camera-major positions (the rig's PCG preconditioner and rhs): 21 upper of
+// sum Z Z^T over same-point runs (Z = the run's Y sum, the diagonal block of the Schur term)
+// | 6 of -sum Y q_p -> partial[chunk][27]; one lane per run, from a per-chunk run record
+// {first position, length, point, camera} so that the point, PU_p and q_p loads leave with
+// the record. In the rotated frame (as k_mf_frame; round 5, replacing the Rd | Jd row form
+// k_mf_diag_rhs, 733 -> 710 us at C5): a row of J_c is D w with
 // D = blockdiag(J_l^T, I) constant per camera and w = [Z x a | a] (slot 0: the projection
 // row a, Z = P - t_a or Q on small-angle tables; slot 1: a R_a in place of a, Z = Q - t_b or
 // X), so a run's W = D W~ with W~ = sum of w j_p^T, its y = s o (D W~ PU) and
@@ -4142,18 +4066,12 @@ void launch_mf_diag_rhs(hipStream_t s, const DevView& v, int nchunk, const int* 
                         const double* points, const double* camtab, const double* scale_c, const double* PU,
                         const double* q, double* partial) {
   if (nchunk <= 0) return;
-  static const int form = getenv("DAB_MF_DIAG") ? atoi(getenv("DAB_MF_DIAG")) : 1;
-  if (form == 1) {
-    const size_t lds =
-        sizeof(double) * (kRtStride * (size_t)v.E + 6 * (size_t)v.NI + 9 * (size_t)v.NC) + sizeof(int) * (size_t)v.E;
-    k_mf_diag_frame<<<std::min(nchunk, kSmallGrid), 256, lds, s>>>(v, nchunk, run_beg, run_rec, points, camtab,
-                                                                   scale_c, PU, q, partial);
-    return;
-  }
-  const size_t lds = small_tabs_bytes(v.E, v.NI);
-  // persistent blocks: the 20-KB tables are staged once per block, not once per chunk
-  k_mf_diag_rhs<<<std::min(nchunk, kSmallGrid), 256, lds, s>>>(v, nchunk, run_beg, run_rec, points, camtab, scale_c,
-                                                                PU, q, partial);
+  // persistent blocks: the tables are staged once per block, not once per chunk (they fit:
+  // NC <= E, so 14 E + 6 NI + 9 NC doubles stay below the 30 E + 6 NI of small_tabs_fit)
+  const size_t lds =
+      sizeof(double) * (kRtStride * (size_t)v.E + 6 * (size_t)v.NI + 9 * (size_t)v.NC) + sizeof(int) * (size_t)v.E;
+  k_mf_diag_frame<<<std::min(nchunk, kSmallGrid), 256, lds, s>>>(v, nchunk, run_beg, run_rec, points, camtab, scale_c,
+                                                                 PU, q, partial);
 }
 
 void launch_backsub(hipStream_t s, const DevView& v, const double* PU, const double* q, YBufs Y,

@@ -1129,7 +1129,7 @@ static int setup_host(dab_handle* h, const dab_problem* p, const std::function<v
   // static camera-major copy of the entries' observation inputs (matrix-free camera passes)
   big_vec<int4> cm_idx(NE);
   // the runs of each chunk as records {first position, length, point, camera} in position
-  // order (k_mf_diag_rhs: its loads need no dependent index load; run_beg[nchunk + 1])
+  // order (k_mf_diag_frame: its loads need no dependent index load; run_beg[nchunk + 1])
   std::vector<int> run_beg(h->nchunk + 1, 0);
   par_for(h->nchunk, [&](long long b, long long e, int) {
     for (int c = (int)b; c < (int)e; ++c) {
