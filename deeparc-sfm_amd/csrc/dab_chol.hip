@@ -44,7 +44,7 @@ struct CholCtx {
 
   hipStream_t side = nullptr;                     // bulk trailing updates (captured into the graph)
   int device = 0;
-  std::vector<hipEvent_t> ev_panel, ev_bulk;      // per block column
+  std::vector<hipEvent_t> ev_panel, ev_bulk, ev_strip;  // per block column
   size_t nblk_alloc = 0;
   // the ~5 x n/64 dependent launches are captured once per (n, buffers) and replayed
   hipGraphExec_t exec = nullptr;
@@ -62,6 +62,8 @@ struct CholCtx {
   bool fuse_panel = true;     // DAB_CHOL_FUSE_PANEL=0: the panel step as its own launch after the column update
   unsigned* pready = nullptr; // per block: L_kk published by the fused column update (zeroed per factorisation)
   int group = 2;            // DAB_CHOL_GROUP: panels per bulk trailing update (2: pairs)
+  bool strip = true;        // DAB_CHOL_STRIP=0: the bulk's first block column inside the bulk launch
+                            // (round 4's schedule) instead of a launch of its own
   bool v1 = false;          // DAB_CHOL_V1=1: the per-step schedule (one bulk update per panel, one
                             // back-substitution launch per block)
 };
@@ -78,6 +80,7 @@ CholCtx* chol_create() {
   c->bulk_grid = std::max(1, 2 * ncu - 64);
   c->ncu = ncu;
   if (const char* e = getenv("DAB_CHOL_V1")) c->v1 = atoi(e) != 0;
+  if (const char* e = getenv("DAB_CHOL_STRIP")) c->strip = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_GROUP")) c->group = std::max(2, atoi(e));
   if (const char* e = getenv("DAB_CHOL_BACK_FLOW")) c->back_flow = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_PREFACTOR")) c->prefactor = atoi(e) != 0;
@@ -102,6 +105,7 @@ void chol_destroy(CholCtx* c) {
   c->mem.clear();
   for (hipEvent_t e : c->ev_panel) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_bulk) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->ev_strip) (void)hipEventDestroy(e);
   stream_give(c->device, c->side);
   delete c;
 }
@@ -1020,11 +1024,13 @@ static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
   if (!c->side && !(c->side = stream_take(c->device))) return -3;
   if (!c->bar && c->mem.alloc(&c->bar, 1) != 0) return -2;
   while ((int)c->ev_panel.size() < nblk) {
-    hipEvent_t a, b;
+    hipEvent_t a, b, d;
     if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess) return -3;
     if (hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) return -3;
+    if (hipEventCreateWithFlags(&d, hipEventDisableTiming) != hipSuccess) return -3;
     c->ev_panel.push_back(a);
     c->ev_bulk.push_back(b);
+    c->ev_strip.push_back(d);
   }
   // small systems launch directly: a graph's instantiation (~5 ms measured) costs more than
   // the host launches it saves over a whole solve (n = 264, 5 blocks: ~20 launches)
@@ -1104,26 +1110,43 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
   // update applies all R panels to the columns >= b + R + 1 while the chain does column b + R.
   const int R = std::max(2, c->group);
   int pending = -1;  // group whose bulk update is still running on s2
+  // strip (round 5): the bulk's first block column (the next group's first column) is a
+  // launch of its own on s2, so the chain's next column update waits for it only and runs
+  // beside the rest of the bulk instead of alone after it; the group's last column waits
+  // for the whole bulk. n = 5994: 5.63 -> 4.95-5.0 ms (scripts/r05ai.sh)
+  const bool strip = c->strip;
   for (int b = 0; b + 1 < nblk; b += R) {
-    if (pending >= 0) (void)hipStreamWaitEvent(s, c->ev_bulk[pending], 0);
+    const int prev = pending;
     pending = -1;
+    if (prev >= 0) (void)hipStreamWaitEvent(s, strip ? c->ev_strip[prev] : c->ev_bulk[prev], 0);
     const int cend = std::min(b + R, nblk);  // first column past the group's panels
     for (int cc = b + 1; cc < cend; ++cc) {  // every panel before the last is NB wide
+      if (strip && prev >= 0 && cc > b + 1) (void)hipStreamWaitEvent(s, c->ev_bulk[prev], 0);
       col(cc, b * NB, (cc - b) * NB);
       panel(cc);
     }
+    if (strip && prev >= 0) (void)hipStreamWaitEvent(s, c->ev_bulk[prev], 0);
     if (cend >= nblk) break;  // the group ended at the last panel (its solve covered the rhs row)
     const int kk = (cend - b) * NB;
-    const int c0 = (cend + 1) * NB, m = n + 1 - c0;
-    if (m > 1) {
+    const int c0 = (cend + (strip ? 2 : 1)) * NB, m = n + 1 - c0;
+    const int cs0 = (cend + 1) * NB, ms = n + 1 - cs0;
+    if (m > 1 || (strip && ms > 1)) {
       (void)hipEventRecord(c->ev_panel[b], s);
       (void)hipStreamWaitEvent(s2, c->ev_panel[b], 0);
-      const int t2 = (m + TB - 1) / TB, ntb = t2 * (t2 + 1) / 2;
-      // the bulk grid leaves CUs free for the panel chain (its dependent MFMA chain would
-      // queue behind the bulk's MFMAs on a shared CU)
-      const int g = std::min(ntb, c->bulk_grid > 0 ? c->bulk_grid : ntb);
-      k_syrk_big<16, 4><<<g, kBigThreads, 0, s2>>>(A, lda, c0, m, b * NB, kk, ntb);
+      if (strip && ms > 1) {
+        const int nts = (ms + NB - 1) / NB;
+        k_syrk_mfma<<<nts, kThreads, 0, s2>>>(A, lda, cs0, ms, b * NB, kk, 1, nts);
+        (void)hipEventRecord(c->ev_strip[b], s2);
+      }
+      if (m > 1) {
+        const int t2 = (m + TB - 1) / TB, ntb = t2 * (t2 + 1) / 2;
+        // the bulk grid leaves CUs free for the panel chain (its dependent MFMA chain would
+        // queue behind the bulk's MFMAs on a shared CU)
+        const int g = std::min(ntb, c->bulk_grid > 0 ? c->bulk_grid : ntb);
+        k_syrk_big<16, 4><<<g, kBigThreads, 0, s2>>>(A, lda, c0, m, b * NB, kk, ntb);
+      }
       (void)hipEventRecord(c->ev_bulk[b], s2);
+      if (strip && ms <= 1) (void)hipEventRecord(c->ev_strip[b], s2);
       pending = b;
     }
     col(cend, b * NB, kk);
