@@ -641,21 +641,22 @@ __global__ __launch_bounds__(kBigThreads, OCC) void k_syrk_big(double* __restric
     const bool skip = diag && wr < wc;
     const int ri0 = bi * TB, rj0 = bj * TB;  // relative to c0
     double ra[PER], rb[PER];
+    // every load unconditional (row clamped to the last one, then zeroed by a select; kk is a
+    // multiple of KC: panels are NB wide), so the chunk loop carries no exec-mask branches
+    const bool va = ri0 + lr < m, vb = rj0 + lr < m;
+    const double* srca = A + (size_t)(c0 + min(ri0 + lr, m - 1)) * lda + k0 + lh;
+    const double* srcb = A + (size_t)(c0 + min(rj0 + lr, m - 1)) * lda + k0 + lh;
     auto gload = [&](int ch) {
-      const int ia = ri0 + lr, ib = rj0 + lr;
 #pragma unroll
-      for (int q = 0; q < PER; q += 2) {
-        const int kc = ch * KC + lh + q;
-        ra[q] = ra[q + 1] = rb[q] = rb[q + 1] = 0.0;
-        if (ia < m) {
-          const double* src = A + (size_t)(c0 + ia) * lda + k0 + kc;
-          ra[q] = kc < kk ? src[0] : 0.0;
-          ra[q + 1] = kc + 1 < kk ? src[1] : 0.0;
-        }
-        if (!diag && ib < m) {
-          const double* src = A + (size_t)(c0 + ib) * lda + k0 + kc;
-          rb[q] = kc < kk ? src[0] : 0.0;
-          rb[q + 1] = kc + 1 < kk ? src[1] : 0.0;
+      for (int q = 0; q < PER; ++q) {
+        const double x = srca[ch * KC + q];
+        ra[q] = va ? x : 0.0;
+      }
+      if (!diag) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+          const double x = srcb[ch * KC + q];
+          rb[q] = vb ? x : 0.0;
         }
       }
     };

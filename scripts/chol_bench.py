@@ -11,6 +11,9 @@ sys.path.insert(0, ROOT)
 import _pkgload  # noqa: E402
 
 pkg = _pkgload.load()
+if os.environ.get("DAB_LIB"):  # another build of libdab (A/B)
+    abi = sys.modules[pkg.__name__ + "._abi"]
+    abi._LIB = abi.load_library(os.path.join(ROOT, os.environ["DAB_LIB"]))
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 6000
 rng = np.random.default_rng(0)
 M = rng.standard_normal((n, n)) / np.sqrt(n)
