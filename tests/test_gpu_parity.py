@@ -688,13 +688,17 @@ def test_noise_free_problem_matches_oracle(pkg, orc, gpu, kind):
 
 
 @pytest.mark.parametrize("knob", ["DAB_CHOL_BACK_FLOW=0", "DAB_CHOL_FUSE_PANEL=0", "DAB_CHOL_PREFACTOR=0",
-                                  "DAB_CHOL_V1=1", "DAB_CHOL_GROUP=3", "DAB_CHOL_GRAPH_MIN=1"])
+                                  "DAB_CHOL_V1=1", "DAB_CHOL_GROUP=3", "DAB_CHOL_GRAPH_MIN=1",
+                                  "DAB_CHOL_STRIP=0", "DAB_CHOL_STRIP=0,DAB_CHOL_GRAPH_MIN=1",
+                                  "DAB_CHOL_GROUP=3,DAB_CHOL_GRAPH_MIN=1"])
 def test_cholesky_schedules_agree(pkg, gpu, knob, monkeypatch):
     """The dense Cholesky's schedules — the dataflow back substitution against the
     grid-barrier one, the panel step fused into the column update against its own launch,
     the diagonal block factored by the column update against every panel work-group, and
-    the round-1 per-step schedule, bulk updates over panel triples instead of pairs, and the
-    captured graph against direct launches (13 blocks launch directly by default) — solve
+    the round-1 per-step schedule, bulk updates over panel triples instead of pairs, the
+    round-5 strip schedule (the bulk's first block column a launch of its own) against the
+    single bulk launch, and the captured graph against direct launches (13 blocks launch
+    directly by default) — solve
     the same systems: the EXPLICIT LM trajectories agree to 1e-10 relative. n = 6 x 130 =
     780 (13 blocks, a short last block)."""
     prob = pkg.synth(kind=0, num_cameras=130, num_points=6000, obs_per_point=8, seed=57)
