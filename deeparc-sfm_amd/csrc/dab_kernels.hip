@@ -1885,8 +1885,10 @@ constexpr int kBalPW = 8;              // point waves per work-group
 constexpr int kBalCW = 16 - kBalPW;    // camera waves
 constexpr int kBalFrame = 28;          // doubles per shared camera frame: R t K J_l small
 // first part of a two-part camera chunk, in 1/1024: the older waves (part 0) get more, since
-// the SIMDs' oldest-first issue starves the younger ones (round 3's per-wave timeline)
-constexpr int kCamSplit = 688;
+// the SIMDs' oldest-first issue starves the younger ones (round 3's per-wave timeline: 688 for
+// k_eval_fused; re-swept for k_eval_bal in round 5, scripts/r05aq.sh: 840 at 21.8 us against
+// 22.0-22.3 us for 600-780 and 900-960, interleaved repetitions on one box)
+constexpr int kCamSplit = 840;
 bool fused_eval_fits(const DevView& v, int nchunk, int ngen, int ncross, int grid) {
   return !v.any_comp && ncross == 0 && ngen == 0 && nchunk == v.NC && v.NC > 0 && v.E <= kLdsCams &&
          v.NI <= kLdsCams && v.NC <= (kBalCW / 2) * grid;
