@@ -1,0 +1,506 @@
+// Decomposition of the dense Cholesky's bulk update (k_syrk_big, dab_chol.hip) at the n = 5994
+// shapes: the shipped kernel, the same kernel without its C tile traffic (MFMA + LDS pipeline
+// only), and C traffic only (no MFMA); plus the fp64 MFMA issue ceiling (16x16x4, independent
+// accumulators, 4 waves per SIMD) with the in-kernel clock.
+// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 scripts/syrk_big_probe.hip -o scripts/syrk_big_probe
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// ---- MFMA ceiling: each wave 8 independent accumulators, `iters` rounds ----
+__global__ __launch_bounds__(256) void k_mfma_peak(double* out, int iters, unsigned long long* clk) {
+  const int lane = threadIdx.x & 63;
+  double a = 1.0 + 1e-3 * lane, b = 1.0 - 1e-3 * lane;
+  dbl4 acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = dbl4{0.1 * i, 0.0, 0.0, 0.0};
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[i], 0, 0, 0);
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+  if (s == 12345.678) out[threadIdx.x] = s;
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    clk[0] = t1 - t0;
+    clk[1] = r1 - r0;
+  }
+}
+
+// ---- k_syrk_big (dab_chol.hip), MODE 0 as shipped, 1 no C load / store, 2 C only ----
+constexpr int TB = 128;
+constexpr int kBigThreads = 512;
+template <int KC, int OCC, int MODE>
+__global__ __launch_bounds__(kBigThreads, OCC) void k_big(double* __restrict__ A, int lda, int c0, int m, int k0,
+                                                          int kk, int ntiles, int never) {
+  constexpr int LKC = KC + 2;
+  constexpr int PER = KC / 4;
+  constexpr int TPR = KC / PER;
+  __shared__ double sm[2 * 2 * TB * LKC];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+  const int qd = w >> 1, wr = qd >> 1, wc = qd & 1, half = w & 1;
+  const int lr = tid / TPR, lh = (tid % TPR) * PER;
+  const int nch = (kk + KC - 1) / KC;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    int bi = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
+    while (bi * (bi + 1) / 2 > t) --bi;
+    const int bj = t - bi * (bi + 1) / 2;
+    const bool diag = bi == bj;
+    const bool skip = diag && wr < wc;
+    const int ri0 = bi * TB, rj0 = bj * TB;
+    double ra[PER], rb[PER];
+    const bool va = ri0 + lr < m, vb = rj0 + lr < m;
+    const double* srca = A + (size_t)(c0 + min(ri0 + lr, m - 1)) * lda + k0 + lh;
+    const double* srcb = A + (size_t)(c0 + min(rj0 + lr, m - 1)) * lda + k0 + lh;
+    auto gload = [&](int ch) {
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const double x = srca[ch * KC + q];
+        ra[q] = va ? x : 0.0;
+      }
+      if (!diag) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+          const double x = srcb[ch * KC + q];
+          rb[q] = vb ? x : 0.0;
+        }
+      }
+    };
+    auto sstore = [&](int st) {
+      double* a = sm + (size_t)(2 * st) * TB * LKC + lr * LKC + lh;
+#pragma unroll
+      for (int q = 0; q < PER; q += 2) *reinterpret_cast<double2*>(a + q) = make_double2(ra[q], ra[q + 1]);
+      if (!diag) {
+        double* b = a + TB * LKC;
+#pragma unroll
+        for (int q = 0; q < PER; q += 2) *reinterpret_cast<double2*>(b + q) = make_double2(rb[q], rb[q + 1]);
+      }
+    };
+    dbl4 acc[4][2];
+#pragma unroll
+    for (int tr = 0; tr < 4; ++tr)
+#pragma unroll
+      for (int tc = 0; tc < 2; ++tc)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int row = ri0 + 64 * wr + 16 * tr + lk + 4 * reg, col = rj0 + 64 * wc + 32 * half + 16 * tc + li;
+          if (MODE == 1)
+            acc[tr][tc][reg] = 0.0;
+          else
+            acc[tr][tc][reg] = (!skip && row < m && col < m) ? A[(size_t)(c0 + row) * lda + c0 + col] : 0.0;
+        }
+    if (MODE != 2) {
+      gload(0);
+      __syncthreads();
+      sstore(0);
+      __syncthreads();
+      for (int ch = 0; ch < nch; ++ch) {
+        const int st = ch & 1;
+        if (ch + 1 < nch) gload(ch + 1);
+        if (!skip) {
+          const double* As = sm + (size_t)(2 * st) * TB * LKC;
+          const double* Bs = diag ? As : As + TB * LKC;
+#pragma unroll
+          for (int ks = 0; ks < KC / 4; ++ks) {
+            double fa[4], fb[2];
+#pragma unroll
+            for (int tr = 0; tr < 4; ++tr) fa[tr] = -As[(64 * wr + 16 * tr + li) * LKC + 4 * ks + lk];
+#pragma unroll
+            for (int tc = 0; tc < 2; ++tc) fb[tc] = Bs[(64 * wc + 32 * half + 16 * tc + li) * LKC + 4 * ks + lk];
+#pragma unroll
+            for (int tr = 0; tr < 4; ++tr)
+#pragma unroll
+              for (int tc = 0; tc < 2; ++tc)
+                acc[tr][tc] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[tr], fb[tc], acc[tr][tc], 0, 0, 0);
+          }
+        }
+        if (ch + 1 < nch) sstore(st ^ 1);
+        __syncthreads();
+      }
+    } else {
+#pragma unroll
+      for (int tr = 0; tr < 4; ++tr)
+#pragma unroll
+        for (int tc = 0; tc < 2; ++tc) acc[tr][tc] *= -1.0;
+    }
+    if (!skip && (MODE != 1 || never)) {
+#pragma unroll
+      for (int tr = 0; tr < 4; ++tr)
+#pragma unroll
+        for (int tc = 0; tc < 2; ++tc)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) {
+            const int row = ri0 + 64 * wr + 16 * tr + lk + 4 * reg, col = rj0 + 64 * wc + 32 * half + 16 * tc + li;
+            if (row < m && col < m) A[(size_t)(c0 + row) * lda + c0 + col] = acc[tr][tc][reg];
+          }
+    }
+  }
+}
+
+
+// ---- candidate: persistent (one work-group per CU, 2 waves per SIMD), the NEXT tile's C
+// prefetched into registers during the current tile's last two K chunks; same MFMA order
+// per element as k_big<.,.,0> (bitwise the same result) ----
+template <int KC>
+__global__ __launch_bounds__(kBigThreads, 2) void k_big2(double* __restrict__ A, int lda, int c0, int m, int k0,
+                                                        int kk, int ntiles) {
+  constexpr int LKC = KC + 2;
+  constexpr int PER = KC / 4;
+  constexpr int TPR = KC / PER;
+  __shared__ double sm[2 * 2 * TB * LKC];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+  const int qd = w >> 1, wr = qd >> 1, wc = qd & 1, half = w & 1;
+  const int lr = tid / TPR, lh = (tid % TPR) * PER;
+  const int nch = (kk + KC - 1) / KC;
+  auto coords = [&](int t, int& bi, int& bj) {
+    bi = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
+    while (bi * (bi + 1) / 2 > t) --bi;
+    bj = t - bi * (bi + 1) / 2;
+  };
+  // C of tile t into cv: every load unconditional (clamped), zeroed by a select
+  auto cload = [&](int t, dbl4(&cv)[4][2]) {
+    int bi, bj;
+    coords(t, bi, bj);
+    const int ri0 = bi * TB, rj0 = bj * TB;
+#pragma unroll
+    for (int tr = 0; tr < 4; ++tr)
+#pragma unroll
+      for (int tc = 0; tc < 2; ++tc)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int row = ri0 + 64 * wr + 16 * tr + lk + 4 * reg, col = rj0 + 64 * wc + 32 * half + 16 * tc + li;
+          const double x = A[(size_t)(c0 + min(row, m - 1)) * lda + c0 + min(col, m - 1)];
+          cv[tr][tc][reg] = (row < m && col < m) ? x : 0.0;
+        }
+  };
+  dbl4 acc[4][2], nxt[4][2];
+  int t = blockIdx.x;
+  if (t < ntiles) cload(t, acc);
+  for (; t < ntiles; t += gridDim.x) {
+    int bi, bj;
+    coords(t, bi, bj);
+    const bool diag = bi == bj;
+    const bool skip = diag && wr < wc;
+    const int ri0 = bi * TB, rj0 = bj * TB;
+    double ra[PER], rb[PER];
+    const bool va = ri0 + lr < m, vb = rj0 + lr < m;
+    const double* srca = A + (size_t)(c0 + min(ri0 + lr, m - 1)) * lda + k0 + lh;
+    const double* srcb = A + (size_t)(c0 + min(rj0 + lr, m - 1)) * lda + k0 + lh;
+    auto gload = [&](int ch) {
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const double x = srca[ch * KC + q];
+        ra[q] = va ? x : 0.0;
+      }
+      if (!diag) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+          const double x = srcb[ch * KC + q];
+          rb[q] = vb ? x : 0.0;
+        }
+      }
+    };
+    auto sstore = [&](int st) {
+      double* a = sm + (size_t)(2 * st) * TB * LKC + lr * LKC + lh;
+#pragma unroll
+      for (int q = 0; q < PER; q += 2) *reinterpret_cast<double2*>(a + q) = make_double2(ra[q], ra[q + 1]);
+      if (!diag) {
+        double* b = a + TB * LKC;
+#pragma unroll
+        for (int q = 0; q < PER; q += 2) *reinterpret_cast<double2*>(b + q) = make_double2(rb[q], rb[q + 1]);
+      }
+    };
+    const int tn = min(t + (int)gridDim.x, ntiles - 1);  // clamped: the prefetch is unconditional
+    gload(0);
+    __syncthreads();
+    sstore(0);
+    __syncthreads();
+    const int cpre = nch >= 2 ? nch - 2 : 0;
+    for (int ch = 0; ch < nch; ++ch) {
+      const int st = ch & 1;
+      if (ch + 1 < nch) gload(ch + 1);
+      if (ch == cpre) cload(tn, nxt);  // after the tile's last chunk load (in-order vmcnt)
+      if (!skip) {
+        const double* As = sm + (size_t)(2 * st) * TB * LKC;
+        const double* Bs = diag ? As : As + TB * LKC;
+#pragma unroll
+        for (int ks = 0; ks < KC / 4; ++ks) {
+          double fa[4], fb[2];
+#pragma unroll
+          for (int tr = 0; tr < 4; ++tr) fa[tr] = -As[(64 * wr + 16 * tr + li) * LKC + 4 * ks + lk];
+#pragma unroll
+          for (int tc = 0; tc < 2; ++tc) fb[tc] = Bs[(64 * wc + 32 * half + 16 * tc + li) * LKC + 4 * ks + lk];
+#pragma unroll
+          for (int tr = 0; tr < 4; ++tr)
+#pragma unroll
+            for (int tc = 0; tc < 2; ++tc)
+              acc[tr][tc] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[tr], fb[tc], acc[tr][tc], 0, 0, 0);
+        }
+      }
+      if (ch + 1 < nch) sstore(st ^ 1);
+      __syncthreads();
+    }
+    if (!skip) {
+#pragma unroll
+      for (int tr = 0; tr < 4; ++tr)
+#pragma unroll
+        for (int tc = 0; tc < 2; ++tc)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) {
+            const int row = ri0 + 64 * wr + 16 * tr + lk + 4 * reg, col = rj0 + 64 * wc + 32 * half + 16 * tc + li;
+            if (row < m && col < m) A[(size_t)(c0 + row) * lda + c0 + col] = acc[tr][tc][reg];
+          }
+    }
+#pragma unroll
+    for (int tr = 0; tr < 4; ++tr)
+#pragma unroll
+      for (int tc = 0; tc < 2; ++tc) acc[tr][tc] = nxt[tr][tc];
+  }
+}
+
+static float time_big2(double* A, int lda, int n, int m, int kk, int reps, int grid) {
+  const int c0 = n + 1 - m, t2 = (m + TB - 1) / TB, ntb = t2 * (t2 + 1) / 2;
+  const int g = std::min(ntb, grid);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int r = 0; r < 3; ++r) k_big2<16><<<g, kBigThreads>>>(A, lda, c0, m, 0, kk, ntb);
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) k_big2<16><<<g, kBigThreads>>>(A, lda, c0, m, 0, kk, ntb);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  CK(hipGetLastError());
+  return 1e3f * ms / reps;
+}
+
+// ---- candidate 3: each 128 x 128 tile as two 64 x 128 row halves in sequence (8 waves of
+// 32 x 32, 4 waves per SIMD as shipped), the next half's C prefetched into registers during
+// the current half's last two K chunks (halves of one tile, then the work-group's next tile);
+// same MFMA order per element as the shipped kernel ----
+template <int KC, int CP = 2>
+__global__ __launch_bounds__(kBigThreads, 4) void k_big3(double* __restrict__ A, int lda, int c0, int m, int k0,
+                                                        int kk, int ntiles) {
+  constexpr int LKC = KC + 2;
+  constexpr int PA = KC / 8;  // A (the half's 64 rows): 8 loader threads per row
+  constexpr int PB = KC / 4;  // B (the tile's 128 columns): 4 loader threads per row
+  constexpr int SA = 64 * LKC, SS = SA + TB * LKC;
+  __shared__ double sm[2 * SS];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+  const int wrow = 32 * (w & 1), wcol = 32 * (w >> 1);
+  const int ar = tid >> 3, ah = (tid & 7) * PA, br = tid >> 2, bh = (tid & 3) * PB;
+  const int nch = kk / KC, nunits = 2 * ntiles, ustep = 2 * (int)gridDim.x;
+  auto coords = [&](int t, int& bi, int& bj) {
+    bi = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
+    while (bi * (bi + 1) / 2 > t) --bi;
+    bj = t - bi * (bi + 1) / 2;
+  };
+  auto cload = [&](int u, dbl4(&cv)[2][2]) {
+    int bi, bj;
+    coords(u >> 1, bi, bj);
+    const int r0 = bi * TB + 64 * (u & 1) + wrow, q0 = bj * TB + wcol;
+#pragma unroll
+    for (int tr = 0; tr < 2; ++tr)
+#pragma unroll
+      for (int tc = 0; tc < 2; ++tc)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int row = r0 + 16 * tr + lk + 4 * reg, col = q0 + 16 * tc + li;
+          // clamped address, no select: an element outside the matrix is never stored, and
+          // no element inside depends on it (a select here becomes a branch + wait per load)
+          cv[tr][tc][reg] = A[(size_t)(c0 + min(row, m - 1)) * lda + c0 + min(col, m - 1)];
+        }
+  };
+  dbl4 acc[2][2], nxt[2][2];
+  int u = 2 * (int)blockIdx.x;
+  if (u < nunits) cload(u, acc);
+  while (u < nunits) {
+    const int h = u & 1;
+    int bi, bj;
+    coords(u >> 1, bi, bj);
+    const bool skip = bi == bj && (w >> 2) > h;  // a strictly upper 64 x 64 quadrant
+    const int ri0 = bi * TB + 64 * h, rj0 = bj * TB;
+    double ra[PA], rb[PB];
+    const double* srca = A + (size_t)(c0 + min(ri0 + ar, m - 1)) * lda + k0 + ah;
+    const double* srcb = A + (size_t)(c0 + min(rj0 + br, m - 1)) * lda + k0 + bh;
+    auto gload = [&](int ch) {
+#pragma unroll
+      for (int q = 0; q < PA; ++q) ra[q] = srca[ch * KC + q];
+#pragma unroll
+      for (int q = 0; q < PB; ++q) rb[q] = srcb[ch * KC + q];
+    };
+    auto sstore = [&](int st) {
+      double* a = sm + (size_t)st * SS + ar * LKC + ah;
+#pragma unroll
+      for (int q = 0; q < PA; q += 2) *reinterpret_cast<double2*>(a + q) = make_double2(ra[q], ra[q + 1]);
+      double* b = sm + (size_t)st * SS + SA + br * LKC + bh;
+#pragma unroll
+      for (int q = 0; q < PB; q += 2) *reinterpret_cast<double2*>(b + q) = make_double2(rb[q], rb[q + 1]);
+    };
+    const int un = h == 0 ? u + 1 : u - 1 + ustep;
+    const int unc = min(un, nunits - 1);  // clamped: the prefetch is unconditional
+    gload(0);
+    __syncthreads();
+    sstore(0);
+    __syncthreads();
+    const int cpre = nch >= CP ? nch - CP : 0;
+    for (int ch = 0; ch < nch; ++ch) {
+      const int st = ch & 1;
+      if (ch + 1 < nch) gload(ch + 1);
+      if (ch == cpre) cload(unc, nxt);  // after the half's last chunk load (in-order vmcnt)
+      if (!skip) {
+        const double* As = sm + (size_t)st * SS;
+        const double* Bs = As + SA;
+#pragma unroll
+        for (int ks = 0; ks < KC / 4; ++ks) {
+          double fa[2], fb[2];
+#pragma unroll
+          for (int tr = 0; tr < 2; ++tr) fa[tr] = -As[(wrow + 16 * tr + li) * LKC + 4 * ks + lk];
+#pragma unroll
+          for (int tc = 0; tc < 2; ++tc) fb[tc] = Bs[(wcol + 16 * tc + li) * LKC + 4 * ks + lk];
+#pragma unroll
+          for (int tr = 0; tr < 2; ++tr)
+#pragma unroll
+            for (int tc = 0; tc < 2; ++tc)
+              acc[tr][tc] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[tr], fb[tc], acc[tr][tc], 0, 0, 0);
+        }
+      }
+      if (ch + 1 < nch) sstore(st ^ 1);
+      __syncthreads();
+    }
+    if (!skip) {
+#pragma unroll
+      for (int tr = 0; tr < 2; ++tr)
+#pragma unroll
+        for (int tc = 0; tc < 2; ++tc)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) {
+            const int row = ri0 + wrow + 16 * tr + lk + 4 * reg, col = rj0 + wcol + 16 * tc + li;
+            if (row < m && col < m) A[(size_t)(c0 + row) * lda + c0 + col] = acc[tr][tc][reg];
+          }
+    }
+#pragma unroll
+    for (int tr = 0; tr < 2; ++tr)
+#pragma unroll
+      for (int tc = 0; tc < 2; ++tc) acc[tr][tc] = nxt[tr][tc];
+    u = un;
+  }
+}
+
+template <int CP>
+static float time_big3(double* A, int lda, int n, int m, int kk, int reps, int grid) {
+  const int c0 = n + 1 - m, t2 = (m + TB - 1) / TB, ntb = t2 * (t2 + 1) / 2;
+  const int g = std::min(ntb, grid);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int r = 0; r < 3; ++r) k_big3<16, CP><<<g, kBigThreads>>>(A, lda, c0, m, 0, kk, ntb);
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) k_big3<16, CP><<<g, kBigThreads>>>(A, lda, c0, m, 0, kk, ntb);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  CK(hipGetLastError());
+  return 1e3f * ms / reps;
+}
+
+template <int MODE>
+static float time_big(double* A, int lda, int n, int m, int kk, int reps) {
+  const int c0 = n + 1 - m, t2 = (m + TB - 1) / TB, ntb = t2 * (t2 + 1) / 2;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int r = 0; r < 3; ++r) k_big<16, 4, MODE><<<ntb, kBigThreads>>>(A, lda, c0, m, 0, kk, ntb, 0);
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) k_big<16, 4, MODE><<<ntb, kBigThreads>>>(A, lda, c0, m, 0, kk, ntb, 0);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  CK(hipGetLastError());
+  return 1e3f * ms / reps;
+}
+
+int main() {
+  int ncu = 0;
+  CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+  const int n = 5994, lda = 6016;
+  double* A;
+  CK(hipMalloc(&A, sizeof(double) * (size_t)lda * (n + 1)));
+  {
+    std::vector<double> h((size_t)lda * (n + 1));
+    for (size_t i = 0; i < h.size(); ++i) h[i] = 1e-3 * (double)((i * 2654435761u) % 1000) / 1000.0;
+    CK(hipMemcpy(A, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+  }
+
+  // bitwise: the candidate against the shipped kernel, one launch each on copies of A
+  {
+    const size_t N = (size_t)lda * (n + 1);
+    double *A1, *A2;
+    CK(hipMalloc(&A1, N * sizeof(double)));
+    CK(hipMalloc(&A2, N * sizeof(double)));
+    std::vector<double> h1(N), h2(N);
+    for (int m : {5739, 3939, 2000, 333, 100}) {
+      const int c0 = n + 1 - m, t2 = (m + TB - 1) / TB, ntb = t2 * (t2 + 1) / 2;
+      CK(hipMemcpy(A1, A, N * sizeof(double), hipMemcpyDeviceToDevice));
+      CK(hipMemcpy(A2, A, N * sizeof(double), hipMemcpyDeviceToDevice));
+      k_big<16, 4, 0><<<ntb, kBigThreads>>>(A1, lda, c0, m, 0, 128, ntb, 0);
+      k_big3<16><<<std::min(ntb, 2 * ncu), kBigThreads>>>(A2, lda, c0, m, 0, 128, ntb);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(h1.data(), A1, N * sizeof(double), hipMemcpyDeviceToHost));
+      CK(hipMemcpy(h2.data(), A2, N * sizeof(double), hipMemcpyDeviceToHost));
+      size_t diff = 0;
+      for (size_t i = 0; i < N; ++i) diff += memcmp(&h1[i], &h2[i], 8) != 0;
+      printf("bitwise m=%5d: %zu differing doubles\n", m, diff);
+    }
+    CK(hipFree(A1));
+    CK(hipFree(A2));
+  }
+  for (int m : {5739, 4459, 3939, 2000}) {
+    const int kk = 128, reps = 20;
+    const float t0 = time_big<0>(A, lda, n, m, kk, reps);
+    const float t3 = time_big3<2>(A, lda, n, m, kk, reps, 2 * ncu);
+    const float t4 = time_big3<2>(A, lda, n, m, kk, reps, 1 << 30);
+    const float t5 = time_big3<4>(A, lda, n, m, kk, reps, 1 << 30);
+    const float t6 = time_big3<6>(A, lda, n, m, kk, reps, 1 << 30);
+    const float t7 = time_big<0>(A, lda, n, m, kk, reps);
+    printf("m=%5d  shipped %6.1f/%6.1f us  halves: persistent %6.1f  grid=tiles CP2 %6.1f CP4 %6.1f CP6 %6.1f us\n", m, t0, t7,
+           t3, t4, t5, t6);
+  }
+  for (int m : {5739, 4459, 3939, 2000}) {
+    const int kk = 128, reps = 20;
+    const float t0 = time_big<0>(A, lda, n, m, kk, reps);
+    const float t1 = time_big<1>(A, lda, n, m, kk, reps);
+    const float t2 = time_big<2>(A, lda, n, m, kk, reps);
+    const int tt = (m + TB - 1) / TB;
+    const double fl = (double)m * m * kk, by = 8.0 * m * (m + TB) / 2 * 2;
+    printf("m=%5d tiles=%4d  shipped %7.1f us (%5.1f TF)  no-C %7.1f us (%5.1f TF)  C-only %7.1f us (%5.2f TB/s)\n", m,
+           tt * (tt + 1) / 2, t0, fl / (t0 * 1e-6) / 1e12, t1, fl / (t1 * 1e-6) / 1e12, t2, by / (t2 * 1e-6) / 1e12);
+  }
+  CK(hipFree(A));
+  return 0;
+}
