@@ -250,6 +250,15 @@ void launch_final_sum(hipStream_t s, int grid, int K, const double* partial, dou
 // (three independent chains) instead of ~120 instructions with long-latency steps — the
 // table build is on the critical path of every evaluation pass (k_eval_bal's ablation: the
 // tables alone took 4 of a C3 launch's 23.5 us)
+// fma(a, b, k) with the 64-bit constant k in an SGPR pair (one VOP3 v_fma_f64, bitwise the
+// same as fma()): left to itself hipcc materialises every Horner coefficient into VGPRs (two
+// v_mov_b32 per step, since v_fmac needs its addend in the destination), which tripled the
+// VALU count of each series — the point tables of every k_eval_bal work-group run them
+__device__ __forceinline__ double fma_sk(double a, double b, double k) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+  return r;
+}
 template <int OFF>
 __device__ __forceinline__ double rodrigues_series(double x) {
   // coefficients (-1)^k / (2k + 1 + OFF)!, k = 0 .. 15
@@ -275,7 +284,7 @@ __device__ __forceinline__ double rodrigues_series(double x) {
   const double* k = OFF == 0 ? c : OFF == 1 ? d : e;
   double r = k[15];
 #pragma unroll
-  for (int i = 14; i >= 0; --i) r = fma(r, x, k[i]);
+  for (int i = 14; i >= 0; --i) r = fma_sk(r, x, k[i]);
   return r;
 }
 // R (row-major), t, Rd, Jd of one extrinsic (w, t): the table every pass reads
