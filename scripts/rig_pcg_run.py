@@ -16,6 +16,9 @@ sys.path.insert(0, ROOT)
 import _pkgload  # noqa: E402
 
 pkg = _pkgload.load()
+if os.environ.get("DAB_LIB"):  # another build of libdab (A/B)
+    abi = sys.modules[pkg.__name__ + "._abi"]
+    abi._LIB = abi.load_library(os.path.join(ROOT, os.environ["DAB_LIB"]))
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c5_rig_16x64"
 f32 = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 prob = pkg.synth(**pkg.CONFIGS[cfg])
