@@ -1,7 +1,8 @@
 // Decomposition of the dense Cholesky's bulk update (k_syrk_big, dab_chol.hip) at the n = 5994
 // shapes: the shipped kernel, the same kernel without its C tile traffic (MFMA + LDS pipeline
-// only), and C traffic only (no MFMA); plus the fp64 MFMA issue ceiling (16x16x4, independent
-// accumulators, 4 waves per SIMD) with the in-kernel clock.
+// only), and C traffic only (no MFMA); and two candidates that prefetch the next tile's C into
+// registers during the current tile's last K chunks (bitwise checked against the shipped kernel):
+// one work-group per CU (k_big2) and each super-tile as two row halves (k_big3).
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 scripts/syrk_big_probe.hip -o scripts/syrk_big_probe
 #include <hip/hip_runtime.h>
 
@@ -22,29 +23,6 @@
   } while (0)
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
-
-// ---- MFMA ceiling: each wave 8 independent accumulators, `iters` rounds ----
-__global__ __launch_bounds__(256) void k_mfma_peak(double* out, int iters, unsigned long long* clk) {
-  const int lane = threadIdx.x & 63;
-  double a = 1.0 + 1e-3 * lane, b = 1.0 - 1e-3 * lane;
-  dbl4 acc[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i] = dbl4{0.1 * i, 0.0, 0.0, 0.0};
-  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-  for (int it = 0; it < iters; ++it) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[i], 0, 0, 0);
-  }
-  const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-  double s = 0.0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
-  if (s == 12345.678) out[threadIdx.x] = s;
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    clk[0] = t1 - t0;
-    clk[1] = r1 - r0;
-  }
-}
 
 // ---- k_syrk_big (dab_chol.hip), MODE 0 as shipped, 1 no C load / store, 2 C only ----
 constexpr int TB = 128;
@@ -190,8 +168,7 @@ __global__ __launch_bounds__(kBigThreads, 2) void k_big2(double* __restrict__ A,
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) {
           const int row = ri0 + 64 * wr + 16 * tr + lk + 4 * reg, col = rj0 + 64 * wc + 32 * half + 16 * tc + li;
-          const double x = A[(size_t)(c0 + min(row, m - 1)) * lda + c0 + min(col, m - 1)];
-          cv[tr][tc][reg] = (row < m && col < m) ? x : 0.0;
+          cv[tr][tc][reg] = A[(size_t)(c0 + min(row, m - 1)) * lda + c0 + min(col, m - 1)];
         }
   };
   dbl4 acc[4][2], nxt[4][2];
@@ -204,21 +181,14 @@ __global__ __launch_bounds__(kBigThreads, 2) void k_big2(double* __restrict__ A,
     const bool skip = diag && wr < wc;
     const int ri0 = bi * TB, rj0 = bj * TB;
     double ra[PER], rb[PER];
-    const bool va = ri0 + lr < m, vb = rj0 + lr < m;
     const double* srca = A + (size_t)(c0 + min(ri0 + lr, m - 1)) * lda + k0 + lh;
     const double* srcb = A + (size_t)(c0 + min(rj0 + lr, m - 1)) * lda + k0 + lh;
     auto gload = [&](int ch) {
 #pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        const double x = srca[ch * KC + q];
-        ra[q] = va ? x : 0.0;
-      }
+      for (int q = 0; q < PER; ++q) ra[q] = srca[ch * KC + q];
       if (!diag) {
 #pragma unroll
-        for (int q = 0; q < PER; ++q) {
-          const double x = srcb[ch * KC + q];
-          rb[q] = vb ? x : 0.0;
-        }
+        for (int q = 0; q < PER; ++q) rb[q] = srcb[ch * KC + q];
       }
     };
     auto sstore = [&](int st) {
@@ -473,9 +443,17 @@ int main() {
       CK(hipDeviceSynchronize());
       CK(hipMemcpy(h1.data(), A1, N * sizeof(double), hipMemcpyDeviceToHost));
       CK(hipMemcpy(h2.data(), A2, N * sizeof(double), hipMemcpyDeviceToHost));
+      size_t diff3 = 0;
+      for (size_t i = 0; i < N; ++i) diff3 += memcmp(&h1[i], &h2[i], 8) != 0;
+      CK(hipMemcpy(A2, A, N * sizeof(double), hipMemcpyDeviceToDevice));
+      k_big2<16><<<std::min(ntb, ncu), kBigThreads>>>(A2, lda, c0, m, 0, 128, ntb);
+      CK(hipDeviceSynchronize());
+      printf("bitwise m=%5d: halves %zu differing doubles\n", m, diff3);
+      CK(hipMemcpy(h1.data(), A1, N * sizeof(double), hipMemcpyDeviceToHost));
+      CK(hipMemcpy(h2.data(), A2, N * sizeof(double), hipMemcpyDeviceToHost));
       size_t diff = 0;
       for (size_t i = 0; i < N; ++i) diff += memcmp(&h1[i], &h2[i], 8) != 0;
-      printf("bitwise m=%5d: %zu differing doubles\n", m, diff);
+      printf("bitwise m=%5d: one work-group per CU %zu differing doubles\n", m, diff);
     }
     CK(hipFree(A1));
     CK(hipFree(A2));
@@ -488,8 +466,9 @@ int main() {
     const float t5 = time_big3<4>(A, lda, n, m, kk, reps, 1 << 30);
     const float t6 = time_big3<6>(A, lda, n, m, kk, reps, 1 << 30);
     const float t7 = time_big<0>(A, lda, n, m, kk, reps);
-    printf("m=%5d  shipped %6.1f/%6.1f us  halves: persistent %6.1f  grid=tiles CP2 %6.1f CP4 %6.1f CP6 %6.1f us\n", m, t0, t7,
-           t3, t4, t5, t6);
+    const float t8 = time_big2(A, lda, n, m, kk, reps, ncu);
+    printf("m=%5d  shipped %6.1f/%6.1f us  halves: persistent %6.1f  grid=tiles CP2 %6.1f CP4 %6.1f CP6 %6.1f us"
+           "  one work-group per CU %6.1f us\n", m, t0, t7, t3, t4, t5, t6, t8);
   }
   for (int m : {5739, 4459, 3939, 2000}) {
     const int kk = 128, reps = 20;
