@@ -388,29 +388,36 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
       for (int reg = 0; reg < 4; ++reg) {
         const int row = bi * NB + wr * 32 + a2 * 16 + lk + 4 * reg;
         const int col = bj * NB + wc * 32 + b2 * 16 + li;
-        acc[a2][b2][reg] = (!skip && row < m && col < m) ? A[(size_t)(r0 + row) * lda + r0 + col] : 0.0;
+        // clamped, unconditional: an element outside the matrix (or in a skipped quadrant)
+        // is never stored, and no stored element depends on it
+        acc[a2][b2][reg] = A[(size_t)(r0 + min(row, m - 1)) * lda + r0 + min(col, m - 1)];
       }
   for (int k = k0; k < k0 + kk; k += NB) {
   const int kb = min(NB, k0 + kk - k);
   if (k != k0) __syncthreads();  // the previous chunk's LDS reads are done
-  // coalesced tile loads: 8 rows per pass, 32 double2 per row
+  // coalesced tile loads: 8 rows per pass, 32 double2 per row. Every load unconditional
+  // (row and column clamped into the matrix; a row past m only feeds outputs that are never
+  // stored), the columns past kb zeroed by a 0/1 factor: a select or a branch here made
+  // hipcc wait for each load before the next (one L2 round trip per row pass)
+  const int c2 = tid & 31;
+  const int ka = k + min(2 * c2, kb - 1), kb1 = k + min(2 * c2 + 1, kb - 1);
+  const double f0 = 2 * c2 < kb ? 1.0 : 0.0, f1 = 2 * c2 + 1 < kb ? 1.0 : 0.0;
+  double2 va[NB / 8], vb[NB / 8];
 #pragma unroll
   for (int q = 0; q < NB / 8; ++q) {
-    const int rr = (tid >> 5) + 8 * q, c2 = tid & 31;
-    const int ra = bi * NB + rr, rb = bj * NB + rr;
-    double2 va = make_double2(0.0, 0.0), vb = make_double2(0.0, 0.0);
-    if (ra < m) {
-      const double* src = A + (size_t)(r0 + ra) * lda + k + 2 * c2;
-      va.x = 2 * c2 < kb ? src[0] : 0.0;
-      va.y = 2 * c2 + 1 < kb ? src[1] : 0.0;
+    const int rr = (tid >> 5) + 8 * q;
+    const double* sa = A + (size_t)(r0 + min(bi * NB + rr, m - 1)) * lda;
+    va[q] = make_double2(sa[ka], sa[kb1]);
+    if (!diag) {
+      const double* sb = A + (size_t)(r0 + min(bj * NB + rr, m - 1)) * lda;
+      vb[q] = make_double2(sb[ka], sb[kb1]);
     }
-    if (!diag && rb < m) {
-      const double* src = A + (size_t)(r0 + rb) * lda + k + 2 * c2;
-      vb.x = 2 * c2 < kb ? src[0] : 0.0;
-      vb.y = 2 * c2 + 1 < kb ? src[1] : 0.0;
-    }
-    *reinterpret_cast<double2*>(&Pa[rr * LDP + 2 * c2]) = va;
-    if (!diag) *reinterpret_cast<double2*>(&Pb[rr * LDP + 2 * c2]) = vb;
+  }
+#pragma unroll
+  for (int q = 0; q < NB / 8; ++q) {
+    const int rr = (tid >> 5) + 8 * q;
+    *reinterpret_cast<double2*>(&Pa[rr * LDP + 2 * c2]) = make_double2(va[q].x * f0, va[q].y * f1);
+    if (!diag) *reinterpret_cast<double2*>(&Pb[rr * LDP + 2 * c2]) = make_double2(vb[q].x * f0, vb[q].y * f1);
   }
   __syncthreads();
   const double* PB = diag ? Pa : Pb;
