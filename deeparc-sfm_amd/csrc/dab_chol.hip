@@ -617,95 +617,103 @@ __global__ __launch_bounds__(kThreads) void k_trsv_back(const double* __restrict
 // Bulk trailing update of a panel PAIR on 128 x 128 super-tiles (rank kk <= 128: the two
 // 64-wide panels of the pair, so the trailing matrix is read and written once per two
 // panel steps): C(i, j) -= sum_{q in [k0, k0 + kk)} A(i, q) A(j, q) for c0 <= j <= i <
-// c0 + m. Persistent: work-group g walks the lower super-tiles t = g, g + grid, ...; per
-// tile the product streams through LDS in 16-wide K chunks, double-buffered (the next
-// chunk's global loads are in flight during the current chunk's MFMAs). Wave w owns the
-// 64 x 64 quadrant (w >> 1, w & 1): 4 x 4 tiles of v_mfma_f64_16x16x4f64, 64 fp64
-// accumulators per lane; a diagonal super-tile skips its strictly upper quadrant. All LDS
-// is one __shared__ array (a second one can make hipcc drain vmcnt before every ds_read).
+// c0 + m. Persistent: work-group g walks the lower super-tiles t = g, g + grid, ...; each
+// super-tile as two 64 x 128 row halves in sequence (units u = 2t + h). Per half the product
+// streams through LDS in 16-wide K chunks, double-buffered (the next chunk's global loads in
+// flight during the current chunk's MFMAs); wave w owns the 32 x 32 block (w & 1, w >> 1):
+// 2 x 2 tiles of v_mfma_f64_16x16x4f64, 16 accumulators per lane. The NEXT unit's C is
+// loaded into registers during the current unit's last CP chunks (after their chunk loads:
+// vmcnt counts in order), so the trailing matrix's HBM traffic overlaps the MFMAs instead of
+// stalling every unit's start (round 5, scripts/syrk_big_probe.hip: 126 -> 118 us at m =
+// 5739, 55.5 -> 51-52 us at m = 3939; the whole-tile form's C load and store were serial
+// with its MFMAs). Every element is C + the same MFMA sequence in k as before: bitwise the
+// same factor. A diagonal super-tile skips its strictly upper 64 x 64 quadrant. All LDS is
+// one __shared__ array (a second one can make hipcc drain vmcnt before every ds_read).
 constexpr int TB = 128;  // super-tile
 constexpr int kBigThreads = 512;
-// 8 waves: wave w owns the 64 x 32 half (w & 1) of quadrant w >> 1 (rows 64 (q >> 1), cols
-// 64 (q & 1)): 4 x 2 MFMA tiles, 32 accumulators per lane, so that ~110 VGPRs give 4 waves per
-// SIMD (two work-groups per CU) and one wave's waits are covered by another's MFMAs.
-template <int KC, int OCC>  // K chunk, waves per SIMD
-__global__ __launch_bounds__(kBigThreads, OCC) void k_syrk_big(double* __restrict__ A, int lda, int c0, int m, int k0,
-                                                            int kk, int ntiles) {
-  constexpr int LKC = KC + 2;                   // LDS row stride (doubles)
-  constexpr int PER = KC / 4;                   // doubles per thread and operand per chunk
-  constexpr int TPR = KC / PER;                 // loader threads per row (4)
-  __shared__ double sm[2 * 2 * TB * LKC];       // [stage][A | B][row][LKC]
+template <int KC, int CP>  // K chunk, chunks of the C prefetch window
+__global__ __launch_bounds__(kBigThreads, 4) void k_syrk_big(double* __restrict__ A, int lda, int c0, int m, int k0,
+                                                        int kk, int ntiles) {
+  constexpr int LKC = KC + 2;
+  constexpr int PA = KC / 8;  // A (the half's 64 rows): 8 loader threads per row
+  constexpr int PB = KC / 4;  // B (the tile's 128 columns): 4 loader threads per row
+  constexpr int SA = 64 * LKC, SS = SA + TB * LKC;
+  __shared__ double sm[2 * SS];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
-  const int qd = w >> 1, wr = qd >> 1, wc = qd & 1, half = w & 1;
-  const int lr = tid / TPR, lh = (tid % TPR) * PER;  // loader: row lr, k columns lh .. lh + PER - 1
-  const int nch = (kk + KC - 1) / KC;
-  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    int bi = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+  const int wrow = 32 * (w & 1), wcol = 32 * (w >> 1);
+  const int ar = tid >> 3, ah = (tid & 7) * PA, br = tid >> 2, bh = (tid & 3) * PB;
+  const int nch = kk / KC, nunits = 2 * ntiles, ustep = 2 * (int)gridDim.x;
+  auto coords = [&](int t, int& bi, int& bj) {
+    bi = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
     while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
     while (bi * (bi + 1) / 2 > t) --bi;
-    const int bj = t - bi * (bi + 1) / 2;
-    const bool diag = bi == bj;
-    const bool skip = diag && wr < wc;
-    const int ri0 = bi * TB, rj0 = bj * TB;  // relative to c0
-    double ra[PER], rb[PER];
-    // every load unconditional (row clamped to the last one, then zeroed by a select; kk is a
-    // multiple of KC: panels are NB wide), so the chunk loop carries no exec-mask branches
-    const bool va = ri0 + lr < m, vb = rj0 + lr < m;
-    const double* srca = A + (size_t)(c0 + min(ri0 + lr, m - 1)) * lda + k0 + lh;
-    const double* srcb = A + (size_t)(c0 + min(rj0 + lr, m - 1)) * lda + k0 + lh;
-    auto gload = [&](int ch) {
+    bj = t - bi * (bi + 1) / 2;
+  };
+  auto cload = [&](int u, dbl4(&cv)[2][2]) {
+    int bi, bj;
+    coords(u >> 1, bi, bj);
+    const int r0 = bi * TB + 64 * (u & 1) + wrow, q0 = bj * TB + wcol;
 #pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        const double x = srca[ch * KC + q];
-        ra[q] = va ? x : 0.0;
-      }
-      if (!diag) {
-#pragma unroll
-        for (int q = 0; q < PER; ++q) {
-          const double x = srcb[ch * KC + q];
-          rb[q] = vb ? x : 0.0;
-        }
-      }
-    };
-    auto sstore = [&](int st) {
-      double* a = sm + (size_t)(2 * st) * TB * LKC + lr * LKC + lh;
-#pragma unroll
-      for (int q = 0; q < PER; q += 2) *reinterpret_cast<double2*>(a + q) = make_double2(ra[q], ra[q + 1]);
-      if (!diag) {
-        double* b = a + TB * LKC;
-#pragma unroll
-        for (int q = 0; q < PER; q += 2) *reinterpret_cast<double2*>(b + q) = make_double2(rb[q], rb[q + 1]);
-      }
-    };
-    dbl4 acc[4][2];
-#pragma unroll
-    for (int tr = 0; tr < 4; ++tr)
+    for (int tr = 0; tr < 2; ++tr)
 #pragma unroll
       for (int tc = 0; tc < 2; ++tc)
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) {
-          const int row = ri0 + 64 * wr + 16 * tr + lk + 4 * reg, col = rj0 + 64 * wc + 32 * half + 16 * tc + li;
-          acc[tr][tc][reg] = (!skip && row < m && col < m) ? A[(size_t)(c0 + row) * lda + c0 + col] : 0.0;
+          const int row = r0 + 16 * tr + lk + 4 * reg, col = q0 + 16 * tc + li;
+          // clamped address, no select: an element outside the matrix is never stored, and
+          // no element inside depends on it (a select here becomes a branch + wait per load)
+          cv[tr][tc][reg] = A[(size_t)(c0 + min(row, m - 1)) * lda + c0 + min(col, m - 1)];
         }
+  };
+  dbl4 acc[2][2], nxt[2][2];
+  int u = 2 * (int)blockIdx.x;
+  if (u < nunits) cload(u, acc);
+  while (u < nunits) {
+    const int h = u & 1;
+    int bi, bj;
+    coords(u >> 1, bi, bj);
+    const bool skip = bi == bj && (w >> 2) > h;  // a strictly upper 64 x 64 quadrant
+    const int ri0 = bi * TB + 64 * h, rj0 = bj * TB;
+    double ra[PA], rb[PB];
+    const double* srca = A + (size_t)(c0 + min(ri0 + ar, m - 1)) * lda + k0 + ah;
+    const double* srcb = A + (size_t)(c0 + min(rj0 + br, m - 1)) * lda + k0 + bh;
+    auto gload = [&](int ch) {
+#pragma unroll
+      for (int q = 0; q < PA; ++q) ra[q] = srca[ch * KC + q];
+#pragma unroll
+      for (int q = 0; q < PB; ++q) rb[q] = srcb[ch * KC + q];
+    };
+    auto sstore = [&](int st) {
+      double* a = sm + (size_t)st * SS + ar * LKC + ah;
+#pragma unroll
+      for (int q = 0; q < PA; q += 2) *reinterpret_cast<double2*>(a + q) = make_double2(ra[q], ra[q + 1]);
+      double* b = sm + (size_t)st * SS + SA + br * LKC + bh;
+#pragma unroll
+      for (int q = 0; q < PB; q += 2) *reinterpret_cast<double2*>(b + q) = make_double2(rb[q], rb[q + 1]);
+    };
+    const int un = h == 0 ? u + 1 : u - 1 + ustep;
+    const int unc = min(un, nunits - 1);  // clamped: the prefetch is unconditional
     gload(0);
-    __syncthreads();  // the previous tile's LDS reads are done
+    __syncthreads();
     sstore(0);
     __syncthreads();
+    const int cpre = nch >= CP ? nch - CP : 0;
     for (int ch = 0; ch < nch; ++ch) {
       const int st = ch & 1;
       if (ch + 1 < nch) gload(ch + 1);
+      if (ch == cpre) cload(unc, nxt);  // after the half's last chunk load (in-order vmcnt)
       if (!skip) {
-        const double* As = sm + (size_t)(2 * st) * TB * LKC;
-        const double* Bs = diag ? As : As + TB * LKC;
+        const double* As = sm + (size_t)st * SS;
+        const double* Bs = As + SA;
 #pragma unroll
         for (int ks = 0; ks < KC / 4; ++ks) {
-          double fa[4], fb[2];
+          double fa[2], fb[2];
 #pragma unroll
-          for (int tr = 0; tr < 4; ++tr) fa[tr] = -As[(64 * wr + 16 * tr + li) * LKC + 4 * ks + lk];
+          for (int tr = 0; tr < 2; ++tr) fa[tr] = -As[(wrow + 16 * tr + li) * LKC + 4 * ks + lk];
 #pragma unroll
-          for (int tc = 0; tc < 2; ++tc) fb[tc] = Bs[(64 * wc + 32 * half + 16 * tc + li) * LKC + 4 * ks + lk];
+          for (int tc = 0; tc < 2; ++tc) fb[tc] = Bs[(wcol + 16 * tc + li) * LKC + 4 * ks + lk];
 #pragma unroll
-          for (int tr = 0; tr < 4; ++tr)
+          for (int tr = 0; tr < 2; ++tr)
 #pragma unroll
             for (int tc = 0; tc < 2; ++tc)
               acc[tr][tc] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[tr], fb[tc], acc[tr][tc], 0, 0, 0);
@@ -716,17 +724,23 @@ __global__ __launch_bounds__(kBigThreads, OCC) void k_syrk_big(double* __restric
     }
     if (!skip) {
 #pragma unroll
-      for (int tr = 0; tr < 4; ++tr)
+      for (int tr = 0; tr < 2; ++tr)
 #pragma unroll
         for (int tc = 0; tc < 2; ++tc)
 #pragma unroll
           for (int reg = 0; reg < 4; ++reg) {
-            const int row = ri0 + 64 * wr + 16 * tr + lk + 4 * reg, col = rj0 + 64 * wc + 32 * half + 16 * tc + li;
+            const int row = ri0 + wrow + 16 * tr + lk + 4 * reg, col = rj0 + wcol + 16 * tc + li;
             if (row < m && col < m) A[(size_t)(c0 + row) * lda + c0 + col] = acc[tr][tc][reg];
           }
     }
+#pragma unroll
+    for (int tr = 0; tr < 2; ++tr)
+#pragma unroll
+      for (int tc = 0; tc < 2; ++tc) acc[tr][tc] = nxt[tr][tc];
+    u = un;
   }
 }
+
 
 // Back substitution L^T y = z in ONE launch (instead of one per block): grid G <= CUs,
 // every work-group resident. Per block b, last first, every work-group computes y_b =
