@@ -1,16 +1,16 @@
 #!/bin/bash
-# Round-5 final record on the final library (sixth run: after the SGPR-constant series): -m gpu suite, smoke, the profile set (PMC
+# Round-5 final record on the final library (seventh run: after the Cholesky load fixes): -m gpu suite, smoke, the profile set (PMC
 # traffic + VALU, bench line, kernel stats), k_eval_bal's instruction mix
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
-timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/r05zi_pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/r05zi_pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r05zi_smoke.log 2>&1
-rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/r05zi_smoke.log; [ $rc -eq 0 ] || exit $rc
-TAG=r05zi bash scripts/gpu_prof.sh || exit $?
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/r05zj_pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/r05zj_pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r05zj_smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/r05zj_smoke.log; [ $rc -eq 0 ] || exit $rc
+TAG=r05zj bash scripts/gpu_prof.sh || exit $?
 MIX="SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT"
-rm -rf gpurun_out/r05zi_mix
-timeout -s KILL 120 rocprofv3 --pmc $MIX -d gpurun_out/r05zi_mix -o run --output-format csv -- python3 bench.py --no-cpu --no-lm --no-c2 --no-c4 --no-rig --no-c1 --steps 10 --warmup 2 > gpurun_out/r05zi_mix.log 2>&1
+rm -rf gpurun_out/r05zj_mix
+timeout -s KILL 120 rocprofv3 --pmc $MIX -d gpurun_out/r05zj_mix -o run --output-format csv -- python3 bench.py --no-cpu --no-lm --no-c2 --no-c4 --no-rig --no-c1 --steps 10 --warmup 2 > gpurun_out/r05zj_mix.log 2>&1
 rc=$?; echo "mix rc=$rc"; [ $rc -eq 0 ] || exit $rc
-python3 scripts/pmc_mix.py k_eval_bal gpurun_out/r05zi_mix | tee gpurun_out/r05zi_mix.txt
+python3 scripts/pmc_mix.py k_eval_bal gpurun_out/r05zj_mix | tee gpurun_out/r05zj_mix.txt
