@@ -1135,7 +1135,7 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
   // strip (round 5): the bulk's first block column (the next group's first column) is a
   // launch of its own on s2, so the chain's next column update waits for it only and runs
   // beside the rest of the bulk instead of alone after it; the group's last column waits
-  // for the whole bulk. n = 5994: 5.63 -> 4.95-5.0 ms (scripts/r05ai.sh)
+  // for the whole bulk. n = 5994: 5.63 -> 4.95-5.0 ms (scripts/runs/r05ai.sh)
   const bool strip = c->strip;
   for (int b = 0; b + 1 < nblk; b += R) {
     const int prev = pending;

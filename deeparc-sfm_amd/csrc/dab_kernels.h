@@ -32,6 +32,11 @@ constexpr int kFxCopies = 32;   // shards (work-group b adds into shard b % kFxC
 constexpr int kFxWords = kFxStride * kFxCopies;
 constexpr int kFxLimbs = 5;
 constexpr int kFxBad = kFxLimbs;  // word of the non-finite count
+// word kFxErr of shard 0: error bits of the pass that filled the set (k_eval_bal's bounded
+// waits). It is zeroed with the set and summed by the cost's all-reduce, so a wait that ran
+// out on one rank is seen by every rank at the same read.
+constexpr int kFxErr = kFxBad + 1;
+inline unsigned long long cost_fx_err(const unsigned long long* words) { return words[kFxErr]; }
 // host side: the summed shards of one set -> {sum r^2, non-finite count}
 inline void cost_fx_total(const unsigned long long* words, double& sum, double& bad) {
   unsigned long long acc[kFxLimbs + 1] = {0, 0, 0, 0, 0, 0};
@@ -122,12 +127,18 @@ void launch_eval_cams(hipStream_t s, const DevView& v, const ChunkLists& cl, con
 // point side -> V, g, cost in fixed point as launch_eval_points): one launch, camera and
 // point waves side by side. fused_eval_fits: whether the problem qualifies for `grid`.
 bool fused_eval_fits(const DevView& v, int nchunk, int ngen, int ncross, int grid);
-// k_eval_bal (needs v.obs_e, the packed point-side records): side 0 both halves; 1 the point
-// side only (V, g, cost); 2 the camera side only (ug) — the multi-rank split schedule runs the
-// same machine code with a run-time side, so both schedules give bitwise the same sums;
-// 3..6 timing ablations (wrong results). camtab non-null: R,t and the camera frames copied
-// from the tables of the current x instead of built. err: error word (a bounded wait timed
-// out; 0 = ok)
+// k_eval_bal (needs v.obs_e, the packed point-side records): side kSideBoth both halves;
+// kSidePoints the point side only (V, g, cost; the camera waves return at once, no frames);
+// kSideCams the camera side only (ug; the point waves return at once, no tables, no
+// intrinsic DMA) — the multi-rank split schedule runs the same machine code with a run-time
+// side, so both schedules give bitwise the same sums; | kSideTestTimeout (a test flag) a frame
+// wait that never completes, so the pass must fail closed. Builds with -DDAB_ABLATIONS add the
+// timing ablations 3..6 (wrong results); release builds never launch them (eval_pass
+// refuses DAB_EVAL_SIDE outside {0, 7}). camtab non-null: R,t and the camera frames copied
+// from the tables of the current x instead of built. err: sticky per-handle error word;
+// costfx[kFxErr] (shard 0) gets the same bits, so the error travels with the cost's
+// all-reduce and every rank fails the same call (0 = ok)
+constexpr int kSideBoth = 0, kSidePoints = 1, kSideCams = 2, kSideTestTimeout = 16;
 void launch_eval_bal(hipStream_t s, const DevView& v, const int* chunk_beg, const double* points, const double* ext,
                      const double* camtab, double* V, double* g, double* ug, unsigned long long* costfx,
                      unsigned long long* fx_next, unsigned* err, int grid, int side);

@@ -1895,7 +1895,7 @@ constexpr int kBalCW = 16 - kBalPW;    // camera waves
 constexpr int kBalFrame = 28;          // doubles per shared camera frame: R t K J_l small
 // first part of a two-part camera chunk, in 1/1024: the older waves (part 0) get more, since
 // the SIMDs' oldest-first issue starves the younger ones (round 3's per-wave timeline: 688 for
-// k_eval_fused; re-swept for k_eval_bal in round 5, scripts/r05aq.sh: 840 at 21.8 us against
+// k_eval_fused; re-swept for k_eval_bal in round 5, scripts/runs/r05aq.sh: 840 at 21.8 us against
 // 22.0-22.3 us for 600-780 and 900-960, interleaved repetitions on one box)
 constexpr int kCamSplit = 840;
 bool fused_eval_fits(const DevView& v, int nchunk, int ngen, int ncross, int grid) {
@@ -1918,13 +1918,16 @@ static int fused_wps(int nslice, int E, int grid) {
   return w;
 }
 // spin on a work-group word until it reaches `want`, bounded by an iteration count (~2^20
-// sleeps, a fraction of a second; then the error word gets `code` and the wave goes on, its
-// results void: the pass fails closed)
-__device__ __forceinline__ void lds_wait_ge(const unsigned* w, unsigned want, unsigned* err, unsigned code) {
+// sleeps, a fraction of a second; then the error words get `code` and the wave goes on, its
+// results void: the pass fails closed). err: the handle's sticky word (dab_sync); errfx: the
+// pass's cost set (word kFxErr), all-reduced with the cost so that every rank fails together
+__device__ __forceinline__ void lds_wait_ge(const unsigned* w, unsigned want, unsigned* err,
+                                            unsigned long long* errfx, unsigned code) {
   for (unsigned n = 0; __hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want; ++n) {
     __builtin_amdgcn_s_sleep(1);
     if (n > (1u << 20)) {
       __hip_atomic_fetch_or(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_or(errfx + kFxErr, (unsigned long long)code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
   }
@@ -1995,13 +1998,26 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     if (lane == 0) __hip_atomic_store(&tbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
 
+  // what this launch runs (the split schedule's point-side launch builds no camera frames, its
+  // camera-side launch no point tables and no intrinsic DMA); the timing ablations 3..6 exist
+  // only in -DDAB_ABLATIONS builds
+  const bool test_timeout = (side & kSideTestTimeout) != 0;
+  side &= ~kSideTestTimeout;
+#ifdef DAB_ABLATIONS
+  const bool abl_tables_only = side == 3, abl_no_tabs = side == 4 || side == 5, abl_no_frames = side == 4 || side == 6;
+#else
+  constexpr bool abl_tables_only = false, abl_no_tabs = false, abl_no_frames = false;
+#endif
   if (wave >= kBalPW) {
     // ---------------- camera side ----------------
+    if (side == kSidePoints || abl_tables_only) {
+      DAB_STAMP(3);
+      return;
+    }
     const int cw = wave - kBalPW, part = cw / nsl, slot = cw - part * nsl;
     const int c = cam_of(slot);  // one round (fused_eval_fits / fused_wpc)
-    if (cw == 0 && side != 4 && side != 6) build_frames();
-    if (side == 1 || side == 3 || c >= v.NC) {  // timing ablations: 3 the tables only, 5 no point tables,
-                                                 // 6 no camera frames (both sides run, wrong results)
+    if (cw == 0 && !abl_no_frames) build_frames();
+    if (c >= v.NC) {
       DAB_STAMP(3);
       return;
     }
@@ -2016,9 +2032,9 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     for (int i = 0; i < 27; ++i) acc[i] = 0.0;
     const double* fr = cfr[slot];
     eval_cams_gather_f(v.cm_pt, v.cm_xy, points, lo + lane, hi, acc, [&]() {
-      // the frames, built while the first gathers fly (side 7, a test: a frame flag that never
-      // comes — the wait must run out and fail the pass closed)
-      if (side != 4 && side != 6) lds_wait_ge(&tbar, side == 7 ? 2u : 1u, err, 1u);
+      // the frames, built while the first gathers fly (kSideTestTimeout, a test: a frame flag
+      // that never comes — the wait must run out and fail the pass closed)
+      if (!abl_no_frames) lds_wait_ge(&tbar, test_timeout ? 2u : 1u, err, costfx, 1u);
       const UniFrame f(UniFrame::FromShared{}, fr);
       DAB_STAMP(1);
       return f;
@@ -2050,9 +2066,13 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   }
 
   // ---------------- point side ----------------
+  if (side == kSideCams) {  // the split schedule's camera-side launch: nothing for the point waves
+    DAB_STAMP(3);
+    return;
+  }
   const size_t NPs = (size_t)v.NP;
   const int pw = wave, pslots = kBalPW / wps, slot = pw / wps, part = pw - slot * wps;
-  const int rounds = (side == 2 || side == 3) ? 0 : (v.nslice + pslots * gridDim.x - 1) / (pslots * gridDim.x);
+  const int rounds = abl_tables_only ? 0 : (v.nslice + pslots * gridDim.x - 1) / (pslots * gridDim.x);
   constexpr int D = 3;
   int qe[D];      // packed records (ext | intr << 16, -1 = padding)
   double2 qxy[D];
@@ -2083,7 +2103,7 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   // a C3 launch went to the point tables, r05l)
   constexpr int kTabPer = (kLdsCams + kBalPW * 64 - 1) / (kBalPW * 64);
   double xr[kTabPer][12];  // camtab: R,t as they are; else the 6 parameters
-  const bool tabs_now = side != 4 && side != 5;
+  const bool tabs_now = !abl_no_tabs;
   if (tabs_now) {
 #pragma unroll
     for (int j = 0; j < kTabPer; ++j) {
@@ -2133,9 +2153,9 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   // barrier of the point waves only (LDS counter): own LDS writes and the K LDS-DMA retired
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_fetch_add(&kbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  lds_wait_ge(&kbar, (unsigned)kBalPW, err, 1u);
+  lds_wait_ge(&kbar, (unsigned)kBalPW, err, costfx, 1u);
   DAB_STAMP(1);
-  if (side == 2 || side == 3) return;
+  if (abl_tables_only) return;
   const LdsTabs<true, false> tabs{rt_s, k_s, nullptr, v.intr};
   double acc[2] = {0.0, 0.0};
   for (int r = 0; r < rounds; ++r) {

@@ -124,8 +124,17 @@ void pinned_give(void* p, size_t bytes) {
 
 extern "C" int dab_release_caches(void) {
   std::lock_guard<std::mutex> lk(dab::cache_mu());
-  for (auto& kv : dab::stream_cache())
+  // only idle cached objects live here (a handle takes its streams out of the cache and
+  // gives them back on destroy), so live handles are unaffected; each device's streams are
+  // destroyed with that device current
+  int cur = 0;
+  const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+  for (auto& kv : dab::stream_cache()) {
+    if (kv.second.empty()) continue;
+    (void)hipSetDevice(kv.first);
     for (hipStream_t s : kv.second) (void)hipStreamDestroy(s);
+  }
+  if (have_cur) (void)hipSetDevice(cur);
   dab::stream_cache().clear();
   for (auto& kv : dab::pinned_cache())
     for (void* p : kv.second) (void)hipHostFree(p);
@@ -298,10 +307,12 @@ struct Knobs {
   int p2p = -1;             // DAB_P2P: one-shot xGMI all-reduce of small sums (-1 auto: RCCL handles
                             // only; 1 also on host-staged handles, the one-GPU rehearsal; 0 off)
   int setup_host = 0;       // DAB_SETUP_HOST=1: dab_set_problem's host passes instead of the device ones
-  int eval_side = 0;        // DAB_EVAL_SIDE (timing ablation, wrong results): k_eval_bal's single launch runs
-                            // 1 the point side only, 2 the camera side only, 3 the tables only, 4 no
-                            // tables or frames, 5 no point tables, 6 no camera frames; 7 (test) a
-                            // frame wait that times out (the pass must fail with DAB_E_DEVICE)
+  int eval_side = 0;        // DAB_EVAL_SIDE: 7 (test) a k_eval_bal frame wait that times out (the pass
+                            // must fail with DAB_E_DEVICE on every rank). Builds with -DDAB_ABLATIONS
+                            // also take the timing ablations (wrong results) 1 the point side only, 2
+                            // the camera side only, 3 the tables only, 4 no tables or frames, 5 no
+                            // point tables, 6 no camera frames; a release build refuses them
+                            // (eval_side_ok: DAB_E_INVALID) instead of returning wrong sums
   int fused_tab = -1;       // DAB_FUSED_TAB: the fused pass reads the camera tables of the current x
                             // instead of building them in every work-group — -1 (default) when they
                             // exist already (the LM loop: the accepted candidate's tables), 1 always
@@ -326,6 +337,14 @@ struct Knobs {
     get("DAB_FUSED_TAB", fused_tab);
     get("DAB_SETUP_HOST", setup_host);
     get("DAB_EVAL_SIDE", eval_side);
+  }
+  // the evaluation side this build accepts from DAB_EVAL_SIDE
+  bool eval_side_ok() const {
+#ifdef DAB_ABLATIONS
+    return eval_side >= 0 && eval_side <= 7;
+#else
+    return eval_side == 0 || eval_side == 7;
+#endif
   }
 };
 
@@ -2799,6 +2818,9 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
   hipStream_t s = h->stream;
   const DevView& v = h->view;
   bool overlapped = false;
+  if (!h->knobs.eval_side_ok())
+    return set_error(DAB_E_INVALID, "DAB_EVAL_SIDE=" + std::to_string(h->knobs.eval_side) +
+                                        " is a timing ablation (wrong results): only -DDAB_ABLATIONS builds run it");
   // the fused pass reads the tables when the caller has them (the LM loop) — C3: 21.3
   // against 23.2 us per launch — but does not launch a table build of its own for them
   // (k_cam_tables in front of the pass cost more than it saves: 25.6 against 23.9 us per
@@ -2816,8 +2838,10 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
     launch_eval_bal(s, v, h->d_chunk_beg, h->d_points, h->d_ext, fused_tab ? h->d_camtab : nullptr, h->d_V, h->d_g,
                     h->ug(), h->cost_fx(h->fx_last), h->cost_fx(h->fx_last ^ 1), h->xerr(), grid, side);
   };
+  // DAB_EVAL_SIDE=7: the test's frame wait that never completes; ablation builds: 1..6
+  const int test_flag = h->knobs.eval_side == 7 ? kSideTestTimeout : 0;
   if (h->fused && !h->fused_split) {  // both halves of the pass in one launch
-    eval_fused(h->ncu, h->knobs.eval_side);
+    eval_fused(h->ncu, h->knobs.eval_side == 7 ? kSideBoth | test_flag : h->knobs.eval_side);
     if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
     if (h->NC > 0) CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
     return 0;
@@ -2827,7 +2851,7 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
     // RCCL all-reduce runs on the communication stream during the point side (which
     // leaves one CU per XCD free for it: eval_grid)
     if (ev_mid) HIP_OK(hipEventRecord(ev_mid, s));
-    eval_fused(h->ncu, 2);
+    eval_fused(h->ncu, kSideCams | test_flag);
     bool ovl = false;
     if (h->can_overlap()) {
       HIP_OK(hipEventRecord(h->ev_cam, s));
@@ -2838,7 +2862,7 @@ static int eval_pass(dab_handle* h, bool camtab_ready, hipEvent_t ev_mid = nullp
     } else {
       CHECK_RC(h->allreduce(h->d_camred, h->camred_count(), ncclSum));
     }
-    eval_fused(h->eval_grid, 1);
+    eval_fused(h->eval_grid, kSidePoints);
     if (ev_end) HIP_OK(hipEventRecord(ev_end, s));
     if (ovl) HIP_OK(hipStreamWaitEvent(s, h->ev_comm, 0));
     return 0;
@@ -2916,12 +2940,18 @@ static int eval_jacobian_and_blocks(dab_handle* h, bool with_norms, bool tables_
   return 0;
 }
 
-// k_eval_bal's error word: a bounded work-group wait timed out, the pass's results are void
-static int xerr_check(dab_handle* h) {
+// k_eval_bal's error bits: a bounded work-group wait timed out, the pass's results are void
+static int xerr_fail(unsigned long long e) {
+  return set_error(DAB_E_DEVICE, "evaluation pass: a work-group wait timed out (code " + std::to_string(e) + ")");
+}
+// the handle's sticky error word (dab_sync after bench passes), cleared once read
+static int xerr_check_sticky(dab_handle* h) {
   unsigned e = 0;
   std::memcpy(&e, h->h_scal + S_XERR, sizeof(e));
   if (e == 0) return 0;
-  return set_error(DAB_E_DEVICE, "evaluation pass: a work-group wait timed out (code " + std::to_string(e) + ")");
+  HIP_OK(hipMemsetAsync(h->d_scal + S_XERR, 0, sizeof(double), h->stream));
+  HIP_OK(hipStreamSynchronize(h->stream));
+  return xerr_fail(e);
 }
 static int read_scalars(dab_handle* h) {
   HIP_OK(hipMemcpyAsync(h->h_scal, h->d_scal, sizeof(double) * S_NSLOTS, hipMemcpyDeviceToHost, h->stream));
@@ -2931,14 +2961,20 @@ static int read_scalars(dab_handle* h) {
   // before any decision is taken on it (every rank's next call fails the same way)
   CHECK_RC(p2p_check(h->p2p_main));
   CHECK_RC(p2p_check(h->p2p_comm));
-  CHECK_RC(xerr_check(h));
   if (h->cost_fx_pending) {
     // the last evaluation pass left its cost in fixed point (cost_fx_commit): exact
-    // integer limb sums, converted once here
+    // integer limb sums, converted once here. Its error bits (kFxErr) were summed over the
+    // ranks with the cost (allreduce_cost), so a wait that ran out on any rank fails this
+    // call on every rank, before any decision is taken on the pass
     unsigned long long w[kFxWords];
     std::memcpy(w, h->h_scal + S_CFX + (size_t)kFxWords * h->fx_last, sizeof(w));
-    cost_fx_total(w, h->h_scal[S_COST], h->h_scal[S_COST_BAD]);
     h->cost_fx_pending = false;
+    if (const unsigned long long e = cost_fx_err(w)) {
+      HIP_OK(hipMemsetAsync(h->d_scal + S_XERR, 0, sizeof(double), h->stream));  // reported here
+      HIP_OK(hipStreamSynchronize(h->stream));
+      return xerr_fail(e);
+    }
+    cost_fx_total(w, h->h_scal[S_COST], h->h_scal[S_COST_BAD]);
   }
   return 0;
 }
@@ -3056,6 +3092,9 @@ static int solve_impl(dab_handle* h, const dab_options* opt_in, dab_summary* sum
   const bool in_global = true;  (void)in_global;
 
   // ---- iteration 0 ----
+  // a solve starts with a clean sticky error word (a timed-out wait of an earlier call was
+  // reported by that call)
+  HIP_OK(hipMemsetAsync(h->d_scal + S_XERR, 0, sizeof(double), s));
   double t0 = now_s();
   CHECK_RC(eval_jacobian_and_blocks(h, true));
   CHECK_RC(read_scalars(h));
@@ -3523,7 +3562,7 @@ extern "C" int dab_sync(dab_handle* h) {
   HIP_OK(hipStreamSynchronize(h->stream));
   if (h->d_scal) {
     HIP_OK(hipMemcpy(h->h_scal + S_XERR, h->d_scal + S_XERR, sizeof(double), hipMemcpyDeviceToHost));
-    CHECK_RC(xerr_check(h));
+    CHECK_RC(xerr_check_sticky(h));
   }
   return 0;
 }

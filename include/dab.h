@@ -215,7 +215,10 @@ int dab_create_dist_host(int device, int rank, int world_size, dab_host_allreduc
  * instead of reused. */
 int dab_destroy(dab_handle* h);
 /* Destroys the cached streams and frees the cached pinned blocks (an embedding process that
- * resets the device, or wants the memory back). Call with no handle alive. */
+ * resets the device, or wants the memory back). Safe with handles alive: it touches only
+ * the idle objects in the cache, never a live handle's own streams or pinned blocks (each
+ * stream is destroyed with its own device current, the caller's device restored). To get
+ * every stream back, destroy the handles first. */
 int dab_release_caches(void);
 
 /* ---- problem upload / solve ------------------------------------------------------------

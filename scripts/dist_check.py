@@ -35,6 +35,17 @@ def main():
     ap.add_argument("--expect-no-p2p", action="store_true",
                     help="fail if the peer-to-peer path is in use (its set-up self-test must have "
                     "failed over to the other collectives)")
+    ap.add_argument("--solvers", default="explicit,pcg,auto",
+                    help="comma list of the linear solvers to check (explicit, pcg, auto)")
+    ap.add_argument("--tol", type=float, default=1e-8,
+                    help="largest relative per-iteration cost difference against the single handle")
+    ap.add_argument("--expect-cg-equal", action="store_true",
+                    help="fail unless every iteration's CG count equals the single handle's")
+    ap.add_argument("--expect-auto", default="",
+                    help="fail unless AUTO ran this solver on the ranks (explicit | pcg)")
+    ap.add_argument("--timeout-rank", type=int, default=-1,
+                    help="this rank's evaluation pass runs a frame wait that never completes "
+                    "(DAB_EVAL_SIDE=7): every rank's dab_solve must fail with the timeout, none may hang")
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dev = a.device if a.device >= 0 else int(os.environ.get("LOCAL_RANK", "0"))
@@ -54,6 +65,36 @@ def main():
         t = torch.from_numpy(arr)
         dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
 
+    if a.timeout_rank >= 0:
+        # one rank's pass times out inside the launch; its error word travels with the cost's
+        # all-reduce, so every rank must fail the same call (DAB_E_DEVICE), none may hang
+        if rank == a.timeout_rank:
+            os.environ["DAB_EVAL_SIDE"] = "7"  # read when the handle is created
+        glob = pkg.synth(**pkg.CONFIGS[a.config]) if a.config else \
+            pkg.synth(kind=0, num_cameras=40, num_points=4000, obs_per_point=6, seed=61)
+        s = pkg.Solver(dev, rank, world, uid, host_allreduce=gloo_allreduce if a.host_collective else None)
+        msg = ""
+        try:
+            s.set_problem(glob.copy().shard(rank, world))
+            sched = s.eval_fused()
+            s.solve(pkg.options(max_num_iterations=3))
+        except RuntimeError as e:
+            msg = str(e)
+        finally:
+            s.close()
+        failed = torch.tensor([1 if "timed out" in msg else 0], dtype=torch.int32)
+        dist.all_reduce(failed)
+        if rank == 0:
+            ok = int(failed.item()) == world and sched == 2
+            sys.stdout.write(f"DIST_CHECK {'OK' if ok else 'FAIL'} timeout: {int(failed.item())}/{world} ranks "
+                             f"failed closed, eval schedule {sched}, rank 0: {msg!r}\n")
+            sys.stdout.flush()
+        dist.destroy_process_group()
+        return
+
+    names = {"explicit": pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR, "pcg": pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG,
+             "auto": pkg.DAB_LINEAR_SOLVER_AUTO}
+    solvers = [names[x] for x in a.solvers.split(",")]
     out = {}
     for kind in ((a.config,) if a.config else ("bal", "rig")):
         if kind == "bal":
@@ -68,8 +109,7 @@ def main():
             for _ in range(3):
                 h = pkg.Solver(dev, rank, world, uid, host_allreduce=gloo_allreduce if a.host_collective else None)
                 live.append(h)
-        for li, lst in enumerate((pkg.DAB_LINEAR_SOLVER_EXPLICIT_SCHUR, pkg.DAB_LINEAR_SOLVER_IMPLICIT_SCHUR_PCG,
-                                  pkg.DAB_LINEAR_SOLVER_AUTO)):
+        for li, lst in enumerate(solvers):
             opts = pkg.options(max_num_iterations=a.iters, linear_solver_type=lst)
             ref = None
             if rank == 0:
@@ -110,6 +150,8 @@ def main():
                     iters=(summ["num_iterations"], rs["num_iterations"]),
                     term=(summ["termination"], rs["termination"]),
                     max_rel_cost=float(max(abs(x - y) / abs(y) for x, y in zip(ca[:n], cb[:n]))),
+                    cg_equal=[it["linear_solver_iterations"] for it in summ["iterations"]]
+                    == [it["linear_solver_iterations"] for it in rs["iterations"]],
                     final=(summ["final_cost"], rs["final_cost"]),
                     dpts=float(np.abs(pts.numpy() - rp).max()),
                     dext=float(np.abs(ext.numpy() - re).max()),
@@ -120,8 +162,12 @@ def main():
             h.close()
     if rank == 0:
         print(json.dumps(out, indent=1))
+        auto_want = names.get(a.expect_auto, None)
         bad = [k for k, v in out.items()
-               if v["iters"][0] != v["iters"][1] or v["max_rel_cost"] > 1e-8 or v["dpts"] > 1e-6
+               if v["iters"][0] != v["iters"][1] or v["max_rel_cost"] > a.tol or v["dpts"] > 1e-6
+               or (a.expect_cg_equal and not v["cg_equal"])
+               or (auto_want is not None and k.endswith(f"_{pkg.DAB_LINEAR_SOLVER_AUTO}")
+                   and v["solver_used"][0] != auto_want)
                or v["dext"] > 1e-6 or not v["ext_ranks_equal"]
                or (not k.startswith("rig") and v["eval_schedule"] != 2)  # BAL shards: the split fused pass
                or (a.expect_p2p and v["p2p"] != 1)

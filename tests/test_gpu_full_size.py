@@ -140,6 +140,29 @@ def test_c4_shape_two_ranks_match_single_handle(gpu):
     assert "DIST_CHECK OK" in p.stdout, p.stdout[-3000:]
 
 
+def test_c4_shape_four_ranks_p2p_match_single_handle(gpu):
+    """BASELINE config 4 as the 8-GPU node runs it, rehearsed on one GPU: the C3 global
+    problem point-sharded over FOUR ranks, every camera-sized sum (the camera blocks on the
+    communication stream beside the point side, the PCG products and preconditioner blocks,
+    the fixed-point cost words) through the one-shot peer-to-peer all-reduce (same-device
+    IPC, DAB_P2P=1). AUTO must pick PCG (a large camera system on several ranks), the
+    transport must report P2P, and the LM trajectory must equal the single handle's to 1e-12
+    per iteration with the same CG counts."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, DAB_P2P="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "scripts", "dist_check.py"), "--device", "0", "--host-collective",
+           "--config", "c3_1kcam", "--iters", "3", "--solvers", "pcg,auto", "--tol", "1e-12",
+           "--expect-auto", "pcg", "--expect-p2p", "--expect-cg-equal"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "DIST_CHECK OK" in p.stdout, p.stdout[-3000:]
+    assert "not verified" not in p.stderr, p.stderr[-3000:]
+
+
 def test_near_branch_jacobian_gap_vs_autodiff(pkg, orc, gpu):
     """The analytic HIP Jacobian against the golden vectors (1e-11 everywhere) and against the
     oracle's forward-mode autodiff, whose w = aa / theta loses digits just above Ceres'

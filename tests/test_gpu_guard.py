@@ -13,6 +13,7 @@ process-wide mode, so each case runs in a fresh child process:
   * the net's self-test (DAB_DEV_GUARD=2 dirties one canary after set-up): the set-up must
     fail with DAB_E_DEVICE naming the overrun block, not return normally."""
 import os
+import socket
 import subprocess
 import sys
 
@@ -97,5 +98,63 @@ def test_eval_pass_wait_timeout_fails_closed(pkg, gpu, monkeypatch):
         assert s.eval_fused() == 1
         with pytest.raises(RuntimeError, match="timed out"):
             s.solve(pkg.options(max_num_iterations=2))
+        # the failure was reported by that call: the next call starts clean and fails on its
+        # own pass again (not on a stale word)
+        with pytest.raises(RuntimeError, match="timed out"):
+            s.solve(pkg.options(max_num_iterations=2))
+    finally:
+        s.close()
+    # the same handle without the test side solves normally after a re-create
+    monkeypatch.delenv("DAB_EVAL_SIDE")
+    s = pkg.Solver(0)
+    try:
+        s.set_problem(prob.copy())
+        assert s.solve(pkg.options(max_num_iterations=2))["num_iterations"] >= 1
+    finally:
+        s.close()
+
+
+@pytest.mark.parametrize("bad_rank", [0, 1])
+def test_eval_pass_wait_timeout_fails_every_rank(gpu, bad_rank):
+    """The same bounded wait running out on ONE rank of a sharded solve (the split schedule's
+    camera-side launch): its error bits ride in the fixed-point cost words, which every rank
+    all-reduces before it reads the pass, so every rank's dab_solve fails with the timeout
+    at the same call — no rank goes on into the next collective and hangs."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "scripts", "dist_check.py"), "--device", "0", "--host-collective",
+           "--timeout-rank", str(bad_rank)]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "DIST_CHECK OK" in p.stdout, p.stdout[-3000:]
+
+
+@pytest.mark.parametrize("side", ["1", "2", "3", "4", "5", "6"])
+def test_release_library_refuses_eval_ablations(pkg, gpu, monkeypatch, side):
+    """DAB_EVAL_SIDE's timing ablations (half a pass, no tables, no frames: wrong sums by
+    design) exist only in -DDAB_ABLATIONS builds. With the variable set, the release library
+    must either return exactly the unset run's results or fail (it fails: DAB_E_INVALID);
+    it may never return rc 0 with wrong numbers."""
+    prob = pkg.synth(kind=0, num_cameras=30, num_points=2000, obs_per_point=5, seed=91)
+    opts = pkg.options(max_num_iterations=3)
+    s = pkg.Solver(0)
+    try:
+        s.set_problem(prob.copy())
+        ref = s.solve(opts)
+    finally:
+        s.close()
+    monkeypatch.setenv("DAB_EVAL_SIDE", side)
+    s = pkg.Solver(0)
+    try:
+        s.set_problem(prob.copy())
+        try:
+            got = s.solve(opts)
+        except RuntimeError as e:
+            assert "timing ablation" in str(e), e
+        else:
+            assert [it["cost"] for it in got["iterations"]] == [it["cost"] for it in ref["iterations"]]
     finally:
         s.close()

@@ -48,6 +48,38 @@ def test_jacobian_kernel_vs_oracle(pkg, orc, gpu, kind):
     assert err.max() < 1e-9, err.max()
 
 
+def test_rotations_near_pi_match_oracle(pkg, orc, gpu):
+    """cam_table's power series for sin(th)/th, (1-cos th)/th^2 and (th-sin th)/th^3 runs up
+    to |w| = pi, where sin(th)/th -> 0 and the alternating series cancels terms of ~3.7. Camera
+    rotations with |w| in [2.5, pi) (and a few just above pi: the closed form), every
+    observation in front of its camera: the residuals and Jacobians (k_jacobian_full) against
+    the oracle's Ceres-equivalent AngleAxisRotatePoint + autodiff, and the LM trajectory through
+    the fused evaluation pass (whose tables are built in-kernel by the same series)."""
+    base = pkg.synth(kind=0, num_cameras=48, num_points=3000, obs_per_point=6, seed=77)
+    rng = np.random.default_rng(77)
+    for e in range(base.ext.shape[0]):
+        d = rng.normal(size=3)
+        d /= np.linalg.norm(d)
+        th = rng.uniform(2.5, np.pi - 1e-6) if e % 8 else rng.uniform(np.pi, np.pi + 0.05)
+        base.ext[e, :3] = d * th
+        base.ext[e, 3:] = [rng.normal(scale=0.05), rng.normal(scale=0.05), 2.0]  # points at depth ~2
+    prob = base.copy()
+    r, _ = orc.eval_residuals(pkg, prob)
+    prob.obs_xy += r  # observe the projection, then 1 px noise and perturbed points
+    prob.obs_xy += rng.normal(size=prob.obs_xy.shape)
+    prob.points += rng.normal(scale=1e-3, size=prob.points.shape)
+    th = np.linalg.norm(prob.ext[:, :3], axis=1)
+    assert th.min() > 2.5 and (th < np.pi).sum() >= 40 and (th > np.pi).sum() >= 1
+    rg, J = gpu_jac(pkg, prob.copy())
+    ro, Jo = orc.eval_jacobians(pkg, prob)
+    np.testing.assert_allclose(rg, ro, rtol=0, atol=1e-12 * max(1.0, np.abs(ro).max()))
+    scale = np.abs(Jo).reshape(len(Jo), -1).max(axis=1)
+    err = np.abs(J - Jo).reshape(len(Jo), -1).max(axis=1) / scale
+    assert err.max() < 1e-9, err.max()
+    g, o, ref = run_both(pkg, orc, prob, max_num_iterations=10)
+    assert_same_trajectory(g, o, prob, ref)
+
+
 def test_residual_pass_vs_oracle(pkg, orc, gpu):
     prob = pkg.synth(kind=1, num_arcs=4, num_rings=9, num_points=2000, obs_per_point=6, seed=8)
     s = pkg.Solver(0)
