@@ -20,3 +20,9 @@ DAB_EVAL_SPLIT=1 timeout -k 10 300 rocprofv3 --kernel-trace -d $O/split -o run -
 python3 scripts/split_launch_times.py $O/split | tee $O/split_times.txt
 timeout -k 10 300 rocprofv3 --kernel-trace -d $O/single -o run --output-format csv -- python3 bench.py $SHORT > $O/single.log 2>&1 || { echo "single trace failed"; tail -20 $O/single.log; exit 1; }
 python3 scripts/split_launch_times.py $O/single | tee $O/single_times.txt
+# the 8-rank bench rehearsal on one GPU (eight processes, host-staged collectives) beside the
+# N = 1 line of the same short settings: the c4_* costs must equal N = 1's bitwise
+timeout -k 10 300 python -u bench.py --gpus 1 --steps 5 --warmup 2 --lm-iters 2 --no-cpu > $O/bench1.json 2> $O/bench1.err
+rc=$?; echo "bench1 rc=$rc"; [ $rc -eq 0 ] || exit $rc
+DAB_BENCH_DEVICE=0 DAB_BENCH_HOST_COLLECTIVE=1 timeout -k 10 420 python -u bench.py --gpus 8 --steps 5 --warmup 2 --lm-iters 2 > $O/bench8.json 2> $O/bench8.err
+rc=$?; echo "bench8 rc=$rc"; tail -2 $O/bench8.err; exit $rc
