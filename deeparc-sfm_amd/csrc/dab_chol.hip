@@ -151,9 +151,87 @@ struct RowB {
 };
 #define ROWB(v, j) RowB<0>::get((v), (j))
 
-// wave 0: factor L[o:o+16, o:o+16] in place, its inverse into D[16][DS] by columns (every
-// lane its own column; the compiler keeps the 120 broadcasts live: 256 VGPRs plus AGPRs,
-// fine for the one-work-group-per-CU launch schedule)
+// lane j of each 16-lane row to the whole row as ONE 64-bit DPP move (v_mov_b64_dpp
+// row_newbcast; rowb above is two 32-bit moves)
+template <int J>
+__device__ __forceinline__ double bc64(double v) {
+  return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + J, 0xf, 0xf, true);
+}
+template <int I = 0>
+__device__ __forceinline__ double bc64_rt(double v, int j) {  // j a constant after unrolling
+  if constexpr (I >= 16) return v;
+  else return j == I ? bc64<I>(v) : bc64_rt<I + 1>(v, j);
+}
+
+#ifndef DAB_FACTOR16_V1
+// wave 0: factor L[o:o+16, o:o+16] in place (lane r = row r, the four 16-lane rows of the
+// wave redundant), its inverse into D[16][DS] by columns (lane c: column c). Round 6: the
+// chain of the dense Cholesky runs this 4 times per 64-block column, twice per panel pair
+// on the critical path, and it was instruction bound (1,416 instructions, 3.2 us per call:
+// 272 32-bit DPP moves, 140 selects, 124 AGPR spill moves, a finiteness test per pivot).
+// Now every broadcast is one v_mov_b64_dpp consumed at once (no AGPR spills), L[r][j] =
+// a[j] / sqrt(d) is one multiply for every lane (lane j's a[j] IS d), and the pivots are
+// checked once at the end (a pivot d <= 0, NaN or inf makes sum d or sum 1/sqrt(d)
+// non-finite). Every value is the same operation on the same operands as before: bitwise
+// the same factor and inverse.
+typedef __attribute__((address_space(3))) double lds_f64;
+__device__ __noinline__ void factor16(double (*Lg)[LS], double (*Dg)[DS], int o, bool& bad) {
+  const int lane = threadIdx.x & 63, r = lane & 15;
+  // the blocks live in LDS: LDS-typed pointers, so the accesses need no generic-address
+  // null checks (the __noinline__ call passes generic pointers)
+  lds_f64* Lr = (lds_f64*)(&Lg[o + r][o]);
+  lds_f64* Dc = (lds_f64*)(&Dg[0][r]);
+  double a[16], v0[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    // unconditional (the block's own rows); lane r's entries j > r (the strict upper part,
+    // whatever it holds) are only ever used by lane r itself and are written back as read
+    v0[j] = Lr[j];
+    a[j] = v0[j];
+  }
+  // lane c also carries column c of the inverse, x[i] = (delta_ic - sum_{c<=m<i} L[i][m]
+  // x[m]) / L[i][i]: its sums take each multiplier L[l][j] from the factorisation's own
+  // broadcast of pivot j (x[j] is final once pivot j's 1/L[j][j] is known), so the 120
+  // broadcasts serve both and none stays live (a separate inverse loop after the factor
+  // shared them by CSE and spilled them to AGPRs)
+  const int cc = r;
+  double s[16], x[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s[i] = (i == cc) ? 1.0 : 0.0;
+  double sd = 0.0, sy = 0.0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const double d = bc64_rt(a[j], j);
+    const double y = rsqrt_nr(d);
+    sd += d;
+    sy += y;
+    const double lmj = a[j] * y;  // lane j: d * y = L[j][j]
+    a[j] = lmj;
+    const double nl = -lmj;
+    x[j] = s[j] * y;  // +0 for j < cc: s[j] stays exactly +0 there (every x it saw was +0)
+    const double nx = -x[j];
+    // lanes r < l update entries above the diagonal that are never read: no mask
+#pragma unroll
+    for (int l = j + 1; l < 16; ++l) {
+      const double b = bc64_rt(lmj, l);  // L[l][j]
+      a[l] = fma(b, nl, a[l]);
+      s[l] = fma(b, nx, s[l]);
+      // the inverse's update here, not deferred: left to itself the scheduler sinks these
+      // off-critical-path fmas and keeps the broadcasts b live (spilled to AGPRs)
+      asm volatile("" : "+v"(s[l]));
+    }
+  }
+  bad |= !isfinite(sd) || !isfinite(sy);
+  if (lane < 16) {  // stores without branches: the strict upper part is written back as read
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      Lr[j] = (j <= r) ? a[j] : v0[j];
+      Dc[j * DS] = x[j];
+    }
+  }
+}
+#else
+// round-5 form (DAB_FACTOR16_V1 builds, A/B only)
 __device__ __noinline__ void factor16(double (*L)[LS], double (*D)[DS], int o, bool& bad) {
   const int lane = threadIdx.x & 63, r = lane & 15;
   double a[16], rd[16];
@@ -189,6 +267,7 @@ __device__ __noinline__ void factor16(double (*L)[LS], double (*D)[DS], int o, b
     }
   }
 }
+#endif
 
 // 16x16 tiles on fp64 MFMA (v_mfma_f64_16x16x4f64; A: lane l holds A[l&15][l>>4], B:
 // B[l>>4][l&15], C/D: C[(l>>4) + 4r][l&15]). acc += sign * A B with A(i,k) = As[i0+i][ka+k]

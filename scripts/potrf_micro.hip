@@ -2,7 +2,7 @@
 // SPD 64x64 block (L_kk against a CPU Cholesky) and on a 6000-row panel, with the phase
 // profile of one launch (wall clock, 100 MHz).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/potrf_micro.hip -o scripts/potrf_micro
-// (factor16 as shipped: every multiplier by DPP broadcasts)
+// (factor16 as shipped; -DDAB_FACTOR16_V1 builds the round-5 form for an A/B)
 #define DAB_CHOL_PROFILE
 #include "../deeparc-sfm_amd/csrc/dab_chol.hip"
 
@@ -21,6 +21,10 @@ hipStream_t stream_take(int) {
   return s;
 }
 void stream_give(int, hipStream_t s) { (void)hipStreamDestroy(s); }
+int set_error(int code, const std::string& msg) {
+  fprintf(stderr, "%s\n", msg.c_str());
+  return code;
+}
 }  // namespace dab
 
 __global__ void k_empty() {}

@@ -1,0 +1,22 @@
+#!/bin/bash
+# round 6: factor16 rewritten (one 64-bit DPP per broadcast, the inverse carried along the
+# factorisation, no AGPR spills): micro-benchmark of the 64x64 panel step both ways, the
+# n = 5994 factor + solve A/B (round-5 factor16 in scripts/ab/libdab_f16v1.so), parity
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/r06b; mkdir -p $O
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+for v in 0 1; do timeout -k 10 60 ./scripts/potrf_micro_$v > $O/potrf_micro_$v.txt 2>&1 || { echo "potrf_micro_$v failed"; cat $O/potrf_micro_$v.txt; exit 1; }; done
+head -14 $O/potrf_micro_0.txt; head -14 $O/potrf_micro_1.txt
+for rep in 1 2 3; do
+  DAB_LIB=scripts/ab/libdab_f16v1.so timeout -k 10 120 python3 scripts/chol_bench.py 5994 >> $O/chol_ab.txt 2>&1 || exit 1
+  echo "^ round-5 factor16" >> $O/chol_ab.txt
+  timeout -k 10 120 python3 scripts/chol_bench.py 5994 >> $O/chol_ab.txt 2>&1 || exit 1
+  echo "^ round-6 factor16" >> $O/chol_ab.txt
+done
+DAB_LIB=scripts/ab/libdab_f16v1.so DAB_DUMP=$O/x_v1.npy timeout -k 10 120 python3 scripts/chol_bench.py 5994 > /dev/null 2>&1 || exit 1
+DAB_DUMP=$O/x_v2.npy timeout -k 10 120 python3 scripts/chol_bench.py 5994 > /dev/null 2>&1 || exit 1
+python3 -c "import numpy as np; a=np.load('$O/x_v1.npy'); b=np.load('$O/x_v2.npy'); print('solutions bitwise equal:', bool((a==b).all()), 'max rel diff', float(abs(a-b).max()/abs(a).max()))" >> $O/chol_ab.txt
+cat $O/chol_ab.txt
+timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_gpu_dense.py tests/test_gpu_parity.py tests/test_gpu_full_size.py \
+  -k "dense or cholesky or c3_explicit or c5_explicit or c2_explicit or lm_bal or lm_rig" > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -4 $O/pytest.log; exit $rc
