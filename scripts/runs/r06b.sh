@@ -17,6 +17,10 @@ DAB_LIB=scripts/ab/libdab_f16v1.so DAB_DUMP=$O/x_v1.npy timeout -k 10 120 python
 DAB_DUMP=$O/x_v2.npy timeout -k 10 120 python3 scripts/chol_bench.py 5994 > /dev/null 2>&1 || exit 1
 python3 -c "import numpy as np; a=np.load('$O/x_v1.npy'); b=np.load('$O/x_v2.npy'); print('solutions bitwise equal:', bool((a==b).all()), 'max rel diff', float(abs(a-b).max()/abs(a).max()))" >> $O/chol_ab.txt
 cat $O/chol_ab.txt
+# config 1's first solve on a fresh handle, phase by phase (set-up and solve preparation)
+DAB_SETUP_TIMING=1 timeout -k 10 120 python3 scripts/c1_first.py > $O/c1_first.txt 2>&1 || { echo "c1_first failed"; tail $O/c1_first.txt; exit 1; }
+DAB_DEV_SLAB=1 timeout -k 10 120 python3 scripts/c1_first.py > $O/c1_first_slab.txt 2>&1 || { echo "c1_first slab failed"; exit 1; }
+grep "^rep" $O/c1_first.txt $O/c1_first_slab.txt
 timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_gpu_dense.py tests/test_gpu_parity.py tests/test_gpu_full_size.py \
   -k "dense or cholesky or c3_explicit or c5_explicit or c2_explicit or lm_bal or lm_rig" > $O/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -4 $O/pytest.log; exit $rc
