@@ -162,6 +162,22 @@ __device__ __forceinline__ double bc64_rt(double v, int j) {  // j a constant af
   if constexpr (I >= 16) return v;
   else return j == I ? bc64<I>(v) : bc64_rt<I + 1>(v, j);
 }
+#ifdef DAB_F16_ASM
+// acc += (lane l's v, within each 16-lane row) * w as one v_fmac_f64 with a DPP64 source
+template <int L>
+__device__ __forceinline__ void fmac_bc(double& acc, double v, double w) {
+  asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+               : "+v"(acc)
+               : "v"(v), "v"(w), "i"(L));
+}
+template <int I = 0>
+__device__ __forceinline__ void fmac_bc_rt(double& acc, double v, double w, int l) {
+  if constexpr (I < 16) {
+    if (l == I) fmac_bc<I>(acc, v, w);
+    else fmac_bc_rt<I + 1>(acc, v, w, l);
+  }
+}
+#endif
 
 #ifndef DAB_FACTOR16_V1
 // wave 0: factor L[o:o+16, o:o+16] in place (lane r = row r, the four 16-lane rows of the
@@ -213,12 +229,21 @@ __device__ __noinline__ void factor16(double (*Lg)[LS], double (*Dg)[DS], int o,
     // lanes r < l update entries above the diagonal that are never read: no mask
 #pragma unroll
     for (int l = j + 1; l < 16; ++l) {
+#ifdef DAB_F16_ASM
+      // the broadcast folded into the fmas as a DPP64 source operand (v_fmac_f64 with
+      // row_newbcast:l): two instructions per (j, l) instead of three. s_nop 1: the two wait
+      // states a DPP read needs after the VALU write of its source (the compiler does not
+      // see into the asm)
+      fmac_bc_rt(a[l], lmj, nl, l);
+      fmac_bc_rt(s[l], lmj, nx, l);
+#else
       const double b = bc64_rt(lmj, l);  // L[l][j]
       a[l] = fma(b, nl, a[l]);
       s[l] = fma(b, nx, s[l]);
       // the inverse's update here, not deferred: left to itself the scheduler sinks these
       // off-critical-path fmas and keeps the broadcasts b live (spilled to AGPRs)
       asm volatile("" : "+v"(s[l]));
+#endif
     }
   }
   bad |= !isfinite(sd) || !isfinite(sy);

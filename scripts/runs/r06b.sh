@@ -5,8 +5,8 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/r06b; mkdir -p $O
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
-for v in 0 1; do timeout -k 10 60 ./scripts/potrf_micro_$v > $O/potrf_micro_$v.txt 2>&1 || { echo "potrf_micro_$v failed"; cat $O/potrf_micro_$v.txt; exit 1; }; done
-head -14 $O/potrf_micro_0.txt; head -14 $O/potrf_micro_1.txt
+for v in 0 1 2; do timeout -k 10 60 ./scripts/potrf_micro_$v > $O/potrf_micro_$v.txt 2>&1 || { echo "potrf_micro_$v failed"; cat $O/potrf_micro_$v.txt; exit 1; }; done
+head -14 $O/potrf_micro_0.txt $O/potrf_micro_1.txt $O/potrf_micro_2.txt
 for rep in 1 2 3; do
   DAB_LIB=scripts/ab/libdab_f16v1.so timeout -k 10 120 python3 scripts/chol_bench.py 5994 >> $O/chol_ab.txt 2>&1 || exit 1
   echo "^ round-5 factor16" >> $O/chol_ab.txt
