@@ -66,6 +66,7 @@ struct CholCtx {
                             // (round 4's schedule) instead of a launch of its own
   bool v1 = false;          // DAB_CHOL_V1=1: the per-step schedule (one bulk update per panel, one
                             // back-substitution launch per block)
+  bool bulk_dma = false;    // DAB_CHOL_BULK_DMA=1: the bulk update with LDS-DMA K chunks (k_syrk_bigd)
 };
 
 CholCtx* chol_create() {
@@ -80,6 +81,7 @@ CholCtx* chol_create() {
   c->bulk_grid = std::max(1, 2 * ncu - 64);
   c->ncu = ncu;
   if (const char* e = getenv("DAB_CHOL_V1")) c->v1 = atoi(e) != 0;
+  if (const char* e = getenv("DAB_CHOL_BULK_DMA")) c->bulk_dma = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_STRIP")) c->strip = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_GROUP")) c->group = std::max(2, atoi(e));
   if (const char* e = getenv("DAB_CHOL_BACK_FLOW")) c->back_flow = atoi(e) != 0;
@@ -846,6 +848,153 @@ __global__ __launch_bounds__(kBigThreads, 4) void k_syrk_big(double* __restrict_
 }
 
 
+// k_syrk_big with its K chunks staged by LDS-DMA (round 6, DAB_CHOL_BULK_DMA=1 for the A/B):
+// the chunks go global -> LDS by global_load_lds_dwordx4 (no VGPR staging, no LDS store
+// pass) into three buffers, two chunks in flight across each barrier (a raw s_barrier and a
+// counted vmcnt: __syncthreads would drain every DMA in flight; CDNA guide, "Pipelining
+// across barriers"), where the register-staged kernel keeps one chunk in flight and waits
+// for it before its LDS store. One buffer = the unit's 64 A rows and 128 B rows x KC = 16
+// doubles, unpadded (the DMA writes 1 KB lane-linear pieces), so the 16-B pieces of row r
+// are XOR-swizzled by (r >> 1) & 7 on the source address: the 16 rows of a fragment read
+// land on 16 different bank groups. Every MFMA takes the same operands in the same order as
+// k_syrk_big: bitwise the same factor.
+constexpr int kDmaBufs = 3;
+template <int CP>
+__global__ __launch_bounds__(kBigThreads, 4) void k_syrk_bigd(double* __restrict__ A, int lda, int c0, int m, int k0,
+                                                         int kk, int ntiles) {
+  constexpr int KC = 16;                        // doubles per row and chunk (8 pieces of 16 B)
+  constexpr int SB = (64 + TB) * KC;            // doubles per buffer: A rows then B rows
+  constexpr int kPieces = SB / 2;               // 1536 pieces per chunk
+  constexpr int kIns = kPieces / 64;            // 24 DMA instructions per chunk
+  constexpr int kInsWave = kIns / (kBigThreads / 64);  // 3 per wave
+  __shared__ __align__(16) double sm[kDmaBufs * SB];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+  const int wrow = 32 * (w & 1), wcol = 32 * (w >> 1);
+  const int nch = kk / KC, nunits = 2 * ntiles, ustep = 2 * (int)gridDim.x;
+  auto coords = [&](int t, int& bi, int& bj) {
+    bi = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
+    while (bi * (bi + 1) / 2 > t) --bi;
+    bj = t - bi * (bi + 1) / 2;
+  };
+  auto cload = [&](int u, dbl4(&cv)[2][2]) {
+    int bi, bj;
+    coords(u >> 1, bi, bj);
+    const int r0 = bi * TB + 64 * (u & 1) + wrow, q0 = bj * TB + wcol;
+#pragma unroll
+    for (int tr = 0; tr < 2; ++tr)
+#pragma unroll
+      for (int tc = 0; tc < 2; ++tc)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int row = r0 + 16 * tr + lk + 4 * reg, col = q0 + 16 * tc + li;
+          cv[tr][tc][reg] = A[(size_t)(c0 + min(row, m - 1)) * lda + c0 + min(col, m - 1)];
+        }
+  };
+  // element (row, col) of a buffer's A (b = 0) or B (b = 1) rows: piece col / 2 of the row,
+  // swizzled by the row
+  auto at = [](int row, int col) { return row * KC + 2 * ((col >> 1) ^ ((row >> 1) & 7)) + (col & 1); };
+  dbl4 acc[2][2], nxt[2][2];
+  // the accumulators' C values used here, before any DMA is in flight: otherwise the
+  // compiler's wait for these ordinary loads lands inside the chunk loop as a vmcnt(0)
+  // every chunk (it cannot count the DMA), draining the pipeline
+  auto settle = [&]() {
+#pragma unroll
+    for (int tr = 0; tr < 2; ++tr)
+#pragma unroll
+      for (int tc = 0; tc < 2; ++tc) asm volatile("" : "+v"(acc[tr][tc]));
+  };
+  int u = 2 * (int)blockIdx.x;
+  if (u < nunits) cload(u, acc);
+  settle();
+  while (u < nunits) {
+    const int h = u & 1;
+    int bi, bj;
+    coords(u >> 1, bi, bj);
+    const bool skip = bi == bj && (w >> 2) > h;  // a strictly upper 64 x 64 quadrant
+    const int ri0 = bi * TB + 64 * h, rj0 = bj * TB;
+    // this lane's three source rows (instruction q of the wave: pieces 64 (w + 8 q) + lane),
+    // the column offset of its piece within a chunk, all clamped into the matrix
+    const double* src[kInsWave];
+#pragma unroll
+    for (int q = 0; q < kInsWave; ++q) {
+      const int p = 64 * (w + (kBigThreads / 64) * q) + lane;
+      const bool isb = p >= 64 * KC / 2;
+      const int r = (isb ? p - 64 * KC / 2 : p) >> 3, s = p & 7;
+      const int grow = isb ? rj0 + r : ri0 + r;
+      src[q] = A + (size_t)(c0 + min(grow, m - 1)) * lda + k0 + 2 * (s ^ ((r >> 1) & 7));
+    }
+    auto dma = [&](int ch) {
+      double* buf = sm + (size_t)(ch % kDmaBufs) * SB;
+#pragma unroll
+      for (int q = 0; q < kInsWave; ++q)
+        __builtin_amdgcn_global_load_lds(src[q] + ch * KC, buf + 128 * (w + (kBigThreads / 64) * q), 16, 0, 0);
+    };
+    const int un = h == 0 ? u + 1 : u - 1 + ustep;
+    const int unc = min(un, nunits - 1);  // clamped: the prefetch is unconditional
+    const int cpre = nch >= CP ? nch - CP : 0;
+    dma(0);
+    if (nch > 1) dma(1);
+    for (int ch = 0; ch < nch; ++ch) {
+      // retire chunk ch's DMA (this wave's); what was issued after it stays in flight: chunk
+      // ch + 1's DMA and, right after the C prefetch (issued in front of chunk cpre + 2's DMA),
+      // the prefetch's 16 loads
+      if (ch + 1 < nch) {
+        if (ch == cpre + 1) asm volatile("s_waitcnt vmcnt(19)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      } else {
+        if (ch == cpre + 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      // every wave's chunk ch landed, and every wave's reads of the buffer chunk ch + 2 reuses
+      // (chunk ch - 1's) retired
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");  // no LDS access moves across the barrier
+      if (ch == cpre) cload(unc, nxt);  // in front of chunk ch + 2's DMA (the count above)
+      if (ch + 2 < nch) dma(ch + 2);
+      if (!skip) {
+        const double* As = sm + (size_t)(ch % kDmaBufs) * SB;
+        const double* Bs = As + 64 * KC;
+#pragma unroll
+        for (int ks = 0; ks < KC / 4; ++ks) {
+          double fa[2], fb[2];
+#pragma unroll
+          for (int tr = 0; tr < 2; ++tr) fa[tr] = -As[at(wrow + 16 * tr + li, 4 * ks + lk)];
+#pragma unroll
+          for (int tc = 0; tc < 2; ++tc) fb[tc] = Bs[at(wcol + 16 * tc + li, 4 * ks + lk)];
+#pragma unroll
+          for (int tr = 0; tr < 2; ++tr)
+#pragma unroll
+            for (int tc = 0; tc < 2; ++tc)
+              acc[tr][tc] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[tr], fb[tc], acc[tr][tc], 0, 0, 0);
+        }
+      }
+    }
+    if (!skip) {
+#pragma unroll
+      for (int tr = 0; tr < 2; ++tr)
+#pragma unroll
+        for (int tc = 0; tc < 2; ++tc)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) {
+            const int row = ri0 + wrow + 16 * tr + lk + 4 * reg, col = rj0 + wcol + 16 * tc + li;
+            if (row < m && col < m) A[(size_t)(c0 + row) * lda + c0 + col] = acc[tr][tc][reg];
+          }
+    }
+#pragma unroll
+    for (int tr = 0; tr < 2; ++tr)
+#pragma unroll
+      for (int tc = 0; tc < 2; ++tc) acc[tr][tc] = nxt[tr][tc];
+    settle();
+    u = un;
+    // the next unit's DMA overwrites buffers 0 and 1: every wave's reads of this unit retired
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
+
 // Back substitution L^T y = z in ONE launch (instead of one per block): grid G <= CUs,
 // every work-group resident. Per block b, last first, every work-group computes y_b =
 // L_bb^-T z_b from the stored 16x16 inverses (redundantly: no hand-off needed for it),
@@ -1269,7 +1418,8 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
         // the bulk grid leaves CUs free for the panel chain (its dependent MFMA chain would
         // queue behind the bulk's MFMAs on a shared CU)
         const int g = std::min(ntb, c->bulk_grid > 0 ? c->bulk_grid : ntb);
-        k_syrk_big<16, 4><<<g, kBigThreads, 0, s2>>>(A, lda, c0, m, b * NB, kk, ntb);
+        if (c->bulk_dma && kk % 16 == 0) k_syrk_bigd<4><<<g, kBigThreads, 0, s2>>>(A, lda, c0, m, b * NB, kk, ntb);
+        else k_syrk_big<16, 4><<<g, kBigThreads, 0, s2>>>(A, lda, c0, m, b * NB, kk, ntb);
       }
       (void)hipEventRecord(c->ev_bulk[b], s2);
       if (strip && ms <= 1) (void)hipEventRecord(c->ev_strip[b], s2);

@@ -13,9 +13,14 @@ for rep in 1 2 3; do
   timeout -k 10 120 python3 scripts/chol_bench.py 5994 >> $O/chol_ab.txt 2>&1 || exit 1
   echo "^ round-6 factor16" >> $O/chol_ab.txt
 done
+for rep in 1 2 3; do
+  DAB_CHOL_BULK_DMA=1 timeout -k 10 120 python3 scripts/chol_bench.py 5994 >> $O/chol_ab.txt 2>&1 || exit 1
+  echo "^ round-6 factor16 + LDS-DMA bulk (k_syrk_bigd)" >> $O/chol_ab.txt
+done
+DAB_CHOL_BULK_DMA=1 DAB_DUMP=$O/x_v3.npy timeout -k 10 120 python3 scripts/chol_bench.py 5994 > /dev/null 2>&1 || exit 1
 DAB_LIB=scripts/ab/libdab_f16v1.so DAB_DUMP=$O/x_v1.npy timeout -k 10 120 python3 scripts/chol_bench.py 5994 > /dev/null 2>&1 || exit 1
 DAB_DUMP=$O/x_v2.npy timeout -k 10 120 python3 scripts/chol_bench.py 5994 > /dev/null 2>&1 || exit 1
-python3 -c "import numpy as np; a=np.load('$O/x_v1.npy'); b=np.load('$O/x_v2.npy'); print('solutions bitwise equal:', bool((a==b).all()), 'max rel diff', float(abs(a-b).max()/abs(a).max()))" >> $O/chol_ab.txt
+python3 -c "import numpy as np; a=np.load('$O/x_v1.npy'); b=np.load('$O/x_v2.npy'); c=np.load('$O/x_v3.npy'); print('factor16 v1 vs v2 bitwise equal:', bool((a==b).all()), 'max rel diff', float(abs(a-b).max()/abs(a).max())); print('bulk dma vs shipped bitwise equal:', bool((c==b).all()), 'max rel diff', float(abs(c-b).max()/abs(b).max()))" >> $O/chol_ab.txt
 cat $O/chol_ab.txt
 # config 1's first solve on a fresh handle, phase by phase (set-up and solve preparation)
 DAB_SETUP_TIMING=1 timeout -k 10 120 python3 scripts/c1_first.py > $O/c1_first.txt 2>&1 || { echo "c1_first failed"; tail $O/c1_first.txt; exit 1; }
