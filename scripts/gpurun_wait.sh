@@ -6,7 +6,7 @@ log=$1; to=$2; shift 2
 for i in $(seq 1 30); do
   /usr/local/graft/bin/gpurun --timeout "$to" -- "$@" > "$log" 2>&1
   rc=$?
-  if grep -q "retry in a few minutes" "$log" && grep -q "run 0.0s" "$log"; then
+  if grep -q "status=transient" "$log" && ! grep -q "run [1-9]" "$log"; then
     sleep 90
     continue
   fi
