@@ -66,7 +66,6 @@ struct CholCtx {
                             // (round 4's schedule) instead of a launch of its own
   bool v1 = false;          // DAB_CHOL_V1=1: the per-step schedule (one bulk update per panel, one
                             // back-substitution launch per block)
-  bool bulk_dma = false;    // DAB_CHOL_BULK_DMA=1: the bulk update with LDS-DMA K chunks (k_syrk_bigd)
 };
 
 CholCtx* chol_create() {
@@ -81,7 +80,6 @@ CholCtx* chol_create() {
   c->bulk_grid = std::max(1, 2 * ncu - 64);
   c->ncu = ncu;
   if (const char* e = getenv("DAB_CHOL_V1")) c->v1 = atoi(e) != 0;
-  if (const char* e = getenv("DAB_CHOL_BULK_DMA")) c->bulk_dma = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_STRIP")) c->strip = atoi(e) != 0;
   if (const char* e = getenv("DAB_CHOL_GROUP")) c->group = std::max(2, atoi(e));
   if (const char* e = getenv("DAB_CHOL_BACK_FLOW")) c->back_flow = atoi(e) != 0;
@@ -138,23 +136,9 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
   return y;
 }
 
-// lane j of each 16-lane row to the whole row (DPP row_newbcast): a VGPR broadcast, no
-// SGPR round trip
-template <int J>
-__device__ __forceinline__ double rowb(double v) {
-  return dpp_full_f64<0x150 + J>(v);
-}
-template <int J, int I = 0>
-struct RowB {
-  static __device__ __forceinline__ double get(double v, int j) {
-    if constexpr (I >= 16) return v;
-    else return j == I ? rowb<I>(v) : RowB<J, I + 1>::get(v, j);
-  }
-};
-#define ROWB(v, j) RowB<0>::get((v), (j))
 
 // lane j of each 16-lane row to the whole row as ONE 64-bit DPP move (v_mov_b64_dpp
-// row_newbcast; rowb above is two 32-bit moves)
+// row_newbcast: a VGPR broadcast, no SGPR round trip; two 32-bit moves before round 6)
 template <int J>
 __device__ __forceinline__ double bc64(double v) {
   return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + J, 0xf, 0xf, true);
@@ -164,24 +148,7 @@ __device__ __forceinline__ double bc64_rt(double v, int j) {  // j a constant af
   if constexpr (I >= 16) return v;
   else return j == I ? bc64<I>(v) : bc64_rt<I + 1>(v, j);
 }
-#ifdef DAB_F16_ASM
-// acc += (lane l's v, within each 16-lane row) * w as one v_fmac_f64 with a DPP64 source
-template <int L>
-__device__ __forceinline__ void fmac_bc(double& acc, double v, double w) {
-  asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-               : "+v"(acc)
-               : "v"(v), "v"(w), "i"(L));
-}
-template <int I = 0>
-__device__ __forceinline__ void fmac_bc_rt(double& acc, double v, double w, int l) {
-  if constexpr (I < 16) {
-    if (l == I) fmac_bc<I>(acc, v, w);
-    else fmac_bc_rt<I + 1>(acc, v, w, l);
-  }
-}
-#endif
 
-#ifndef DAB_FACTOR16_V1
 // wave 0: factor L[o:o+16, o:o+16] in place (lane r = row r, the four 16-lane rows of the
 // wave redundant), its inverse into D[16][DS] by columns (lane c: column c). Round 6: the
 // chain of the dense Cholesky runs this 4 times per 64-block column, twice per panel pair
@@ -231,21 +198,12 @@ __device__ __noinline__ void factor16(double (*Lg)[LS], double (*Dg)[DS], int o,
     // lanes r < l update entries above the diagonal that are never read: no mask
 #pragma unroll
     for (int l = j + 1; l < 16; ++l) {
-#ifdef DAB_F16_ASM
-      // the broadcast folded into the fmas as a DPP64 source operand (v_fmac_f64 with
-      // row_newbcast:l): two instructions per (j, l) instead of three. s_nop 1: the two wait
-      // states a DPP read needs after the VALU write of its source (the compiler does not
-      // see into the asm)
-      fmac_bc_rt(a[l], lmj, nl, l);
-      fmac_bc_rt(s[l], lmj, nx, l);
-#else
       const double b = bc64_rt(lmj, l);  // L[l][j]
       a[l] = fma(b, nl, a[l]);
       s[l] = fma(b, nx, s[l]);
       // the inverse's update here, not deferred: left to itself the scheduler sinks these
       // off-critical-path fmas and keeps the broadcasts b live (spilled to AGPRs)
       asm volatile("" : "+v"(s[l]));
-#endif
     }
   }
   bad |= !isfinite(sd) || !isfinite(sy);
@@ -257,44 +215,6 @@ __device__ __noinline__ void factor16(double (*Lg)[LS], double (*Dg)[DS], int o,
     }
   }
 }
-#else
-// round-5 form (DAB_FACTOR16_V1 builds, A/B only)
-__device__ __noinline__ void factor16(double (*L)[LS], double (*D)[DS], int o, bool& bad) {
-  const int lane = threadIdx.x & 63, r = lane & 15;
-  double a[16], rd[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) a[j] = (j <= r) ? L[o + r][o + j] : 0.0;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const double d = ROWB(a[j], j);
-    bad |= !(d > 0.0) || !isfinite(d);
-    const double y = rsqrt_nr(d);
-    rd[j] = y;  // 1 / L[j][j]
-    const double lmj = (r == j) ? d * y : a[j] * y;
-    a[j] = lmj;
-    // lanes r < l update entries above the diagonal that are never read: no mask
-#pragma unroll
-    for (int l = j + 1; l < 16; ++l) a[l] = fma(-lmj, ROWB(lmj, l), a[l]);
-  }
-  // lane c: column c of the inverse, x[i] = (delta_ic - sum_{c<=m<i} L[i][m] x[m]) / L[i][i]
-  const int cc = r;
-  double x[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    double s = (i == cc) ? 1.0 : 0.0;
-#pragma unroll
-    for (int m = 0; m < i; ++m) s -= ROWB(a[m], i) * x[m];
-    x[i] = (i >= cc) ? s * rd[i] : 0.0;
-  }
-  if (lane < 16) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      if (j <= r) L[o + r][o + j] = a[j];
-      D[j][cc] = x[j];
-    }
-  }
-}
-#endif
 
 // 16x16 tiles on fp64 MFMA (v_mfma_f64_16x16x4f64; A: lane l holds A[l&15][l>>4], B:
 // B[l>>4][l&15], C/D: C[(l>>4) + 4r][l&15]). acc += sign * A B with A(i,k) = As[i0+i][ka+k]
@@ -360,6 +280,31 @@ __device__ __forceinline__ void factor64(double (*L)[LS], double (*D)[16][DS], b
   }
 }
 
+// One wave's 16 panel rows P (LDS, stride LS) <- P L_kk^-T, block column by block column:
+// X_q = (P_q - sum_{r<q} X_r L_{q,r}^T) D_q^T. Right-looking (round 6): as soon as X_q is
+// known its term goes into every later block's accumulator, so the dependent chain is
+// X_q -> the next block's last 4 MFMAs -> X_{q+1} (28 MFMAs deep instead of 40; the other
+// blocks' updates overlap it). Each block's accumulator still takes the terms r = 0, 1, ...
+// in order, the same MFMAs on the same operands as the left-looking form: bitwise the same.
+__device__ __forceinline__ void panel_rows_solve(double* Pf, const double* Lf, const double (*D)[16][DS], int w) {
+  dbl4 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = tile_load<LS>(Pf, 16 * w, 16 * q);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    __builtin_amdgcn_wave_barrier();
+    tile_store<LS>(Pf, 16 * w, 16 * q, acc[q]);
+    __builtin_amdgcn_wave_barrier();
+    dbl4 x = {0.0, 0.0, 0.0, 0.0};
+    mma_nt<LS, DS>(16, x, Pf, 16 * w, 16 * q, &D[q][0][0], 0, 0, 1.0);
+    __builtin_amdgcn_wave_barrier();
+    tile_store<LS>(Pf, 16 * w, 16 * q, x);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int qq = q + 1; qq < 4; ++qq) mma_nt<LS, LS>(16, acc[qq], Pf, 16 * w, 16 * q, Lf, 16 * qq, 16 * q, -1.0);
+  }
+}
+
 // panel rows [r0, r1) (64 per work-group): P <- P L_kk^-T ; work-group 0 stores D and L_kk
 // to the block scratch
 // pre: the diagonal block was factored by the column update in front (k_syrk_mfma with
@@ -420,22 +365,8 @@ __global__ __launch_bounds__(kThreads) void k_panel(double* __restrict__ A, int 
     }
   }
   if (row0 >= r1) return;
-  // wave w solves rows [16w, 16w+16) of P, block column by block column (no barriers:
-  // the rows are its own): T = P_q - X_{<q} L_{q,<q}^T, X_q = T D_q^T
-  double* Pf = &P[0][0];
-  const double* Lf = &L[0][0];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    dbl4 acc = tile_load<LS>(Pf, 16 * w, 16 * q);
-    if (q > 0) mma_nt<LS, LS>(16 * q, acc, Pf, 16 * w, 0, Lf, 16 * q, 0, -1.0);
-    __builtin_amdgcn_wave_barrier();
-    tile_store<LS>(Pf, 16 * w, 16 * q, acc);
-    __builtin_amdgcn_wave_barrier();
-    dbl4 x = {0.0, 0.0, 0.0, 0.0};
-    mma_nt<LS, DS>(16, x, Pf, 16 * w, 16 * q, &D[q][0][0], 0, 0, 1.0);
-    __builtin_amdgcn_wave_barrier();
-    tile_store<LS>(Pf, 16 * w, 16 * q, x);
-  }
+  // wave w solves rows [16w, 16w+16) of P (no barriers: the rows are its own)
+  panel_rows_solve(&P[0][0], &L[0][0], D, w);
   __syncthreads();
   PROF_MARK(10);
 #pragma unroll
@@ -632,20 +563,7 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
       Dsh[idx >> 8][(idx >> 4) & 15][idx & 15] = __hip_atomic_load(fblk + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    double* Pf = &P[0][0];
-    const double* Lf = &L[0][0];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {  // wave w: rows [16 w, 16 w + 16), as k_panel
-      dbl4 t = tile_load<LS>(Pf, 16 * w, 16 * q);
-      if (q > 0) mma_nt<LS, LS>(16 * q, t, Pf, 16 * w, 0, Lf, 16 * q, 0, -1.0);
-      __builtin_amdgcn_wave_barrier();
-      tile_store<LS>(Pf, 16 * w, 16 * q, t);
-      __builtin_amdgcn_wave_barrier();
-      dbl4 x = {0.0, 0.0, 0.0, 0.0};
-      mma_nt<LS, DS>(16, x, Pf, 16 * w, 16 * q, &Dsh[q][0][0], 0, 0, 1.0);
-      __builtin_amdgcn_wave_barrier();
-      tile_store<LS>(Pf, 16 * w, 16 * q, x);
-    }
+    panel_rows_solve(&P[0][0], &L[0][0], Dsh, w);  // wave w: rows [16 w, 16 w + 16), as k_panel
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < NB * NB / kThreads; ++q) {
@@ -847,153 +765,6 @@ __global__ __launch_bounds__(kBigThreads, 4) void k_syrk_big(double* __restrict_
   }
 }
 
-
-// k_syrk_big with its K chunks staged by LDS-DMA (round 6, DAB_CHOL_BULK_DMA=1 for the A/B):
-// the chunks go global -> LDS by global_load_lds_dwordx4 (no VGPR staging, no LDS store
-// pass) into three buffers, two chunks in flight across each barrier (a raw s_barrier and a
-// counted vmcnt: __syncthreads would drain every DMA in flight; CDNA guide, "Pipelining
-// across barriers"), where the register-staged kernel keeps one chunk in flight and waits
-// for it before its LDS store. One buffer = the unit's 64 A rows and 128 B rows x KC = 16
-// doubles, unpadded (the DMA writes 1 KB lane-linear pieces), so the 16-B pieces of row r
-// are XOR-swizzled by (r >> 1) & 7 on the source address: the 16 rows of a fragment read
-// land on 16 different bank groups. Every MFMA takes the same operands in the same order as
-// k_syrk_big: bitwise the same factor.
-constexpr int kDmaBufs = 3;
-template <int CP>
-__global__ __launch_bounds__(kBigThreads, 4) void k_syrk_bigd(double* __restrict__ A, int lda, int c0, int m, int k0,
-                                                         int kk, int ntiles) {
-  constexpr int KC = 16;                        // doubles per row and chunk (8 pieces of 16 B)
-  constexpr int SB = (64 + TB) * KC;            // doubles per buffer: A rows then B rows
-  constexpr int kPieces = SB / 2;               // 1536 pieces per chunk
-  constexpr int kIns = kPieces / 64;            // 24 DMA instructions per chunk
-  constexpr int kInsWave = kIns / (kBigThreads / 64);  // 3 per wave
-  __shared__ __align__(16) double sm[kDmaBufs * SB];
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
-  const int wrow = 32 * (w & 1), wcol = 32 * (w >> 1);
-  const int nch = kk / KC, nunits = 2 * ntiles, ustep = 2 * (int)gridDim.x;
-  auto coords = [&](int t, int& bi, int& bj) {
-    bi = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
-    while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
-    while (bi * (bi + 1) / 2 > t) --bi;
-    bj = t - bi * (bi + 1) / 2;
-  };
-  auto cload = [&](int u, dbl4(&cv)[2][2]) {
-    int bi, bj;
-    coords(u >> 1, bi, bj);
-    const int r0 = bi * TB + 64 * (u & 1) + wrow, q0 = bj * TB + wcol;
-#pragma unroll
-    for (int tr = 0; tr < 2; ++tr)
-#pragma unroll
-      for (int tc = 0; tc < 2; ++tc)
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-          const int row = r0 + 16 * tr + lk + 4 * reg, col = q0 + 16 * tc + li;
-          cv[tr][tc][reg] = A[(size_t)(c0 + min(row, m - 1)) * lda + c0 + min(col, m - 1)];
-        }
-  };
-  // element (row, col) of a buffer's A (b = 0) or B (b = 1) rows: piece col / 2 of the row,
-  // swizzled by the row
-  auto at = [](int row, int col) { return row * KC + 2 * ((col >> 1) ^ ((row >> 1) & 7)) + (col & 1); };
-  dbl4 acc[2][2], nxt[2][2];
-  // the accumulators' C values used here, before any DMA is in flight: otherwise the
-  // compiler's wait for these ordinary loads lands inside the chunk loop as a vmcnt(0)
-  // every chunk (it cannot count the DMA), draining the pipeline
-  auto settle = [&]() {
-#pragma unroll
-    for (int tr = 0; tr < 2; ++tr)
-#pragma unroll
-      for (int tc = 0; tc < 2; ++tc) asm volatile("" : "+v"(acc[tr][tc]));
-  };
-  int u = 2 * (int)blockIdx.x;
-  if (u < nunits) cload(u, acc);
-  settle();
-  while (u < nunits) {
-    const int h = u & 1;
-    int bi, bj;
-    coords(u >> 1, bi, bj);
-    const bool skip = bi == bj && (w >> 2) > h;  // a strictly upper 64 x 64 quadrant
-    const int ri0 = bi * TB + 64 * h, rj0 = bj * TB;
-    // this lane's three source rows (instruction q of the wave: pieces 64 (w + 8 q) + lane),
-    // the column offset of its piece within a chunk, all clamped into the matrix
-    const double* src[kInsWave];
-#pragma unroll
-    for (int q = 0; q < kInsWave; ++q) {
-      const int p = 64 * (w + (kBigThreads / 64) * q) + lane;
-      const bool isb = p >= 64 * KC / 2;
-      const int r = (isb ? p - 64 * KC / 2 : p) >> 3, s = p & 7;
-      const int grow = isb ? rj0 + r : ri0 + r;
-      src[q] = A + (size_t)(c0 + min(grow, m - 1)) * lda + k0 + 2 * (s ^ ((r >> 1) & 7));
-    }
-    auto dma = [&](int ch) {
-      double* buf = sm + (size_t)(ch % kDmaBufs) * SB;
-#pragma unroll
-      for (int q = 0; q < kInsWave; ++q)
-        __builtin_amdgcn_global_load_lds(src[q] + ch * KC, buf + 128 * (w + (kBigThreads / 64) * q), 16, 0, 0);
-    };
-    const int un = h == 0 ? u + 1 : u - 1 + ustep;
-    const int unc = min(un, nunits - 1);  // clamped: the prefetch is unconditional
-    const int cpre = nch >= CP ? nch - CP : 0;
-    dma(0);
-    if (nch > 1) dma(1);
-    for (int ch = 0; ch < nch; ++ch) {
-      // retire chunk ch's DMA (this wave's); what was issued after it stays in flight: chunk
-      // ch + 1's DMA and, right after the C prefetch (issued in front of chunk cpre + 2's DMA),
-      // the prefetch's 16 loads
-      if (ch + 1 < nch) {
-        if (ch == cpre + 1) asm volatile("s_waitcnt vmcnt(19)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      } else {
-        if (ch == cpre + 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      // every wave's chunk ch landed, and every wave's reads of the buffer chunk ch + 2 reuses
-      // (chunk ch - 1's) retired
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");  // no LDS access moves across the barrier
-      if (ch == cpre) cload(unc, nxt);  // in front of chunk ch + 2's DMA (the count above)
-      if (ch + 2 < nch) dma(ch + 2);
-      if (!skip) {
-        const double* As = sm + (size_t)(ch % kDmaBufs) * SB;
-        const double* Bs = As + 64 * KC;
-#pragma unroll
-        for (int ks = 0; ks < KC / 4; ++ks) {
-          double fa[2], fb[2];
-#pragma unroll
-          for (int tr = 0; tr < 2; ++tr) fa[tr] = -As[at(wrow + 16 * tr + li, 4 * ks + lk)];
-#pragma unroll
-          for (int tc = 0; tc < 2; ++tc) fb[tc] = Bs[at(wcol + 16 * tc + li, 4 * ks + lk)];
-#pragma unroll
-          for (int tr = 0; tr < 2; ++tr)
-#pragma unroll
-            for (int tc = 0; tc < 2; ++tc)
-              acc[tr][tc] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[tr], fb[tc], acc[tr][tc], 0, 0, 0);
-        }
-      }
-    }
-    if (!skip) {
-#pragma unroll
-      for (int tr = 0; tr < 2; ++tr)
-#pragma unroll
-        for (int tc = 0; tc < 2; ++tc)
-#pragma unroll
-          for (int reg = 0; reg < 4; ++reg) {
-            const int row = ri0 + wrow + 16 * tr + lk + 4 * reg, col = rj0 + wcol + 16 * tc + li;
-            if (row < m && col < m) A[(size_t)(c0 + row) * lda + c0 + col] = acc[tr][tc][reg];
-          }
-    }
-#pragma unroll
-    for (int tr = 0; tr < 2; ++tr)
-#pragma unroll
-      for (int tc = 0; tc < 2; ++tc) acc[tr][tc] = nxt[tr][tc];
-    settle();
-    u = un;
-    // the next unit's DMA overwrites buffers 0 and 1: every wave's reads of this unit retired
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  }
-}
 
 // Back substitution L^T y = z in ONE launch (instead of one per block): grid G <= CUs,
 // every work-group resident. Per block b, last first, every work-group computes y_b =
@@ -1418,8 +1189,7 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
         // the bulk grid leaves CUs free for the panel chain (its dependent MFMA chain would
         // queue behind the bulk's MFMAs on a shared CU)
         const int g = std::min(ntb, c->bulk_grid > 0 ? c->bulk_grid : ntb);
-        if (c->bulk_dma && kk % 16 == 0) k_syrk_bigd<4><<<g, kBigThreads, 0, s2>>>(A, lda, c0, m, b * NB, kk, ntb);
-        else k_syrk_big<16, 4><<<g, kBigThreads, 0, s2>>>(A, lda, c0, m, b * NB, kk, ntb);
+        k_syrk_big<16, 4><<<g, kBigThreads, 0, s2>>>(A, lda, c0, m, b * NB, kk, ntb);
       }
       (void)hipEventRecord(c->ev_bulk[b], s2);
       if (strip && ms <= 1) (void)hipEventRecord(c->ev_strip[b], s2);

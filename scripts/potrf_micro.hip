@@ -2,7 +2,8 @@
 // SPD 64x64 block (L_kk against a CPU Cholesky) and on a 6000-row panel, with the phase
 // profile of one launch (wall clock, 100 MHz).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/potrf_micro.hip -o scripts/potrf_micro
-// (factor16 as shipped; -DDAB_FACTOR16_V1 builds the round-5 form for an A/B)
+// (factor16 as shipped; the round-5 form and the DPP64-fmac variant are in
+// scripts/experiments/chol_bulk_lds_dma_f16_asm.patch)
 #define DAB_CHOL_PROFILE
 #include "../deeparc-sfm_amd/csrc/dab_chol.hip"
 

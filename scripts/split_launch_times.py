@@ -26,8 +26,11 @@ by = {}
 for r in rows:
     g = int(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0)
     by.setdefault(g, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0)
-for g, ds in sorted(by.items(), reverse=True):
+if len(by) == 1 and os.environ.get("SPLIT_ALTERNATE", "1") == "1":  # one grid: the pass's two launches alternate
+    ds = next(iter(by.values()))
+    by = {"camera side (1st of a pass)": ds[0::2], "point side (2nd)": ds[1::2]}
+for g, ds in sorted(by.items(), key=lambda kv: str(kv[0])):
     ds_sorted = sorted(ds)
-    print(f"{name} grid {g} ({g // 1024} work-groups): {len(ds)} launches, median {statistics.median(ds):.2f} us, "
+    print(f"{name} {g}: {len(ds)} launches, median {statistics.median(ds):.2f} us, "
           f"mean {statistics.mean(ds):.2f} us, p10 {ds_sorted[len(ds) // 10]:.2f} us, "
           f"p90 {ds_sorted[(9 * len(ds)) // 10]:.2f} us")

@@ -28,14 +28,6 @@ def check_solve(pkg, n):
     assert np.linalg.norm(A @ x - b) <= 1e-12 * np.linalg.norm(A) * np.linalg.norm(x)
 
 
-@pytest.mark.parametrize("n", [1000, 2050, 3001])
-def test_dense_spd_solve_bulk_dma_matches_numpy(pkg, gpu, n, monkeypatch):
-    """The bulk update with LDS-DMA K chunks (k_syrk_bigd, DAB_CHOL_BULK_DMA=1): the same
-    MFMA sequence as k_syrk_big, so the same checks hold (and the same solution bits)."""
-    monkeypatch.setenv("DAB_CHOL_BULK_DMA", "1")
-    check_solve(pkg, n)
-
-
 def test_dense_spd_solve_detects_indefinite(pkg, gpu):
     n = 100
     A = np.eye(n)

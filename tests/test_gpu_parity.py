@@ -722,8 +722,7 @@ def test_noise_free_problem_matches_oracle(pkg, orc, gpu, kind):
 @pytest.mark.parametrize("knob", ["DAB_CHOL_BACK_FLOW=0", "DAB_CHOL_FUSE_PANEL=0", "DAB_CHOL_PREFACTOR=0",
                                   "DAB_CHOL_V1=1", "DAB_CHOL_GROUP=3", "DAB_CHOL_GRAPH_MIN=1",
                                   "DAB_CHOL_STRIP=0", "DAB_CHOL_STRIP=0,DAB_CHOL_GRAPH_MIN=1",
-                                  "DAB_CHOL_GROUP=3,DAB_CHOL_GRAPH_MIN=1", "DAB_CHOL_BULK_DMA=1",
-                                  "DAB_CHOL_BULK_DMA=1,DAB_CHOL_GRAPH_MIN=1"])
+                                  "DAB_CHOL_GROUP=3,DAB_CHOL_GRAPH_MIN=1"])
 def test_cholesky_schedules_agree(pkg, gpu, knob, monkeypatch):
     """The dense Cholesky's schedules — the dataflow back substitution against the
     grid-barrier one, the panel step fused into the column update against its own launch,
