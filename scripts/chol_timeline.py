@@ -12,7 +12,12 @@ for f in glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True):
 rows.sort()
 ch = [r for r in rows if "k_panel" in r[2] or "k_syrk" in r[2] or "k_trsv" in r[2] or "fillBuffer" in r[2]]
 # last factorisation: from the last k_panel whose predecessor is a k_trsv_back (or the start)
-starts = [i for i, r in enumerate(ch) if "k_panel" in r[2] and (i == 0 or "k_trsv" in ch[i - 1][2])]
+def prev_kernel(i):  # the previous entry that is not a buffer fill (the schedule zeroes its flags first)
+    j = i - 1
+    while j >= 0 and "fillBuffer" in ch[j][2]:
+        j -= 1
+    return ch[j][2] if j >= 0 else ""
+starts = [i for i, r in enumerate(ch) if "k_panel" in r[2] and (i == 0 or "k_trsv" in prev_kernel(i))]
 if len(starts) < 2:  # the back substitution is not right before the next panel: split on gaps
     starts = [i for i, r in enumerate(ch) if "k_panel" in r[2] and (i == 0 or r[0] - ch[i - 1][1] > 200000)]
 seg = ch[starts[-1]:]
