@@ -304,6 +304,7 @@ struct Knobs {
   int bench_sample = 8;     // DAB_BENCH_SAMPLE: timing-event stride of dab_bench_eval_pass
   int schur_tiles = 1;      // DAB_SCHUR_TILES=0: explicit S from the pair tables even for small NC
   int tile_balance = 1;     // DAB_TILE_BALANCE=0: one work-group per tile and group of batches
+  int tile_minb = 2;        // DAB_TILE_MINB: fewest batches per k_schur_tiles work-group (8 until round 6)
   int p2p = -1;             // DAB_P2P: one-shot xGMI all-reduce of small sums (-1 auto: RCCL handles
                             // only; 1 also on host-staged handles, the one-GPU rehearsal; 0 off)
   int setup_host = 0;       // DAB_SETUP_HOST=1: dab_set_problem's host passes instead of the device ones
@@ -333,6 +334,7 @@ struct Knobs {
     get("DAB_BENCH_SAMPLE", bench_sample);
     get("DAB_SCHUR_TILES", schur_tiles);
     get("DAB_TILE_BALANCE", tile_balance);
+    get("DAB_TILE_MINB", tile_minb);
     get("DAB_P2P", p2p);
     get("DAB_FUSED_TAB", fused_tab);
     get("DAB_SETUP_HOST", setup_host);
@@ -2270,9 +2272,11 @@ static int build_schur_tiles(dab_handle* h, int2* d_sch, const int* d_m) {
   a.nsub = subbeg[ntile];
   int ng = std::max(1, h->ncu / a.nsub);
   if (ng >= 8) ng -= ng % 8;
-  // at least 8 batches per work-group: small problems keep few partials for the sum
+  // at least tile_minb batches per work-group (small problems keep few partials for the sum):
+  // 2 since round 6 — C1's 313 batches on 156 work-groups instead of 39, k_schur_tiles
+  // 153 -> 57 us, its partial sum 7 -> 15 us (scripts/runs/r06h.sh)
   const int smax = *std::max_element(sub.begin(), sub.end());
-  a.ngroup = std::max(1, std::min(ng, a.nbatch / (8 * smax)));
+  a.ngroup = std::max(1, std::min(ng, a.nbatch / (std::max(1, h->knobs.tile_minb) * smax)));
   std::vector<int> blk_nslot(std::max(1, nb), a.ngroup);
   for (int t = 0; t < ntile; ++t)
     for (int k = tb[t]; k < tb[t + 1]; ++k) blk_nslot[k] = a.ngroup * sub[t];
