@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -127,6 +128,15 @@ __device__ long long g_prof[16];
 #else
 #define PROF_MARK(i)
 #endif
+#ifdef DAB_CHOL_STAMPS  // per-work-group phase stamps of the factorisation's launches (A/B builds only)
+constexpr int kStampWg = 512, kStampCb = 128;
+__device__ unsigned long long g_stamp[3 * kStampCb * kStampWg * 8];  // [kind][block column][wg][phase]
+#define CHOL_STAMP(kind, cb, p)                                                                              \
+  if (threadIdx.x == 0 && (cb) >= 0 && (cb) < kStampCb && (int)blockIdx.x < kStampWg)                      \
+    g_stamp[(((size_t)(kind) * kStampCb + (cb)) * kStampWg + blockIdx.x) * 8 + (p)] = __builtin_amdgcn_s_memrealtime();
+#else
+#define CHOL_STAMP(kind, cb, p)
+#endif
 
 // 1/sqrt(d): v_rsq_f64 and two Newton steps
 __device__ __forceinline__ double rsqrt_nr(double d) {
@@ -166,14 +176,13 @@ __device__ __noinline__ void factor16(double (*Lg)[LS], double (*Dg)[DS], int o,
   // null checks (the __noinline__ call passes generic pointers)
   lds_f64* Lr = (lds_f64*)(&Lg[o + r][o]);
   lds_f64* Dc = (lds_f64*)(&Dg[0][r]);
-  double a[16], v0[16];
+  // unconditional (the block's own rows); lane r's entries j > r (the strict upper part,
+  // whatever it holds) are only ever used by lane r itself, and nothing reads the upper part
+  // of a diagonal 16 x 16 block afterwards (factor64's stages and the panel solves read the
+  // blocks below it, the stores of L_kk write zeros there), so it is written back as computed
+  double a[16];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    // unconditional (the block's own rows); lane r's entries j > r (the strict upper part,
-    // whatever it holds) are only ever used by lane r itself and are written back as read
-    v0[j] = Lr[j];
-    a[j] = v0[j];
-  }
+  for (int j = 0; j < 16; ++j) a[j] = Lr[j];
   // lane c also carries column c of the inverse, x[i] = (delta_ic - sum_{c<=m<i} L[i][m]
   // x[m]) / L[i][i]: its sums take each multiplier L[l][j] from the factorisation's own
   // broadcast of pivot j (x[j] is final once pivot j's 1/L[j][j] is known), so the 120
@@ -210,7 +219,7 @@ __device__ __noinline__ void factor16(double (*Lg)[LS], double (*Dg)[DS], int o,
   if (lane < 16) {  // stores without branches: the strict upper part is written back as read
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      Lr[j] = (j <= r) ? a[j] : v0[j];
+      Lr[j] = a[j];
       Dc[j * DS] = x[j];
     }
   }
@@ -389,6 +398,10 @@ __global__ __launch_bounds__(kThreads) void k_panel(double* __restrict__ A, int 
 // L_kk and the inverses (agent-scope stores, then ready = 1) and every other work-group
 // keeps its updated tile, which is its 64 panel rows, waits for ready (bounded: flag |= 2)
 // and solves the rows P <- P L_kk^-T (as k_panel), so the chain loses a launch per block.
+// FACTOR: the fblk / ready paths are compiled in (their factor16 calls hold the kernel at 373
+// registers per lane, one wave per SIMD); the plain update (strips, the per-step schedule) is
+// the FACTOR = false instance.
+template <bool FACTOR>
 __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, int lda, int r0, int m, int k0,
                                                         int kk, int col_only, int ntiles,
                                                         double* __restrict__ fblk = nullptr, int kb_next = 0,
@@ -399,6 +412,8 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
   __shared__ double Dsh[4][16][DS];
   __shared__ int abort_s;
   if (col_only) __builtin_amdgcn_s_setprio(3);  // on the panel chain
+  [[maybe_unused]] const int skind = fblk ? 0 : 1, scb = col_only ? r0 / NB : -1;
+  CHOL_STAMP(skind, scb, 0);
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
   if (t != (int)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
   int bi = t, bj = 0;
@@ -457,6 +472,7 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
     if (!diag) *reinterpret_cast<double2*>(&Pb[rr * LDP + 2 * c2]) = make_double2(vb[q].x * f0, vb[q].y * f1);
   }
   __syncthreads();
+  if (k == k0 && t == (int)blockIdx.x) CHOL_STAMP(skind, scb, 1);
   const double* PB = diag ? Pa : Pb;
   if (skip) continue;
 #pragma unroll 4
@@ -474,6 +490,7 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
   }
   }
   // D layout (f64 16x16x4): col = lane & 15, row = (lane >> 4) + 4 * reg
+  if (t == (int)blockIdx.x) CHOL_STAMP(skind, scb, 2);
 #pragma unroll
   for (int a2 = 0; a2 < 2; ++a2)
 #pragma unroll
@@ -484,7 +501,8 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
         const int col = bj * NB + wc * 32 + b2 * 16 + li;
         if (!skip && row < m && col < m) A[(size_t)(r0 + row) * lda + r0 + col] = acc[a2][b2][reg];
       }
-  if (fblk && col_only && bi == 0) {
+  if (t == (int)blockIdx.x) CHOL_STAMP(skind, scb, 3);
+  if (FACTOR && fblk && col_only && bi == 0) {
     // Pb is free on a diagonal tile: it holds L [NB][LS]
     double (*L)[LS] = reinterpret_cast<double (*)[LS]>(Pb);
     double (*D)[16][DS] = Dsh;
@@ -524,7 +542,8 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
       __syncthreads();
       if (tid == 0) __hip_atomic_store(ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-  } else if (ready && col_only) {
+    CHOL_STAMP(skind, scb, 4);
+  } else if (FACTOR && ready && col_only) {
     // the fused panel step on this tile's rows
     double (*P)[LS] = reinterpret_cast<double (*)[LS]>(Pb);
     double (*L)[LS] = reinterpret_cast<double (*)[LS]>(Pa);
@@ -552,6 +571,7 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
     }
     __syncthreads();
     if (abort_s) return;
+    CHOL_STAMP(skind, scb, 4);
 #pragma unroll
     for (int q = 0; q < NB * NB / kThreads; ++q) {
       const int idx = tid + q * kThreads, i = idx >> 6, j = idx & 63;
@@ -573,6 +593,7 @@ __global__ __launch_bounds__(kThreads) void k_syrk_mfma(double* __restrict__ A, 
     }
   }
   }
+  CHOL_STAMP(skind, scb, 5);
 }
 
 // back substitution step for block [k, k+kb): y_k = L_kk^-T z_k by 16-blocks with the
@@ -689,6 +710,7 @@ __global__ __launch_bounds__(kBigThreads, 4) void k_syrk_big(double* __restrict_
           cv[tr][tc][reg] = A[(size_t)(c0 + min(row, m - 1)) * lda + c0 + min(col, m - 1)];
         }
   };
+  CHOL_STAMP(2, c0 / NB, 0);
   dbl4 acc[2][2], nxt[2][2];
   int u = 2 * (int)blockIdx.x;
   if (u < nunits) cload(u, acc);
@@ -763,6 +785,7 @@ __global__ __launch_bounds__(kBigThreads, 4) void k_syrk_big(double* __restrict_
       for (int tc = 0; tc < 2; ++tc) acc[tr][tc] = nxt[tr][tc];
     u = un;
   }
+  CHOL_STAMP(2, c0 / NB, 5);
 }
 
 
@@ -1045,7 +1068,60 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
                                  int* d_flag);
 
 static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag, bool launch);
+#ifdef DAB_CHOL_STAMPS
+// the stamps of one factorisation (the 4th of the process), per launch: for each phase the
+// median and max over work-groups, in us from the launch's first stamp, and its start
+// relative to the factorisation's first stamp
+static void chol_stamps_dump(int n) {
+  std::vector<unsigned long long> h((size_t)3 * kStampCb * kStampWg * 8);
+  if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_stamp), h.size() * 8) != hipSuccess) return;
+  const int nblk = std::min((n + NB - 1) / NB, kStampCb);
+  unsigned long long t0 = ~0ull;
+  for (unsigned long long v : h)
+    if (v && v < t0) t0 = v;
+  const char* kinds[3] = {"col+panel", "strip", "bulk"};
+  for (int kind = 0; kind < 3; ++kind)
+    for (int cb = 0; cb < nblk; ++cb) {
+      const unsigned long long* base = h.data() + ((size_t)kind * kStampCb + cb) * kStampWg * 8;
+      std::vector<double> ph[8];
+      unsigned long long s0 = ~0ull;
+      for (int wg = 0; wg < kStampWg; ++wg)
+        if (base[wg * 8] && base[wg * 8] < s0) s0 = base[wg * 8];
+      if (s0 == ~0ull) continue;
+      int nwg = 0;
+      for (int wg = 0; wg < kStampWg; ++wg) {
+        if (!base[wg * 8]) continue;
+        ++nwg;
+        for (int p = 0; p < 8; ++p)
+          if (base[wg * 8 + p] >= s0) ph[p].push_back((base[wg * 8 + p] - s0) * 0.01);
+      }
+      fprintf(stderr, "stamps %-9s cb %3d at %8.1f us, %3d wgs:", kinds[kind], cb, (s0 - t0) * 0.01, nwg);
+      for (int p = 0; p < 8; ++p) {
+        if (ph[p].empty()) continue;
+        std::sort(ph[p].begin(), ph[p].end());
+        fprintf(stderr, "  p%d %.1f/%.1f", p, ph[p][ph[p].size() / 2], ph[p].back());
+      }
+      if (kind == 0) {
+        const unsigned long long* w0 = base;  // work-group 0: the diagonal tile and the factor
+        fprintf(stderr, "  | wg0:");
+        for (int p = 0; p < 6; ++p)
+          if (w0[p] >= s0) fprintf(stderr, " %.1f", (w0[p] - s0) * 0.01);
+      }
+      fprintf(stderr, "\n");
+    }
+}
+#endif
 int chol_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y, int* d_flag) {
+#ifdef DAB_CHOL_STAMPS
+  static int calls = 0;
+  if (++calls == 4) {
+    (void)hipStreamSynchronize(s);
+    const int rc = chol_build(c, s, n, A, lda, y, d_flag, true);
+    (void)hipStreamSynchronize(s);
+    chol_stamps_dump(n);
+    return rc;
+  }
+#endif
   return chol_build(c, s, n, A, lda, y, d_flag, true);
 }
 // the scratch and the captured graph of a factorisation of this shape and these buffers,
@@ -1147,8 +1223,11 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
     const int r0 = cb * NB, m = n + 1 - r0;
     if (m <= 1) return;
     const int nt = (m + NB - 1) / NB;
-    k_syrk_mfma<<<nt, kThreads, 0, s>>>(A, lda, r0, m, k, kk, 1, nt, pre ? c->blk + (size_t)cb * kBlk : nullptr,
-                                       kb_of(cb), d_flag, fuse ? c->pready + cb : nullptr);
+    if (pre)
+      k_syrk_mfma<true><<<nt, kThreads, 0, s>>>(A, lda, r0, m, k, kk, 1, nt, c->blk + (size_t)cb * kBlk, kb_of(cb),
+                                                d_flag, fuse ? c->pready + cb : nullptr);
+    else
+      k_syrk_mfma<false><<<nt, kThreads, 0, s>>>(A, lda, r0, m, k, kk, 1, nt);
   };
   panel(0);
   // groups of R = c->group panels (2: the pairs). Within a group the chain updates column c
@@ -1181,7 +1260,7 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
       (void)hipStreamWaitEvent(s2, c->ev_panel[b], 0);
       if (strip && ms > 1) {
         const int nts = (ms + NB - 1) / NB;
-        k_syrk_mfma<<<nts, kThreads, 0, s2>>>(A, lda, cs0, ms, b * NB, kk, 1, nts);
+        k_syrk_mfma<false><<<nts, kThreads, 0, s2>>>(A, lda, cs0, ms, b * NB, kk, 1, nts);
         (void)hipEventRecord(c->ev_strip[b], s2);
       }
       if (m > 1) {
@@ -1242,13 +1321,13 @@ static void enqueue_factor_solve_v1(CholCtx* c, hipStream_t s, int n, double* A,
       (void)hipStreamWaitEvent(s2, c->ev_panel[b], 0);
       const int m2 = m - NB, nt2 = (m2 + NB - 1) / NB;
       const int ntb = nt2 * (nt2 + 1) / 2;
-      k_syrk_mfma<<<std::min(ntb, c->bulk_grid > 0 ? c->bulk_grid : ntb), kThreads, 0, s2>>>(A, lda, r0 + NB, m2, k,
+      k_syrk_mfma<false><<<std::min(ntb, c->bulk_grid > 0 ? c->bulk_grid : ntb), kThreads, 0, s2>>>(A, lda, r0 + NB, m2, k,
                                                                                          kb, 0, ntb);
       (void)hipEventRecord(c->ev_bulk[b], s2);
       bulk = true;
     }
     if (bulk_prev) (void)hipStreamWaitEvent(s, c->ev_bulk[b - 1], 0);
-    if (m > 1) k_syrk_mfma<<<nt, kThreads, 0, s>>>(A, lda, r0, m, k, kb, 1, nt);
+    if (m > 1) k_syrk_mfma<false><<<nt, kThreads, 0, s>>>(A, lda, r0, m, k, kb, 1, nt);
     if (b + 1 < nblk) panel(b + 1);
     bulk_prev = bulk;
   }
