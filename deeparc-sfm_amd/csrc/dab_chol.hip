@@ -54,7 +54,6 @@ struct CholCtx {
   int bulk_grid = 0;  // work-groups of the persistent bulk update (0: one per tile)
   int ncu = 256;
   unsigned* bar = nullptr;  // grid-barrier counter of k_trsv_back_all (zeroed per solve)
-  unsigned* ready = nullptr;  // per block: y_b published (k_trsv_back_flow; zeroed per solve)
   bool back_flow = true;      // DAB_CHOL_BACK_FLOW=0: the grid-barrier back substitution
   bool prefactor = true;      // DAB_CHOL_PREFACTOR=0: every panel work-group factors the diagonal block
   bool nograph = false;       // DAB_CHOL_NOGRAPH=1: launch directly instead of the captured graph (traces)
@@ -121,6 +120,9 @@ void chol_destroy(CholCtx* c) {
 // so the dependent chain per step is one launch instead of potrf -> inverse -> trsm.
 constexpr int LS = NB + 1;
 constexpr int DS = 17;
+// y's "not yet solved" pattern for the back substitution (both 32-bit halves: the double
+// 0x7FF47FF47FF47FF4, a signalling NaN, which no arithmetic produces)
+constexpr unsigned kYPending32 = 0x7FF47FF4u;
 #ifdef DAB_CHOL_PROFILE  // phase timestamps of work-group 0 (scripts/potrf_micro.hip only)
 __device__ long long g_prof[16];
 #define PROF_MARK(i) \
@@ -318,9 +320,13 @@ __device__ __forceinline__ void panel_rows_solve(double* Pf, const double* Lf, c
 // to the block scratch
 // pre: the diagonal block was factored by the column update in front (k_syrk_mfma with
 // fblk), so L_kk and the inverses are read from the block scratch instead
+// yinit / pinit (the factorisation's first panel): the launch also sets y[0, ny) to the
+// back substitution's pending pattern and zeroes pinit[0, np) (the fused steps' flags), so
+// that neither is a fill on the chain
 __global__ __launch_bounds__(kThreads) void k_panel(double* __restrict__ A, int lda, int k, int kb, int r0,
                                                     int r1, double* __restrict__ blk, int* __restrict__ flag,
-                                                    int pre) {
+                                                    int pre, double* __restrict__ yinit = nullptr, int ny = 0,
+                                                    unsigned* __restrict__ pinit = nullptr, int np = 0) {
   __shared__ double L[NB][LS];
   __shared__ double P[NB][LS];
   __shared__ double D[4][16][DS];
@@ -328,6 +334,9 @@ __global__ __launch_bounds__(kThreads) void k_panel(double* __restrict__ A, int 
   // bulk update's waves on shared CUs
   __builtin_amdgcn_s_setprio(3);
   const int tid = threadIdx.x, w = tid >> 6;
+  for (int i = blockIdx.x * kThreads + tid; i < ny; i += gridDim.x * kThreads)
+    yinit[i] = __longlong_as_double((long long)(((unsigned long long)kYPending32 << 32) | kYPending32));
+  for (int i = blockIdx.x * kThreads + tid; i < np; i += gridDim.x * kThreads) pinit[i] = 0u;
   const int row0 = r0 + NB * blockIdx.x;
   if (pre) {
     if (row0 >= r1) return;
@@ -909,11 +918,19 @@ __global__ __launch_bounds__(kThreads) void k_trsv_back_all(const double* __rest
 // that owner is on the critical path per block; everyone else consumes y_b in parallel.
 // The A block of the critical owned column is loaded before the wait. Waits are bounded
 // (flag |= 2 and the work-group ends). Every work-group must be resident (G <= CUs).
+// Round 6: y itself is the flag. It is filled with a signalling-NaN pattern before the
+// launch (no arithmetic result has that bit pattern: computed NaNs are quiet), the owner
+// stores y_b with agent-scope stores and nothing else, and a consumer polls y_b's 64 values
+// until none is the pattern — one memory round trip per block on the chain instead of two
+// (flag, then values) plus the owner's wait for its stores before the flag.
 constexpr int kMaxOwned = 4;
+__device__ __forceinline__ bool y_pending(double v) {
+  return __double_as_longlong(v) == (long long)(((unsigned long long)kYPending32 << 32) | kYPending32);
+}
 __global__ __launch_bounds__(kThreads) void k_trsv_back_flow(const double* __restrict__ A, int lda, int n, int nblk,
                                                              const double* __restrict__ blk,
                                                              const double* __restrict__ z, double* __restrict__ y,
-                                                             unsigned* __restrict__ ready, int* __restrict__ flag) {
+                                                             int* __restrict__ flag) {
   __shared__ double Lk[NB][LS];
   __shared__ double Li[NB][LS];  // L_bb^-1 of the next owned block (built off the critical path)
   __shared__ double Dq[4][16][DS];
@@ -996,11 +1013,7 @@ __global__ __launch_bounds__(kThreads) void k_trsv_back_flow(const double* __res
     }
     __syncthreads();
     if (tid < NB) yy[tid] = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
-    if (tid < 64) {  // wave 0: the stores, drained, then the flag
-      if (tid < kb) __hip_atomic_store(y + k + tid, yy[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (tid == 0) __hip_atomic_store(ready + sb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (tid < kb) __hip_atomic_store(y + k + tid, yy[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
   };
   if (nown == 0) return;
@@ -1027,21 +1040,25 @@ __global__ __launch_bounds__(kThreads) void k_trsv_back_flow(const double* __res
         pa[q] = (mm < kbb && col < n) ? A[(size_t)(kbk + mm) * lda + col] : 0.0;
       }
     }
-    if (tid == 0) {
+    if (tid < NB) {  // wave 0 polls y_b until every value has landed
+      double v = 0.0;
       int spins = 0;
-      while (__hip_atomic_load(ready + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      for (;;) {
+        v = tid < kbb ? __hip_atomic_load(y + kbk + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+        if (!__any(y_pending(v))) break;
         __builtin_amdgcn_s_sleep(1);
         if (++spins > (1 << 22)) {
-          abort_s = 1;
-          atomicOr(flag, 2);
+          if (tid == 0) {
+            abort_s = 1;
+            atomicOr(flag, 2);
+          }
           break;
         }
       }
+      yy[tid] = v;
     }
     __syncthreads();
     if (abort_s) return;
-    if (tid < NB) yy[tid] = tid < kbb ? __hip_atomic_load(y + kbk + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-    __syncthreads();
     for (int j = jmax; j >= 0; --j) {
       const int col = (w + G * j) * NB + i;
       double sacc = 0.0;
@@ -1135,11 +1152,10 @@ static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
   if ((size_t)nblk > c->nblk_alloc) {
     if (c->exec) (void)hipGraphExecDestroy(c->exec);
     c->exec = nullptr;
-    for (void* p : {(void*)c->blk, (void*)c->ready, (void*)c->pready}) c->mem.drop(p);
+    for (void* p : {(void*)c->blk, (void*)c->pready}) c->mem.drop(p);
     c->blk = nullptr;
-    c->ready = c->pready = nullptr;
+    c->pready = nullptr;
     if (c->mem.alloc(&c->blk, (size_t)kBlk * nblk) != 0) return -2;
-    if (c->mem.alloc(&c->ready, (size_t)nblk) != 0) return -2;
     if (c->mem.alloc(&c->pready, (size_t)nblk) != 0) return -2;
     c->nblk_alloc = nblk;
   }
@@ -1188,7 +1204,7 @@ static int chol_build(CholCtx* c, hipStream_t s, int n, double* A, int lda, doub
 }
 
 static void enqueue_back_substitution(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y,
-                                      int* d_flag);
+                                      int* d_flag, bool y_filled);
 static void enqueue_factor_solve_v1(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y,
                                     int* d_flag);
 // Panel PAIRS with lookahead. Chain stream s, per pair (b, b+1): [wait the previous pair's
@@ -1208,7 +1224,6 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
   // every panel after the first follows the column update of its block, which factors the
   // diagonal block (DAB_CHOL_PREFACTOR=0: each panel work-group factors it itself)
   const bool pre = c->prefactor, fuse = pre && c->fuse_panel;
-  if (fuse) (void)hipMemsetAsync(c->pready, 0, sizeof(unsigned) * (size_t)nblk, s);
   auto panel = [&](int b) {
     // done inside the column update in front, except for a last block shorter than NB,
     // whose rows below (the rhs row) sit in the diagonal tile
@@ -1216,7 +1231,11 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
     const int k = b * NB, kb = kb_of(b);
     const int r0 = k + kb, r1 = n + 1;  // includes the rhs row n
     const int grid = std::max(1, (r1 - r0 + NB - 1) / NB);
-    k_panel<<<grid, kThreads, 0, s>>>(A, lda, k, kb, r0, r1, c->blk + (size_t)b * kBlk, d_flag, pre && b > 0);
+    // the first panel also fills y (pending) and zeroes the fused steps' flags
+    const bool first = b == 0;
+    k_panel<<<grid, kThreads, 0, s>>>(A, lda, k, kb, r0, r1, c->blk + (size_t)b * kBlk, d_flag, pre && b > 0,
+                                      first ? y : nullptr, first ? n : 0, first && fuse ? c->pready : nullptr,
+                                      first && fuse ? nblk : 0);
   };
   // column block cb (rows >= its first row, through the rhs row) with panel columns [k, k + kk)
   auto col = [&](int cb, int k, int kk) {
@@ -1278,17 +1297,19 @@ static void enqueue_factor_solve(CholCtx* c, hipStream_t s, int n, double* A, in
     panel(cend);
   }
   if (pending >= 0) (void)hipStreamWaitEvent(s, c->ev_bulk[pending], 0);
-  enqueue_back_substitution(c, s, n, A, lda, y, d_flag);
+  enqueue_back_substitution(c, s, n, A, lda, y, d_flag, true);
 }
 
+// y_filled: the factorisation's first panel launch set y to the pending pattern
 static void enqueue_back_substitution(CholCtx* c, hipStream_t s, int n, double* A, int lda, double* y,
-                                      int* d_flag) {
+                                      int* d_flag, bool y_filled) {
   const int nblk = (n + NB - 1) / NB;
   double* z = A + (size_t)n * lda;
   const int G = std::max(1, std::min(c->ncu / 2, (n + 63) / 64));
   if (c->back_flow && nblk <= G * kMaxOwned) {
-    (void)hipMemsetAsync(c->ready, 0, sizeof(unsigned) * (size_t)nblk, s);
-    k_trsv_back_flow<<<G, kThreads, 0, s>>>(A, lda, n, nblk, c->blk, z, y, c->ready, d_flag);
+    // y_b is pending until its owner stores it (k_trsv_back_flow polls the values themselves)
+    if (!y_filled) (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(y), kYPending32, 2 * (size_t)n, s);
+    k_trsv_back_flow<<<G, kThreads, 0, s>>>(A, lda, n, nblk, c->blk, z, y, d_flag);
     return;
   }
   (void)hipMemsetAsync(c->bar, 0, sizeof(unsigned), s);
