@@ -185,9 +185,12 @@ void launch_entry_y(hipStream_t s, const DevView& v, const double* points, const
                     const double* scale_c, const double* PU, YBufs Y, bool with_pm, double* rec = nullptr);
 // S blocks (Y part): packed[blk][36] = - sum_pairs Y_row Y_col^T (pairs hold positions;
 // Y = the fp64 camera-major planes, stride NE; Yr = scratch [NE][18] for the records, or
-// Y = nullptr when Yr already holds them)
+// Y = nullptr when Yr already holds them). S != nullptr (one rank): the blocks go straight
+// into the dense lower S at (6 c, 6 d) of blk_cam[blk], and the nzero lower blocks without
+// pairs (blk_zero) are zeroed, instead of packed[] and launch_s_unpack's zero + scatter
 void launch_s_blocks(hipStream_t s, int nblk, const int* blk_pair_beg, const int2* pairs,
-                     const double* Y, int NE, double* packed, double* Yr);
+                     const double* Y, int NE, double* packed, double* Yr, double* S = nullptr, int lds = 0,
+                     const int2* blk_cam = nullptr, int nzero = 0, const int2* blk_zero = nullptr);
 // Explicit S for small camera sets without pair tables (k_schur_y + k_schur_tiles): every
 // thread of a work-group owns one 6x6 block of the lower block triangle of S (numbered
 // row-major: block (c, d <= c) = c (c+1)/2 + d) and sums it in registers over the records of

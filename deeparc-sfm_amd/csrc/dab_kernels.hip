@@ -2793,10 +2793,13 @@ __global__ __launch_bounds__(256) void k_y_records(int NE, const double* __restr
 // pair (c, c + 3)) and sums the terms of the pairs i = group, group + 3, ...; the three
 // groups are added in group order at the end (fixed order, deterministic). The old form
 // used 36 lanes on one pair per step.
+// S (one rank): the block goes straight into the dense lower S (rows 6 c + a, columns
+// 6 d + b of block (c, d) = blk_cam[blk]) instead of packed[] (then all-reduced and scattered)
 __global__ __launch_bounds__(256) void k_s_blocks(int nblk, const int* __restrict__ blk_pair_beg,
                                                   const int2* __restrict__ pairs,
                                                   const double* __restrict__ Yr,
-                                                  double* __restrict__ packed) {
+                                                  double* __restrict__ packed, double* __restrict__ S, int lds,
+                                                  const int2* __restrict__ blk_cam) {
   const int blk = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (blk >= nblk) return;  // wave-uniform
@@ -2835,16 +2838,32 @@ __global__ __launch_bounds__(256) void k_s_blocks(int nblk, const int* __restric
   const double g1a = __shfl(acc0, lane + 18), g1b = __shfl(acc1, lane + 18);
   const double g2a = __shfl(acc0, lane + 36), g2b = __shfl(acc1, lane + 36);
   if (lane < 18) {
-    packed[36 * (size_t)blk + 6 * a + c] = -((acc0 + g1a) + g2a);
-    packed[36 * (size_t)blk + 6 * a + c + 3] = -((acc1 + g1b) + g2b);
+    double* o = packed + 36 * (size_t)blk + 6 * a;
+    if (S) {
+      const int2 rc = blk_cam[blk];  // (row cam, col cam), row >= col
+      o = S + (size_t)(6 * rc.x + a) * lds + 6 * rc.y;
+    }
+    o[c] = -((acc0 + g1a) + g2a);
+    o[c + 3] = -((acc1 + g1b) + g2b);
   }
+}
+// the lower blocks of S without any pair (absent from blk_cam): zeros
+__global__ void k_s_zero_blocks(int nzero, const int2* __restrict__ blk_zero, double* __restrict__ S, int lds) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nzero * 36) return;
+  const int blk = t / 36, ab = t - 36 * blk, a = ab / 6, b = ab - 6 * (ab / 6);
+  const int2 rc = blk_zero[blk];
+  S[(size_t)(6 * rc.x + a) * lds + 6 * rc.y + b] = 0.0;
 }
 
 void launch_s_blocks(hipStream_t s, int nblk, const int* blk_pair_beg, const int2* pairs,
-                     const double* Y, int NE, double* packed, double* Yr) {
+                     const double* Y, int NE, double* packed, double* Yr, double* S, int lds, const int2* blk_cam,
+                     int nzero, const int2* blk_zero) {
+  if (S && nzero > 0)
+    k_s_zero_blocks<<<grid_for(nzero * 36, 256, 1 << 20), 256, 0, s>>>(nzero, blk_zero, S, lds);
   if (nblk <= 0) return;
   if (Y) k_y_records<<<(unsigned)(((size_t)kYRec * NE + 255) / 256), 256, 0, s>>>(NE, Y, Yr);
-  k_s_blocks<<<(nblk + 3) / 4, 256, 0, s>>>(nblk, blk_pair_beg, pairs, Yr, packed);
+  k_s_blocks<<<(nblk + 3) / 4, 256, 0, s>>>(nblk, blk_pair_beg, pairs, Yr, packed, S, lds, blk_cam);
 }
 
 template <bool REC>

@@ -416,6 +416,8 @@ struct dab_handle {
   int *d_xchunk_beg = nullptr, *d_xseg_chunk = nullptr;
   int2* d_cross_cam = nullptr;
   int2 *d_pairs = nullptr, *d_blk_cam = nullptr;
+  int2* d_blk_zero = nullptr;  // lower blocks of S without pairs (one rank: zeroed directly)
+  int nzero = 0;
   int* d_blk_pair_beg = nullptr;
   double* d_intr = nullptr;
   double *d_points = nullptr, *d_points_c = nullptr, *d_ext = nullptr, *d_ext_c = nullptr;
@@ -1373,6 +1375,7 @@ static int setup_host(dab_handle* h, const dab_problem* p, const std::function<v
   h->fused_grid = 0;      // so did the single-pass product's partials
   h->mf_grid_n = 0;
   h->nblk = 0;
+  h->nzero = 0;
   h->npairs = 0;
 
   // intrinsics: (cx, cy, fx, fy', k0, k1) with unused distortion terms zeroed
@@ -1927,6 +1930,7 @@ static int setup_device(dab_handle* h, const dab_problem* p, const std::function
   h->fused_grid = 0;
   h->mf_grid_n = 0;
   h->nblk = 0;
+  h->nzero = 0;
   h->npairs = 0;
 
   // intrinsics: (cx, cy, fx, fy', k0, k1) with unused distortion terms zeroed
@@ -2485,6 +2489,7 @@ static int build_schur_tables(dab_handle* h) {
     CHECK_RC(build_schur_tiles(h, tile_sch, tile_m));
     t_ph = now_s();
     h->nblk = 0;
+    h->nzero = 0;
     h->npairs = 0;
     CHECK_RC(h->dev.alloc(&h->d_spack, h->spack_count()));  // ybc only
     phase("tiles: spack alloc");
@@ -2622,9 +2627,24 @@ static int build_schur_tables(dab_handle* h) {
   std::vector<int2> blk_cam(h->nblk);
   for (int b = 0; b < h->nblk; ++b) blk_cam[b] = make_int2((int)(blkkeys[b] / NC), (int)(blkkeys[b] % NC));
 
+  // the lower blocks no pair reaches (blkkeys is sorted): zeroed per step on one rank, where
+  // the blocks are written into S directly
+  std::vector<int2> blk_zero;
+  {
+    size_t j = 0;
+    for (int c = 0; c < NC; ++c)
+      for (int d2 = 0; d2 <= c; ++d2) {
+        const long long key = (long long)c * NC + d2;
+        while (j < blkkeys.size() && blkkeys[j] < key) ++j;
+        if (j >= blkkeys.size() || blkkeys[j] != key) blk_zero.push_back(make_int2(c, d2));
+      }
+  }
+  h->nzero = (int)blk_zero.size();
+
   Dev& d = h->dev;
   if (!on_device) CHECK_RC(upload(&h->d_pairs, d, pairs, s));
   CHECK_RC(upload(&h->d_blk_cam, d, blk_cam, s));
+  if (h->nzero > 0) CHECK_RC(upload(&h->d_blk_zero, d, blk_zero, s));
   CHECK_RC(upload(&h->d_blk_pair_beg, d, blk_pair_beg, s));
   CHECK_RC(d.alloc(&h->d_spack, h->spack_count()));
   const int n = 6 * NC;
@@ -3222,13 +3242,21 @@ static int solve_impl(dab_handle* h, const dab_options* opt_in, dab_summary* sum
       // plane-to-record copy); the slot planes as before (back substitution)
       const bool rec = !yb.f32;
       launch_entry_y(s, v, h->d_points, h->d_camtab, h->d_scale_c, h->d_L, yb, true, rec ? h->d_Yrec : nullptr);
+      // one rank: the S blocks straight into the dense S (nothing to all-reduce), no zero
+      // fill of the whole matrix and no scatter; several: packed, all-reduced, unpacked
+      const bool direct = h->world == 1;
       launch_s_blocks(s, h->nblk, h->d_blk_pair_beg, h->d_pairs, rec ? nullptr : h->d_Y, h->NE, h->packed(),
-                      h->d_Yrec);
+                      h->d_Yrec, direct ? h->d_S : nullptr, h->lds, h->d_blk_cam, h->nzero, h->d_blk_zero);
       launch_cam_rhs_partial(s, v, h->nchunk, h->d_chunk_beg, rec ? h->d_Yrec : h->d_Y, h->d_q, h->d_partial, rec);
       launch_seg_final(s, NC, 6, h->d_seg_chunk, h->d_partial, h->ybc(), h->max_seg_chunks);
-      CHECK_RC(h->allreduce(h->d_spack, h->spack_count(), ncclSum));
-      launch_s_unpack(s, NC, h->nblk, h->d_blk_cam, h->packed(), h->ug(), h->ncross, h->d_cross_cam, h->Ux(),
-                      h->d_scale_c, sc, h->ybc(), h->d_S, h->lds);
+      if (direct) {
+        launch_s_add_u(s, NC, h->ug(), h->ncross, h->d_cross_cam, h->Ux(), h->d_scale_c, sc, h->ybc(), h->d_S,
+                       h->lds);
+      } else {
+        CHECK_RC(h->allreduce(h->d_spack, h->spack_count(), ncclSum));
+        launch_s_unpack(s, NC, h->nblk, h->d_blk_cam, h->packed(), h->ug(), h->ncross, h->d_cross_cam, h->Ux(),
+                        h->d_scale_c, sc, h->ybc(), h->d_S, h->lds);
+      }
       if (chol_factor_solve(h->chol, s, n, h->d_S, h->lds, h->d_yc, h->d_flags + 1) != 0)
         return set_error(DAB_E_DEVICE, "dense Cholesky launch failed");
     }
