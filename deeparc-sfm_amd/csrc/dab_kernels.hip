@@ -2792,44 +2792,74 @@ __global__ __launch_bounds__(256) void k_y_records(int NE, const double* __restr
 // one wave per S block, three pairs per step: lane l < 54 is (group l / 18, row a, column
 // pair (c, c + 3)) and sums the terms of the pairs i = group, group + 3, ...; the three
 // groups are added in group order at the end (fixed order, deterministic). The old form
-// used 36 lanes on one pair per step.
-// S (one rank): the block goes straight into the dense lower S (rows 6 c + a, columns
-// 6 d + b of block (c, d) = blk_cam[blk]) instead of packed[] (then all-reduced and scattered)
+// used 36 lanes on one pair per step. Round 6: each group's 18 lanes load the pair's two
+// records once, one element each (coalesced 144-B records), into the wave's LDS, and every
+// lane takes its row / columns from there — the rows were loaded by every lane that needed
+// them before (9 loads per lane per pair, 4.5x the records' bytes through the L1/TA);
+// the same products and sums: bitwise the same blocks.
 __global__ __launch_bounds__(256) void k_s_blocks(int nblk, const int* __restrict__ blk_pair_beg,
                                                   const int2* __restrict__ pairs,
                                                   const double* __restrict__ Yr,
                                                   double* __restrict__ packed, double* __restrict__ S, int lds,
                                                   const int2* __restrict__ blk_cam) {
+  constexpr int U = 4;                     // pairs per group per step
+  __shared__ double ys[4][3][U][2 * kYRec];  // [wave][group][pair][x record | y record]
   const int blk = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (blk >= nblk) return;  // wave-uniform
   const int grp = lane < 54 ? lane / 18 : 3, k = lane - 18 * (lane / 18);
   const int a = k / 3, c = k - 3 * (k / 3);
+  double* L = &ys[threadIdx.x >> 6][grp < 3 ? grp : 0][0][0];
   double acc0 = 0.0, acc1 = 0.0;
-  auto term = [&](const int2 pr, double& t0, double& t1) {
-    const double* x = Yr + (size_t)kYRec * pr.x + 3 * a;
-    const double* y = Yr + (size_t)kYRec * pr.y + 3 * c;
+  auto term = [&](int u, double& t0, double& t1) {
+    const double* x = L + 2 * kYRec * u + 3 * a;
+    const double* y = L + 2 * kYRec * u + kYRec + 3 * c;
     const double x0 = x[0], x1 = x[1], x2 = x[2];
     t0 = x0 * y[0] + x1 * y[1] + x2 * y[2];
     t1 = x0 * y[9] + x1 * y[10] + x2 * y[11];
+  };
+  auto sync = []() {  // the group's LDS stores visible to its lanes / its reads done
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
   const int e = blk_pair_beg[blk + 1];
   int i = blk_pair_beg[blk] + grp;
   if (grp < 3) {
     // four of the group's pairs in flight per step (twelve per wave)
     for (; i + 9 < e; i += 12) {
-      double t0[4], t1[4];
+      double xv[U], yv[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) term(pairs[i + 3 * u], t0[u], t1[u]);
+      for (int u = 0; u < U; ++u) {
+        const int2 pr = pairs[i + 3 * u];
+        xv[u] = Yr[(size_t)kYRec * pr.x + k];
+        yv[u] = Yr[(size_t)kYRec * pr.y + k];
+      }
+      sync();
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
+        L[2 * kYRec * u + k] = xv[u];
+        L[2 * kYRec * u + kYRec + k] = yv[u];
+      }
+      sync();
+      double t0[U], t1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) term(u, t0[u], t1[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
         acc0 += t0[u];
         acc1 += t1[u];
       }
     }
     for (; i < e; i += 3) {
+      const int2 pr = pairs[i];
+      const double xv = Yr[(size_t)kYRec * pr.x + k], yv = Yr[(size_t)kYRec * pr.y + k];
+      sync();
+      L[k] = xv;
+      L[kYRec + k] = yv;
+      sync();
       double t0, t1;
-      term(pairs[i], t0, t1);
+      term(0, t0, t1);
       acc0 += t0;
       acc1 += t1;
     }
