@@ -3406,6 +3406,13 @@ __global__ __launch_bounds__(256) void k_backsub(DevView v, const double* __rest
 // work-groups, summed in fixed order: bitwise repeatable). All arithmetic fp64.
 constexpr int kMfCams = kMfCamsMax;
 constexpr int kMfBlock = 256;
+// -DDAB_ABL_MF_NOSUMS (timing only, wrong results): the products' sweep-2 camera sums go to
+// a register instead of the per-wave fp64 LDS atomics (scripts/runs/r06y2.sh)
+#ifdef DAB_ABL_MF_NOSUMS
+#define MF_LDS_ADD(ptr, x) (mf_sink += (x))
+#else
+#define MF_LDS_ADD(ptr, x) atomicAdd((ptr), (x))
+#endif
 bool mf_schur_fits(int NC, int E, int NI) { return NC > 0 && NC <= kMfCams && small_tabs_fit(E, NI); }
 __device__ __forceinline__ void mv3(const double* __restrict__ M, const double (&x)[3], double (&o)[3]) {
   o[0] = M[0] * x[0] + M[1] * x[1] + M[2] * x[2];
@@ -3503,6 +3510,16 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const doubl
     }
   };
   double* acc = accs + (threadIdx.x >> 6) * 6 * NCP;
+#ifdef DAB_ABL_MF_NOSUMS
+  double mf_sink = 0.0;  // kept live (a store no run takes) so the sums' arithmetic stays
+  struct SinkGuard {
+    double& s;
+    double* o;
+    __device__ ~SinkGuard() {
+      if (s == -1.25e300) o[0] = s;
+    }
+  } sink_guard{mf_sink, out};
+#endif
   const size_t NPs = (size_t)v.NP;
   auto rot9 = [&](int e, double (&o)[9]) {
     const double2* pp = reinterpret_cast<const double2*>(rt_s + kRtStride * e);
@@ -3656,18 +3673,18 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame(DevView v, const doubl
           double cz[3];
           cross3(Z0, gz, cz);
 #pragma unroll
-          for (int a = 0; a < 3; ++a) atomicAdd(acc + a * NCP + c0, cz[a]);
+          for (int a = 0; a < 3; ++a) MF_LDS_ADD(acc + a * NCP + c0, cz[a]);
 #pragma unroll
-          for (int a = 0; a < 3; ++a) atomicAdd(acc + (3 + a) * NCP + c0, gz[a]);
+          for (int a = 0; a < 3; ++a) MF_LDS_ADD(acc + (3 + a) * NCP + c0, gz[a]);
         }
         if (c1 >= 0) {
           double hz[3], cz[3];
           mtv3(Ra, gz, hz);
           cross3(Z1, hz, cz);
 #pragma unroll
-          for (int a = 0; a < 3; ++a) atomicAdd(acc + a * NCP + c1, cz[a]);
+          for (int a = 0; a < 3; ++a) MF_LDS_ADD(acc + a * NCP + c1, cz[a]);
 #pragma unroll
-          for (int a = 0; a < 3; ++a) atomicAdd(acc + (3 + a) * NCP + c1, hz[a]);
+          for (int a = 0; a < 3; ++a) MF_LDS_ADD(acc + (3 + a) * NCP + c1, hz[a]);
         }
       }
     }
@@ -3797,8 +3814,18 @@ __global__ __launch_bounds__(kMfBlock, 4) void k_mf_frame32(DevView v, const dou
   for (int i = threadIdx.x; i < (kMfBlock / 64) * 6 * NCP; i += blockDim.x) accs[i] = 0.0;
   __syncthreads();
   double* acc = accs + (threadIdx.x >> 6) * 6 * NCP;
+#ifdef DAB_ABL_MF_NOSUMS
+  double mf_sink = 0.0;  // kept live (a store no run takes) so the sums' arithmetic stays
+  struct SinkGuard {
+    double& s;
+    double* o;
+    __device__ ~SinkGuard() {
+      if (s == -1.25e300) o[0] = s;
+    }
+  } sink_guard{mf_sink, out};
+#endif
   auto add = [&](int c, int a, float x) {
-    atomicAdd(acc + a * NCP + c, (double)x);  // fp64 per-wave sums
+    MF_LDS_ADD(acc + a * NCP + c, (double)x);  // fp64 per-wave sums
   };
   auto sum_of = [&](int c, int a) {  // fixed order over the waves
     double t = accs[a * NCP + c];
