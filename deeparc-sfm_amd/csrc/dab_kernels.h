@@ -68,6 +68,8 @@ struct DevView {
   int NI;         // intrinsics
   int nslice;     // SELL-64 slices (64 points each)
   int any_comp;   // some observation is arc∘ring (ext1 >= 0)
+  int uni_affine;  // chunk_uni[c] == (c + uni_ox, c + uni_oi) for every camera chunk c (one
+  int uni_ox, uni_oi;  // chunk per free camera): k_eval_bal's frames skip that load
   const int4* obs_idx;      // (point, ext0, ext1, intr)
   const double2* obs_xy;
   const int4* cm_idx;       // [NE] obs_idx of the entry's observation, w |= kSlotBit for slot 1

@@ -1964,7 +1964,9 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
   auto build_frames = [&]() {
     const int c = cam_of(lane);
     if (lane < nsl && c < v.NC) {
-      const int2 u = v.chunk_uni[c];
+      // the (ext, intr) of the camera's chunk: computed when the map is affine (the usual
+      // BAL numbering), which takes one dependent load off the frames' start
+      const int2 u = v.uni_affine ? make_int2(c + v.uni_ox, c + v.uni_oi) : v.chunk_uni[c];
       double k6[6];  // the intrinsic leaves with the extrinsic (one round trip for both)
 #pragma unroll
       for (int q = 0; q < 6; ++q) k6[q] = v.intr[(size_t)kIntr * u.y + q];

@@ -410,6 +410,7 @@ struct dab_handle {
       *d_ent_pt = nullptr, *d_ent_pos = nullptr, *d_cm_pt = nullptr, *d_ext_col = nullptr;
   int *d_chunk_beg = nullptr, *d_seg_chunk = nullptr;
   int2* d_chunk_uni = nullptr;
+  int uni_affine = 0, uni_ox = 0, uni_oi = 0;  // chunk_uni[c] = (c + ox, c + oi) for every chunk
   unsigned* d_arrivals = nullptr;  // last-arriver counter of the point kernel (kept zeroed)
   int* d_chunk_lists = nullptr;  // uniform chunk ids, then the others
   ChunkLists chunks;
@@ -974,6 +975,20 @@ static int validate_obs(const dab_problem* p) {
 // The host reference path of the set-up (DAB_SETUP_HOST=1; multi-rank problems and sizes
 // setup_device_fits refuses): stable counting sorts and gathers on host threads, then the
 // uploads. setup_device builds the same arrays on the GPU.
+// whether the camera chunks' (ext, intr) pairs are an affine map of the chunk index (one
+// chunk per free camera, both indices offset by a constant): the fused pass then computes them
+static void set_uni_affine(dab_handle* h, const std::vector<int2>& cu) {
+  h->uni_affine = 0;
+  h->uni_ox = h->uni_oi = 0;
+  if (cu.empty() || (int)cu.size() != h->NC) return;
+  const int ox = cu[0].x, oi = cu[0].y;
+  if (ox < 0 || oi < 0) return;
+  for (size_t c = 0; c < cu.size(); ++c)
+    if (cu[c].x != (int)c + ox || cu[c].y != (int)c + oi) return;
+  h->uni_affine = 1;
+  h->uni_ox = ox;
+  h->uni_oi = oi;
+}
 static int setup_host(dab_handle* h, const dab_problem* p, const std::function<void(const char*)>& phase) {
   CHECK_RC(validate_obs(p));
   h->setup_tmp.clear();  // a previous device set-up's scratch (the host path needs none)
@@ -1412,6 +1427,7 @@ static int setup_host(dab_handle* h, const dab_problem* p, const std::function<v
   CHECK_RC(upload(&h->d_cm_xy, d, cm_xy, s));
   CHECK_RC(upload(&h->d_chunk_beg, d, chunk_beg, s));
   CHECK_RC(upload(&h->d_chunk_uni, d, chunk_uni, s));
+  set_uni_affine(h, chunk_uni);
   CHECK_RC(d.alloc(&h->d_arrivals, 1));
   HIP_OK(hipMemsetAsync(h->d_arrivals, 0, sizeof(unsigned), s));
   {
@@ -1533,6 +1549,9 @@ static int setup_buffers(dab_handle* h, const std::function<void(const char*)>& 
   v.NE = NE;
   v.nslice = h->nslice;
   v.any_comp = h->local_compose ? 1 : 0;
+  v.uni_affine = h->uni_affine;
+  v.uni_ox = h->uni_ox;
+  v.uni_oi = h->uni_oi;
   v.obs_idx = h->d_obs_idx;
   v.obs_xy = h->d_obs_xy;
   v.cm_idx = h->d_cm_idx;
@@ -1783,6 +1802,7 @@ static int setup_device(dab_handle* h, const dab_problem* p, const std::function
   std::vector<int2> chunk_uni(nchunk);
   CHECK_RC(d2h(chunk_uni.data(), h->d_chunk_uni, sizeof(int2) * (size_t)nchunk));
   HIP_OK(hipStreamSynchronize(s));
+  set_uni_affine(h, chunk_uni);
   phase("device: camera-major");
 
   // ---- pair-major copy of the composed observations (rig) ----
