@@ -213,6 +213,8 @@ struct SchurTiles {
                                      // off[NC + 1] (int, records before camera c in the batch)
   int hdr_bytes;                     // 16-B multiple
   int batch_cap;                     // records per batch (one LDS buffer)
+  int single;                        // 1: one LDS buffer of kTileLdsMax (batches twice as large, each
+                                     // batch's DMA waited for); 0: two buffers, the next batch in flight
   const int* tile_clast;             // [ntile] last row camera of the tile (its records: a batch prefix)
   const int* tile_slot;              // [ntile][2 kTileThreads] block owned by (thread, half) or -1,
                                      // balanced by the blocks' sampled hit counts
@@ -232,7 +234,7 @@ struct SchurTiles {
 };
 constexpr int kTileThreads = 512;     // threads of a k_schur_tiles work-group (two blocks each)
 constexpr size_t kTileLdsMax = 163840;            // LDS of one k_schur_tiles work-group (at most)
-int schur_tile_batch_cap(int NC);                 // records per batch (one of two LDS buffers)
+int schur_tile_batch_cap(int NC, bool single);    // records per batch (one LDS buffer, or one of two)
 int schur_tile_hdr_bytes(int NC);                 // batch header bytes (16-B multiple)
 void launch_schur_scale(hipStream_t s, int NC, const double* ug, const double* scale_c, int* kx);
 // Y of every record -> yrec[nrec][18]; rhs fixed-point sums added into rhs_out[6 NC]

@@ -2997,9 +2997,13 @@ void launch_s_unpack(hipStream_t s, int NC, int nblk, const int2* blk_cam, const
 // work-group every thread OWNS two blocks of the tile and keeps their 72 sums in registers
 // (the pair of a heavy and a light block by sampled hit counts, so the lanes of a wave have
 // similar work). The records are ordered (batch, camera, point), so a tile whose last row
-// camera is c needs only a prefix of each batch; batches stream through two LDS buffers by
-// LDS-DMA (global_load_lds, no registers): batch b + 1 is in flight while batch b is
-// summed. Per batch, a per-camera mask of the batch's points and per-camera record offsets
+// camera is c needs only a prefix of each batch; batches arrive by LDS-DMA (global_load_lds,
+// no registers) into ONE buffer of the whole LDS (round 6; SchurTiles::single): a batch then
+// holds up to 64 points instead of ~34 at C5, so a lane's hit count per batch is Poisson with
+// twice the mean and the wave's busiest lane (which every lane waits for) wastes less:
+// k_schur_tiles 3.50 -> 3.19 ms at C5 although each batch's DMA is now waited for
+// (profiles/r06z6_*). The two-buffer form (batch b + 1 in flight while batch b is summed)
+// stays as DAB_TILE_SINGLE=0. Per batch, a per-camera mask of the batch's points and per-camera record offsets
 // (the batch header, DMA'd with it) give the records of a (point, camera) pair by a popcount.
 // Each thread walks the points that see both of its cameras in batch order. No atomics:
 // each block's sum has one fixed order (groups' partials then added in group order), so the
@@ -3008,9 +3012,9 @@ constexpr size_t kTileBufBytes = kTileLdsMax / 2;  // one LDS buffer: header are
 __host__ __device__ inline int tile_hdr_bytes(int NC) { return (int)(((size_t)8 * NC + (size_t)4 * (NC + 1) + 15) / 16 * 16); }
 int schur_tile_hdr_bytes(int NC) { return tile_hdr_bytes(NC); }
 __host__ __device__ inline size_t tile_hdr_area(int NC) { return ((size_t)tile_hdr_bytes(NC) + 1023) / 1024 * 1024; }
-int schur_tile_batch_cap(int NC) {
+int schur_tile_batch_cap(int NC, bool single) {
   // records land in whole 1-KB DMA chunks (a chunk's tail lanes repeat its last piece)
-  const size_t area = (kTileBufBytes - tile_hdr_area(NC)) / 1024 * 1024;
+  const size_t area = ((single ? kTileLdsMax : kTileBufBytes) - tile_hdr_area(NC)) / 1024 * 1024;
   return (int)(area / (18 * sizeof(double)));
 }
 
@@ -3216,13 +3220,19 @@ __global__ __launch_bounds__(kTileThreads) void k_schur_tiles(const double* __re
 #pragma unroll
   for (int k = 0; k < 36; ++k) accA[k] = accB[k] = 0.0;
   const int b0 = (int)((long long)a.nbatch * slot / nslot), b1 = (int)((long long)a.nbatch * (slot + 1) / nslot);
-  if (b0 < b1) tile_dma_batch(a, yrec, NC, clast, b0, tile_lds);
+  const bool single = a.single != 0;
+  if (b0 < b1 && !single) tile_dma_batch(a, yrec, NC, clast, b0, tile_lds);
   __syncthreads();  // drains the DMA (vmcnt) and publishes buffer 0
   for (int b = b0; b < b1; ++b) {
-    unsigned char* cur = tile_lds + kTileBufBytes * ((b - b0) & 1);
-    // the next batch streams into the other buffer while this one is summed (the sums
-    // below touch only LDS and registers, so nothing waits for the DMA before the barrier)
-    if (b + 1 < b1) tile_dma_batch(a, yrec, NC, clast, b + 1, tile_lds + kTileBufBytes * ((b + 1 - b0) & 1));
+    unsigned char* cur = single ? tile_lds : tile_lds + kTileBufBytes * ((b - b0) & 1);
+    if (single) {  // one buffer: the batch lands, then it is summed
+      tile_dma_batch(a, yrec, NC, clast, b, tile_lds);
+      __syncthreads();
+    } else if (b + 1 < b1) {
+      // the next batch streams into the other buffer while this one is summed (the sums
+      // below touch only LDS and registers, so nothing waits for the DMA before the barrier)
+      tile_dma_batch(a, yrec, NC, clast, b + 1, tile_lds + kTileBufBytes * ((b + 1 - b0) & 1));
+    }
     const unsigned long long* mask = reinterpret_cast<const unsigned long long*>(cur);
     const int* off = reinterpret_cast<const int*>(cur + 8 * (size_t)NC);
     const double* ly = reinterpret_cast<const double*>(cur + tile_hdr_area(NC));

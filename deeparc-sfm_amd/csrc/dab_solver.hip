@@ -304,6 +304,8 @@ struct Knobs {
   int bench_sample = 8;     // DAB_BENCH_SAMPLE: timing-event stride of dab_bench_eval_pass
   int schur_tiles = 1;      // DAB_SCHUR_TILES=0: explicit S from the pair tables even for small NC
   int tile_balance = 1;     // DAB_TILE_BALANCE=0: one work-group per tile and group of batches
+  int tile_single = 1;      // DAB_TILE_SINGLE=0: k_schur_tiles with two LDS buffers (batches half as
+                            // large, the next one in flight; round 6: one buffer, C5 EXACT 5.5 -> 5.2 ms)
   int tile_minb = 2;        // DAB_TILE_MINB: fewest batches per k_schur_tiles work-group (8 until round 6)
   int p2p = -1;             // DAB_P2P: one-shot xGMI all-reduce of small sums (-1 auto: RCCL handles
                             // only; 1 also on host-staged handles, the one-GPU rehearsal; 0 off)
@@ -335,6 +337,7 @@ struct Knobs {
     get("DAB_SCHUR_TILES", schur_tiles);
     get("DAB_TILE_BALANCE", tile_balance);
     get("DAB_TILE_MINB", tile_minb);
+    get("DAB_TILE_SINGLE", tile_single);
     get("DAB_P2P", p2p);
     get("DAB_FUSED_TAB", fused_tab);
     get("DAB_SETUP_HOST", setup_host);
@@ -2095,7 +2098,8 @@ static int build_schur_tiles(dab_handle* h, int2* d_sch, const int* d_m) {
   const int NP = h->NP, NC = h->NC;
   const bool on_device = d_sch != nullptr;
   Dev& d = h->dev;
-  const int cap = schur_tile_batch_cap(NC);
+  const bool single = h->knobs.tile_single != 0;
+  const int cap = schur_tile_batch_cap(NC, single);
   const int hdr_bytes = schur_tile_hdr_bytes(NC);
   const int nb = (int)tri_n(NC);
   std::vector<int> rec_ptr(NP + 1, 0);
@@ -2308,6 +2312,7 @@ static int build_schur_tiles(dab_handle* h, int2* d_sch, const int* d_m) {
   a.stride = (size_t)a.nelem;
   a.kq = 0;
   a.batch_cap = cap;
+  a.single = single ? 1 : 0;
   a.hdr_bytes = hdr_bytes;
   int *d_cl = nullptr, *d_slot = nullptr;
   CHECK_RC(upload(&d_cl, d, clast, s));
