@@ -1932,13 +1932,19 @@ __device__ __forceinline__ void lds_wait_ge(const unsigned* w, unsigned want, un
     }
   }
 }
+// WPC_, WPS_ > 0: the waves per camera and per slice as compile-time constants (C3: 2, 1;
+// C2: 8, 8), 0: the run-time wpc_rt, wps_rt. Round 6: the constants fold the part cuts'
+// divisions, the part-combine and slice-part loops and the slot arithmetic — C2 9.29 ->
+// 8.44 us per launch, C3 unchanged, bitwise the same sums (profiles/r06zk_*)
+template <int WPC_, int WPS_>
 __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restrict__ chunk_beg,
                                                    const double* __restrict__ points, const double* __restrict__ ext,
                                                    const double* __restrict__ camtab, double* __restrict__ V,
                                                    double* __restrict__ g, double* __restrict__ ug,
                                                    unsigned long long* __restrict__ costfx,
                                                    unsigned long long* __restrict__ fx_next, unsigned* __restrict__ err,
-                                                   int wpc, int wps, int side) {
+                                                   int wpc_rt, int wps_rt, int side) {
+  const int wpc = WPC_ > 0 ? WPC_ : wpc_rt, wps = WPS_ > 0 ? WPS_ : wps_rt;
   __shared__ double rt_s[kLdsCams * 12];
   __shared__ double k_s[kLdsCams * 6];
   __shared__ double csum[kBalCW][27];            // camera waves' sums: [slot * wpc + part]
@@ -2254,7 +2260,12 @@ void launch_eval_bal(hipStream_t s, const DevView& v, const int* chunk_beg, cons
                      const double* camtab, double* V, double* g, double* ug, unsigned long long* costfx,
                      unsigned long long* fx_next, unsigned* err, int grid, int side) {
   const int wpc = fused_wpc(v.NC, grid), wps = fused_wps(v.nslice, v.E, grid);
-  k_eval_bal<<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, camtab, V, g, ug, costfx, fx_next, err, wpc, wps, side);
+  if (wpc == 2 && wps == 1)
+    k_eval_bal<2, 1><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, camtab, V, g, ug, costfx, fx_next, err, wpc, wps, side);
+  else if (wpc == 8 && wps == 8)
+    k_eval_bal<8, 8><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, camtab, V, g, ug, costfx, fx_next, err, wpc, wps, side);
+  else
+    k_eval_bal<0, 0><<<grid, 1024, 0, s>>>(v, chunk_beg, points, ext, camtab, V, g, ug, costfx, fx_next, err, wpc, wps, side);
 }
 
 __global__ __launch_bounds__(256) void k_eval_cross(DevView v, const int* __restrict__ chunk_beg,
