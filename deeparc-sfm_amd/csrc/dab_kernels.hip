@@ -2078,6 +2078,13 @@ __global__ __launch_bounds__(1024) void k_eval_bal(DevView v, const int* __restr
     DAB_STAMP(3);
     return;
   }
+  // a work-group with no slice in any round (slot 0 of round 0 holds its lowest slice, b):
+  // no tables, no rows, nothing to add (small problems: C2's camera work-groups, whose camera
+  // waves then have the CU's issue and memory path to themselves)
+  if ((int)blockIdx.x >= v.nslice) {
+    DAB_STAMP(3);
+    return;
+  }
   const size_t NPs = (size_t)v.NP;
   const int pw = wave, pslots = kBalPW / wps, slot = pw / wps, part = pw - slot * wps;
   const int rounds = abl_tables_only ? 0 : (v.nslice + pslots * gridDim.x - 1) / (pslots * gridDim.x);
