@@ -3,7 +3,7 @@
 # filled with NaN bytes), then the 8-rank bench rehearsal on one GPU (eight processes,
 # host-staged collectives) beside the N = 1 line of the same short settings
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
-O=gpurun_out/r06zh; mkdir -p $O
+O=gpurun_out/${TAG:-r06zh}; mkdir -p $O
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 DAB_DEV_POISON=1 timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 600 --timeout-method thread > $O/pytest_gpu_poison.log 2>&1
 rc=$?; echo "poison pytest rc=$rc"; tail -2 $O/pytest_gpu_poison.log; [ $rc -eq 0 ] || exit $rc
