@@ -667,6 +667,26 @@ def test_schur_tiles_match_pair_tables(pkg, gpu, kind, monkeypatch):
     np.testing.assert_array_equal(pts[0], pts[2])
 
 
+def test_schur_tiles_one_and_two_lds_buffers_agree(pkg, gpu, monkeypatch):
+    """k_schur_tiles streams its batches through one LDS buffer (round 6's default: batches
+    of up to 64 points) or two (DAB_TILE_SINGLE=0: half the records per batch, the next one
+    in flight). The batches differ, so the blocks' partial sums are grouped differently: the
+    same LM trajectory to rounding (cost 1e-12 relative, same iterations and termination)."""
+    prob = pkg.synth(kind=1, num_arcs=8, num_rings=24, num_points=6000, obs_per_point=10, seed=74)
+    res = []
+    for single in ("1", "0"):
+        monkeypatch.setenv("DAB_TILE_SINGLE", single)
+        s = pkg.Solver(0)
+        s.set_problem(prob.copy())
+        res.append(s.solve(pkg.options(max_num_iterations=8)))
+        s.close()
+    a, b = res
+    assert a["schur_assembly"] == 1 and b["schur_assembly"] == 1
+    assert len(a["iterations"]) == len(b["iterations"]) and a["termination"] == b["termination"]
+    np.testing.assert_allclose([it["cost"] for it in a["iterations"]], [it["cost"] for it in b["iterations"]],
+                               rtol=1e-12)
+
+
 @pytest.mark.parametrize("kind", ["bal", "rig"])
 def test_large_initial_cost_matches_oracle(pkg, orc, gpu, kind):
     """A finite cost far beyond the old fixed-point range is an ordinary evaluation for
